@@ -1,0 +1,170 @@
+/*
+ * rt_api.h — C-ABI of the MI355X path-tracer hot path (librt_hip.so).
+ *
+ * This is the drop-in boundary for the reference's one GPU hot path, the Metal compute kernel
+ * `raytracingKernel` (MetalRaytracing/Raytracing.metal:220-831) and the host code that binds and
+ * dispatches it.  Each entry point names the reference interface it replaces:
+ *
+ *   rt_create / rt_destroy     Renderer.init?(metalView:) device+queue+pipeline setup
+ *                              (Renderer.swift:228-341), deinit
+ *   rt_scene_upload            createBuffers: Resource argument buffer, material buffers,
+ *                              vertex/index buffers, light buffer (Renderer.swift:342-420,
+ *                              SubMesh.swift:38-54, Scene.swift:93)
+ *   rt_bvh_build               createMTL4AccelerationStructures BLAS+TLAS build
+ *                              (Renderer.swift:464-606, Utilities.swift:101-290)
+ *   rt_set_instance_transforms updateInstanceDescriptors (Renderer.swift:937-973): current ->
+ *                              previous copy, then new transforms
+ *   rt_skin                    SkinningPass.dispatchSkinning + prev-position copy
+ *                              (SkinningPass.swift:160-211, Renderer.swift:1290-1310)
+ *   rt_bvh_refit               refitMTL4AccelerationStructures (Renderer.swift:1084-1202)
+ *   rt_resize                  createTextures: accumulation ping-pong, random-offset texture,
+ *                              depth/motion/G-buffer targets (Renderer.swift:676-804)
+ *   rt_render_frame            Renderer.draw: argument-table binding + 16x16 dispatch of
+ *                              raytracingKernel + ping-pong swap (Renderer.swift:1405-1503)
+ *   rt_read_radiance/rt_read_aux  (no reference equivalent: the reference never reads back;
+ *                              replaces presenting dstTex/depthTex/motionTex to MetalFX)
+ *
+ * Conventions: every function returns rt_status (0 = OK); rt_last_error(ctx) describes the last
+ * failure.  No exceptions or aborts cross this boundary.  The caller owns every host array and
+ * may free it once the call returns.  One context per GPU, used from one host thread.  All
+ * work is issued on one HIP stream per context (rt_set_stream may substitute the caller's).
+ */
+#ifndef RT_API_H
+#define RT_API_H
+
+#include "rt_types.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef int32_t rt_status;
+#define RT_OK 0
+#define RT_ERR_INVALID_ARG 1
+#define RT_ERR_HIP 2
+#define RT_ERR_IO 3
+#define RT_ERR_OUT_OF_MEMORY 4
+#define RT_ERR_STATE 5
+#define RT_ERR_UNSUPPORTED 6
+#define RT_ERR_NO_DEVICE 7
+
+typedef struct rt_ctx rt_ctx;
+
+/* ---- scene description (caller-owned, copied by rt_scene_upload) ------------------------- */
+
+/* One Submesh: a material group of one mesh (SubMesh.swift:18-54). Indices are u32
+ * (u16 assets are widened, SubMesh.swift:243-265), three per triangle. */
+typedef struct rt_submesh_desc {
+    const uint32_t* indices;
+    uint32_t index_count;
+    uint32_t _pad;
+    Material material;
+} rt_submesh_desc;
+
+/* One Mesh = one instance of the two-level acceleration structure (Mesh.swift:17-68). Vertex
+ * streams follow Model.vertexDescriptor (Model.swift:304-341): positions and normals float3 at
+ * a 16-byte stride, uvs float2 (may be NULL), joint indices ushort4 and weights float4 (NULL
+ * unless skinned).  `transform` is the object->world MTLPackedFloat4x3 of the instance
+ * descriptor (Renderer.swift:547-556). */
+typedef struct rt_mesh_desc {
+    const rt_float3* positions;
+    const rt_float3* normals;
+    const rt_float2* uvs;
+    const uint16_t* joint_indices;
+    const float* joint_weights;
+    uint32_t vertex_count;
+    uint32_t submesh_count;
+    const rt_submesh_desc* submeshes;
+    rt_packed_float4x3 transform;
+    uint32_t joint_count;   /* > 0: skinned mesh (rt_skin rewrites its positions/normals) */
+    uint32_t _pad;
+} rt_mesh_desc;
+
+typedef struct rt_scene_desc {
+    uint32_t mesh_count;
+    uint32_t light_count;
+    const rt_mesh_desc* meshes;
+    const Light* lights;
+} rt_scene_desc;
+
+/* ---- context ------------------------------------------------------------------------------- */
+
+#define RT_PIPELINE_MEGAKERNEL 0  /* one thread per pixel, the reference's kernel shape */
+#define RT_PIPELINE_WAVEFRONT 1   /* generate / extend / shade / connect / resolve queues */
+
+typedef struct rt_opts {
+    int32_t device;     /* HIP device ordinal */
+    int32_t pipeline;   /* RT_PIPELINE_* */
+    int32_t reserved[6];
+} rt_opts;
+
+/* Image-space tile partition for multi-GPU rendering: the image is cut into
+ * tile_size x tile_size tiles numbered row-major; this rank renders tiles with
+ * tile_id % nranks == rank.  A NULL tile set (or nranks <= 1) renders the whole image. */
+typedef struct rt_tile_set {
+    int32_t tile_size;
+    int32_t rank;
+    int32_t nranks;
+    int32_t _pad;
+} rt_tile_set;
+
+typedef struct rt_stats {
+    uint64_t closest_rays;  /* closest-hit queries traced in the last frame (incl. primary) */
+    uint64_t shadow_rays;   /* any-hit shadow queries traced in the last frame */
+    uint64_t node_visits;   /* BVH nodes fetched (counting frames only, see rt_set_counting) */
+    uint64_t tri_tests;     /* triangles tested (counting frames only) */
+    uint64_t paths;         /* pixel samples started */
+    uint64_t bvh_nodes;     /* nodes in the current BVH */
+    uint64_t triangles;     /* triangles in the current scene */
+    uint64_t device_bytes;  /* device memory held by the context */
+    float last_frame_ms;    /* device time of the last rt_render_frame (HIP events) */
+    float kernel_ms[7];     /* per-stage device time of the last frame, pipeline-specific */
+} rt_stats;
+
+rt_status rt_create(const rt_opts* opts, rt_ctx** out);
+rt_status rt_destroy(rt_ctx* ctx);
+const char* rt_last_error(const rt_ctx* ctx);   /* ctx may be NULL: last global error */
+rt_status rt_set_stream(rt_ctx* ctx, void* hip_stream);  /* NULL restores the own stream */
+
+rt_status rt_scene_upload(rt_ctx* ctx, const rt_scene_desc* scene);
+rt_status rt_bvh_build(rt_ctx* ctx);
+rt_status rt_bvh_refit(rt_ctx* ctx);
+rt_status rt_set_instance_transforms(rt_ctx* ctx, const rt_packed_float4x3* transforms, uint32_t count);
+/* Linear-blend skinning of one skinned mesh (Skinning.metal:7-49). `joint_matrices` are
+ * column-major float4x4 (host memory). Copies current positions to previous first. */
+rt_status rt_skin(rt_ctx* ctx, uint32_t mesh_index, const float* joint_matrices, uint32_t joint_count);
+
+/* (Re)create the per-pixel targets; `random_offsets` is W*H uint32 (row-major). Resets history. */
+rt_status rt_resize(rt_ctx* ctx, int32_t width, int32_t height, const uint32_t* random_offsets);
+
+/* Render one frame (asynchronous; rt_wait to block). Reads the history written by the previous
+ * call, writes the new accumulation and swaps (Renderer.swift:1492-1494). */
+rt_status rt_render_frame(rt_ctx* ctx, const Uniforms* uniforms, const rt_tile_set* tiles);
+rt_status rt_wait(rt_ctx* ctx);
+
+/* Copies of the latest outputs into caller host memory: radiance RGBA float32 W*H*4 (the
+ * accumulation target just written; the reference stores it as RGBA16F), depth W*H,
+ * motion W*H*2 (pixels, +Y down), G-buffer 4 planes of W*H*4 (diffuse, specular, normal,
+ * roughness) or NULL. Rows are in the kernel's tid.y order (row 0 = bottom of the view). */
+rt_status rt_read_radiance(rt_ctx* ctx, float* rgba);
+rt_status rt_read_aux(rt_ctx* ctx, float* depth, float* motion, float* gbuffer);
+
+/* Multi-GPU: pack this rank's tiles of the latest radiance into a device buffer of
+ * rt_tile_count(...) * tile_size^2 * 4 floats, and the inverse on the gathering rank
+ * (writing into the latest radiance target). Device pointers; ordered on the ctx stream. */
+int32_t rt_tile_count(int32_t width, int32_t height, const rt_tile_set* tiles);
+rt_status rt_pack_tiles(rt_ctx* ctx, const rt_tile_set* tiles, void* device_dst);
+rt_status rt_unpack_tiles(rt_ctx* ctx, const rt_tile_set* tiles, const void* device_src);
+
+/* Device ray/node counters: when enabled, frames also count BVH node visits / triangle tests
+ * (a few percent slower). Ray counts are always collected. */
+rt_status rt_set_counting(rt_ctx* ctx, int32_t enabled);
+rt_status rt_get_stats(rt_ctx* ctx, rt_stats* out);
+
+/* Library build identification (kernel code object arch etc). */
+const char* rt_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RT_API_H */

@@ -1,0 +1,319 @@
+"""metal4-raytracing_amd — MI355X-native path tracer for the raytracingKernel hot path.
+
+Python host mirror of the reference's Swift interface for this path, over the C-ABI
+library librt_hip.so (include/rt_api.h, include/rt_scene.h):
+
+    Scene      ~ MetalRaytracing/Scene.swift + AppScene.swift (models, lights, orbit camera)
+    Renderer   ~ MetalRaytracing/Renderer.swift (knobs with didSet -> frameIndex = 0,
+                 updateUniforms, draw, accumulation ping-pong)
+
+The compute path is the HIP library; there is no CPU fallback: importing this package on a
+machine without the built library raises, and Renderer() raises without a HIP device.
+Load it with importlib.import_module("metal4-raytracing_amd") (the directory name has a dash).
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+from . import _abi
+from ._abi import (Camera, Float3, Light, MaterialOverride, PackedFloat4x3, SceneDesc, Stats, TileSet, Uniforms,
+                   f3)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "librt_hip.so")
+ASSET_DIR_DEFAULT = os.environ.get("RT_ASSET_DIR", os.path.join(os.path.dirname(_HERE), "assets"))
+
+_lib = None
+
+
+class RTError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"rt status {code}: {msg}")
+        self.code = code
+
+
+def lib():
+    """The loaded librt_hip.so (raises if it was not built — no fallback)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"{LIB_PATH} is missing: run __graft_entry__.build() (make -C metal4-raytracing_amd)")
+        # torch bundles its own libamdhip64.so.7 (same soname as /opt/rocm's). Load torch first so
+        # the process holds ONE HIP runtime; torch.distributed / tensors then share it with us.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
+        _lib = _abi.declare(C.CDLL(LIB_PATH))
+    return _lib
+
+
+def _check(st, ctx=None, scene=None):
+    if st != 0:
+        if scene is not None:
+            msg = lib().rt_scene_last_error(scene)
+        else:
+            msg = lib().rt_last_error(ctx)
+        raise RTError(st, (msg or b"").decode())
+
+
+def version():
+    return lib().rt_version().decode()
+
+
+def uniforms_default(width, height, light_count=2):
+    u = Uniforms()
+    lib().rt_uniforms_default(width, height, light_count, C.byref(u))
+    return u
+
+
+def camera_default(width, height):
+    c = Camera()
+    lib().rt_camera_default(width, height, C.byref(c))
+    return c
+
+
+def random_offsets(seed, width, height):
+    """splitmix64(seed) % 2^20 per pixel, row-major (Renderer.swift:719-738, seeded)."""
+    out = np.empty(width * height, dtype=np.uint32)
+    lib().rt_random_offsets(seed, width, height, out.ctypes.data_as(C.POINTER(C.c_uint32)))
+    return out
+
+
+def glass_override():
+    o = MaterialOverride()
+    lib().rt_material_override_glass(C.byref(o))
+    return o
+
+
+class Scene:
+    """Host scene (Scene.swift / AppScene.swift / Model.swift OBJ path)."""
+
+    def __init__(self, handle=None):
+        if handle is None:
+            h = C.c_void_p()
+            _check(lib().rt_scene_new(C.byref(h)))
+            handle = h
+        self._h = handle
+        self.synthetic = False
+
+    @classmethod
+    def preset(cls, name, asset_dir=None):
+        h = C.c_void_p()
+        synth = C.c_int32(0)
+        st = lib().rt_scene_preset(name.encode(), (asset_dir or ASSET_DIR_DEFAULT).encode(), C.byref(h),
+                                   C.byref(synth))
+        if st != 0:
+            msg = lib().rt_scene_last_error(h) if h.value else lib().rt_last_error(None)
+            if h.value:
+                lib().rt_scene_free(h)
+            raise RTError(st, (msg or b"").decode())
+        s = cls(h)
+        s.synthetic = bool(synth.value)
+        return s
+
+    def add_model(self, obj_path, position, rotation=(0, 0, 0), scale=1.0, material_override=None):
+        """Model(name:position:rotation:scale:materialOverride:) for an OBJ file."""
+        p = (C.c_float * 3)(*position)
+        r = (C.c_float * 3)(*rotation)
+        _check(lib().rt_scene_add_obj(self._h, obj_path.encode(), p, r, scale,
+                                      C.byref(material_override) if material_override else None), scene=self._h)
+
+    def add_procedural(self, kind, position, rotation=(0, 0, 0), scale=1.0, material_override=None, mtl_path=None):
+        p = (C.c_float * 3)(*position)
+        r = (C.c_float * 3)(*rotation)
+        _check(lib().rt_scene_add_procedural(self._h, kind.encode(), mtl_path.encode() if mtl_path else None, p, r,
+                                             scale, C.byref(material_override) if material_override else None),
+               scene=self._h)
+
+    def set_lights(self, lights):
+        arr = (Light * len(lights))(*lights)
+        _check(lib().rt_scene_set_lights(self._h, arr, len(lights)), scene=self._h)
+
+    def set_light_intensity(self, intensity):
+        _check(lib().rt_scene_set_light_intensity(self._h, intensity), scene=self._h)
+
+    def desc(self):
+        d = SceneDesc()
+        _check(lib().rt_scene_get_desc(self._h, C.byref(d)), scene=self._h)
+        return d
+
+    @property
+    def triangle_count(self):
+        return int(lib().rt_scene_triangle_count(self._h))
+
+    @property
+    def light_count(self):
+        return int(self.desc().light_count)
+
+    def joint_matrices(self, mesh_index, time_seconds, capacity=256):
+        out = np.zeros((capacity, 16), dtype=np.float32)
+        n = C.c_uint32(0)
+        _check(lib().rt_scene_joint_matrices(self._h, mesh_index, time_seconds,
+                                             out.ctypes.data_as(C.POINTER(C.c_float)), capacity, C.byref(n)),
+               scene=self._h)
+        return out[: n.value].copy()
+
+    def close(self):
+        if self._h:
+            lib().rt_scene_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+_KNOBS = {
+    # Renderer.swift:52-192 property -> (Uniforms field, default)
+    "samplesPerPixel": ("samplesPerPixel", 2),
+    "maxBounces": ("maxBounces", 2),
+    "accumulationWeight": ("accumulationWeight", 0.9),
+    "useMotionAdaptiveAccumulation": ("enableMotionAdaptiveAccumulation", True),
+    "motionAccumulationMinWeight": ("motionAccumulationMinWeight", 0.1),
+    "motionAccumulationLowThresholdPixels": ("motionAccumulationLowThresholdPixels", 0.5),
+    "motionAccumulationHighThresholdPixels": ("motionAccumulationHighThresholdPixels", 4.0),
+    "useMotionAdaptiveSampling": ("enableMotionAdaptiveSampling", True),
+    "motionSamplingMaxExtraSamples": ("motionSamplingMaxExtraSamples", 2),
+    "motionSamplingLowThresholdPixels": ("motionSamplingLowThresholdPixels", 1.0),
+    "motionSamplingHighThresholdPixels": ("motionSamplingHighThresholdPixels", 6.0),
+    "debugTextureMode": ("debugTextureMode", 0),
+    "shadingMode": ("shadingMode", 0),
+    "useTemporalDenoiser": ("enableDenoiseGBuffer", False),
+}
+
+
+class Renderer:
+    """Renderer.swift for the hot path: owns a device context, the uniforms and the frame index.
+
+    Setting any knob resets frameIndex to 0 (the reference's didSet { frameIndex = 0 }).
+    draw() = updateUniforms + raytracingKernel dispatch + accumulation swap.
+    """
+
+    def __init__(self, scene, width, height, device=0, pipeline="megakernel", seed=1, stream=None):
+        object.__setattr__(self, "_ctx", None)
+        self.scene = scene
+        self.width, self.height = int(width), int(height)
+        opts = _abi.Opts()
+        opts.device = device
+        opts.pipeline = {"megakernel": 0, "wavefront": 1}[pipeline]
+        ctx = C.c_void_p()
+        _check(lib().rt_create(C.byref(opts), C.byref(ctx)))
+        object.__setattr__(self, "_ctx", ctx)
+        if stream is not None:
+            _check(lib().rt_set_stream(ctx, C.c_void_p(stream)), ctx)
+        d = scene.desc()
+        self.light_count = int(d.light_count)
+        _check(lib().rt_scene_upload(ctx, C.byref(d)), ctx)
+        _check(lib().rt_bvh_build(ctx), ctx)
+        self.random = random_offsets(seed, self.width, self.height)
+        _check(lib().rt_resize(ctx, self.width, self.height, self.random.ctypes.data_as(C.POINTER(C.c_uint32))), ctx)
+        self.camera = camera_default(self.width, self.height)
+        self.previousCamera = None
+        self.frameIndex = 0
+        self._knobs = {k: v for k, (_, v) in _KNOBS.items()}
+
+    def __getattr__(self, name):
+        knobs = self.__dict__.get("_knobs")
+        if knobs is not None and name in knobs:
+            return knobs[name]
+        raise AttributeError(name)
+
+    def __setattr__(self, name, value):
+        if name in _KNOBS and "_knobs" in self.__dict__:
+            self._knobs[name] = value
+            self.__dict__["frameIndex"] = 0  # didSet { frameIndex = 0 }
+            return
+        object.__setattr__(self, name, value)
+
+    # --- Renderer.updateUniforms (Renderer.swift:608-664) ---
+    def uniforms(self):
+        u = uniforms_default(self.width, self.height, self.light_count)
+        for k, (field, _) in _KNOBS.items():
+            v = self._knobs[k]
+            setattr(u, field, int(v) if isinstance(v, bool) else v)
+        u.camera = self.camera
+        u.previousCamera = self.previousCamera if self.previousCamera is not None else self.camera
+        u.frameIndex = self.frameIndex
+        return u
+
+    def draw(self, tiles=None):
+        u = self.uniforms()
+        ts = None
+        if tiles is not None:
+            ts = TileSet(tiles[0], tiles[1], tiles[2], 0)
+        _check(lib().rt_render_frame(self._ctx, C.byref(u), C.byref(ts) if ts else None), self._ctx)
+        self.__dict__["frameIndex"] = self.frameIndex + 1
+        self.previousCamera = self.camera
+        return u
+
+    def wait(self):
+        _check(lib().rt_wait(self._ctx), self._ctx)
+
+    def set_counting(self, on):
+        _check(lib().rt_set_counting(self._ctx, 1 if on else 0), self._ctx)
+
+    def stats(self):
+        s = Stats()
+        _check(lib().rt_get_stats(self._ctx, C.byref(s)), self._ctx)
+        return s
+
+    def radiance(self):
+        out = np.empty((self.height, self.width, 4), dtype=np.float32)
+        _check(lib().rt_read_radiance(self._ctx, out.ctypes.data_as(C.POINTER(C.c_float))), self._ctx)
+        return out
+
+    def aux(self, gbuffer=False):
+        depth = np.empty((self.height, self.width), dtype=np.float32)
+        motion = np.empty((self.height, self.width, 2), dtype=np.float32)
+        gb = np.empty((4, self.height, self.width, 4), dtype=np.float32) if gbuffer else None
+        FP = C.POINTER(C.c_float)
+        _check(lib().rt_read_aux(self._ctx, depth.ctypes.data_as(FP), motion.ctypes.data_as(FP),
+                                 gb.ctypes.data_as(FP) if gb is not None else None), self._ctx)
+        return depth, motion, gb
+
+    def set_instance_transforms(self, mats):
+        """mats: (n, 4, 3) packed column-major object->world (updateInstanceDescriptors)."""
+        arr = np.ascontiguousarray(mats, dtype=np.float32).reshape(-1, 12)
+        _check(lib().rt_set_instance_transforms(self._ctx, arr.ctypes.data_as(C.POINTER(PackedFloat4x3)),
+                                                arr.shape[0]), self._ctx)
+
+    def skin(self, mesh_index, joints):
+        j = np.ascontiguousarray(joints, dtype=np.float32)
+        _check(lib().rt_skin(self._ctx, mesh_index, j.ctypes.data_as(C.POINTER(C.c_float)), j.shape[0]), self._ctx)
+
+    def refit(self):
+        _check(lib().rt_bvh_refit(self._ctx), self._ctx)
+
+    def rebuild(self):
+        _check(lib().rt_bvh_build(self._ctx), self._ctx)
+
+    def tile_count(self, tile_size, rank, nranks):
+        ts = TileSet(tile_size, rank, nranks, 0)
+        return int(lib().rt_tile_count(self.width, self.height, C.byref(ts)))
+
+    def pack_tiles(self, tile_size, rank, nranks, device_ptr):
+        ts = TileSet(tile_size, rank, nranks, 0)
+        _check(lib().rt_pack_tiles(self._ctx, C.byref(ts), C.c_void_p(device_ptr)), self._ctx)
+
+    def unpack_tiles(self, tile_size, rank, nranks, device_ptr):
+        ts = TileSet(tile_size, rank, nranks, 0)
+        _check(lib().rt_unpack_tiles(self._ctx, C.byref(ts), C.c_void_p(device_ptr)), self._ctx)
+
+    def set_stream(self, stream_handle):
+        _check(lib().rt_set_stream(self._ctx, C.c_void_p(stream_handle) if stream_handle else None), self._ctx)
+
+    def close(self):
+        ctx = self.__dict__.get("_ctx")
+        if ctx:
+            lib().rt_destroy(ctx)
+            object.__setattr__(self, "_ctx", None)
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -1,0 +1,623 @@
+// rt_api.cpp — C-ABI implementation (include/rt_api.h): device memory, scene upload, BVH,
+// per-pixel targets, frame dispatch.  Mirrors the responsibilities of the reference's Renderer
+// (MetalRaytracing/Renderer.swift) for the hot path; all device work is issued in order on one
+// HIP stream per context (the reference's MTL4CommandQueue + events, Renderer.swift:1405-1503).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/rt_api.h"
+#include "rt_bvh.h"
+#include "rt_kernels.h"
+
+using namespace rt;
+
+namespace {
+thread_local std::string g_err;
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+};
+
+struct MeshInfo {
+    uint32_t vbase = 0, vcount = 0, joint_count = 0;
+    bool skinned = false;
+};
+}  // namespace
+
+struct rt_ctx {
+    int device = 0;
+    int pipeline = RT_PIPELINE_MEGAKERNEL;
+    hipStream_t own_stream = nullptr, stream = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    std::string err;
+    bool counting = false;
+    bool frame_pending = false;
+
+    // host scene copies
+    std::vector<float4> h_pos, h_nrm;
+    std::vector<uint4> h_tri_info;
+    std::vector<float> h_inst;
+    std::vector<Material> h_mat;
+    std::vector<Light> h_lights;
+    std::vector<MeshInfo> meshes;
+    std::vector<float> h_world;   // 9 floats per triangle
+    int max_sub = 1;
+    uint32_t num_tris = 0, num_verts = 0, num_inst = 0;
+    bool scene_ready = false, bvh_ready = false;
+    bool world_dirty = false;  // device positions/transforms changed since h_world was computed
+
+    // BVH
+    BvhResult bvh;
+    std::vector<uint32_t> level_nodes;
+    std::vector<uint32_t> level_off;
+
+    // device buffers
+    DevBuf d_pos, d_prev_pos, d_nrm, d_rest_pos, d_rest_nrm, d_jidx, d_jw, d_joints;
+    DevBuf d_tri_info, d_inst, d_prev_inst, d_mat, d_lights, d_halton;
+    DevBuf d_tris, d_nodes, d_slot_to_tri, d_levels;
+    DevBuf d_random, d_accum[2], d_depth, d_motion, d_gbuffer, d_counters;
+    int width = 0, height = 0;
+    int read_idx = 0;   // accum[read_idx] = history (TextureIndexAccumulation)
+    unsigned long long* h_counters = nullptr;  // pinned
+    rt_stats stats{};
+};
+
+#define FAIL(ctx, code, msg)                 \
+    do {                                     \
+        if (ctx) (ctx)->err = (msg);         \
+        g_err = (msg);                       \
+        return (code);                       \
+    } while (0)
+
+#define HIPC(ctx, expr)                                                                            \
+    do {                                                                                           \
+        hipError_t e_ = (expr);                                                                    \
+        if (e_ != hipSuccess) {                                                                    \
+            std::string m_ = std::string(#expr) + ": " + hipGetErrorString(e_);                    \
+            if (ctx) (ctx)->err = m_;                                                              \
+            g_err = m_;                                                                            \
+            return e_ == hipErrorOutOfMemory ? RT_ERR_OUT_OF_MEMORY : RT_ERR_HIP;                  \
+        }                                                                                          \
+    } while (0)
+
+static rt_status dev_alloc(rt_ctx* c, DevBuf& b, size_t bytes) {
+    if (b.p && b.bytes >= bytes && bytes > 0) return RT_OK;
+    if (b.p) { hipFree(b.p); b.p = nullptr; b.bytes = 0; }
+    if (bytes == 0) return RT_OK;
+    HIPC(c, hipMalloc(&b.p, bytes));
+    b.bytes = bytes;
+    return RT_OK;
+}
+static rt_status dev_upload(rt_ctx* c, DevBuf& b, const void* src, size_t bytes) {
+    rt_status st = dev_alloc(c, b, bytes);
+    if (st) return st;
+    if (bytes) HIPC(c, hipMemcpyAsync(b.p, src, bytes, hipMemcpyHostToDevice, c->stream));
+    return RT_OK;
+}
+static void dev_free(DevBuf& b) {
+    if (b.p) hipFree(b.p);
+    b.p = nullptr;
+    b.bytes = 0;
+}
+
+static std::vector<HaltonDim> halton_table() {
+    std::vector<HaltonDim> t;
+    uint32_t n = 2;
+    while ((int)t.size() < RT_HALTON_DIMS) {
+        bool prime = true;
+        for (auto& h : t) {
+            if (h.b * h.b > n) break;
+            if (n % h.b == 0) { prime = false; break; }
+        }
+        if (prime) {
+            HaltonDim h;
+            h.b = n;
+            uint32_t l = 0;
+            while ((1u << l) < n) ++l;              // 2^(l-1) < b <= 2^l
+            h.m = (uint32_t)(((1ull << (31 + l)) + n - 1) / n);
+            h.sh = l - 1;
+            h.invB = 1.0f / (float)n;
+            t.push_back(h);
+        }
+        ++n;
+    }
+    return t;
+}
+
+// host object->world, identical arithmetic to rt::xform on the device
+static void xform_host(const float* m, const float4& p, float* out) {
+    for (int r = 0; r < 3; ++r) out[r] = ((m[0 + r] * p.x + m[3 + r] * p.y) + m[6 + r] * p.z) + m[9 + r] * 1.0f;
+}
+
+static size_t ctx_bytes(const rt_ctx* c) {
+    const DevBuf* all[] = {&c->d_pos, &c->d_prev_pos, &c->d_nrm, &c->d_rest_pos, &c->d_rest_nrm, &c->d_jidx, &c->d_jw,
+                           &c->d_joints, &c->d_tri_info, &c->d_inst, &c->d_prev_inst, &c->d_mat, &c->d_lights,
+                           &c->d_halton, &c->d_tris, &c->d_nodes, &c->d_slot_to_tri, &c->d_levels, &c->d_random,
+                           &c->d_accum[0], &c->d_accum[1], &c->d_depth, &c->d_motion, &c->d_gbuffer, &c->d_counters};
+    size_t s = 0;
+    for (auto* b : all) s += b->bytes;
+    return s;
+}
+
+extern "C" {
+
+const char* rt_version(void) {
+    return "rt_hip 0.1 (gfx950, BVH2 watertight, megakernel)";
+}
+
+const char* rt_last_error(const rt_ctx* ctx) { return ctx ? ctx->err.c_str() : g_err.c_str(); }
+
+rt_status rt_create(const rt_opts* opts, rt_ctx** out) {
+    if (!out) FAIL((rt_ctx*)nullptr, RT_ERR_INVALID_ARG, "out is null");
+    *out = nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) FAIL((rt_ctx*)nullptr, RT_ERR_NO_DEVICE, "no HIP device");
+    rt_ctx* c = new (std::nothrow) rt_ctx();
+    if (!c) FAIL((rt_ctx*)nullptr, RT_ERR_OUT_OF_MEMORY, "alloc ctx");
+    if (opts) {
+        c->device = opts->device;
+        c->pipeline = opts->pipeline;
+    }
+    if (c->device < 0 || c->device >= ndev) { delete c; FAIL((rt_ctx*)nullptr, RT_ERR_INVALID_ARG, "bad device ordinal"); }
+    if (c->pipeline != RT_PIPELINE_MEGAKERNEL && c->pipeline != RT_PIPELINE_WAVEFRONT) {
+        delete c;
+        FAIL((rt_ctx*)nullptr, RT_ERR_INVALID_ARG, "bad pipeline");
+    }
+    hipError_t e = hipSetDevice(c->device);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreate(&c->ev0);
+    if (e == hipSuccess) e = hipEventCreate(&c->ev1);
+    if (e == hipSuccess) e = hipHostMalloc((void**)&c->h_counters, sizeof(unsigned long long) * kCntSlots, 0);
+    if (e != hipSuccess) {
+        g_err = std::string("HIP init: ") + hipGetErrorString(e);
+        delete c;
+        return RT_ERR_HIP;
+    }
+    c->stream = c->own_stream;
+    auto tab = halton_table();
+    rt_status st = dev_upload(c, c->d_halton, tab.data(), tab.size() * sizeof(HaltonDim));
+    if (!st) st = dev_alloc(c, c->d_counters, sizeof(unsigned long long) * kCntSlots);
+    if (!st && hipStreamSynchronize(c->stream) != hipSuccess) st = RT_ERR_HIP;
+    if (st) {
+        g_err = c->err;
+        rt_destroy(c);
+        return st;
+    }
+    *out = c;
+    return RT_OK;
+}
+
+rt_status rt_destroy(rt_ctx* c) {
+    if (!c) return RT_OK;
+    hipSetDevice(c->device);
+    if (c->stream) hipStreamSynchronize(c->stream);
+    DevBuf* all[] = {&c->d_pos, &c->d_prev_pos, &c->d_nrm, &c->d_rest_pos, &c->d_rest_nrm, &c->d_jidx, &c->d_jw,
+                     &c->d_joints, &c->d_tri_info, &c->d_inst, &c->d_prev_inst, &c->d_mat, &c->d_lights, &c->d_halton,
+                     &c->d_tris, &c->d_nodes, &c->d_slot_to_tri, &c->d_levels, &c->d_random, &c->d_accum[0],
+                     &c->d_accum[1], &c->d_depth, &c->d_motion, &c->d_gbuffer, &c->d_counters};
+    for (auto* b : all) dev_free(*b);
+    if (c->h_counters) hipHostFree(c->h_counters);
+    if (c->ev0) hipEventDestroy(c->ev0);
+    if (c->ev1) hipEventDestroy(c->ev1);
+    if (c->own_stream) hipStreamDestroy(c->own_stream);
+    delete c;
+    return RT_OK;
+}
+
+rt_status rt_set_stream(rt_ctx* c, void* s) {
+    if (!c) FAIL(c, RT_ERR_INVALID_ARG, "null ctx");
+    c->stream = s ? (hipStream_t)s : c->own_stream;
+    return RT_OK;
+}
+
+rt_status rt_scene_upload(rt_ctx* c, const rt_scene_desc* sd) {
+    if (!c || !sd) FAIL(c, RT_ERR_INVALID_ARG, "null argument");
+    HIPC(c, hipSetDevice(c->device));
+    if (sd->mesh_count == 0) FAIL(c, RT_ERR_INVALID_ARG, "scene has no meshes");
+    if (sd->light_count == 0 || !sd->lights) FAIL(c, RT_ERR_INVALID_ARG, "scene has no lights");
+    if (sd->mesh_count >= (1u << 24)) FAIL(c, RT_ERR_UNSUPPORTED, "too many meshes");
+    int max_sub = 1;
+    uint64_t nv = 0, nt = 0;
+    for (uint32_t m = 0; m < sd->mesh_count; ++m) {
+        const rt_mesh_desc& md = sd->meshes[m];
+        if (!md.positions || !md.normals) FAIL(c, RT_ERR_INVALID_ARG, "mesh without positions/normals");
+        if (md.submesh_count == 0 || !md.submeshes) FAIL(c, RT_ERR_INVALID_ARG, "mesh without submeshes");
+        if (md.submesh_count > 256) FAIL(c, RT_ERR_UNSUPPORTED, "more than 256 submeshes in a mesh");
+        if (md.joint_count && (!md.joint_indices || !md.joint_weights)) FAIL(c, RT_ERR_INVALID_ARG, "skinned mesh without joint streams");
+        max_sub = std::max(max_sub, (int)md.submesh_count);
+        nv += md.vertex_count;
+        for (uint32_t s = 0; s < md.submesh_count; ++s) {
+            const rt_submesh_desc& sm = md.submeshes[s];
+            if (sm.index_count % 3) FAIL(c, RT_ERR_INVALID_ARG, "index count not a multiple of 3");
+            if (sm.index_count && !sm.indices) FAIL(c, RT_ERR_INVALID_ARG, "null indices");
+            if (sm.material.textureFlags != 0)
+                FAIL(c, RT_ERR_UNSUPPORTED, "textured materials are not supported yet (SURVEY §8f rank 2)");
+            for (uint32_t i = 0; i < sm.index_count; ++i)
+                if (sm.indices[i] >= md.vertex_count) FAIL(c, RT_ERR_INVALID_ARG, "index out of range");
+            nt += sm.index_count / 3;
+        }
+    }
+    if (nt >= (1ull << 31) || nv >= (1ull << 32)) FAIL(c, RT_ERR_UNSUPPORTED, "scene too large");
+    c->max_sub = max_sub;
+    c->num_inst = sd->mesh_count;
+    c->num_tris = (uint32_t)nt;
+    c->num_verts = (uint32_t)nv;
+    c->h_pos.assign(nv, make_float4(0, 0, 0, 0));
+    c->h_nrm.assign(nv, make_float4(0, 0, 0, 0));
+    c->h_tri_info.resize(nt);
+    c->h_inst.assign(12 * (size_t)sd->mesh_count, 0.0f);
+    Material zero_mat;
+    std::memset(&zero_mat, 0, sizeof zero_mat);
+    c->h_mat.assign((size_t)max_sub * sd->mesh_count, zero_mat);
+    c->meshes.assign(sd->mesh_count, MeshInfo());
+    c->h_world.resize(9 * nt);
+    uint32_t vbase = 0, tri = 0;
+    std::vector<uint16_t> jidx;
+    std::vector<float> jw;
+    bool any_skin = false;
+    for (uint32_t m = 0; m < sd->mesh_count; ++m) {
+        const rt_mesh_desc& md = sd->meshes[m];
+        MeshInfo& mi = c->meshes[m];
+        mi.vbase = vbase;
+        mi.vcount = md.vertex_count;
+        mi.joint_count = md.joint_count;
+        mi.skinned = md.joint_count > 0;
+        any_skin |= mi.skinned;
+        std::memcpy(&c->h_inst[12 * m], &md.transform, 48);
+        for (uint32_t v = 0; v < md.vertex_count; ++v) {
+            const rt_float3& p = md.positions[v];
+            const rt_float3& n = md.normals[v];
+            c->h_pos[vbase + v] = make_float4(p.x, p.y, p.z, 0.0f);
+            c->h_nrm[vbase + v] = make_float4(n.x, n.y, n.z, 0.0f);
+        }
+        for (uint32_t s = 0; s < md.submesh_count; ++s) {
+            const rt_submesh_desc& sm = md.submeshes[s];
+            c->h_mat[(size_t)m * max_sub + s] = sm.material;
+            for (uint32_t k = 0; k < sm.index_count / 3; ++k) {
+                uint4 ti;
+                ti.x = vbase + sm.indices[3 * k + 0];
+                ti.y = vbase + sm.indices[3 * k + 1];
+                ti.z = vbase + sm.indices[3 * k + 2];
+                ti.w = (m << 8) | s;
+                c->h_tri_info[tri] = ti;
+                const float* M = &c->h_inst[12 * m];
+                xform_host(M, c->h_pos[ti.x], &c->h_world[9 * (size_t)tri + 0]);
+                xform_host(M, c->h_pos[ti.y], &c->h_world[9 * (size_t)tri + 3]);
+                xform_host(M, c->h_pos[ti.z], &c->h_world[9 * (size_t)tri + 6]);
+                ++tri;
+            }
+        }
+        vbase += md.vertex_count;
+    }
+    c->h_lights.assign(sd->lights, sd->lights + sd->light_count);
+    rt_status st;
+    if ((st = dev_upload(c, c->d_pos, c->h_pos.data(), nv * 16))) return st;
+    if ((st = dev_upload(c, c->d_prev_pos, c->h_pos.data(), nv * 16))) return st;  // previousPositions = positions (SubMesh.swift:60)
+    if ((st = dev_upload(c, c->d_nrm, c->h_nrm.data(), nv * 16))) return st;
+    if ((st = dev_upload(c, c->d_tri_info, c->h_tri_info.data(), nt * 16))) return st;
+    if ((st = dev_upload(c, c->d_inst, c->h_inst.data(), c->h_inst.size() * 4))) return st;
+    if ((st = dev_upload(c, c->d_prev_inst, c->h_inst.data(), c->h_inst.size() * 4))) return st;
+    if ((st = dev_upload(c, c->d_mat, c->h_mat.data(), c->h_mat.size() * sizeof(Material)))) return st;
+    if ((st = dev_upload(c, c->d_lights, c->h_lights.data(), c->h_lights.size() * sizeof(Light)))) return st;
+    if (any_skin) {
+        // rest pose + joint streams of every skinned mesh (positions of static meshes unused)
+        jidx.assign(4 * (size_t)nv, 0);
+        jw.assign(4 * (size_t)nv, 0.0f);
+        uint32_t maxj = 0;
+        for (uint32_t m = 0; m < sd->mesh_count; ++m) {
+            const rt_mesh_desc& md = sd->meshes[m];
+            if (!md.joint_count) continue;
+            maxj = std::max(maxj, md.joint_count);
+            std::memcpy(&jidx[4 * (size_t)c->meshes[m].vbase], md.joint_indices, 8 * (size_t)md.vertex_count);
+            std::memcpy(&jw[4 * (size_t)c->meshes[m].vbase], md.joint_weights, 16 * (size_t)md.vertex_count);
+        }
+        if ((st = dev_upload(c, c->d_rest_pos, c->h_pos.data(), nv * 16))) return st;
+        if ((st = dev_upload(c, c->d_rest_nrm, c->h_nrm.data(), nv * 16))) return st;
+        if ((st = dev_upload(c, c->d_jidx, jidx.data(), jidx.size() * 2))) return st;
+        if ((st = dev_upload(c, c->d_jw, jw.data(), jw.size() * 4))) return st;
+        if ((st = dev_alloc(c, c->d_joints, (size_t)maxj * 64))) return st;
+    }
+    HIPC(c, hipStreamSynchronize(c->stream));
+    c->scene_ready = true;
+    c->bvh_ready = false;
+    return RT_OK;
+}
+
+rt_status rt_bvh_build(rt_ctx* c) {
+    if (!c) FAIL(c, RT_ERR_INVALID_ARG, "null ctx");
+    if (!c->scene_ready) FAIL(c, RT_ERR_STATE, "rt_bvh_build before rt_scene_upload");
+    HIPC(c, hipSetDevice(c->device));
+    HIPC(c, hipStreamSynchronize(c->stream));
+    // current world-space triangles (may have been skinned / re-transformed on the device)
+    if (c->world_dirty) {
+        HIPC(c, hipMemcpy(c->h_pos.data(), c->d_pos.p, (size_t)c->num_verts * 16, hipMemcpyDeviceToHost));
+        for (uint32_t t = 0; t < c->num_tris; ++t) {
+            const uint4& ti = c->h_tri_info[t];
+            const float* M = &c->h_inst[12 * (ti.w >> 8)];
+            xform_host(M, c->h_pos[ti.x], &c->h_world[9 * (size_t)t + 0]);
+            xform_host(M, c->h_pos[ti.y], &c->h_world[9 * (size_t)t + 3]);
+            xform_host(M, c->h_pos[ti.z], &c->h_world[9 * (size_t)t + 6]);
+        }
+        c->world_dirty = false;
+    }
+    c->bvh = build_bvh2(c->h_world.data(), c->num_tris, 4, kStackSize - 2);
+    if (c->bvh.max_depth > kStackSize) FAIL(c, RT_ERR_STATE, "BVH deeper than traversal stack");
+    const uint32_t n = c->num_tris;
+    std::vector<float4> tris(3 * (size_t)n);
+    for (uint32_t k = 0; k < n; ++k) {
+        uint32_t id = c->bvh.tri_order[k];
+        const float* w = &c->h_world[9 * (size_t)id];
+        uint32_t idb = id;
+        float idf;
+        std::memcpy(&idf, &idb, 4);
+        tris[3 * k + 0] = make_float4(w[0], w[1], w[2], idf);
+        tris[3 * k + 1] = make_float4(w[3], w[4], w[5], 0.0f);
+        tris[3 * k + 2] = make_float4(w[6], w[7], w[8], 0.0f);
+    }
+    // nodes grouped by depth for the level-synchronous refit
+    std::vector<int> depth(c->bvh.nodes.size(), 0);
+    int maxd = 0;
+    for (size_t k = 1; k < c->bvh.nodes.size(); ++k) {
+        depth[k] = depth[c->bvh.parent[k]] + 1;
+        maxd = std::max(maxd, depth[k]);
+    }
+    c->level_off.assign(maxd + 2, 0);
+    for (int d : depth) c->level_off[d + 1]++;
+    for (int d = 0; d <= maxd; ++d) c->level_off[d + 1] += c->level_off[d];
+    c->level_nodes.assign(c->bvh.nodes.size(), 0);
+    std::vector<uint32_t> fill(c->level_off.begin(), c->level_off.end() - 1);
+    for (size_t k = 0; k < depth.size(); ++k) c->level_nodes[fill[depth[k]]++] = (uint32_t)k;
+    rt_status st;
+    if ((st = dev_upload(c, c->d_tris, tris.data(), tris.size() * 16))) return st;
+    if ((st = dev_upload(c, c->d_nodes, c->bvh.nodes.data(), c->bvh.nodes.size() * sizeof(Bvh2Node)))) return st;
+    if ((st = dev_upload(c, c->d_slot_to_tri, c->bvh.tri_order.data(), (size_t)n * 4))) return st;
+    if ((st = dev_upload(c, c->d_levels, c->level_nodes.data(), c->level_nodes.size() * 4))) return st;
+    HIPC(c, hipStreamSynchronize(c->stream));
+    c->bvh_ready = true;
+    return RT_OK;
+}
+
+rt_status rt_bvh_refit(rt_ctx* c) {
+    if (!c) FAIL(c, RT_ERR_INVALID_ARG, "null ctx");
+    if (!c->bvh_ready) FAIL(c, RT_ERR_STATE, "rt_bvh_refit before rt_bvh_build");
+    HIPC(c, hipSetDevice(c->device));
+    launch_flatten((const uint4*)c->d_tri_info.p, (const uint32_t*)c->d_slot_to_tri.p, (const float4*)c->d_pos.p,
+                   (const float*)c->d_inst.p, (float4*)c->d_tris.p, c->num_tris, c->stream);
+    for (int d = (int)c->level_off.size() - 2; d >= 0; --d) {
+        uint32_t off = c->level_off[d], cnt = c->level_off[d + 1] - off;
+        launch_refit_level((Bvh2Node*)c->d_nodes.p, (const float4*)c->d_tris.p, (const uint32_t*)c->d_levels.p + off,
+                           cnt, c->bvh.pad, c->stream);
+    }
+    HIPC(c, hipGetLastError());
+    return RT_OK;
+}
+
+rt_status rt_set_instance_transforms(rt_ctx* c, const rt_packed_float4x3* t, uint32_t count) {
+    if (!c || !t) FAIL(c, RT_ERR_INVALID_ARG, "null argument");
+    if (!c->scene_ready || count != c->num_inst) FAIL(c, RT_ERR_INVALID_ARG, "transform count != mesh count");
+    HIPC(c, hipSetDevice(c->device));
+    // prev <- cur (Renderer.swift:939-944), then the new transforms
+    HIPC(c, hipMemcpyAsync(c->d_prev_inst.p, c->d_inst.p, c->h_inst.size() * 4, hipMemcpyDeviceToDevice, c->stream));
+    std::memcpy(c->h_inst.data(), t, (size_t)count * 48);
+    HIPC(c, hipMemcpyAsync(c->d_inst.p, c->h_inst.data(), c->h_inst.size() * 4, hipMemcpyHostToDevice, c->stream));
+    HIPC(c, hipStreamSynchronize(c->stream));
+    c->world_dirty = true;
+    return RT_OK;
+}
+
+rt_status rt_skin(rt_ctx* c, uint32_t mesh_index, const float* joints, uint32_t joint_count) {
+    if (!c || !joints) FAIL(c, RT_ERR_INVALID_ARG, "null argument");
+    if (!c->scene_ready || mesh_index >= c->meshes.size()) FAIL(c, RT_ERR_INVALID_ARG, "bad mesh index");
+    const MeshInfo& mi = c->meshes[mesh_index];
+    if (!mi.skinned) FAIL(c, RT_ERR_INVALID_ARG, "mesh is not skinned");
+    if (joint_count != mi.joint_count) FAIL(c, RT_ERR_INVALID_ARG, "joint count mismatch");
+    HIPC(c, hipSetDevice(c->device));
+    HIPC(c, hipMemcpyAsync(c->d_joints.p, joints, (size_t)joint_count * 64, hipMemcpyHostToDevice, c->stream));
+    // previousPositions <- positions (Renderer.swift:1290-1303)
+    HIPC(c, hipMemcpyAsync((float4*)c->d_prev_pos.p + mi.vbase, (float4*)c->d_pos.p + mi.vbase, (size_t)mi.vcount * 16,
+                           hipMemcpyDeviceToDevice, c->stream));
+    launch_skin((const float4*)c->d_rest_pos.p + mi.vbase, (const float4*)c->d_rest_nrm.p + mi.vbase,
+                (const ushort4*)c->d_jidx.p + mi.vbase, (const float4*)c->d_jw.p + mi.vbase, (const float*)c->d_joints.p,
+                (float4*)c->d_pos.p + mi.vbase, (float4*)c->d_nrm.p + mi.vbase, mi.vcount, c->stream);
+    HIPC(c, hipGetLastError());
+    HIPC(c, hipStreamSynchronize(c->stream));  // joint upload buffer is reused next call
+    c->world_dirty = true;
+    return RT_OK;
+}
+
+rt_status rt_resize(rt_ctx* c, int32_t w, int32_t h, const uint32_t* offsets) {
+    if (!c || !offsets) FAIL(c, RT_ERR_INVALID_ARG, "null argument");
+    if (w <= 0 || h <= 0 || (int64_t)w * h > (1ll << 30)) FAIL(c, RT_ERR_INVALID_ARG, "bad size");
+    HIPC(c, hipSetDevice(c->device));
+    size_t n = (size_t)w * h;
+    rt_status st;
+    if ((st = dev_upload(c, c->d_random, offsets, n * 4))) return st;
+    for (int i = 0; i < 2; ++i) {
+        if ((st = dev_alloc(c, c->d_accum[i], n * 16))) return st;
+        HIPC(c, hipMemsetAsync(c->d_accum[i].p, 0, n * 16, c->stream));
+    }
+    if ((st = dev_alloc(c, c->d_depth, n * 4))) return st;
+    if ((st = dev_alloc(c, c->d_motion, n * 8))) return st;
+    HIPC(c, hipMemsetAsync(c->d_depth.p, 0, n * 4, c->stream));
+    HIPC(c, hipMemsetAsync(c->d_motion.p, 0, n * 8, c->stream));
+    dev_free(c->d_gbuffer);
+    HIPC(c, hipStreamSynchronize(c->stream));
+    c->width = w;
+    c->height = h;
+    c->read_idx = 0;
+    return RT_OK;
+}
+
+int32_t rt_tile_count(int32_t w, int32_t h, const rt_tile_set* t) {
+    int ts = (t && t->tile_size > 0) ? t->tile_size : 64;
+    int nr = (t && t->nranks > 0) ? t->nranks : 1;
+    int rk = (t && t->nranks > 0) ? t->rank : 0;
+    int tx = (w + ts - 1) / ts, ty = (h + ts - 1) / ts;
+    int total = tx * ty;
+    if (rk >= total) return 0;
+    return (total - rk + nr - 1) / nr;
+}
+
+static rt_status resolve_tiles(rt_ctx* c, const rt_tile_set* t, int& ts, int& rank, int& nranks, int& tiles_x, int& own) {
+    ts = (t && t->tile_size > 0) ? t->tile_size : 64;
+    nranks = (t && t->nranks > 0) ? t->nranks : 1;
+    rank = (t && t->nranks > 0) ? t->rank : 0;
+    if (ts % 16 != 0) FAIL(c, RT_ERR_INVALID_ARG, "tile_size must be a multiple of 16");
+    if (rank < 0 || rank >= nranks) FAIL(c, RT_ERR_INVALID_ARG, "bad rank");
+    tiles_x = (c->width + ts - 1) / ts;
+    own = rt_tile_count(c->width, c->height, t);
+    return RT_OK;
+}
+
+rt_status rt_render_frame(rt_ctx* c, const Uniforms* U, const rt_tile_set* tiles) {
+    if (!c || !U) FAIL(c, RT_ERR_INVALID_ARG, "null argument");
+    if (!c->bvh_ready) FAIL(c, RT_ERR_STATE, "rt_render_frame before rt_bvh_build");
+    if (!c->width) FAIL(c, RT_ERR_STATE, "rt_render_frame before rt_resize");
+    if (U->width != c->width || U->height != c->height) FAIL(c, RT_ERR_INVALID_ARG, "uniforms size != targets size");
+    if (U->lightCount < 1 || U->lightCount > (int)c->h_lights.size()) FAIL(c, RT_ERR_INVALID_ARG, "bad lightCount");
+    if (U->maxBounces > RT_MAX_BOUNCES) FAIL(c, RT_ERR_UNSUPPORTED, "maxBounces > 12 exceeds the Halton table");
+    if (U->samplesPerPixel > 4096 || U->motionSamplingMaxExtraSamples > 4096) FAIL(c, RT_ERR_INVALID_ARG, "bad spp");
+    HIPC(c, hipSetDevice(c->device));
+    int ts, rank, nranks, tiles_x, own;
+    rt_status st = resolve_tiles(c, tiles, ts, rank, nranks, tiles_x, own);
+    if (st) return st;
+    size_t n = (size_t)c->width * c->height;
+    if (U->enableDenoiseGBuffer && !c->d_gbuffer.p) {
+        if ((st = dev_alloc(c, c->d_gbuffer, 4 * n * 16))) return st;
+        HIPC(c, hipMemsetAsync(c->d_gbuffer.p, 0, 4 * n * 16, c->stream));
+    }
+    DevScene S;
+    S.tris = (const float4*)c->d_tris.p;
+    S.nodes = (const Bvh2Node*)c->d_nodes.p;
+    S.tri_info = (const uint4*)c->d_tri_info.p;
+    S.pos = (const float4*)c->d_pos.p;
+    S.prev_pos = (const float4*)c->d_prev_pos.p;
+    S.nrm = (const float4*)c->d_nrm.p;
+    S.inst = (const float*)c->d_inst.p;
+    S.prev_inst = (const float*)c->d_prev_inst.p;
+    S.materials = (const Material*)c->d_mat.p;
+    S.lights = (const Light*)c->d_lights.p;
+    S.halton = (const HaltonDim*)c->d_halton.p;
+    S.max_submeshes = c->max_sub;
+    S.num_tris = (int)c->num_tris;
+    FrameParams P;
+    P.U = *U;
+    P.random = (const uint32_t*)c->d_random.p;
+    P.accum_in = (const float4*)c->d_accum[c->read_idx].p;
+    P.accum_out = (float4*)c->d_accum[1 - c->read_idx].p;
+    P.depth = (float*)c->d_depth.p;
+    P.motion = (float2*)c->d_motion.p;
+    P.gbuffer = U->enableDenoiseGBuffer ? (float4*)c->d_gbuffer.p : nullptr;
+    P.counters = (unsigned long long*)c->d_counters.p;
+    P.tile_size = ts;
+    P.rank = rank;
+    P.nranks = nranks;
+    P.tiles_x = tiles_x;
+    HIPC(c, hipMemsetAsync(c->d_counters.p, 0, sizeof(unsigned long long) * kCntSlots, c->stream));
+    HIPC(c, hipEventRecord(c->ev0, c->stream));
+    int nblocks = own * (ts / 16) * (ts / 16);
+    if (nblocks > 0) launch_megakernel(S, P, nblocks, c->counting, c->stream);
+    HIPC(c, hipGetLastError());
+    HIPC(c, hipEventRecord(c->ev1, c->stream));
+    HIPC(c, hipMemcpyAsync(c->h_counters, c->d_counters.p, sizeof(unsigned long long) * kCntSlots,
+                           hipMemcpyDeviceToHost, c->stream));
+    c->read_idx = 1 - c->read_idx;  // swap accumulationTargets (Renderer.swift:1492-1494)
+    c->frame_pending = true;
+    return RT_OK;
+}
+
+rt_status rt_wait(rt_ctx* c) {
+    if (!c) FAIL(c, RT_ERR_INVALID_ARG, "null ctx");
+    HIPC(c, hipSetDevice(c->device));
+    HIPC(c, hipStreamSynchronize(c->stream));
+    if (c->frame_pending) {
+        float ms = 0.0f;
+        HIPC(c, hipEventElapsedTime(&ms, c->ev0, c->ev1));
+        c->stats.last_frame_ms = ms;
+        c->stats.kernel_ms[0] = ms;
+        c->stats.closest_rays = c->h_counters[kCntClosest];
+        c->stats.shadow_rays = c->h_counters[kCntShadow];
+        c->stats.node_visits = c->h_counters[kCntNodes];
+        c->stats.tri_tests = c->h_counters[kCntTris];
+        c->stats.paths = c->h_counters[kCntPaths];
+        c->frame_pending = false;
+        if (c->h_counters[kCntOverflow]) FAIL(c, RT_ERR_STATE, "traversal stack overflow");
+    }
+    return RT_OK;
+}
+
+rt_status rt_read_radiance(rt_ctx* c, float* rgba) {
+    if (!c || !rgba) FAIL(c, RT_ERR_INVALID_ARG, "null argument");
+    if (!c->width) FAIL(c, RT_ERR_STATE, "no targets");
+    rt_status st = rt_wait(c);
+    if (st) return st;
+    HIPC(c, hipMemcpy(rgba, c->d_accum[c->read_idx].p, (size_t)c->width * c->height * 16, hipMemcpyDeviceToHost));
+    return RT_OK;
+}
+
+rt_status rt_read_aux(rt_ctx* c, float* depth, float* motion, float* gbuffer) {
+    if (!c) FAIL(c, RT_ERR_INVALID_ARG, "null ctx");
+    if (!c->width) FAIL(c, RT_ERR_STATE, "no targets");
+    rt_status st = rt_wait(c);
+    if (st) return st;
+    size_t n = (size_t)c->width * c->height;
+    if (depth) HIPC(c, hipMemcpy(depth, c->d_depth.p, n * 4, hipMemcpyDeviceToHost));
+    if (motion) HIPC(c, hipMemcpy(motion, c->d_motion.p, n * 8, hipMemcpyDeviceToHost));
+    if (gbuffer) {
+        if (!c->d_gbuffer.p) FAIL(c, RT_ERR_STATE, "G-buffer was never enabled");
+        HIPC(c, hipMemcpy(gbuffer, c->d_gbuffer.p, 4 * n * 16, hipMemcpyDeviceToHost));
+    }
+    return RT_OK;
+}
+
+rt_status rt_pack_tiles(rt_ctx* c, const rt_tile_set* t, void* dst) {
+    if (!c || !dst) FAIL(c, RT_ERR_INVALID_ARG, "null argument");
+    if (!c->width) FAIL(c, RT_ERR_STATE, "no targets");
+    int ts, rank, nranks, tiles_x, own;
+    rt_status st = resolve_tiles(c, t, ts, rank, nranks, tiles_x, own);
+    if (st) return st;
+    HIPC(c, hipSetDevice(c->device));
+    launch_pack_tiles((const float4*)c->d_accum[c->read_idx].p, (float4*)dst, c->width, c->height, ts, rank, nranks,
+                      tiles_x, own, c->stream);
+    HIPC(c, hipGetLastError());
+    return RT_OK;
+}
+
+rt_status rt_unpack_tiles(rt_ctx* c, const rt_tile_set* t, const void* src) {
+    if (!c || !src) FAIL(c, RT_ERR_INVALID_ARG, "null argument");
+    if (!c->width) FAIL(c, RT_ERR_STATE, "no targets");
+    int ts, rank, nranks, tiles_x, own;
+    rt_status st = resolve_tiles(c, t, ts, rank, nranks, tiles_x, own);
+    if (st) return st;
+    HIPC(c, hipSetDevice(c->device));
+    launch_unpack_tiles((const float4*)src, (float4*)c->d_accum[c->read_idx].p, c->width, c->height, ts, rank, nranks,
+                        tiles_x, own, c->stream);
+    HIPC(c, hipGetLastError());
+    return RT_OK;
+}
+
+rt_status rt_set_counting(rt_ctx* c, int32_t enabled) {
+    if (!c) FAIL(c, RT_ERR_INVALID_ARG, "null ctx");
+    c->counting = enabled != 0;
+    return RT_OK;
+}
+
+rt_status rt_get_stats(rt_ctx* c, rt_stats* out) {
+    if (!c || !out) FAIL(c, RT_ERR_INVALID_ARG, "null argument");
+    rt_status st = rt_wait(c);
+    if (st) return st;
+    c->stats.bvh_nodes = c->bvh.nodes.size();
+    c->stats.triangles = c->num_tris;
+    c->stats.device_bytes = ctx_bytes(c);
+    *out = c->stats;
+    return RT_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,264 @@
+// rt_bvh.cpp — binned-SAH BVH2 builder over world-space triangles (see rt_bvh.h).
+#include "rt_bvh.h"
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+
+namespace rt {
+
+namespace {
+
+struct Box {
+    float lo[3], hi[3];
+    void reset() { for (int k = 0; k < 3; ++k) { lo[k] = INFINITY; hi[k] = -INFINITY; } }
+    void grow(const Box& b) { for (int k = 0; k < 3; ++k) { lo[k] = std::min(lo[k], b.lo[k]); hi[k] = std::max(hi[k], b.hi[k]); } }
+    void grow(const float* p) { for (int k = 0; k < 3; ++k) { lo[k] = std::min(lo[k], p[k]); hi[k] = std::max(hi[k], p[k]); } }
+    float area() const {
+        float d0 = hi[0] - lo[0], d1 = hi[1] - lo[1], d2 = hi[2] - lo[2];
+        if (!(d0 >= 0.0f)) return 0.0f;
+        return 2.0f * (d0 * d1 + d1 * d2 + d2 * d0);
+    }
+};
+
+struct TmpNode {
+    Box box;
+    int left = -1, right = -1;
+    uint32_t start = 0, count = 0;
+};
+
+constexpr int kBins = 32;
+
+struct Builder {
+    const std::vector<Box>& tri_box;
+    const std::vector<float>& cen;  // 3 per tri
+    std::vector<uint32_t>& idx;
+    std::vector<TmpNode> nodes;
+    int max_leaf, depth_limit, max_depth = 0;
+
+    Builder(const std::vector<Box>& tb, const std::vector<float>& c, std::vector<uint32_t>& i, int ml, int dl)
+        : tri_box(tb), cen(c), idx(i), max_leaf(ml), depth_limit(dl) {}
+
+    static int ceil_log2(uint32_t x) { int r = 0; while ((1u << r) < x) ++r; return r; }
+
+    int make_leaf(uint32_t s, uint32_t e, const Box& b) {
+        TmpNode n;
+        n.box = b; n.start = s; n.count = e - s;
+        nodes.push_back(n);
+        return (int)nodes.size() - 1;
+    }
+
+    int build(uint32_t s, uint32_t e, int depth) {
+        max_depth = std::max(max_depth, depth);
+        Box b; b.reset();
+        Box cb; cb.reset();
+        for (uint32_t i = s; i < e; ++i) { b.grow(tri_box[idx[i]]); cb.grow(&cen[3 * idx[i]]); }
+        uint32_t n = e - s;
+        if (n <= 1) return make_leaf(s, e, b);
+        // axis = largest centroid extent
+        int axis = 0;
+        float ext[3];
+        for (int k = 0; k < 3; ++k) ext[k] = cb.hi[k] - cb.lo[k];
+        if (ext[1] > ext[axis]) axis = 1;
+        if (ext[2] > ext[axis]) axis = 2;
+        uint32_t mid = s;
+        bool median = depth + ceil_log2((n + max_leaf - 1) / max_leaf) >= depth_limit - 1;
+        bool split_found = false;
+        if (ext[axis] <= 0.0f) {
+            // all centroids coincide: leaf if small, otherwise object-median
+            if (n <= (uint32_t)max_leaf) return make_leaf(s, e, b);
+            median = true;
+        }
+        if (!median) {
+            // binned SAH over all three axes
+            float best_cost = INFINITY;
+            int best_axis = -1, best_bin = -1;
+            for (int a = 0; a < 3; ++a) {
+                if (ext[a] <= 0.0f) continue;
+                Box bb[kBins];
+                uint32_t bc[kBins] = {0};
+                for (auto& x : bb) x.reset();
+                float scale = kBins / ext[a];
+                for (uint32_t i = s; i < e; ++i) {
+                    int bi = (int)((cen[3 * idx[i] + a] - cb.lo[a]) * scale);
+                    bi = std::min(std::max(bi, 0), kBins - 1);
+                    bb[bi].grow(tri_box[idx[i]]);
+                    bc[bi]++;
+                }
+                float rarea[kBins];
+                uint32_t rcnt[kBins];
+                Box acc; acc.reset();
+                uint32_t c = 0;
+                for (int i = kBins - 1; i > 0; --i) {
+                    acc.grow(bb[i]); c += bc[i];
+                    rarea[i] = acc.area(); rcnt[i] = c;
+                }
+                acc.reset(); c = 0;
+                for (int i = 0; i < kBins - 1; ++i) {
+                    acc.grow(bb[i]); c += bc[i];
+                    if (c == 0 || rcnt[i + 1] == 0) continue;
+                    float cost = acc.area() * c + rarea[i + 1] * rcnt[i + 1];
+                    if (cost < best_cost) { best_cost = cost; best_axis = a; best_bin = i; }
+                }
+            }
+            float pa = b.area();
+            float leaf_cost = (float)n;                             // C_isect = 1
+            float split_cost = 1.0f + (pa > 0 ? best_cost / pa : INFINITY);  // C_trav = 1
+            if (best_axis >= 0 && (split_cost < leaf_cost || n > (uint32_t)max_leaf)) {
+                float scale = kBins / ext[best_axis];
+                auto it = std::partition(idx.begin() + s, idx.begin() + e, [&](uint32_t t) {
+                    int bi = (int)((cen[3 * t + best_axis] - cb.lo[best_axis]) * scale);
+                    bi = std::min(std::max(bi, 0), kBins - 1);
+                    return bi <= best_bin;
+                });
+                mid = (uint32_t)(it - idx.begin());
+                if (mid > s && mid < e) split_found = true;
+            } else if (n <= (uint32_t)max_leaf) {
+                return make_leaf(s, e, b);
+            }
+        }
+        if (!split_found) {
+            if (n <= (uint32_t)max_leaf && !median) return make_leaf(s, e, b);
+            mid = s + n / 2;
+            std::nth_element(idx.begin() + s, idx.begin() + mid, idx.begin() + e, [&](uint32_t x, uint32_t y) {
+                float cx = cen[3 * x + axis], cy = cen[3 * y + axis];
+                return cx < cy || (cx == cy && x < y);
+            });
+        }
+        if (n <= (uint32_t)max_leaf && median) return make_leaf(s, e, b);
+        int me = (int)nodes.size();
+        nodes.emplace_back();
+        nodes[me].box = b;
+        int l = build(s, mid, depth + 1);
+        int r = build(mid, e, depth + 1);
+        nodes[me].left = l;
+        nodes[me].right = r;
+        return me;
+    }
+};
+
+void set_child(Bvh2Node& n, int slot, const Box& b, float pad) {
+    n.lx[2 * slot] = b.lo[0] - pad; n.lx[2 * slot + 1] = b.hi[0] + pad;
+    n.ly[2 * slot] = b.lo[1] - pad; n.ly[2 * slot + 1] = b.hi[1] + pad;
+    n.lz[2 * slot] = b.lo[2] - pad; n.lz[2 * slot + 1] = b.hi[2] + pad;
+}
+
+void set_empty(Bvh2Node& n, int slot) {
+    n.lx[2 * slot] = INFINITY; n.lx[2 * slot + 1] = -INFINITY;
+    n.ly[2 * slot] = INFINITY; n.ly[2 * slot + 1] = -INFINITY;
+    n.lz[2 * slot] = INFINITY; n.lz[2 * slot + 1] = -INFINITY;
+    n.child[slot] = -1;  // leaf at slot 0 with zero triangles
+    n.count[slot] = 0;
+}
+
+}  // namespace
+
+BvhResult build_bvh2(const float* v, uint32_t n, int max_leaf, int depth_limit) {
+    BvhResult out;
+    std::vector<Box> tb(n);
+    std::vector<float> cen(3 * (size_t)n);
+    float maxabs = 1.0f;
+    for (uint32_t i = 0; i < n; ++i) {
+        tb[i].reset();
+        for (int k = 0; k < 3; ++k) tb[i].grow(v + 9 * (size_t)i + 3 * k);
+        for (int a = 0; a < 3; ++a) {
+            cen[3 * i + a] = 0.5f * (tb[i].lo[a] + tb[i].hi[a]);
+            maxabs = std::max(maxabs, std::max(std::fabs(tb[i].lo[a]), std::fabs(tb[i].hi[a])));
+        }
+    }
+    out.pad = 4e-6f * maxabs;
+    std::vector<uint32_t> idx(n);
+    for (uint32_t i = 0; i < n; ++i) idx[i] = i;
+    Builder b(tb, cen, idx, max_leaf, depth_limit);
+    b.nodes.reserve(2 * (size_t)n / std::max(1, max_leaf) + 16);
+    if (n == 0) {
+        Bvh2Node r;
+        std::memset(&r, 0, sizeof r);
+        set_empty(r, 0);
+        set_empty(r, 1);
+        out.nodes.push_back(r);
+        out.parent.push_back(-1);
+        return out;
+    }
+    int root = b.build(0, n, 0);
+    out.max_depth = b.max_depth;
+    out.tri_order = idx;
+    // flatten: one Bvh2Node per inner TmpNode, DFS order
+    std::vector<int> map(b.nodes.size(), -1);
+    std::vector<int> stack;
+    if (b.nodes[root].left < 0) {
+        Bvh2Node r;
+        std::memset(&r, 0, sizeof r);
+        set_child(r, 0, b.nodes[root].box, out.pad);
+        r.child[0] = ~(int32_t)b.nodes[root].start;
+        r.count[0] = (int32_t)b.nodes[root].count;
+        set_empty(r, 1);
+        out.nodes.push_back(r);
+        out.parent.push_back(-1);
+        return out;
+    }
+    // assign indices in DFS (pre-order, left first)
+    stack.push_back(root);
+    std::vector<int> order;
+    while (!stack.empty()) {
+        int t = stack.back();
+        stack.pop_back();
+        map[t] = (int)order.size();
+        order.push_back(t);
+        const TmpNode& tn = b.nodes[t];
+        if (b.nodes[tn.right].left >= 0) stack.push_back(tn.right);
+        if (b.nodes[tn.left].left >= 0) stack.push_back(tn.left);
+    }
+    out.nodes.resize(order.size());
+    out.parent.assign(order.size(), -1);
+    for (size_t k = 0; k < order.size(); ++k) {
+        const TmpNode& tn = b.nodes[order[k]];
+        Bvh2Node& o = out.nodes[k];
+        std::memset(&o, 0, sizeof o);
+        int ch[2] = {tn.left, tn.right};
+        for (int s = 0; s < 2; ++s) {
+            const TmpNode& c = b.nodes[ch[s]];
+            set_child(o, s, c.box, out.pad);
+            if (c.left >= 0) {
+                o.child[s] = map[ch[s]];
+                o.count[s] = 0;
+                out.parent[map[ch[s]]] = (int)k;
+            } else {
+                o.child[s] = ~(int32_t)c.start;
+                o.count[s] = (int32_t)c.count;
+            }
+        }
+    }
+    return out;
+}
+
+void refit_bvh2(BvhResult& bvh, const float* v) {
+    // children have larger indices than parents (pre-order) -> sweep backwards
+    for (int k = (int)bvh.nodes.size() - 1; k >= 0; --k) {
+        Bvh2Node& nd = bvh.nodes[k];
+        for (int s = 0; s < 2; ++s) {
+            Box b; b.reset();
+            if (nd.child[s] >= 0) {
+                const Bvh2Node& c = bvh.nodes[nd.child[s]];
+                for (int cs = 0; cs < 2; ++cs) {
+                    Box cb;
+                    cb.lo[0] = c.lx[2 * cs] + bvh.pad; cb.hi[0] = c.lx[2 * cs + 1] - bvh.pad;
+                    cb.lo[1] = c.ly[2 * cs] + bvh.pad; cb.hi[1] = c.ly[2 * cs + 1] - bvh.pad;
+                    cb.lo[2] = c.lz[2 * cs] + bvh.pad; cb.hi[2] = c.lz[2 * cs + 1] - bvh.pad;
+                    if (c.child[cs] < 0 && c.count[cs] == 0) continue;
+                    b.grow(cb);
+                }
+            } else {
+                if (nd.count[s] == 0) continue;
+                uint32_t first = (uint32_t)~nd.child[s];
+                for (int32_t t = 0; t < nd.count[s]; ++t) {
+                    uint32_t tri = bvh.tri_order[first + t];
+                    for (int q = 0; q < 3; ++q) b.grow(v + 9 * (size_t)tri + 3 * q);
+                }
+            }
+            set_child(nd, s, b, bvh.pad);
+        }
+    }
+}
+
+}  // namespace rt

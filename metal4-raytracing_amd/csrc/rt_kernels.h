@@ -1,0 +1,50 @@
+// rt_kernels.h — kernel parameter blocks and launch entry points (device code lives in *.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include "rt_device.h"
+
+namespace rt {
+
+constexpr int kHaltonLds = 64;   // first Halton dimensions staged in LDS per block
+
+enum CounterSlot { kCntClosest = 0, kCntShadow = 1, kCntNodes = 2, kCntTris = 3, kCntPaths = 4, kCntOverflow = 5, kCntSlots = 8 };
+
+struct FrameParams {
+    Uniforms U;
+    const uint32_t* random;
+    const float4* accum_in;    // history (TextureIndexAccumulation, read)
+    float4* accum_out;         // new accumulation (TextureIndexPreviousAccumulation, write)
+    float* depth;
+    float2* motion;            // read (previous frame) + write, in place
+    float4* gbuffer;           // 4 planes or null
+    unsigned long long* counters;
+    int tile_size, rank, nranks, tiles_x;
+};
+
+__device__ __forceinline__ unsigned long long wave_sum(uint32_t v) {
+    unsigned long long s = v;
+    #pragma unroll
+    for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+    return s;
+}
+
+void launch_megakernel(const DevScene& S, const FrameParams& P, int nblocks, bool count, hipStream_t stream);
+
+// Wavefront pipeline (rt_wavefront.hip)
+struct WavefrontBuffers;
+void launch_wavefront(const DevScene& S, const FrameParams& P, WavefrontBuffers& W, bool count, hipStream_t stream,
+                      float* stage_ms);
+
+// Utility kernels (rt_util.hip)
+void launch_pack_tiles(const float4* src, float4* dst, int width, int height, int tile, int rank, int nranks,
+                       int tiles_x, int own, hipStream_t s);
+void launch_unpack_tiles(const float4* src, float4* dst, int width, int height, int tile, int rank, int nranks,
+                         int tiles_x, int own, hipStream_t s);
+void launch_skin(const float4* rest_pos, const float4* rest_nrm, const ushort4* jidx, const float4* jw,
+                 const float* joints, float4* out_pos, float4* out_nrm, uint32_t n, hipStream_t s);
+void launch_flatten(const uint4* tri_info, const uint32_t* slot_to_tri, const float4* pos, const float* inst,
+                    float4* tris, uint32_t n, hipStream_t s);
+void launch_refit_level(Bvh2Node* nodes, const float4* tris, const uint32_t* level_nodes, uint32_t count, float pad,
+                        hipStream_t s);
+
+}  // namespace rt

@@ -1,0 +1,844 @@
+// rt_scene.cpp — host scene ingest (C++ mirror of the reference's Swift scene layer).
+//
+//   class Scene      ~ MetalRaytracing/Scene.swift:10-170 (lights, orbit camera)
+//   class Model      ~ MetalRaytracing/Model.swift:29-205 (OBJ path, T*R*S transform, overrides)
+//   struct Mesh      ~ MetalRaytracing/Mesh.swift:17-68   (one MDLMesh = one instance)
+//   struct Submesh   ~ MetalRaytracing/SubMesh.swift:18-324 (material group, u32 indices)
+//
+// OBJ/MTL ingest restates the ModelIO conventions the reference relies on:
+// one mesh per `o` object, one submesh per material (first-appearance order), one vertex per
+// unique (v, vt, vn) tuple, fan triangulation of polygons, normals left zero when the file has
+// no `vn` (Raytracing.metal:395-397 then falls back to -ray.direction), Kd->baseColor,
+// Ks->specular, Ke->emission, Ni->refractionIndex (default 1), d->opacity (default 1, clamped),
+// specularExponent left 0 (Material(material:) only reads it for a float3 property,
+// SubMesh.swift:309-311).  ModelIO itself is unvendored: its exact triangulation/dedup order
+// is parity-unpinned and documented in DESIGN.md.
+#include "../../include/rt_scene.h"
+
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+namespace rt {
+
+// ---- column-major float4x4 helpers (Utilities.swift:302-355) --------------------------------
+struct M4 { float m[16]; };  // m[col*4 + row]
+
+static M4 m4_identity() { M4 r{}; r.m[0] = r.m[5] = r.m[10] = r.m[15] = 1.0f; return r; }
+static M4 m4_mul(const M4& a, const M4& b) {
+    M4 r{};
+    for (int c = 0; c < 4; ++c)
+        for (int rr = 0; rr < 4; ++rr) {
+            float s = 0.0f;
+            for (int k = 0; k < 4; ++k) s = s + a.m[k * 4 + rr] * b.m[c * 4 + k];
+            r.m[c * 4 + rr] = s;
+        }
+    return r;
+}
+static M4 m4_translate(const float t[3]) { M4 r = m4_identity(); r.m[12] = t[0]; r.m[13] = t[1]; r.m[14] = t[2]; return r; }
+static M4 m4_scale(float s) { M4 r = m4_identity(); r.m[0] = s; r.m[5] = s; r.m[10] = s; return r; }
+// matrix_float4x4.rotate(radians:axis:) (Utilities.swift:318-331)
+static M4 m4_rotate_axis(float radians, float ax, float ay, float az) {
+    float len = std::sqrt(ax * ax + ay * ay + az * az);
+    float x = ax / len, y = ay / len, z = az / len;
+    float ct = cosf(radians), st = sinf(radians), ci = 1.0f - ct;
+    M4 r{};
+    r.m[0] = ct + x * x * ci;     r.m[1] = y * x * ci + z * st; r.m[2] = z * x * ci - y * st;  r.m[3] = 0;
+    r.m[4] = x * y * ci - z * st; r.m[5] = ct + y * y * ci;     r.m[6] = z * y * ci + x * st;  r.m[7] = 0;
+    r.m[8] = x * z * ci + y * st; r.m[9] = y * z * ci - x * st; r.m[10] = ct + z * z * ci;     r.m[11] = 0;
+    r.m[12] = 0; r.m[13] = 0; r.m[14] = 0; r.m[15] = 1;
+    return r;
+}
+// rotate(r) = rotateX(r.x) * rotateY(r.y) * rotateZ(r.z) (Utilities.swift:345-347)
+static M4 m4_rotate(const float r[3]) {
+    return m4_mul(m4_mul(m4_rotate_axis(r[0], 1, 0, 0), m4_rotate_axis(r[1], 0, 1, 0)), m4_rotate_axis(r[2], 0, 0, 1));
+}
+// worldTransform = T * R * S (Model.swift:55-58, Mesh.swift:61-66)
+static M4 model_transform(const float pos[3], const float rot[3], float scale) {
+    return m4_mul(m4_mul(m4_translate(pos), m4_rotate(rot)), m4_scale(scale));
+}
+static rt_packed_float4x3 pack4x3(const M4& a) {  // Renderer.swift:1393-1401
+    rt_packed_float4x3 p;
+    for (int c = 0; c < 4; ++c)
+        for (int r = 0; r < 3; ++r) p.columns[c][r] = a.m[c * 4 + r];
+    return p;
+}
+
+static rt_float3 f3(float x, float y, float z) { rt_float3 v; v.x = x; v.y = y; v.z = z; v._pad = 0.0f; return v; }
+
+struct Submesh {
+    std::string material_name;
+    std::vector<uint32_t> indices;
+    Material material;
+};
+
+struct Skin {
+    // Synthetic skeleton for the robot stand-in (config 5): a chain of joints along +Y.
+    std::vector<int> parent;
+    std::vector<M4> rest_local;      // local rest transforms
+    std::vector<M4> inverse_bind;    // inverse of global bind transforms
+    double duration = 2.0;
+};
+
+struct Mesh {
+    std::string name;
+    std::vector<rt_float3> positions, normals;
+    std::vector<rt_float2> uvs;
+    bool has_uvs = false;
+    std::vector<uint16_t> joint_indices;  // ushort4 per vertex
+    std::vector<float> joint_weights;     // float4 per vertex
+    std::vector<Submesh> submeshes;
+    M4 transform;
+    uint32_t joint_count = 0;
+    std::shared_ptr<Skin> skin;
+};
+
+struct Model {
+    std::string name;
+    float position[3], rotation[3], scale;
+    std::vector<Mesh> meshes;
+};
+
+static Material default_material() {
+    Material m;
+    std::memset(&m, 0, sizeof(m));
+    m.refractionIndex = 1.0f;   // SubMesh.swift:295-296
+    m.opacity = 1.0f;
+    m.textureFlags = 0;
+    return m;
+}
+
+// ModelMaterialOverride application (SubMesh.swift:272-288)
+static void apply_override(Material& m, const rt_material_override* ov) {
+    if (!ov) return;
+    if (ov->has_base_color) m.baseColor = f3(ov->base_color[0], ov->base_color[1], ov->base_color[2]);
+    if (ov->has_refraction_index) m.refractionIndex = std::max(ov->refraction_index, 1.0f);
+    if (ov->has_opacity) m.opacity = std::min(std::max(ov->opacity, 0.0f), 1.0f);
+}
+
+// ---- MTL -------------------------------------------------------------------------------------
+static bool parse_mtl(const std::string& path, std::map<std::string, Material>& out) {
+    FILE* f = std::fopen(path.c_str(), "r");
+    if (!f) return false;
+    char line[4096];
+    Material* cur = nullptr;
+    while (std::fgets(line, sizeof line, f)) {
+        char* p = line;
+        while (*p == ' ' || *p == '\t') ++p;
+        char key[64] = {0};
+        int n = 0;
+        if (std::sscanf(p, "%63s%n", key, &n) != 1) continue;
+        const char* rest = p + n;
+        if (!std::strcmp(key, "newmtl")) {
+            char name[1024] = {0};
+            std::sscanf(rest, " %1023[^\r\n]", name);
+            out[name] = default_material();
+            cur = &out[name];
+        } else if (cur) {
+            float a = 0, b = 0, c = 0;
+            int k = std::sscanf(rest, "%f %f %f", &a, &b, &c);
+            if (!std::strcmp(key, "Kd") && k >= 3) cur->baseColor = f3(a, b, c);
+            else if (!std::strcmp(key, "Ks") && k >= 3) cur->specular = f3(a, b, c);
+            else if (!std::strcmp(key, "Ke") && k >= 3) cur->emission = f3(a, b, c);
+            else if (!std::strcmp(key, "Ni") && k >= 1) cur->refractionIndex = a;
+            else if (!std::strcmp(key, "d") && k >= 1) cur->opacity = std::min(std::max(a, 0.0f), 1.0f);
+            else if (!std::strcmp(key, "Tr") && k >= 1) cur->opacity = std::min(std::max(1.0f - a, 0.0f), 1.0f);
+            // map_* texture statements: texture path is §8f "next"; textureFlags stay 0.
+        }
+    }
+    std::fclose(f);
+    return true;
+}
+
+static std::string dir_of(const std::string& p) {
+    size_t s = p.find_last_of('/');
+    return s == std::string::npos ? std::string(".") : p.substr(0, s);
+}
+
+// ---- OBJ -------------------------------------------------------------------------------------
+struct ObjKey {
+    int v, t, n;
+    bool operator==(const ObjKey& o) const { return v == o.v && t == o.t && n == o.n; }
+};
+struct ObjKeyHash {
+    size_t operator()(const ObjKey& k) const {
+        return (size_t)k.v * 73856093u ^ (size_t)k.t * 19349663u ^ (size_t)k.n * 83492791u;
+    }
+};
+
+static bool load_obj(const std::string& path, std::vector<Mesh>& meshes, std::string& err) {
+    FILE* f = std::fopen(path.c_str(), "r");
+    if (!f) { err = "cannot open " + path; return false; }
+    std::vector<float> V, VT, VN;
+    std::map<std::string, Material> mtl;
+    Mesh* mesh = nullptr;
+    std::unordered_map<ObjKey, uint32_t, ObjKeyHash> dedup;
+    std::map<std::string, size_t> sub_of;
+    size_t cur_sub = (size_t)-1;
+    std::string cur_mtl = "";
+    auto start_mesh = [&](const std::string& name) {
+        meshes.emplace_back();
+        mesh = &meshes.back();
+        mesh->name = name;
+        mesh->transform = m4_identity();
+        dedup.clear();
+        sub_of.clear();
+        cur_sub = (size_t)-1;
+    };
+    auto select_sub = [&]() {
+        if (!mesh) start_mesh("default");
+        auto it = sub_of.find(cur_mtl);
+        if (it == sub_of.end()) {
+            Submesh s;
+            s.material_name = cur_mtl;
+            auto mi = mtl.find(cur_mtl);
+            s.material = (mi != mtl.end()) ? mi->second : default_material();
+            mesh->submeshes.push_back(s);
+            cur_sub = mesh->submeshes.size() - 1;
+            sub_of[cur_mtl] = cur_sub;
+        } else {
+            cur_sub = it->second;
+        }
+    };
+    char line[1 << 14];
+    std::vector<uint32_t> poly;
+    while (std::fgets(line, sizeof line, f)) {
+        char* p = line;
+        while (*p == ' ' || *p == '\t') ++p;
+        if (p[0] == 'v' && p[1] == ' ') {
+            float x = 0, y = 0, z = 0;
+            std::sscanf(p + 2, "%f %f %f", &x, &y, &z);
+            V.push_back(x); V.push_back(y); V.push_back(z);
+        } else if (p[0] == 'v' && p[1] == 't') {
+            float x = 0, y = 0;
+            std::sscanf(p + 2, "%f %f", &x, &y);
+            VT.push_back(x); VT.push_back(y);
+        } else if (p[0] == 'v' && p[1] == 'n') {
+            float x = 0, y = 0, z = 0;
+            std::sscanf(p + 2, "%f %f %f", &x, &y, &z);
+            VN.push_back(x); VN.push_back(y); VN.push_back(z);
+        } else if (p[0] == 'o' && (p[1] == ' ' || p[1] == '\t')) {
+            char name[1024] = {0};
+            std::sscanf(p + 1, " %1023[^\r\n]", name);
+            start_mesh(name);
+        } else if (!std::strncmp(p, "mtllib", 6)) {
+            char name[1024] = {0};
+            std::sscanf(p + 6, " %1023[^\r\n]", name);
+            parse_mtl(dir_of(path) + "/" + name, mtl);
+        } else if (!std::strncmp(p, "usemtl", 6)) {
+            char name[1024] = {0};
+            std::sscanf(p + 6, " %1023[^\r\n]", name);
+            cur_mtl = name;
+            cur_sub = (size_t)-1;
+        } else if (p[0] == 'f' && (p[1] == ' ' || p[1] == '\t')) {
+            if (!mesh) start_mesh("default");
+            if (cur_sub == (size_t)-1) select_sub();
+            poly.clear();
+            char* q = p + 1;
+            while (*q) {
+                while (*q == ' ' || *q == '\t') ++q;
+                if (!*q || *q == '\n' || *q == '\r') break;
+                int vi = 0, ti = 0, ni = 0;
+                vi = (int)std::strtol(q, &q, 10);
+                if (*q == '/') {
+                    ++q;
+                    if (*q != '/') ti = (int)std::strtol(q, &q, 10);
+                    if (*q == '/') { ++q; ni = (int)std::strtol(q, &q, 10); }
+                }
+                while (*q && *q != ' ' && *q != '\t' && *q != '\n' && *q != '\r') ++q;
+                int nv = (int)V.size() / 3, nt = (int)VT.size() / 2, nn = (int)VN.size() / 3;
+                if (vi < 0) vi = nv + vi + 1;
+                if (ti < 0) ti = nt + ti + 1;
+                if (ni < 0) ni = nn + ni + 1;
+                if (vi <= 0 || vi > nv || ti > nt || ni > nn) { err = "bad face index in " + path; std::fclose(f); return false; }
+                ObjKey key{vi, ti, ni};
+                auto it = dedup.find(key);
+                uint32_t idx;
+                if (it == dedup.end()) {
+                    idx = (uint32_t)mesh->positions.size();
+                    dedup.emplace(key, idx);
+                    mesh->positions.push_back(f3(V[3 * (vi - 1)], V[3 * (vi - 1) + 1], V[3 * (vi - 1) + 2]));
+                    mesh->normals.push_back(ni > 0 ? f3(VN[3 * (ni - 1)], VN[3 * (ni - 1) + 1], VN[3 * (ni - 1) + 2]) : f3(0, 0, 0));
+                    rt_float2 uv; uv.x = 0; uv.y = 0;
+                    if (ti > 0) { uv.x = VT[2 * (ti - 1)]; uv.y = VT[2 * (ti - 1) + 1]; mesh->has_uvs = true; }
+                    mesh->uvs.push_back(uv);
+                } else {
+                    idx = it->second;
+                }
+                poly.push_back(idx);
+            }
+            auto& ind = mesh->submeshes[cur_sub].indices;
+            for (size_t k = 2; k < poly.size(); ++k) {  // fan triangulation
+                ind.push_back(poly[0]); ind.push_back(poly[k - 1]); ind.push_back(poly[k]);
+            }
+        }
+    }
+    std::fclose(f);
+    // drop empty submeshes / meshes
+    for (auto& m : meshes) {
+        std::vector<Submesh> keep;
+        for (auto& s : m.submeshes) if (!s.indices.empty()) keep.push_back(std::move(s));
+        m.submeshes.swap(keep);
+    }
+    std::vector<Mesh> keepm;
+    for (auto& m : meshes) if (!m.submeshes.empty()) keepm.push_back(std::move(m));
+    meshes.swap(keepm);
+    if (meshes.empty()) { err = "no faces in " + path; return false; }
+    return true;
+}
+
+// ---- procedural stand-ins ----------------------------------------------------------------------
+static void compute_vertex_normals(Mesh& m) {
+    std::vector<double> acc(m.positions.size() * 3, 0.0);
+    for (auto& s : m.submeshes)
+        for (size_t t = 0; t + 2 < s.indices.size(); t += 3) {
+            const rt_float3& a = m.positions[s.indices[t]];
+            const rt_float3& b = m.positions[s.indices[t + 1]];
+            const rt_float3& c = m.positions[s.indices[t + 2]];
+            double e1[3] = {(double)b.x - a.x, (double)b.y - a.y, (double)b.z - a.z};
+            double e2[3] = {(double)c.x - a.x, (double)c.y - a.y, (double)c.z - a.z};
+            double n[3] = {e1[1] * e2[2] - e1[2] * e2[1], e1[2] * e2[0] - e1[0] * e2[2], e1[0] * e2[1] - e1[1] * e2[0]};
+            for (int k = 0; k < 3; ++k)
+                for (int j = 0; j < 3; ++j) acc[3 * s.indices[t + k] + j] += n[j];
+        }
+    m.normals.resize(m.positions.size());
+    for (size_t i = 0; i < m.positions.size(); ++i) {
+        double* n = &acc[3 * i];
+        double l = std::sqrt(n[0] * n[0] + n[1] * n[1] + n[2] * n[2]);
+        if (l > 0) m.normals[i] = f3((float)(n[0] / l), (float)(n[1] / l), (float)(n[2] / l));
+        else m.normals[i] = f3(0, 0, 0);
+    }
+}
+
+// Fit positions into the box [-h, h] per axis (centred), preserving nothing else.
+static void fit_box(Mesh& m, const double half[3]) {
+    double lo[3] = {1e30, 1e30, 1e30}, hi[3] = {-1e30, -1e30, -1e30};
+    for (auto& p : m.positions) {
+        double v[3] = {p.x, p.y, p.z};
+        for (int k = 0; k < 3; ++k) { lo[k] = std::min(lo[k], v[k]); hi[k] = std::max(hi[k], v[k]); }
+    }
+    for (auto& p : m.positions) {
+        double v[3] = {p.x, p.y, p.z};
+        for (int k = 0; k < 3; ++k) {
+            double c = 0.5 * (lo[k] + hi[k]), e = 0.5 * (hi[k] - lo[k]);
+            v[k] = (v[k] - c) / e * half[k];
+        }
+        p = f3((float)v[0], (float)v[1], (float)v[2]);
+    }
+}
+
+// Closed tube of U x V quads around a (2,3) torus knot with bumps: 2*U*V triangles.
+// dragon: U=10627, V=41 -> 871,414 triangles, the triangle count of the Stanford dragon
+// asset named by BASELINE.json; bounds ~ (0.45, 0.317, 0.2) half-extents so that at the
+// AppScene transform (scale 1.2 at y=0.38, AppScene.swift:16-21) it rests on the floor.
+static Mesh make_knot(const char* name, int U, int V, double tube, double bump, const double half[3]) {
+    Mesh m;
+    m.name = name;
+    m.transform = m4_identity();
+    m.positions.reserve((size_t)U * V);
+    const double TWO_PI = 6.283185307179586;
+    for (int i = 0; i < U; ++i) {
+        double t = TWO_PI * i / U;
+        // trefoil knot and its derivative
+        double cx = std::sin(t) + 2.0 * std::sin(2 * t), cy = std::cos(t) - 2.0 * std::cos(2 * t), cz = -std::sin(3 * t);
+        double dx = std::cos(t) + 4.0 * std::cos(2 * t), dy = -std::sin(t) + 4.0 * std::sin(2 * t), dz = -3.0 * std::cos(3 * t);
+        double dl = std::sqrt(dx * dx + dy * dy + dz * dz);
+        dx /= dl; dy /= dl; dz /= dl;
+        // B = normalize(T x Z), N = B x T
+        double bx = dy * 1.0 - dz * 0.0, by = dz * 0.0 - dx * 1.0, bz = 0.0;
+        double bl = std::sqrt(bx * bx + by * by + bz * bz);
+        bx /= bl; by /= bl; bz /= bl;
+        double nx = by * dz - bz * dy, ny = bz * dx - bx * dz, nz = bx * dy - by * dx;
+        for (int j = 0; j < V; ++j) {
+            double ph = TWO_PI * j / V;
+            double r = tube * (1.0 + bump * std::sin(13.0 * t + 3.0 * ph) * std::cos(7.0 * t - 2.0 * ph)
+                               + 0.5 * bump * std::sin(57.0 * t + 5.0 * ph));
+            double px = cx + r * (std::cos(ph) * nx + std::sin(ph) * bx);
+            double py = cy + r * (std::cos(ph) * ny + std::sin(ph) * by);
+            double pz = cz + r * (std::cos(ph) * nz + std::sin(ph) * bz);
+            m.positions.push_back(f3((float)px, (float)py, (float)pz));
+        }
+    }
+    Submesh s;
+    s.indices.reserve((size_t)U * V * 6);
+    for (int i = 0; i < U; ++i) {
+        int i1 = (i + 1) % U;
+        for (int j = 0; j < V; ++j) {
+            int j1 = (j + 1) % V;
+            uint32_t a = i * V + j, b = i1 * V + j, c = i1 * V + j1, d = i * V + j1;
+            s.indices.push_back(a); s.indices.push_back(b); s.indices.push_back(c);
+            s.indices.push_back(a); s.indices.push_back(c); s.indices.push_back(d);
+        }
+    }
+    s.material = default_material();
+    m.submeshes.push_back(std::move(s));
+    fit_box(m, half);
+    compute_vertex_normals(m);
+    m.uvs.assign(m.positions.size(), rt_float2{0.0f, 0.0f});
+    return m;
+}
+
+// Lumpy UV sphere: 2*U*(R-1) triangles (bunny stand-in: U=463, R=76 -> 69,450 triangles).
+static Mesh make_blob(const char* name, int U, int R, const double half[3]) {
+    Mesh m;
+    m.name = name;
+    m.transform = m4_identity();
+    const double PI = 3.141592653589793;
+    // rings 1..R-1 plus two poles
+    m.positions.push_back(f3(0, 1, 0));
+    for (int r = 1; r < R; ++r) {
+        double th = PI * r / R;
+        for (int u = 0; u < U; ++u) {
+            double ph = 2 * PI * u / U;
+            double rad = 1.0 + 0.18 * std::sin(3 * th) * std::cos(2 * ph) + 0.07 * std::sin(11 * th + 5 * ph)
+                         + (th < 0.9 ? 0.35 * std::exp(-20.0 * std::pow(std::sin(ph) - 0.6, 2)) * (0.9 - th) : 0.0);
+            m.positions.push_back(f3((float)(rad * std::sin(th) * std::cos(ph)), (float)(rad * std::cos(th)),
+                                     (float)(rad * std::sin(th) * std::sin(ph))));
+        }
+    }
+    m.positions.push_back(f3(0, -1, 0));
+    uint32_t south = (uint32_t)m.positions.size() - 1;
+    Submesh s;
+    auto ring = [&](int r, int u) -> uint32_t { return 1 + (uint32_t)((r - 1) * U + (u % U)); };
+    for (int u = 0; u < U; ++u) { s.indices.push_back(0); s.indices.push_back(ring(1, u + 1)); s.indices.push_back(ring(1, u)); }
+    for (int r = 1; r < R - 1; ++r)
+        for (int u = 0; u < U; ++u) {
+            uint32_t a = ring(r, u), b = ring(r, u + 1), c = ring(r + 1, u + 1), d = ring(r + 1, u);
+            s.indices.push_back(a); s.indices.push_back(b); s.indices.push_back(c);
+            s.indices.push_back(a); s.indices.push_back(c); s.indices.push_back(d);
+        }
+    for (int u = 0; u < U; ++u) { s.indices.push_back(south); s.indices.push_back(ring(R - 1, u)); s.indices.push_back(ring(R - 1, u + 1)); }
+    s.material = default_material();
+    s.material.baseColor = f3(0.8f, 0.8f, 0.8f);
+    m.submeshes.push_back(std::move(s));
+    fit_box(m, half);
+    compute_vertex_normals(m);
+    m.uvs.assign(m.positions.size(), rt_float2{0.0f, 0.0f});
+    return m;
+}
+
+// Skinned robot stand-in (config 5): a segmented capsule "arm" of J joints along +Y whose
+// joints bend about Z over time.  4 joint influences per vertex (Model.swift:304-341 streams).
+static Mesh make_robot(int J, int rings_per_joint, int U) {
+    Mesh m;
+    m.name = "robot";
+    m.transform = m4_identity();
+    const double PI = 3.141592653589793;
+    const double seg = 0.6, radius = 0.18;
+    int R = J * rings_per_joint + 1;
+    for (int r = 0; r < R; ++r) {
+        double y = seg * J * r / (R - 1);
+        double rad = radius * (0.75 + 0.25 * std::cos(2 * PI * r / rings_per_joint));
+        double jf = y / seg;  // joint coordinate
+        int j0 = std::min((int)std::floor(jf - 0.5), J - 1);
+        for (int u = 0; u < U; ++u) {
+            double ph = 2 * PI * u / U;
+            m.positions.push_back(f3((float)(rad * std::cos(ph)), (float)y, (float)(rad * std::sin(ph))));
+            // weights: blend between joint j0 and j0+1 around the joint boundary
+            uint16_t ji[4] = {0, 0, 0, 0};
+            float w[4] = {1, 0, 0, 0};
+            if (j0 < 0) { ji[0] = 0; }
+            else if (j0 >= J - 1) { ji[0] = (uint16_t)(J - 1); }
+            else {
+                double t = jf - (j0 + 0.5);
+                ji[0] = (uint16_t)j0; ji[1] = (uint16_t)(j0 + 1);
+                w[0] = (float)(1.0 - t); w[1] = (float)t;
+            }
+            for (int k = 0; k < 4; ++k) { m.joint_indices.push_back(ji[k]); m.joint_weights.push_back(w[k]); }
+        }
+    }
+    Submesh s;
+    for (int r = 0; r + 1 < R; ++r)
+        for (int u = 0; u < U; ++u) {
+            uint32_t a = r * U + u, b = r * U + (u + 1) % U, c = (r + 1) * U + (u + 1) % U, d = (r + 1) * U + u;
+            s.indices.push_back(a); s.indices.push_back(c); s.indices.push_back(b);
+            s.indices.push_back(a); s.indices.push_back(d); s.indices.push_back(c);
+        }
+    s.material = default_material();
+    s.material.baseColor = f3(0.7f, 0.72f, 0.75f);
+    m.submeshes.push_back(std::move(s));
+    compute_vertex_normals(m);
+    m.uvs.assign(m.positions.size(), rt_float2{0.0f, 0.0f});
+    m.joint_count = (uint32_t)J;
+    auto skin = std::make_shared<Skin>();
+    for (int j = 0; j < J; ++j) {
+        skin->parent.push_back(j - 1);
+        float t[3] = {0.0f, j == 0 ? 0.0f : (float)seg, 0.0f};
+        skin->rest_local.push_back(m4_translate(t));
+    }
+    // global bind = chain of rest locals; inverse bind = translate(-y)
+    for (int j = 0; j < J; ++j) {
+        float t[3] = {0.0f, -(float)(seg * j), 0.0f};
+        skin->inverse_bind.push_back(m4_translate(t));
+    }
+    m.skin = skin;
+    return m;
+}
+
+}  // namespace rt
+
+using namespace rt;
+
+struct rt_scene {
+    std::vector<Model> models;
+    std::vector<Light> lights;
+    std::string err;
+    // flattened description caches
+    std::vector<rt_mesh_desc> mesh_descs;
+    std::vector<std::vector<rt_submesh_desc>> sub_descs;
+};
+
+static Light area_light_default() {  // Scene.setupLight (Scene.swift:161-169)
+    Light l;
+    std::memset(&l, 0, sizeof l);
+    l.type = LightTypeAreaLight;
+    l.position = f3(0.0f, 1.98f, 0.0f);
+    l.forward = f3(0.0f, -1.0f, 0.0f);
+    l.right = f3(0.25f, 0.0f, 0.0f);
+    l.up = f3(0.0f, 0.0f, 0.25f);
+    l.color = f3(4.0f, 4.0f, 4.0f);
+    return l;
+}
+static Light spot_light_default() {  // Light.spotLight(...) (Scene.swift:88, :200-208)
+    Light l;
+    std::memset(&l, 0, sizeof l);
+    l.type = LightTypeSpotlight;
+    l.position = f3(2.0f, 1.0f, 4.0f);
+    l.direction = f3(-1.5f, -0.5f, -1.5f);
+    l.coneAngle = 25.0f / 180.0f * 3.14159265358979323846f;
+    l.color = f3(4.0f, 4.0f, 4.0f);
+    return l;
+}
+
+extern "C" {
+
+void rt_material_override_glass(rt_material_override* out) {
+    std::memset(out, 0, sizeof *out);
+    out->has_base_color = 1;
+    out->base_color[0] = 0.95f; out->base_color[1] = 0.98f; out->base_color[2] = 1.0f;
+    out->has_refraction_index = 1; out->refraction_index = 1.52f;
+    out->has_opacity = 1; out->opacity = 0.08f;
+}
+
+rt_status rt_scene_new(rt_scene** out) {
+    if (!out) return RT_ERR_INVALID_ARG;
+    rt_scene* s = new (std::nothrow) rt_scene();
+    if (!s) return RT_ERR_OUT_OF_MEMORY;
+    // Scene.init: lights = [light1 (area), light3 (spot)]; light2 is built but unused (Scene.swift:82-91)
+    s->lights.push_back(area_light_default());
+    s->lights.push_back(spot_light_default());
+    *out = s;
+    return RT_OK;
+}
+
+rt_status rt_scene_free(rt_scene* scene) { delete scene; return RT_OK; }
+const char* rt_scene_last_error(const rt_scene* scene) { return scene ? scene->err.c_str() : "null scene"; }
+
+static void finish_model(rt_scene* s, Model&& model, const rt_material_override* ov) {
+    M4 T = model_transform(model.position, model.rotation, model.scale);
+    for (auto& m : model.meshes) {
+        m.transform = T;
+        for (auto& sm : m.submeshes) apply_override(sm.material, ov);  // Model.swift:198-205
+    }
+    s->models.push_back(std::move(model));
+}
+
+rt_status rt_scene_add_obj(rt_scene* s, const char* obj_path, const float position[3],
+                           const float rotation[3], float scale, const rt_material_override* ov) {
+    if (!s || !obj_path || !position) return RT_ERR_INVALID_ARG;
+    Model model;
+    model.name = obj_path;
+    for (int k = 0; k < 3; ++k) { model.position[k] = position[k]; model.rotation[k] = rotation ? rotation[k] : 0.0f; }
+    model.scale = scale;
+    std::string err;
+    if (!load_obj(obj_path, model.meshes, err)) { s->err = err; return RT_ERR_IO; }
+    finish_model(s, std::move(model), ov);
+    return RT_OK;
+}
+
+rt_status rt_scene_add_procedural(rt_scene* s, const char* kind, const char* mtl_path,
+                                  const float position[3], const float rotation[3], float scale,
+                                  const rt_material_override* ov) {
+    if (!s || !kind || !position) return RT_ERR_INVALID_ARG;
+    Model model;
+    model.name = kind;
+    for (int k = 0; k < 3; ++k) { model.position[k] = position[k]; model.rotation[k] = rotation ? rotation[k] : 0.0f; }
+    model.scale = scale;
+    std::string k = kind;
+    if (k == "dragon") {
+        const double half[3] = {0.45, 0.3166, 0.2};
+        Mesh m = make_knot("dragon", 10627, 41, 0.42, 0.12, half);
+        // dragon.mtl: Kd 1 0 0, Ks .2, Ke 0, Ni 1, d 1 (AssetResources/dragon.mtl)
+        m.submeshes[0].material.baseColor = f3(1.0f, 0.0f, 0.0f);
+        m.submeshes[0].material.specular = f3(0.2f, 0.2f, 0.2f);
+        model.meshes.push_back(std::move(m));
+    } else if (k == "bunny") {
+        const double half[3] = {0.40, 0.3166, 0.32};
+        model.meshes.push_back(make_blob("bunny", 463, 76, half));
+    } else if (k == "robot") {
+        // height 3.0 units at scale 1 -> at the AppScene robot slot use scale ~0.5.
+        model.meshes.push_back(make_robot(5, 24, 96));
+    } else {
+        s->err = "unknown procedural kind " + k;
+        return RT_ERR_INVALID_ARG;
+    }
+    if (mtl_path) {
+        std::map<std::string, Material> mtl;
+        if (!parse_mtl(mtl_path, mtl) || mtl.empty()) { s->err = std::string("cannot read ") + mtl_path; return RT_ERR_IO; }
+        model.meshes[0].submeshes[0].material = mtl.begin()->second;
+    }
+    finish_model(s, std::move(model), ov);
+    return RT_OK;
+}
+
+rt_status rt_scene_set_lights(rt_scene* s, const Light* lights, uint32_t count) {
+    if (!s || (count && !lights)) return RT_ERR_INVALID_ARG;
+    s->lights.assign(lights, lights + count);
+    return RT_OK;
+}
+
+rt_status rt_scene_set_light_intensity(rt_scene* s, float intensity) {
+    if (!s) return RT_ERR_INVALID_ARG;
+    for (auto& l : s->lights) l.color = f3(intensity, intensity, intensity);
+    return RT_OK;
+}
+
+static bool file_exists(const std::string& p) {
+    FILE* f = std::fopen(p.c_str(), "r");
+    if (f) std::fclose(f);
+    return f != nullptr;
+}
+
+rt_status rt_scene_preset(const char* name_c, const char* asset_dir_c, rt_scene** out, int32_t* is_synthetic) {
+    if (!name_c || !out) return RT_ERR_INVALID_ARG;
+    std::string name = name_c, dir = asset_dir_c ? asset_dir_c : ".";
+    bool force_synth = false;
+    const std::string suf = "_synthetic";
+    if (name.size() > suf.size() && name.compare(name.size() - suf.size(), suf.size(), suf) == 0) {
+        force_synth = true;
+        name = name.substr(0, name.size() - suf.size());
+    }
+    rt_scene* s = nullptr;
+    rt_status st = rt_scene_new(&s);
+    if (st) return st;
+    int synth = 0;
+    const float zero[3] = {0, 0, 0};
+    auto obj = [&](const char* n, float px, float py, float pz, float sc) -> rt_status {
+        float p[3] = {px, py, pz};
+        return rt_scene_add_obj(s, (dir + "/" + n + ".obj").c_str(), p, zero, sc, nullptr);
+    };
+    // AppScene.swift:14-28 — models after the (optional) hero object
+    auto base = [&]() -> rt_status {
+        rt_status r;
+        if ((r = obj("plane", 0, 0, 0, 10))) return r;
+        if ((r = obj("sphere", -1.9f, 0.0f, 0.3f, 1))) return r;
+        if ((r = obj("sphere", 2.9f, 0.0f, -0.5f, 2))) return r;
+        return obj("plane-back", 0, 0, -1.5f, 10);
+    };
+    auto hero = [&](const char* kind, const rt_material_override* ov) -> rt_status {
+        float pos[3] = {0.3f, 0.38f, 2.5f};
+        float rot[3] = {0.0f, 3.14159265358979323846f / 2.0f * 1.2f, 0.0f};
+        std::string real = dir + "/" + kind + ".obj";
+        if (!force_synth && file_exists(real)) return rt_scene_add_obj(s, real.c_str(), pos, rot, 1.2f, ov);
+        synth = 1;
+        std::string mtl = dir + "/" + kind + ".mtl";
+        return rt_scene_add_procedural(s, kind, file_exists(mtl) ? mtl.c_str() : nullptr, pos, rot, 1.2f, ov);
+    };
+    rt_material_override glass;
+    rt_material_override_glass(&glass);
+    if (name == "c1") {
+        st = base();
+    } else if (name == "c2") {
+        if (!(st = hero("bunny", nullptr))) st = base();
+    } else if (name == "c3" || name == "c3g") {
+        if (!(st = hero("dragon", &glass))) st = base();
+    } else if (name == "c3d") {
+        if (!(st = hero("dragon", nullptr))) st = base();
+    } else if (name == "c5" || name == "app") {
+        float rp[3] = {-0.5f, 0.0f, 1.0f};
+        synth = 1;
+        st = rt_scene_add_procedural(s, "robot", nullptr, rp, zero, 0.5f, nullptr);
+        if (!st && name == "app") {
+            if (!(st = hero("dragon", &glass))) {
+                if (!(st = obj("train", -0.3f, 0.0f, 0.4f, 0.5f))) st = obj("treefir", 0.5f, 0.0f, -0.2f, 0.7f);
+            }
+        }
+        if (!st) st = base();
+    } else {
+        s->err = "unknown preset " + name;
+        st = RT_ERR_INVALID_ARG;
+    }
+    if (st) {
+        if (out) *out = s;  // let the caller read the error, then free
+        return st;
+    }
+    if (is_synthetic) *is_synthetic = synth;
+    *out = s;
+    return RT_OK;
+}
+
+rt_status rt_scene_get_desc(rt_scene* s, rt_scene_desc* out) {
+    if (!s || !out) return RT_ERR_INVALID_ARG;
+    s->mesh_descs.clear();
+    s->sub_descs.clear();
+    for (auto& model : s->models)
+        for (auto& m : model.meshes) {
+            std::vector<rt_submesh_desc> subs;
+            for (auto& sm : m.submeshes) {
+                rt_submesh_desc d;
+                std::memset(&d, 0, sizeof d);
+                d.indices = sm.indices.data();
+                d.index_count = (uint32_t)sm.indices.size();
+                d.material = sm.material;
+                subs.push_back(d);
+            }
+            s->sub_descs.push_back(std::move(subs));
+        }
+    size_t k = 0;
+    for (auto& model : s->models)
+        for (auto& m : model.meshes) {
+            rt_mesh_desc d;
+            std::memset(&d, 0, sizeof d);
+            d.positions = m.positions.data();
+            d.normals = m.normals.data();
+            d.uvs = m.has_uvs ? m.uvs.data() : nullptr;
+            d.joint_indices = m.joint_indices.empty() ? nullptr : m.joint_indices.data();
+            d.joint_weights = m.joint_weights.empty() ? nullptr : m.joint_weights.data();
+            d.vertex_count = (uint32_t)m.positions.size();
+            d.submesh_count = (uint32_t)m.submeshes.size();
+            d.submeshes = s->sub_descs[k].data();
+            d.transform = pack4x3(m.transform);
+            d.joint_count = m.joint_count;
+            s->mesh_descs.push_back(d);
+            ++k;
+        }
+    out->mesh_count = (uint32_t)s->mesh_descs.size();
+    out->meshes = s->mesh_descs.data();
+    out->light_count = (uint32_t)s->lights.size();
+    out->lights = s->lights.data();
+    return RT_OK;
+}
+
+uint64_t rt_scene_triangle_count(const rt_scene* s) {
+    uint64_t n = 0;
+    if (!s) return 0;
+    for (auto& model : s->models)
+        for (auto& m : model.meshes)
+            for (auto& sm : m.submeshes) n += sm.indices.size() / 3;
+    return n;
+}
+
+rt_status rt_scene_joint_matrices(rt_scene* s, uint32_t mesh_index, double time_seconds,
+                                  float* out, uint32_t capacity, uint32_t* joint_count) {
+    if (!s || !out) return RT_ERR_INVALID_ARG;
+    uint32_t k = 0;
+    Mesh* mesh = nullptr;
+    for (auto& model : s->models)
+        for (auto& m : model.meshes) { if (k == mesh_index) mesh = &m; ++k; }
+    if (!mesh || !mesh->skin) { s->err = "mesh is not skinned"; return RT_ERR_INVALID_ARG; }
+    Skin& sk = *mesh->skin;
+    uint32_t J = (uint32_t)sk.parent.size();
+    if (capacity < J) return RT_ERR_INVALID_ARG;
+    // Model.update: local = rest * animated rotation; global via parents; joint = global * invBind
+    double t = std::fmod(time_seconds, sk.duration);
+    std::vector<M4> global(J);
+    for (uint32_t j = 0; j < J; ++j) {
+        float ang = (float)(0.35 * std::sin(6.283185307179586 * t / sk.duration + 0.9 * j) * (j == 0 ? 0.3 : 1.0));
+        M4 local = m4_mul(sk.rest_local[j], m4_rotate_axis(ang, 0, 0, 1));
+        global[j] = sk.parent[j] >= 0 ? m4_mul(global[sk.parent[j]], local) : local;
+    }
+    // SkinningPass.updateSkinningJointMatrices: geomBind^-1 * (global*invBind) * geomBind, geomBind = I
+    for (uint32_t j = 0; j < J; ++j) {
+        M4 jm = m4_mul(global[j], sk.inverse_bind[j]);
+        std::memcpy(out + 16 * j, jm.m, sizeof jm.m);
+    }
+    if (joint_count) *joint_count = J;
+    return RT_OK;
+}
+
+void rt_camera_orbit(int32_t width, int32_t height, const float target[3], float azimuth,
+                     float elevation, float distance, float fov_degrees, Camera* out) {
+    // Scene.makeOrbitCamera (Scene.swift:126-159)
+    float safe = std::max(0.001f, distance);
+    float limit = 3.14159265358979323846f / 2.0f - 0.001f;
+    float el = std::max(-limit, std::min(limit, elevation));
+    float x = safe * cosf(el) * sinf(azimuth);
+    float y = safe * sinf(el);
+    float z = safe * cosf(el) * cosf(azimuth);
+    float pos[3] = {target[0] + x, target[1] + y, target[2] + z};
+    float fw[3] = {target[0] - pos[0], target[1] - pos[1], target[2] - pos[2]};
+    float fl = std::sqrt(fw[0] * fw[0] + fw[1] * fw[1] + fw[2] * fw[2]);
+    for (float& v : fw) v /= fl;
+    // right = normalize(cross(forward, worldUp(0,1,0)))
+    float rt_[3] = {fw[1] * 0.0f - fw[2] * 1.0f, fw[2] * 0.0f - fw[0] * 0.0f, fw[0] * 1.0f - fw[1] * 0.0f};
+    float rl = std::sqrt(rt_[0] * rt_[0] + rt_[1] * rt_[1] + rt_[2] * rt_[2]);
+    if (rl < 0.0001f) { rt_[0] = 1; rt_[1] = 0; rt_[2] = 0; }
+    else for (float& v : rt_) v /= rl;
+    // up = normalize(cross(right, forward))
+    float up[3] = {rt_[1] * fw[2] - rt_[2] * fw[1], rt_[2] * fw[0] - rt_[0] * fw[2], rt_[0] * fw[1] - rt_[1] * fw[0]};
+    float ul = std::sqrt(up[0] * up[0] + up[1] * up[1] + up[2] * up[2]);
+    for (float& v : up) v /= ul;
+    float fov = fov_degrees * (3.14159265358979323846f / 180.0f);
+    float aspect = (float)width / (float)height;
+    float h = tanf(fov / 2.0f);
+    float w = aspect * h;
+    out->position = f3(pos[0], pos[1], pos[2]);
+    out->right = f3(rt_[0] * w, rt_[1] * w, rt_[2] * w);
+    out->up = f3(up[0] * h, up[1] * h, up[2] * h);
+    out->forward = f3(fw[0], fw[1], fw[2]);
+}
+
+void rt_camera_default(int32_t width, int32_t height, Camera* out) {
+    // Scene.setupCamera (Scene.swift:111-124): target 0, position (0, 1, 5.38), fov 45
+    const float target[3] = {0, 0, 0};
+    float off[3] = {0.0f, 1.0f, 5.38f};
+    float dist = std::max(0.001f, std::sqrt(off[0] * off[0] + off[1] * off[1] + off[2] * off[2]));
+    float az = atan2f(off[0], off[2]);
+    float el = asinf(off[1] / dist);
+    rt_camera_orbit(width, height, target, az, el, dist, 45.0f, out);
+}
+
+void rt_uniforms_default(int32_t width, int32_t height, int32_t light_count, Uniforms* u) {
+    std::memset(u, 0, sizeof *u);
+    u->width = width;
+    u->height = height;
+    u->blocksWide = (width + 15) / 16;
+    u->frameIndex = 0;
+    u->lightCount = light_count;
+    u->samplesPerPixel = 2;
+    u->maxBounces = 2;
+    rt_camera_default(width, height, &u->camera);
+    u->previousCamera = u->camera;
+    u->debugTextureMode = 0;
+    u->accumulationWeight = 0.9f;
+    u->enableDenoiseGBuffer = 0;
+    u->shadingMode = ShadingModePBR;
+    u->enableMotionAdaptiveAccumulation = 1;
+    u->motionAccumulationMinWeight = 0.1f;
+    u->motionAccumulationLowThresholdPixels = 0.5f;
+    u->motionAccumulationHighThresholdPixels = 4.0f;
+    u->enableMotionAdaptiveSampling = 1;
+    u->motionSamplingMaxExtraSamples = 2;
+    u->motionSamplingLowThresholdPixels = 1.0f;
+    u->motionSamplingHighThresholdPixels = 6.0f;
+}
+
+void rt_random_offsets(uint64_t seed, int32_t width, int32_t height, uint32_t* out) {
+    uint64_t st = seed;
+    size_t n = (size_t)width * (size_t)height;
+    for (size_t i = 0; i < n; ++i) {
+        uint64_t z = (st += 0x9E3779B97F4A7C15ull);
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+        z = z ^ (z >> 31);
+        out[i] = (uint32_t)(z % (1024u * 1024u));
+    }
+}
+
+}  // extern "C"

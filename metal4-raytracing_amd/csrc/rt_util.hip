@@ -1,0 +1,153 @@
+// rt_util.hip — small data-movement kernels around the hot path:
+//   tile pack/unpack for the multi-GPU gather,
+//   linear-blend skinning (Skinning.metal:7-49),
+//   world-space triangle flatten + level-synchronous BVH refit (refitMTL4AccelerationStructures,
+//   Renderer.swift:1084-1202).
+#include "rt_kernels.h"
+
+namespace rt {
+
+// ---- tiles ----------------------------------------------------------------------------------
+__global__ void pack_tiles_k(const float4* __restrict__ src, float4* __restrict__ dst, int width, int height, int tile,
+                             int rank, int nranks, int tiles_x, int own) {
+    size_t per = (size_t)tile * tile;
+    size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= per * own) return;
+    int k = (int)(i / per), r = (int)(i % per);
+    int tid = rank + k * nranks;
+    int x = (tid % tiles_x) * tile + r % tile, y = (tid / tiles_x) * tile + r / tile;
+    dst[i] = (x < width && y < height) ? src[(size_t)y * width + x] : make_float4(0, 0, 0, 0);
+}
+__global__ void unpack_tiles_k(const float4* __restrict__ src, float4* __restrict__ dst, int width, int height, int tile,
+                               int rank, int nranks, int tiles_x, int own) {
+    size_t per = (size_t)tile * tile;
+    size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= per * own) return;
+    int k = (int)(i / per), r = (int)(i % per);
+    int tid = rank + k * nranks;
+    int x = (tid % tiles_x) * tile + r % tile, y = (tid / tiles_x) * tile + r / tile;
+    if (x < width && y < height) dst[(size_t)y * width + x] = src[i];
+}
+void launch_pack_tiles(const float4* src, float4* dst, int width, int height, int tile, int rank, int nranks,
+                       int tiles_x, int own, hipStream_t s) {
+    size_t n = (size_t)tile * tile * own;
+    if (!n) return;
+    hipLaunchKernelGGL(pack_tiles_k, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, src, dst, width, height, tile,
+                       rank, nranks, tiles_x, own);
+}
+void launch_unpack_tiles(const float4* src, float4* dst, int width, int height, int tile, int rank, int nranks,
+                         int tiles_x, int own, hipStream_t s) {
+    size_t n = (size_t)tile * tile * own;
+    if (!n) return;
+    hipLaunchKernelGGL(unpack_tiles_k, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, src, dst, width, height,
+                       tile, rank, nranks, tiles_x, own);
+}
+
+// ---- skinning (Skinning.metal:7-49) ---------------------------------------------------------
+__device__ __forceinline__ float4 m4v(const float* m, float x, float y, float z, float w) {
+    // float4x4 * float4, column-major: ((c0*x + c1*y) + c2*z) + c3*w
+    float4 r;
+    r.x = ((m[0] * x + m[4] * y) + m[8] * z) + m[12] * w;
+    r.y = ((m[1] * x + m[5] * y) + m[9] * z) + m[13] * w;
+    r.z = ((m[2] * x + m[6] * y) + m[10] * z) + m[14] * w;
+    r.w = ((m[3] * x + m[7] * y) + m[11] * z) + m[15] * w;
+    return r;
+}
+__global__ void skin_k(const float4* __restrict__ rest_pos, const float4* __restrict__ rest_nrm,
+                       const ushort4* __restrict__ jidx, const float4* __restrict__ jw, const float* __restrict__ joints,
+                       float4* __restrict__ out_pos, float4* __restrict__ out_nrm, uint32_t n) {
+    uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
+    if (v >= n) return;
+    float4 p = rest_pos[v], q = rest_nrm[v];
+    ushort4 ix = jidx[v];
+    float4 w = jw[v];
+    float ws = ((w.x + w.y) + w.z) + w.w;
+    if (ws < 0.0001f) w = make_float4(1.0f, 0.0f, 0.0f, 0.0f);
+    const unsigned short js[4] = {ix.x, ix.y, ix.z, ix.w};
+    const float ww[4] = {w.x, w.y, w.z, w.w};
+    float4 sp = make_float4(0, 0, 0, 0);
+    float sn[3] = {0, 0, 0};
+    #pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        float4 a = m4v(joints + 16 * js[k], p.x, p.y, p.z, 1.0f);
+        sp.x = sp.x + ww[k] * a.x; sp.y = sp.y + ww[k] * a.y; sp.z = sp.z + ww[k] * a.z; sp.w = sp.w + ww[k] * a.w;
+    }
+    #pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        float4 a = m4v(joints + 16 * js[k], q.x, q.y, q.z, 0.0f);
+        sn[0] = sn[0] + ww[k] * a.x; sn[1] = sn[1] + ww[k] * a.y; sn[2] = sn[2] + ww[k] * a.z;
+    }
+    out_pos[v] = make_float4(sp.x, sp.y, sp.z, 0.0f);
+    out_nrm[v] = make_float4(sn[0], sn[1], sn[2], 0.0f);
+}
+void launch_skin(const float4* rest_pos, const float4* rest_nrm, const ushort4* jidx, const float4* jw,
+                 const float* joints, float4* out_pos, float4* out_nrm, uint32_t n, hipStream_t s) {
+    if (!n) return;
+    hipLaunchKernelGGL(skin_k, dim3((n + 255) / 256), dim3(256), 0, s, rest_pos, rest_nrm, jidx, jw, joints, out_pos,
+                       out_nrm, n);
+}
+
+// ---- flatten world-space triangles into BVH slot order ----------------------------------------
+__global__ void flatten_k(const uint4* __restrict__ tri_info, const uint32_t* __restrict__ slot_to_tri,
+                          const float4* __restrict__ pos, const float* __restrict__ inst, float4* __restrict__ tris,
+                          uint32_t n) {
+    uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n) return;
+    uint32_t id = slot_to_tri[k];
+    uint4 ti = tri_info[id];
+    const float* M = inst + 12 * (ti.w >> 8);
+    uint32_t vi[3] = {ti.x, ti.y, ti.z};
+    #pragma unroll
+    for (int q = 0; q < 3; ++q) {
+        f3 w = xform(M, ld3(pos[vi[q]]), 1.0f);
+        tris[3 * k + q] = make_float4(w.x, w.y, w.z, q == 0 ? __uint_as_float(id) : 0.0f);
+    }
+}
+void launch_flatten(const uint4* tri_info, const uint32_t* slot_to_tri, const float4* pos, const float* inst,
+                    float4* tris, uint32_t n, hipStream_t s) {
+    if (!n) return;
+    hipLaunchKernelGGL(flatten_k, dim3((n + 255) / 256), dim3(256), 0, s, tri_info, slot_to_tri, pos, inst, tris, n);
+}
+
+// ---- level-synchronous refit: one launch per tree level, deepest first ------------------------
+__global__ void refit_level_k(Bvh2Node* __restrict__ nodes, const float4* __restrict__ tris,
+                              const uint32_t* __restrict__ level_nodes, uint32_t count, float pad) {
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= count) return;
+    Bvh2Node nd = nodes[level_nodes[i]];
+    #pragma unroll
+    for (int s = 0; s < 2; ++s) {
+        float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+        if (nd.child[s] >= 0) {
+            const Bvh2Node& c = nodes[nd.child[s]];
+            for (int cs = 0; cs < 2; ++cs) {
+                if (c.child[cs] < 0 && c.count[cs] == 0) continue;
+                lo[0] = fminf(lo[0], c.lx[2 * cs]); hi[0] = fmaxf(hi[0], c.lx[2 * cs + 1]);
+                lo[1] = fminf(lo[1], c.ly[2 * cs]); hi[1] = fmaxf(hi[1], c.ly[2 * cs + 1]);
+                lo[2] = fminf(lo[2], c.lz[2 * cs]); hi[2] = fmaxf(hi[2], c.lz[2 * cs + 1]);
+            }
+        } else {
+            if (nd.count[s] == 0) continue;
+            int first = ~nd.child[s];
+            for (int t = 0; t < nd.count[s]; ++t)
+                for (int q = 0; q < 3; ++q) {
+                    float4 v = tris[3 * (first + t) + q];
+                    lo[0] = fminf(lo[0], v.x); hi[0] = fmaxf(hi[0], v.x);
+                    lo[1] = fminf(lo[1], v.y); hi[1] = fmaxf(hi[1], v.y);
+                    lo[2] = fminf(lo[2], v.z); hi[2] = fmaxf(hi[2], v.z);
+                }
+            for (int a = 0; a < 3; ++a) { lo[a] -= pad; hi[a] += pad; }
+        }
+        nd.lx[2 * s] = lo[0]; nd.lx[2 * s + 1] = hi[0];
+        nd.ly[2 * s] = lo[1]; nd.ly[2 * s + 1] = hi[1];
+        nd.lz[2 * s] = lo[2]; nd.lz[2 * s + 1] = hi[2];
+    }
+    nodes[level_nodes[i]] = nd;
+}
+void launch_refit_level(Bvh2Node* nodes, const float4* tris, const uint32_t* level_nodes, uint32_t count, float pad,
+                        hipStream_t s) {
+    if (!count) return;
+    hipLaunchKernelGGL(refit_level_k, dim3((count + 255) / 256), dim3(256), 0, s, nodes, tris, level_nodes, count, pad);
+}
+
+}  // namespace rt

@@ -1,0 +1,20 @@
+"""Shared helpers for the parity tests (tolerances and comparison)."""
+import numpy as np
+
+# North-star parity bar (BASELINE.json): per-pixel relative L2 of RGB radiance <= 1e-4.
+REL_L2_TOL = 1e-4
+
+
+def rel_l2_per_pixel(a, b):
+    """Per-pixel ||a-b|| / max(||b||, 1e-6) over RGB."""
+    a = np.asarray(a, np.float64)[..., :3]
+    b = np.asarray(b, np.float64)[..., :3]
+    num = np.linalg.norm(a - b, axis=-1)
+    den = np.maximum(np.linalg.norm(b, axis=-1), 1e-6)
+    return num / den
+
+
+def parity_report(gpu, ref):
+    e = rel_l2_per_pixel(gpu, ref)
+    exact = np.mean(np.all(np.asarray(gpu)[..., :3] == np.asarray(ref)[..., :3], axis=-1))
+    return dict(max_rel=float(e.max()), n_bad=int((e > REL_L2_TOL).sum()), frac_bitwise=float(exact))

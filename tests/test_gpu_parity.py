@@ -1,0 +1,135 @@
+"""GPU parity: the HIP path (through the C-ABI) against the CPU oracle on the same scene, seed and
+uniforms.  Bar: per-pixel relative L2 of radiance <= 1e-4 (BASELINE.json north star); in practice
+the two are bit-identical because both evaluate the same operation order, so the
+tests also report the bitwise fraction and require it for integer-like outputs (ray counts).
+"""
+import numpy as np
+import pytest
+
+from helpers import REL_L2_TOL, parity_report
+
+pytestmark = pytest.mark.gpu
+
+
+def _render_pair(rt, orc, preset, W, H, assets, frames=1, seed=7, **knobs):
+    scene = rt.Scene.preset(preset, assets)
+    R = rt.Renderer(scene, W, H, seed=seed)
+    for k, v in knobs.items():
+        setattr(R, k, v)
+    osc = orc.OracleScene(scene.desc())
+    prev = None
+    motion = None
+    out = []
+    for f in range(frames):
+        u = R.draw()
+        R.wait()
+        g = R.radiance()
+        gd, gm, _ = R.aux()
+        st = R.stats()
+        o = osc.render(u, R.random, accum_in=prev, motion_in=motion)
+        prev = o["radiance"]
+        motion = o["motion"]
+        out.append((g, gd, gm, st, o))
+    return out
+
+
+@pytest.mark.parametrize("preset,W,H,spp,bounces,mode", [
+    ("c1", 64, 64, 1, 1, 0),          # config 1 (plumbing case), small
+    ("c1", 256, 256, 1, 1, 0),        # config 1 at its full size
+    ("c1", 96, 64, 2, 4, 0),          # more bounces, non-square
+    ("c1", 64, 48, 2, 3, 1),          # legacy shading (ShadingModeLegacy)
+])
+def test_c1_parity(rt, orc, assets, preset, W, H, spp, bounces, mode):
+    (g, gd, gm, st, o), = _render_pair(rt, orc, preset, W, H, assets, samplesPerPixel=spp, maxBounces=bounces,
+                                       shadingMode=mode)
+    rep = parity_report(g, o["radiance"])
+    print(rep, st.closest_rays, o["closest_rays"], st.shadow_rays, o["shadow_rays"])
+    assert rep["n_bad"] == 0, rep
+    assert np.array_equal(gd, o["depth"])
+    assert np.array_equal(gm, o["motion"])
+    assert st.closest_rays == o["closest_rays"] and st.shadow_rays == o["shadow_rays"]
+    assert st.paths == o["paths"]
+
+
+def test_glass_dragon_parity(rt, orc, assets):
+    """C3g scene (glass dragon stand-in, 871k tris) at reduced resolution, 8 bounces."""
+    (g, gd, gm, st, o), = _render_pair(rt, orc, "c3g", 96, 54, assets, samplesPerPixel=2, maxBounces=8)
+    rep = parity_report(g, o["radiance"])
+    print(rep)
+    assert rep["n_bad"] == 0, rep
+    assert st.closest_rays == o["closest_rays"] and st.shadow_rays == o["shadow_rays"]
+
+
+def test_bunny_parity(rt, orc, assets):
+    (g, gd, gm, st, o), = _render_pair(rt, orc, "c2", 80, 45, assets, samplesPerPixel=2, maxBounces=4)
+    rep = parity_report(g, o["radiance"])
+    assert rep["n_bad"] == 0, rep
+
+
+def test_temporal_accumulation(rt, orc, assets):
+    """frameIndex > 0: EMA with the history target (Raytracing.metal:796-817), 3 frames."""
+    frames = _render_pair(rt, orc, "c1", 48, 48, assets, frames=3, samplesPerPixel=1, maxBounces=2)
+    for g, gd, gm, st, o in frames:
+        rep = parity_report(g, o["radiance"])
+        assert rep["n_bad"] == 0, rep
+
+
+@pytest.mark.parametrize("mode", range(1, 8))
+def test_debug_modes(rt, orc, assets, mode):
+    (g, gd, gm, st, o), = _render_pair(rt, orc, "c1", 32, 32, assets, debugTextureMode=mode)
+    assert parity_report(g, o["radiance"])["n_bad"] == 0
+
+
+def test_gbuffer(rt, orc, assets):
+    scene = rt.Scene.preset("c1", assets)
+    R = rt.Renderer(scene, 40, 30, seed=3)
+    R.useTemporalDenoiser = True
+    u = R.draw()
+    _, _, gb = R.aux(gbuffer=True)
+    o = orc.OracleScene(scene.desc()).render(u, R.random, gbuffer=True)
+    assert np.array_equal(gb, o["gbuffer"])
+
+
+def test_tiles_bitwise(rt, assets):
+    """Tile-split rendering is bitwise identical to the full-image render."""
+    import torch
+    scene = rt.Scene.preset("c1", assets)
+    W, H, T = 200, 136, 64
+    full = rt.Renderer(scene, W, H, seed=5)
+    full.maxBounces = 3
+    full.draw()
+    ref = full.radiance()
+    n = 3
+    canvas = np.zeros_like(ref)
+    for rank in range(n):
+        R = rt.Renderer(scene, W, H, seed=5)
+        R.maxBounces = 3
+        R.draw(tiles=(T, rank, n))
+        cnt = R.tile_count(T, rank, n)
+        buf = torch.empty((cnt, T, T, 4), dtype=torch.float32, device="cuda")
+        R.pack_tiles(T, rank, n, buf.data_ptr())
+        R.wait()
+        torch.cuda.synchronize()
+        packed = buf.cpu().numpy()
+        tx = (W + T - 1) // T
+        for k in range(cnt):
+            tid = rank + k * n
+            x0, y0 = (tid % tx) * T, (tid // tx) * T
+            w, h = min(T, W - x0), min(T, H - y0)
+            canvas[y0:y0 + h, x0:x0 + w] = packed[k, :h, :w]
+    assert np.array_equal(canvas, ref)
+
+
+def test_counting_frame_matches(rt, assets):
+    """Counting frames produce the same image; node/triangle counters are populated."""
+    scene = rt.Scene.preset("c1", assets)
+    R = rt.Renderer(scene, 64, 64, seed=9)
+    R.draw()
+    a = R.radiance()
+    R2 = rt.Renderer(scene, 64, 64, seed=9)
+    R2.set_counting(True)
+    R2.draw()
+    b = R2.radiance()
+    st = R2.stats()
+    assert np.array_equal(a, b)
+    assert st.node_visits > st.closest_rays and st.tri_tests > 0
