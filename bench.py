@@ -1,0 +1,242 @@
+#!/usr/bin/env python3
+"""Headline benchmark: Grays/s + ms/frame, dragon scene, 1920x1080x4spp, 8 bounces (BASELINE.json
+metric; workload = configs[2], the dragon config that fits one MI355X).
+
+One step = one frame of the hot path (raytracingKernel equivalent) over the whole image.
+N GPUs (one process per GPU, torch.distributed over RCCL): the frame is tile-partitioned
+(64x64 tiles, tile_id % N == rank), every rank renders its tiles, packs them, and rank 0
+gathers the packed radiance over RCCL/xGMI and unpacks it into the full frame ("strong"
+scaling: the frame is fixed, N GPUs share it).
+
+Grays/s = (closest-hit + shadow rays traced, all ranks) / wall time of the K timed frames
+(barrier + device sync on both sides, max over ranks).  Inputs (scene, BVH, random offsets)
+are resident in HBM before the timed region.
+"""
+import argparse
+import importlib
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: 8.0 TB/s spec
+
+# Algorithmic bytes: per traced ray 32 B in (o, tmin, d, tmax) + 16 B hit out;
+# per BVH node fetched 64 B; per triangle tested 48 B; per closest hit shading 16 B tri record
+# + 3x16 B normals + 48 B instance transform; per pixel 4 B offset + 16 B history read +
+# 16 B accumulation write + 4 B depth + 8+8 B motion read/write.
+B_RAY = 48
+B_NODE = 64
+B_TRI = 48
+B_HIT = 16 + 48 + 48
+B_PIXEL = 4 + 16 + 16 + 4 + 16
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=16)
+    p.add_argument("--warmup", type=int, default=2)
+    p.add_argument("--scene", default="c3g")
+    p.add_argument("--width", type=int, default=1920)
+    p.add_argument("--height", type=int, default=1080)
+    p.add_argument("--spp", type=int, default=4)
+    p.add_argument("--bounces", type=int, default=8)
+    p.add_argument("--tile", type=int, default=64)
+    p.add_argument("--pipeline", default="megakernel")
+    p.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample time")
+    p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--traffic-csv", default=None, help="rocprofv3 --pmc counter_collection.csv for traffic")
+    return p.parse_args()
+
+
+def main():
+    a = parse()
+    import torch
+    import torch.distributed as dist
+    rt = importlib.import_module("metal4-raytracing_amd")
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    n = max(world, 1)
+
+    scene = rt.Scene.preset(a.scene)
+    t0 = time.time()
+    R = rt.Renderer(scene, a.width, a.height, device=local, pipeline=a.pipeline, seed=3)
+    setup_s = time.time() - t0
+    R.samplesPerPixel = a.spp
+    R.maxBounces = a.bounces
+    tiles = (a.tile, rank, n) if n > 1 else None
+    own = R.tile_count(a.tile, rank, n)
+    max_own = max(R.tile_count(a.tile, r, n) for r in range(n))
+    T = a.tile
+    dev = torch.device("cuda", local)
+    packed = torch.zeros((max_own, T, T, 4), dtype=torch.float32, device=dev) if n > 1 else None
+    gather_list = [torch.empty_like(packed) for _ in range(n)] if (n > 1 and rank == 0) else None
+
+    def frame():
+        R.draw(tiles=tiles)
+        R.wait()
+        st = R.stats()
+        if n > 1:
+            R.pack_tiles(T, rank, n, packed.data_ptr())
+            R.wait()
+            dist.gather(packed, gather_list, dst=0)
+            if rank == 0:
+                torch.cuda.current_stream().synchronize()
+                for r in range(1, n):
+                    R.unpack_tiles(T, r, n, gather_list[r].data_ptr())
+                R.wait()
+        return st
+
+    def barrier():
+        if n > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    # counting frame (untimed): node visits / triangle tests per ray for the roofline numerator
+    R.set_counting(True)
+    R.frameIndex = 0
+    cst = frame()
+    R.set_counting(False)
+    rays_c = cst.closest_rays + cst.shadow_rays
+    nodes_per_ray = cst.node_visits / max(rays_c, 1)
+    tris_per_ray = cst.tri_tests / max(rays_c, 1)
+    R.samplesPerPixel = a.spp  # resets frameIndex (didSet)
+
+    for _ in range(a.warmup):
+        frame()
+    barrier()
+    t0 = time.perf_counter()
+    rays = 0
+    kernel_ms = []
+    closest = 0
+    for _ in range(a.steps):
+        st = frame()
+        rays += st.closest_rays + st.shadow_rays
+        closest += st.closest_rays
+        kernel_ms.append(st.last_frame_ms)
+    barrier()
+    dt = time.perf_counter() - t0
+
+    tot = torch.tensor([dt, float(rays), float(closest), float(np.mean(kernel_ms))], dtype=torch.float64, device=dev)
+    if n > 1:
+        mx = tot.clone()
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        sm = tot.clone()
+        dist.all_reduce(sm, op=dist.ReduceOp.SUM)
+        dt, rays, closest, kms = float(mx[0]), float(sm[1]), float(sm[2]), float(mx[3])
+    else:
+        kms = float(tot[3])
+    if rank != 0:
+        dist.destroy_process_group()
+        return
+
+    value = rays / dt / 1e9
+    ms_per_step = dt / a.steps * 1e3
+    # roofline of the dominant (only) kernel, per launch
+    rays_per_launch = rays / a.steps / n
+    closest_per_launch = closest / a.steps / n
+    pixels_per_launch = a.width * a.height / n
+    bytes_per_launch = (rays_per_launch * (B_RAY + nodes_per_ray * B_NODE + tris_per_ray * B_TRI)
+                        + closest_per_launch * B_HIT + pixels_per_launch * B_PIXEL)
+    achieved = bytes_per_launch / (kms * 1e-3) / 1e9
+    traffic = None
+    if a.traffic_csv and os.path.exists(a.traffic_csv):
+        traffic = read_traffic(a.traffic_csv)
+
+    cpu = None
+    if not a.no_cpu and n == 1:
+        cpu = cpu_baseline(rt, scene, R, a)
+
+    line = {
+        "metric": "Grays/sec (closest-hit + shadow rays traced) at 1920x1080x4spp, dragon; ms/frame",
+        "value": round(value, 4),
+        "unit": "Grays/s",
+        "n_gpus": n,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": round(ms_per_step, 3),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic: procedural 871,414-triangle dragon stand-in (dragon.obj absent from the reference "
+                "snapshot), real plane/sphere OBJ assets, seeded random offsets" if scene.synthetic else
+                "reference OBJ assets, seeded random offsets",
+        "config": {
+            "workload": f"{a.scene}: glass dragon scene (configs[2]) {a.width}x{a.height}x{a.spp}spp, {a.bounces} bounces, "
+                        f"one frame per step, {'tile-split ' + str(T) + 'px + RCCL gather' if n > 1 else 'single GPU'}",
+            "scene": a.scene, "triangles": scene.triangle_count, "width": a.width, "height": a.height,
+            "spp": a.spp, "max_bounces": a.bounces, "pipeline": a.pipeline, "parallelism": f"tiles{n}",
+            "rays_per_frame": int(rays / a.steps), "kernel_ms_per_frame": round(kms, 3),
+            "setup_s": round(setup_s, 2),
+        },
+        "roofline": {
+            "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+            "kernel": "rt::megakernel<false>" if a.pipeline == "megakernel" else "wavefront",
+            "bytes_per_launch": int(bytes_per_launch), "nodes_per_ray": round(nodes_per_ray, 2),
+            "tris_per_ray": round(tris_per_ray, 2),
+        },
+        "cpu_baseline": cpu,
+    }
+    print(json.dumps(line), flush=True)
+    if n > 1:
+        dist.destroy_process_group()
+
+
+def read_traffic(path):
+    """Per-launch HBM bytes from a rocprofv3 --pmc FETCH_SIZE/WRITE_SIZE CSV (KB units; gfx950
+    FETCH_SIZE reports half of wide reads -> x2, MI355X_MICROARCH.md §HBM)."""
+    import csv
+    fetch, write, n = 0.0, 0.0, 0
+    with open(path) as f:
+        for row in csv.DictReader(f):
+            if "megakernel" not in row.get("Kernel_Name", "") and "wavefront" not in row.get("Kernel_Name", ""):
+                continue
+            name = row.get("Counter_Name", "")
+            v = float(row.get("Counter_Value", 0))
+            if name == "FETCH_SIZE":
+                fetch += v
+                n += 1
+            elif name == "WRITE_SIZE":
+                write += v
+    if n == 0:
+        return None
+    return int((2 * fetch + write) * 1024 / n)
+
+
+def cpu_baseline(rt, scene, R, a):
+    """The C oracle (oracle/, a port) on a bounded row subset of the same frame, host cores."""
+    import oracle
+    threads = min(16, os.cpu_count() or 1)
+    osc = oracle.OracleScene(scene.desc())
+    u = R.uniforms()
+    u.frameIndex = 0
+    probe_step = 64
+    t0 = time.perf_counter()
+    o = osc.render(u, R.random, row_start=0, row_step=probe_step, threads=threads)
+    t_probe = time.perf_counter() - t0
+    step = max(1, int(probe_step * t_probe / max(a.cpu_seconds, 0.1)))
+    step = min(step, probe_step)
+    t0 = time.perf_counter()
+    o = osc.render(u, R.random, row_start=0, row_step=step, threads=threads)
+    t = time.perf_counter() - t0
+    rays = o["closest_rays"] + o["shadow_rays"]
+    return {"value": round(rays / t / 1e9, 6), "unit": "Grays/s", "cores": threads, "kind": "port",
+            "sample": f"every {step}th row of frame 0 ({(a.height + step - 1) // step} rows x {a.width} px x "
+                      f"{a.spp} spp), {rays} rays in {t:.1f} s"}
+
+
+if __name__ == "__main__":
+    main()
