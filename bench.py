@@ -119,12 +119,15 @@ def main():
     t0 = time.perf_counter()
     rays = 0
     kernel_ms = []
+    stage_ms = np.zeros(7)
     closest = 0
     for _ in range(a.steps):
         st = frame()
         rays += st.closest_rays + st.shadow_rays
         closest += st.closest_rays
         kernel_ms.append(st.last_frame_ms)
+        stage_ms += np.array(list(st.kernel_ms))
+        last_st = st
     barrier()
     dt = time.perf_counter() - t0
 
@@ -180,6 +183,8 @@ def main():
             "spp": a.spp, "max_bounces": a.bounces, "pipeline": a.pipeline, "parallelism": f"tiles{n}",
             "rays_per_frame": int(rays / a.steps), "kernel_ms_per_frame": round(kms, 3),
             "setup_s": round(setup_s, 2),
+            "stage_ms": [round(x / a.steps, 3) for x in stage_ms[:6]],
+            "pipeline_used": ["megakernel", "wavefront"][last_st.pipeline], "iterations": last_st.iterations,
         },
         "roofline": {
             "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -118,7 +118,10 @@ typedef struct rt_stats {
     uint64_t triangles;     /* triangles in the current scene */
     uint64_t device_bytes;  /* device memory held by the context */
     float last_frame_ms;    /* device time of the last rt_render_frame (HIP events) */
-    float kernel_ms[7];     /* per-stage device time of the last frame, pipeline-specific */
+    float kernel_ms[7];     /* per-stage device time of the last frame: megakernel [0];
+                               wavefront [0] generate [1] extend [2] shade [3] connect [4] resolve */
+    int32_t pipeline;       /* RT_PIPELINE_* that rendered the last frame */
+    int32_t iterations;     /* wavefront: extend/shade/connect rounds of the last frame */
 } rt_stats;
 
 rt_status rt_create(const rt_opts* opts, rt_ctx** out);

@@ -135,6 +135,8 @@ class Stats(C.Structure):
         ("device_bytes", C.c_uint64),
         ("last_frame_ms", C.c_float),
         ("kernel_ms", C.c_float * 7),
+        ("pipeline", C.c_int32),
+        ("iterations", C.c_int32),
     ]
 
 

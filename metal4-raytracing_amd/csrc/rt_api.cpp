@@ -67,6 +67,12 @@ struct rt_ctx {
     int read_idx = 0;   // accum[read_idx] = history (TextureIndexAccumulation)
     unsigned long long* h_counters = nullptr;  // pinned
     rt_stats stats{};
+
+    // wavefront pipeline state
+    WavefrontBuffers wf;
+    DevBuf d_wf_color, d_wf_accum, d_wf_meta, d_wf_q0, d_wf_q1, d_wf_hits, d_wf_sq, d_wf_counts, d_wf_mprev, d_wf_extra;
+    int wf_iterations = 0;
+    bool last_wavefront = false;
 };
 
 #define FAIL(ctx, code, msg)                 \
@@ -140,16 +146,60 @@ static size_t ctx_bytes(const rt_ctx* c) {
     const DevBuf* all[] = {&c->d_pos, &c->d_prev_pos, &c->d_nrm, &c->d_rest_pos, &c->d_rest_nrm, &c->d_jidx, &c->d_jw,
                            &c->d_joints, &c->d_tri_info, &c->d_inst, &c->d_prev_inst, &c->d_mat, &c->d_lights,
                            &c->d_halton, &c->d_tris, &c->d_nodes, &c->d_slot_to_tri, &c->d_levels, &c->d_random,
-                           &c->d_accum[0], &c->d_accum[1], &c->d_depth, &c->d_motion, &c->d_gbuffer, &c->d_counters};
+                           &c->d_accum[0], &c->d_accum[1], &c->d_depth, &c->d_motion, &c->d_gbuffer, &c->d_counters,
+                           &c->d_wf_color, &c->d_wf_accum, &c->d_wf_meta, &c->d_wf_q0, &c->d_wf_q1, &c->d_wf_hits,
+                           &c->d_wf_sq, &c->d_wf_counts, &c->d_wf_mprev, &c->d_wf_extra};
     size_t s = 0;
     for (auto* b : all) s += b->bytes;
     return s;
 }
 
+static rt_status ensure_wavefront(rt_ctx* c, size_t own_px, int spp, int max_extra) {
+    WavefrontBuffers& W = c->wf;
+    size_t paths = own_px * (size_t)(spp + max_extra);
+    size_t npix = (size_t)c->width * c->height;
+    if (paths >= (1ull << 32)) FAIL(c, RT_ERR_UNSUPPORTED, "too many paths for one frame");
+    rt_status st;
+    if (W.cap_paths < paths) {
+        size_t qe = wavefront_queue_entries(paths);
+        if ((st = dev_alloc(c, c->d_wf_color, paths * 16))) return st;
+        if ((st = dev_alloc(c, c->d_wf_accum, paths * 16))) return st;
+        if ((st = dev_alloc(c, c->d_wf_meta, paths * 16))) return st;
+        if ((st = dev_alloc(c, c->d_wf_q0, qe * 32))) return st;
+        if ((st = dev_alloc(c, c->d_wf_q1, qe * 32))) return st;
+        if ((st = dev_alloc(c, c->d_wf_hits, qe * 16))) return st;
+        if ((st = dev_alloc(c, c->d_wf_sq, qe * 48))) return st;
+        W.cap_paths = paths;
+        W.queue_entries = qe;
+    }
+    if (W.cap_pixels < npix || W.cap_pixels < own_px) {
+        size_t px = std::max(npix, own_px);
+        if ((st = dev_alloc(c, c->d_wf_mprev, px * 8))) return st;
+        if ((st = dev_alloc(c, c->d_wf_extra, px * 8))) return st;
+        W.cap_pixels = px;
+    }
+    if (!c->d_wf_counts.p) {
+        if ((st = dev_alloc(c, c->d_wf_counts, kWfCountWords * 4))) return st;
+        HIPC(c, hipHostMalloc((void**)&W.h_counts, kWfCountWords * 4, 0));
+        for (auto& e : W.ev) HIPC(c, hipEventCreate(&e));
+    }
+    W.p_color = (float4*)c->d_wf_color.p;
+    W.p_accum = (float4*)c->d_wf_accum.p;
+    W.p_meta = (uint4*)c->d_wf_meta.p;
+    W.q[0] = (float4*)c->d_wf_q0.p;
+    W.q[1] = (float4*)c->d_wf_q1.p;
+    W.hits = (float4*)c->d_wf_hits.p;
+    W.sq = (float4*)c->d_wf_sq.p;
+    W.counts = (uint32_t*)c->d_wf_counts.p;
+    W.motion_prev = (float2*)c->d_wf_mprev.p;
+    W.px_extra = (uint2*)c->d_wf_extra.p;
+    return RT_OK;
+}
+
 extern "C" {
 
 const char* rt_version(void) {
-    return "rt_hip 0.1 (gfx950, BVH2 watertight, megakernel)";
+    return "rt_hip 0.2 (gfx950, BVH2 watertight, megakernel + wavefront)";
 }
 
 const char* rt_last_error(const rt_ctx* ctx) { return ctx ? ctx->err.c_str() : g_err.c_str(); }
@@ -201,9 +251,14 @@ rt_status rt_destroy(rt_ctx* c) {
     DevBuf* all[] = {&c->d_pos, &c->d_prev_pos, &c->d_nrm, &c->d_rest_pos, &c->d_rest_nrm, &c->d_jidx, &c->d_jw,
                      &c->d_joints, &c->d_tri_info, &c->d_inst, &c->d_prev_inst, &c->d_mat, &c->d_lights, &c->d_halton,
                      &c->d_tris, &c->d_nodes, &c->d_slot_to_tri, &c->d_levels, &c->d_random, &c->d_accum[0],
-                     &c->d_accum[1], &c->d_depth, &c->d_motion, &c->d_gbuffer, &c->d_counters};
+                     &c->d_accum[1], &c->d_depth, &c->d_motion, &c->d_gbuffer, &c->d_counters,
+                     &c->d_wf_color, &c->d_wf_accum, &c->d_wf_meta, &c->d_wf_q0, &c->d_wf_q1, &c->d_wf_hits,
+                     &c->d_wf_sq, &c->d_wf_counts, &c->d_wf_mprev, &c->d_wf_extra};
     for (auto* b : all) dev_free(*b);
     if (c->h_counters) hipHostFree(c->h_counters);
+    if (c->wf.h_counts) hipHostFree(c->wf.h_counts);
+    for (auto& e : c->wf.ev)
+        if (e) hipEventDestroy(e);
     if (c->ev0) hipEventDestroy(c->ev0);
     if (c->ev1) hipEventDestroy(c->ev1);
     if (c->own_stream) hipStreamDestroy(c->own_stream);
@@ -521,11 +576,27 @@ rt_status rt_render_frame(rt_ctx* c, const Uniforms* U, const rt_tile_set* tiles
     P.nranks = nranks;
     P.tiles_x = tiles_x;
     HIPC(c, hipMemsetAsync(c->d_counters.p, 0, sizeof(unsigned long long) * kCntSlots, c->stream));
+    // DebugTextureModeMotion reads sample 0's motion from later samples of the same pixel
+    // (Raytracing.metal:483): only the per-pixel kernel orders samples that way.
+    bool wavefront = c->pipeline == RT_PIPELINE_WAVEFRONT && U->debugTextureMode != DebugTextureModeMotion;
+    if (wavefront) {
+        int spp = std::max(U->samplesPerPixel, 1);
+        int max_extra = U->enableMotionAdaptiveSampling ? std::max(U->motionSamplingMaxExtraSamples, 0) : 0;
+        if ((st = ensure_wavefront(c, (size_t)own * ts * ts, spp, max_extra))) return st;
+    }
     HIPC(c, hipEventRecord(c->ev0, c->stream));
-    int nblocks = own * (ts / 16) * (ts / 16);
-    if (nblocks > 0) launch_megakernel(S, P, nblocks, c->counting, c->stream);
+    for (float& k : c->stats.kernel_ms) k = 0.0f;
+    if (wavefront) {
+        const char* err = nullptr;
+        if (own > 0 && !run_wavefront(S, P, c->wf, own, c->counting, c->stream, c->stats.kernel_ms, &c->wf_iterations, &err))
+            FAIL(c, RT_ERR_HIP, std::string("wavefront: ") + (err ? err : "?"));
+    } else {
+        int nblocks = own * (ts / 16) * (ts / 16);
+        if (nblocks > 0) launch_megakernel(S, P, nblocks, c->counting, c->stream);
+    }
     HIPC(c, hipGetLastError());
     HIPC(c, hipEventRecord(c->ev1, c->stream));
+    c->last_wavefront = wavefront;
     HIPC(c, hipMemcpyAsync(c->h_counters, c->d_counters.p, sizeof(unsigned long long) * kCntSlots,
                            hipMemcpyDeviceToHost, c->stream));
     c->read_idx = 1 - c->read_idx;  // swap accumulationTargets (Renderer.swift:1492-1494)
@@ -541,7 +612,9 @@ rt_status rt_wait(rt_ctx* c) {
         float ms = 0.0f;
         HIPC(c, hipEventElapsedTime(&ms, c->ev0, c->ev1));
         c->stats.last_frame_ms = ms;
-        c->stats.kernel_ms[0] = ms;
+        if (!c->last_wavefront) c->stats.kernel_ms[0] = ms;
+        c->stats.pipeline = c->last_wavefront ? RT_PIPELINE_WAVEFRONT : RT_PIPELINE_MEGAKERNEL;
+        c->stats.iterations = c->last_wavefront ? c->wf_iterations : 0;
         c->stats.closest_rays = c->h_counters[kCntClosest];
         c->stats.shadow_rays = c->h_counters[kCntShadow];
         c->stats.node_visits = c->h_counters[kCntNodes];

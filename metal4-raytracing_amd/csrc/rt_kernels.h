@@ -30,10 +30,33 @@ __device__ __forceinline__ unsigned long long wave_sum(uint32_t v) {
 
 void launch_megakernel(const DevScene& S, const FrameParams& P, int nblocks, bool count, hipStream_t stream);
 
-// Wavefront pipeline (rt_wavefront.hip)
-struct WavefrontBuffers;
-void launch_wavefront(const DevScene& S, const FrameParams& P, WavefrontBuffers& W, bool count, hipStream_t stream,
-                      float* stage_ms);
+// Wavefront pipeline (rt_wavefront.hip): path state SoA indexed by path id
+// (own pixel index * spp + sample; extra samples after base_paths), ray queues of
+// {float4 o (w = path id), float4 d}, hit records {t, tri id, u, v}, shadow queue of
+// {float4 o (w = path id), float4 d (w = tmax), float4 contribution}.
+constexpr int kShards = 8;        // queue segments (one allocation counter each)
+constexpr int kWfCountWords = 32; // [0..7] queue 0, [8..15] queue 1, [16..23] shadow, [24] extra allocator
+struct WavefrontBuffers {
+    size_t queue_entries = 0;     // kShards segments of queue_entries / kShards
+    float4* p_color = nullptr;
+    float4* p_accum = nullptr;
+    uint4* p_meta = nullptr;      // (pixel, sample, bounce | tpass << 8 | step << 16, halton index)
+    float4* q[2] = {nullptr, nullptr};
+    float4* hits = nullptr;
+    float4* sq = nullptr;
+    uint32_t* counts = nullptr;   // device: [0],[1] ray queues, [2] shadow queue, [3] extra-path allocator
+    uint32_t* h_counts = nullptr; // pinned host mirror
+    float2* motion_prev = nullptr;
+    uint2* px_extra = nullptr;    // per own pixel: (first extra path - base_paths, count)
+    size_t cap_paths = 0;         // base + extra paths
+    size_t cap_pixels = 0;
+    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+};
+// Runs one frame; returns false on a HIP error (message in *err). stage_ms: [0] generate,
+// [1] extend, [2] shade, [3] connect, [4] resolve (+extra-sample bookkeeping).
+bool run_wavefront(const DevScene& S, const FrameParams& P, WavefrontBuffers& W, int own_tiles, bool count,
+                   hipStream_t stream, float* stage_ms, int* iterations, const char** err);
+size_t wavefront_queue_entries(size_t paths);
 
 // Utility kernels (rt_util.hip)
 void launch_pack_tiles(const float4* src, float4* dst, int width, int height, int tile, int rank, int nranks,

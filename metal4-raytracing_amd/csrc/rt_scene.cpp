@@ -372,12 +372,106 @@ static Mesh make_knot(const char* name, int U, int V, double tube, double bump, 
         for (int j = 0; j < V; ++j) {
             int j1 = (j + 1) % V;
             uint32_t a = i * V + j, b = i1 * V + j, c = i1 * V + j1, d = i * V + j1;
-            s.indices.push_back(a); s.indices.push_back(b); s.indices.push_back(c);
-            s.indices.push_back(a); s.indices.push_back(c); s.indices.push_back(d);
+            s.indices.push_back(a); s.indices.push_back(c); s.indices.push_back(b);   // outward winding
+            s.indices.push_back(a); s.indices.push_back(d); s.indices.push_back(c);
         }
     }
     s.material = default_material();
     m.submeshes.push_back(std::move(s));
+    fit_box(m, half);
+    compute_vertex_normals(m);
+    m.uvs.assign(m.positions.size(), rt_float2{0.0f, 0.0f});
+    return m;
+}
+
+// Append a closed "swept" surface (UV-sphere topology, poles at both ends) around a spine:
+// 2 * U * (R - 1) triangles.  point(s, phi) = C(s) + r(s, phi) * (cos phi N + sin phi B).
+template <class Spine, class Radius>
+static void append_swept(Mesh& m, int U, int R, Spine spine, Radius radius) {
+    const double PI = 3.141592653589793;
+    uint32_t base = (uint32_t)m.positions.size();
+    double c[3], t[3];
+    auto frame = [&](double s, double* C, double* N, double* B) {
+        double h = 1e-4, a[3], b[3];
+        spine(s, C);
+        spine(std::min(1.0, s + h), a);
+        spine(std::max(0.0, s - h), b);
+        double T[3] = {a[0] - b[0], a[1] - b[1], a[2] - b[2]};
+        double tl = std::sqrt(T[0] * T[0] + T[1] * T[1] + T[2] * T[2]);
+        for (double& v : T) v /= tl;
+        B[0] = T[1]; B[1] = -T[0]; B[2] = 0.0;  // T x Z
+        double bl = std::sqrt(B[0] * B[0] + B[1] * B[1]);
+        B[0] /= bl; B[1] /= bl;
+        N[0] = B[1] * T[2] - B[2] * T[1];
+        N[1] = B[2] * T[0] - B[0] * T[2];
+        N[2] = B[0] * T[1] - B[1] * T[0];
+    };
+    spine(0.0, c);
+    m.positions.push_back(f3((float)c[0], (float)c[1], (float)c[2]));
+    for (int r = 1; r < R; ++r) {
+        double s = (double)r / R, C[3], N[3], B[3];
+        frame(s, C, N, B);
+        for (int u = 0; u < U; ++u) {
+            double ph = 2 * PI * u / U;
+            double rr = radius(s, ph);
+            m.positions.push_back(f3((float)(C[0] + rr * (std::cos(ph) * N[0] + std::sin(ph) * B[0])),
+                                     (float)(C[1] + rr * (std::cos(ph) * N[1] + std::sin(ph) * B[1])),
+                                     (float)(C[2] + rr * (std::cos(ph) * N[2] + std::sin(ph) * B[2]))));
+        }
+    }
+    spine(1.0, t);
+    m.positions.push_back(f3((float)t[0], (float)t[1], (float)t[2]));
+    uint32_t south = (uint32_t)m.positions.size() - 1;
+    auto& ind = m.submeshes[0].indices;
+    auto ring = [&](int r, int u) -> uint32_t { return base + 1 + (uint32_t)((r - 1) * U + (u % U)); };
+    for (int u = 0; u < U; ++u) { ind.push_back(base); ind.push_back(ring(1, u + 1)); ind.push_back(ring(1, u)); }
+    for (int r = 1; r < R - 1; ++r)
+        for (int u = 0; u < U; ++u) {
+            uint32_t a = ring(r, u), b = ring(r, u + 1), cc = ring(r + 1, u + 1), d = ring(r + 1, u);
+            ind.push_back(a); ind.push_back(b); ind.push_back(cc);
+            ind.push_back(a); ind.push_back(cc); ind.push_back(d);
+        }
+    for (int u = 0; u < U; ++u) { ind.push_back(south); ind.push_back(ring(R - 1, u)); ind.push_back(ring(R - 1, u + 1)); }
+}
+
+// Dragon stand-in: one closed, compact, detailed surface like the Stanford dragon — a curved
+// body swept along an S-shaped spine (thick middle, head bulge, thin tail) with scale-like
+// displacement, plus four legs.  Exactly 871,414 triangles (body 2*560*740 + legs
+// 3*(2*64*83) + 2*41*131); half-extents (0.45, 0.3166, 0.2) so that at the AppScene transform
+// (scale 1.2 at y = 0.38, AppScene.swift:16-21) it rests on the floor.
+static Mesh make_dragon(const double half[3]) {
+    Mesh m;
+    m.name = "dragon";
+    m.transform = m4_identity();
+    m.submeshes.emplace_back();
+    m.submeshes[0].material = default_material();
+    const double PI = 3.141592653589793;
+    auto body_spine = [&](double s, double* C) {
+        C[0] = 2.2 * (s - 0.5);
+        C[1] = 0.30 * std::sin(2 * PI * s + 0.6) + 0.25 * s;
+        C[2] = 0.22 * std::sin(PI * s) * std::sin(3 * PI * s);
+    };
+    auto body_r = [&](double s, double ph) {
+        double r = 0.34 * std::pow(std::sin(PI * s), 0.65) * (1.0 + 0.35 * std::exp(-60.0 * (s - 0.86) * (s - 0.86)));
+        r *= 1.0 + 0.05 * std::sin(90.0 * s + 7.0 * ph) * std::sin(11.0 * ph) + 0.025 * std::sin(310.0 * s) * std::cos(23.0 * ph);
+        return r;
+    };
+    append_swept(m, 560, 741, body_spine, body_r);
+    struct Leg { double s, side; int U, R; };
+    const Leg legs[4] = {{0.32, 1.0, 64, 84}, {0.32, -1.0, 64, 84}, {0.66, 1.0, 64, 84}, {0.66, -1.0, 41, 132}};
+    for (const Leg& L : legs) {
+        double C0[3];
+        body_spine(L.s, C0);
+        auto leg_spine = [&](double s, double* C) {
+            C[0] = C0[0] + 0.08 * s;
+            C[1] = C0[1] - 0.62 * s;
+            C[2] = C0[2] + L.side * (0.10 + 0.12 * s);
+        };
+        auto leg_r = [&](double s, double ph) {
+            return 0.075 * std::pow(std::sin(PI * s), 0.5) * (1.0 + 0.04 * std::sin(40.0 * s + 5.0 * ph));
+        };
+        append_swept(m, L.U, L.R, leg_spine, leg_r);
+    }
     fit_box(m, half);
     compute_vertex_normals(m);
     m.uvs.assign(m.positions.size(), rt_float2{0.0f, 0.0f});
@@ -571,9 +665,11 @@ rt_status rt_scene_add_procedural(rt_scene* s, const char* kind, const char* mtl
     for (int k = 0; k < 3; ++k) { model.position[k] = position[k]; model.rotation[k] = rotation ? rotation[k] : 0.0f; }
     model.scale = scale;
     std::string k = kind;
-    if (k == "dragon") {
+    if (k == "dragon" || k == "knot") {
         const double half[3] = {0.45, 0.3166, 0.2};
-        Mesh m = make_knot("dragon", 10627, 41, 0.42, 0.12, half);
+        // "knot": the thin-tube torus-knot variant kept as a traversal torture test (rays refracted
+        // inside a long thin glass tube visit ~1000 boxes each)
+        Mesh m = k == "dragon" ? make_dragon(half) : make_knot("knot", 10627, 41, 0.42, 0.12, half);
         // dragon.mtl: Kd 1 0 0, Ks .2, Ke 0, Ni 1, d 1 (AssetResources/dragon.mtl)
         m.submeshes[0].material.baseColor = f3(1.0f, 0.0f, 0.0f);
         m.submeshes[0].material.specular = f3(0.2f, 0.2f, 0.2f);
@@ -660,6 +756,13 @@ rt_status rt_scene_preset(const char* name_c, const char* asset_dir_c, rt_scene*
         if (!(st = hero("dragon", &glass))) st = base();
     } else if (name == "c3d") {
         if (!(st = hero("dragon", nullptr))) st = base();
+    } else if (name == "c3k") {
+        float pos[3] = {0.3f, 0.38f, 2.5f};
+        float rot[3] = {0.0f, 3.14159265358979323846f / 2.0f * 1.2f, 0.0f};
+        synth = 1;
+        std::string mtl = dir + "/dragon.mtl";
+        if (!(st = rt_scene_add_procedural(s, "knot", file_exists(mtl) ? mtl.c_str() : nullptr, pos, rot, 1.2f, &glass)))
+            st = base();
     } else if (name == "c5" || name == "app") {
         float rp[3] = {-0.5f, 0.0f, 1.0f};
         synth = 1;

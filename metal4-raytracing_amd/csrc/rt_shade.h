@@ -1,0 +1,343 @@
+// rt_shade.h — one hit-processing step of a path: everything raytracingKernel does between two
+// intersector calls (Raytracing.metal:324-774).  Shared by the per-pixel megakernel and the
+// wavefront `shade` stage so both pipelines evaluate exactly the same operation sequence.
+//
+// Given the current ray and its closest hit, shade_step updates the path registers (throughput
+// `color`, `accum`, bounce / step / transparencyPasses), optionally emits a shadow ray whose
+// contribution the caller adds to `accum` when it is unoccluded (Raytracing.metal:741-743 /
+// :667-669), and either rewrites the ray for the next iteration (next = true) or ends the path.
+#pragma once
+#include "rt_kernels.h"
+
+namespace rt {
+
+struct HaltonTab {
+    const HaltonDim* lds;
+    const HaltonDim* glob;
+    __device__ __forceinline__ float operator()(int i, int d) const {
+        return halton_fast(i, d < kHaltonLds ? lds[d] : glob[d]);
+    }
+};
+
+struct PathRegs {
+    f3 color;
+    f3 accum;
+    int bounce, step, tpass;
+};
+
+struct StepResult {
+    bool next;             // trace rayO/rayD again
+    bool shadow;           // trace shadow ray; add contrib to accum when unoccluded
+    f3 so, sd, contrib;
+    float stmax;
+    bool primary;          // bounce 0 / sample 0 hit: depth + motion (:342-389)
+    float depth;
+    f2 motion;
+    bool gbuf;             // first hit of sample 0 with the G-buffer enabled (:506-515)
+    float4 g0, g1, g2, g3;
+};
+
+__device__ __forceinline__ f3 ldf3(const rt_float3& v) { return mk3(v.x, v.y, v.z); }
+
+__host__ __device__ __forceinline__ bool needs_full(const Uniforms& U) {
+    return U.debugTextureMode != DebugTextureModeNone || U.enableDenoiseGBuffer != 0;
+}
+
+// prevMotion / hadPrimaryHit / motionVector: only read by DebugTextureModeMotion.
+// FULL = false compiles out the debug-visualisation and G-buffer branches (the caller selects
+// FULL = true whenever uniforms.debugTextureMode != 0 or enableDenoiseGBuffer != 0).
+template <bool FULL>
+__device__ __forceinline__ void shade_step(const DevScene& S, const Uniforms& U, const HaltonTab& halton, int hidx,
+                                           int sampleIndex, f3& rayO, f3& rayD, const Hit& h, PathRegs& p,
+                                           bool gbuf_pending, f2 prevMotion, bool hadPrimaryHit, f2 motionVector,
+                                           StepResult& r) {
+    r.next = false;
+    r.shadow = false;
+    r.primary = false;
+    r.gbuf = false;
+    uint4 ti = S.tri_info[h.id];
+    int instanceIndex = (int)(ti.w >> 8);
+    int geometryIndex = (int)(ti.w & 0xffu);
+    const float* M = S.inst + 12 * instanceIndex;                                       // :329-333
+    f3 P_ = rayO + rayD * h.t;                                                          // :336
+    const Material& mat = S.materials[instanceIndex * S.max_submeshes + geometryIndex]; // :337-339
+    float bu = h.u, bv = h.v, bw = (1.0f - bu) - bv;                                    // :63-65
+    const Camera& cam = U.camera;
+    f3 cright = ldf3(cam.right), cup = ldf3(cam.up), cfwd = ldf3(cam.forward);
+
+    if (p.bounce == 0 && sampleIndex == 0) {                                            // :342-389
+        f3 op = (bu * ld3(S.pos[ti.y]) + bv * ld3(S.pos[ti.z])) + bw * ld3(S.pos[ti.x]);
+        f3 pp = (bu * ld3(S.prev_pos[ti.y]) + bv * ld3(S.prev_pos[ti.z])) + bw * ld3(S.prev_pos[ti.x]);
+        f3 worldPos = xform(M, op, 1.0f);
+        f3 prevWorldPos = xform(S.prev_inst + 12 * instanceIndex, pp, 1.0f);
+        f3 viewPos = worldPos - ldf3(cam.position);
+        float sx = dot(viewPos, cright), sy = dot(viewPos, cup);
+        float depth = dot(viewPos, cfwd);
+        r.depth = fmaxf(depth, 1.0e-3f);
+        float dd = fmaxf(depth, 0.001f);
+        sx = sx / dd;
+        sy = sy / dd;
+        const Camera& pc = U.previousCamera;
+        f3 pv = prevWorldPos - ldf3(pc.position);
+        float psx = dot(pv, ldf3(pc.right)), psy = dot(pv, ldf3(pc.up));
+        float pd = fmaxf(dot(pv, ldf3(pc.forward)), 0.001f);
+        psx = psx / pd;
+        psy = psy / pd;
+        float mnx = sx - psx, mny = sy - psy;
+        float rightScale = fmaxf(length(cright), 1e-5f);
+        float upScale = fmaxf(length(cup), 1e-5f);
+        float mpx = mnx * ((float)U.width / (2.0f * rightScale));
+        float mpy = mny * ((float)U.height / (2.0f * upScale));
+        r.motion.x = mpx;
+        r.motion.y = -mpy;
+        r.primary = true;
+    }
+
+    f3 objN = (bu * ld3(S.nrm[ti.y]) + bv * ld3(S.nrm[ti.z])) + bw * ld3(S.nrm[ti.x]); // :391
+    f3 Ng = normalize(xform(M, objN, 0.0f));                                          // :392-393
+    if (length(objN) < 1e-10f) Ng = -rayD;                                            // :395-397
+
+    f3 albedo = ldf3(mat.baseColor);                                                  // :399
+    // textureFlags == 0 for every uploaded material (rt_scene_upload rejects others)
+    const float roughness = 1.0f, metallic = 0.0f, ao = 1.0f;                         // :431-446
+    float opacity = clampf(mat.opacity, 0.0f, 1.0f);                                  // :448
+    f3 emission = ldf3(mat.emission);                                                 // :453
+
+    if (FULL && U.debugTextureMode != DebugTextureModeNone) {                         // :459-490
+        f3 dc = mk3(0.0f, 0.0f, 0.0f);
+        int m = U.debugTextureMode;
+        if (m == DebugTextureModeBaseColor) dc = mk3(1.0f, 0.0f, 1.0f);
+        else if (m == DebugTextureModeNormal) dc = Ng * 0.5f + mk3(0.5f, 0.5f, 0.5f);
+        else if (m == DebugTextureModeRoughness) dc = mk3(roughness, roughness, roughness);
+        else if (m == DebugTextureModeMetallic) dc = mk3(metallic, metallic, metallic);
+        else if (m == DebugTextureModeAO) dc = mk3(1.0f, 0.0f, 1.0f);
+        else if (m == DebugTextureModeEmission) dc = emission;
+        else if (m == DebugTextureModeMotion) {
+            f2 mp = r.primary ? r.motion : (hadPrimaryHit ? motionVector : prevMotion);
+            float scx = clampf(mp.x * 0.05f, -1.0f, 1.0f), scy = clampf(mp.y * 0.05f, -1.0f, 1.0f);
+            float mag = clampf(sqrtf(mp.x * mp.x + mp.y * mp.y) * 0.1f, 0.0f, 1.0f);
+            dc = mk3(scx * 0.5f + 0.5f, scy * 0.5f + 0.5f, mag);
+        }
+        p.accum = dc;
+        return;  // break
+    }
+
+    f3 shadingNormal = Ng;                                                            // :492 (no normal map)
+
+    if (FULL && gbuf_pending && U.enableDenoiseGBuffer != 0 && sampleIndex == 0) {   // :506-515
+        float rr = clampf(roughness, 0.0f, 1.0f);
+        f3 da = albedo * (1.0f - metallic);
+        f3 sa = mix3(mk3(0.04f, 0.04f, 0.04f), albedo, metallic);
+        f3 on = shadingNormal * 0.5f + mk3(0.5f, 0.5f, 0.5f);
+        r.g0 = make_float4(da.x, da.y, da.z, 1.0f);
+        r.g1 = make_float4(sa.x, sa.y, sa.z, 1.0f);
+        r.g2 = make_float4(on.x, on.y, on.z, 1.0f);
+        r.g3 = make_float4(rr, 0.0f, 0.0f, 1.0f);
+        r.gbuf = true;
+    }
+
+    float clampedOpacity = clampf(opacity, 0.0f, 1.0f);                              // :517-576
+    float ior = fmaxf(mat.refractionIndex, 1.0f);
+    if (clampedOpacity < 0.999f || ior > 1.01f) {
+        f3 N = shadingNormal, I = rayD;
+        float cosi = clampf(dot(-I, N), -1.0f, 1.0f);
+        float etaI = 1.0f, etaT = ior;
+        if (cosi < 0.0f) {
+            cosi = -cosi;
+            N = -N;
+            float tmp = etaI;
+            etaI = etaT;
+            etaT = tmp;
+        }
+        float eta = etaI / etaT;
+        float k = 1.0f - (eta * eta) * (1.0f - cosi * cosi);
+        float f0 = (etaT - etaI) / (etaT + etaI);
+        f0 = f0 * f0;
+        float F = f0 + (1.0f - f0) * pow5(clampf(1.0f - cosi, 0.0f, 1.0f));
+        float transmission = 1.0f - clampedOpacity;
+        float reflectWeight = F;
+        float refractWeight = (1.0f - F) * transmission;
+        float totalWeight = fmaxf(reflectWeight + refractWeight, 1e-4f);
+        float reflectProb = reflectWeight / totalWeight;
+        float choice = halton(hidx, 2 + p.step * 6 + 5);
+        bool consumeBounce = true;
+        if (k < 0.0f || choice < reflectProb) {
+            f3 reflectDir = normalize(I - (2.0f * dot(I, N)) * N);
+            rayO = P_ + reflectDir * 1e-3f;
+            rayD = reflectDir;
+            p.color = p.color * totalWeight;
+        } else {
+            float cosT = sqrtf(fmaxf(k, 0.0f));
+            f3 refractDir = normalize(eta * I + (eta * cosi - cosT) * N);
+            rayO = P_ + refractDir * 1e-3f;
+            rayD = refractDir;
+            p.color = p.color * (totalWeight * albedo);
+            consumeBounce = false;
+        }
+        p.step++;
+        if (consumeBounce) {
+            p.bounce++;
+            p.tpass = 0;
+        } else {
+            p.tpass++;
+            if (p.tpass > U.maxBounces) {
+                p.bounce++;
+                p.tpass = 0;
+            }
+        }
+        r.next = p.bounce < U.maxBounces;
+        return;
+    }
+
+    float perceptualRoughness = clampf(roughness, 0.04f, 1.0f);                       // :578-582
+    float alpha = perceptualRoughness * perceptualRoughness;
+    f3 diffuseColor = albedo;
+    f3 F0 = mix3(mk3(0.04f, 0.04f, 0.04f), albedo, metallic);
+    f3 V = normalize(-rayD);
+
+    p.accum = p.accum + p.color * emission;                                           // :585
+
+    float lightSample = halton(hidx, 2 + p.step * 6 + 0);                             // :588-591
+    int lightIndex = min((int)(lightSample * (float)U.lightCount), U.lightCount - 1);
+    const Light& light = S.lights[lightIndex];
+    f3 Ldir, lightColor;
+    float lightDistance;
+    f3 lpos = ldf3(light.position), lcol = ldf3(light.color);
+    if (light.type == LightTypeAreaLight) {                                           // :597-606, :95-129
+        float ux = halton(hidx, 2 + p.step * 6 + 1), uy = halton(hidx, 2 + p.step * 6 + 2);
+        ux = ux * 2.0f - 1.0f;
+        uy = uy * 2.0f - 1.0f;
+        f3 sp = (lpos + ldf3(light.right) * ux) + ldf3(light.up) * uy;
+        Ldir = sp - P_;
+        lightDistance = length(Ldir);
+        float inv = 1.0f / fmaxf(lightDistance, 1e-3f);
+        Ldir = Ldir * inv;
+        lightColor = lcol * (inv * inv);
+        lightColor = lightColor * saturate(dot(-Ldir, ldf3(light.forward)));
+    } else if (light.type == LightTypeSpotlight) {                                    // :608-632
+        Ldir = lpos - P_;
+        lightDistance = length(Ldir);
+        float inv = 1.0f / fmaxf(lightDistance, 1e-3f);
+        Ldir = Ldir * inv;
+        lightColor = mk3(0.0f, 0.0f, 0.0f);
+        f3 coneDirection = normalize(ldf3(light.direction));
+        float spotResult = dot(-Ldir, coneDirection);
+        if (spotResult > cos_pinned(light.coneAngle)) lightColor = (lcol * inv) * inv;
+    } else if (light.type == LightTypePointlight) {                                   // :633-638
+        Ldir = lpos - P_;
+        lightDistance = length(Ldir);
+        float inv = 1.0f / fmaxf(lightDistance, 1e-3f);
+        Ldir = Ldir * inv;
+        lightColor = (lcol * inv) * inv;
+    } else {                                                                          // :639-643
+        Ldir = -normalize(ldf3(light.direction));
+        lightDistance = INFINITY;
+        lightColor = lcol;
+    }
+    lightColor = lightColor * (float)U.lightCount;                                    // :647
+    f3 origin = P_ + Ng * 1e-3f;                                                      // :660, :683, :720, :769
+
+    if (U.shadingMode == ShadingModeLegacy) {                                         // :649-690
+        f3 L = normalize(Ldir);
+        float NdotL = saturate(dot(shadingNormal, L));
+        f3 legacyColor = p.color * albedo;
+        if (length(legacyColor) < 0.001f) return;
+        if (length(lightColor) > 0.0001f && NdotL > 0.0f) {
+            r.shadow = true;
+            r.so = origin;
+            r.sd = Ldir;
+            r.stmax = lightDistance - 1e-3f;
+            r.contrib = (legacyColor * lightColor) * NdotL;
+        }
+        p.color = legacyColor * ao;
+        if (length(p.color) < 0.001f) return;
+        float r0 = halton(hidx, 2 + p.step * 5 + 3), r1 = halton(hidx, 2 + p.step * 5 + 4);
+        rayD = alignHemisphereWithNormal(sampleCosineWeightedHemisphere(r0, r1), shadingNormal);
+        rayO = origin;
+        p.step++;
+        p.bounce++;
+        p.tpass = 0;
+        r.next = p.bounce < U.maxBounces;
+        return;
+    }
+
+    if (length(lightColor) > 0.0001f) {                                               // :692-744
+        f3 L = normalize(Ldir);
+        f3 H = normalize(V + L);
+        float NdotL = saturate(dot(shadingNormal, L));
+        float NdotV = saturate(dot(shadingNormal, V));
+        float NdotH = saturate(dot(shadingNormal, H));
+        float VdotH = saturate(dot(V, H));
+        f3 F = fresnelSchlick(VdotH, F0);
+        float D = distributionGGX(NdotH, alpha);
+        float kk = perceptualRoughness + 1.0f;
+        kk = (kk * kk) / 8.0f;
+        float G = geometrySmith(NdotV, NdotL, kk);
+        f3 specular = ((D * G) * F) / fmaxf((4.0f * NdotV) * NdotL, 1e-4f);
+        f3 kD = (mk3(1.0f, 1.0f, 1.0f) - F) * (1.0f - metallic);
+        f3 diffuse = (kD * diffuseColor) / RT_PI;
+        f3 direct = ((diffuse + specular) * lightColor) * NdotL;
+        r.shadow = true;
+        r.so = origin;
+        r.sd = Ldir;
+        r.stmax = lightDistance - 1e-3f;
+        r.contrib = p.color * direct;
+    }
+
+    p.color = p.color * ((diffuseColor * (1.0f - metallic)) * ao);                    // :748
+    if (length(p.color) < 0.001f) return;                                             // :751-753
+    float r0 = halton(hidx, 2 + p.step * 5 + 3), r1 = halton(hidx, 2 + p.step * 5 + 4);  // :763-764
+    rayD = alignHemisphereWithNormal(sampleCosineWeightedHemisphere(r0, r1), shadingNormal);
+    rayO = origin;                                                                    // :769-770
+    p.step++;
+    p.bounce++;
+    p.tpass = 0;
+    r.next = p.bounce < U.maxBounces;
+}
+
+// Primary ray for (pixel, sample) (Raytracing.metal:270-292).
+__device__ __forceinline__ void primary_ray(const Uniforms& U, const HaltonTab& halton, int px, int py, int hidx,
+                                            f3& o, f3& d) {
+    float rx = halton(hidx, 0), ry = halton(hidx, 1);
+    float spx = (float)px + rx, spy = (float)py + ry;
+    float uvx = spx / (float)U.width, uvy = spy / (float)U.height;
+    uvx = uvx * 2.0f - 1.0f;
+    uvy = uvy * 2.0f - 1.0f;
+    const Camera& cam = U.camera;
+    o = ldf3(cam.position);
+    d = normalize((uvx * ldf3(cam.right) + uvy * ldf3(cam.up)) + ldf3(cam.forward));
+}
+
+// Motion-adaptive extra samples after sample 0 (Raytracing.metal:779-789).
+__device__ __forceinline__ int extra_samples(const Uniforms& U, int maxExtra, f2 mv, f2 pm) {
+    float motionMag = fmaxf(sqrtf(mv.x * mv.x + mv.y * mv.y), sqrtf(pm.x * pm.x + pm.y * pm.y));
+    float low = fmaxf(U.motionSamplingLowThresholdPixels, 0.0f);
+    float high = fmaxf(U.motionSamplingHighThresholdPixels, low + 1e-3f);
+    float t = clampf((motionMag - low) / (high - low), 0.0f, 1.0f);
+    int e = (int)roundf(t * (float)maxExtra);
+    return min(max(e, 0), maxExtra);
+}
+
+// Average + temporal EMA (Raytracing.metal:792-817).
+__device__ __forceinline__ f3 resolve_pixel(const Uniforms& U, f3 total, int totalSamples, f2 mv, f2 pm,
+                                            const float4* accum_in, size_t pix) {
+    total = total / (float)max(totalSamples, 1);
+    if (U.frameIndex > 0) {
+        float4 pc = accum_in[pix];
+        f3 prevColor = mk3(pc.x, pc.y, pc.z);
+        float historyWeight = clampf(U.accumulationWeight, 0.0f, 0.95f);
+        if (U.enableMotionAdaptiveAccumulation != 0) {
+            float motionMag = fmaxf(sqrtf(mv.x * mv.x + mv.y * mv.y), sqrtf(pm.x * pm.x + pm.y * pm.y));
+            float low = fmaxf(U.motionAccumulationLowThresholdPixels, 0.0f);
+            float high = fmaxf(U.motionAccumulationHighThresholdPixels, low + 1e-3f);
+            float t = clampf((motionMag - low) / (high - low), 0.0f, 1.0f);
+            float minWeight = clampf(U.motionAccumulationMinWeight, 0.0f, 0.95f);
+            minWeight = fminf(minWeight, historyWeight);
+            historyWeight = mixf(historyWeight, minWeight, t);
+        }
+        total = mix3(total, prevColor, historyWeight);
+    }
+    return total;
+}
+
+}  // namespace rt

@@ -1,0 +1,812 @@
+// rt_wavefront.hip — wavefront path tracer for gfx950.
+//
+// The per-pixel loop of raytracingKernel (Raytracing.metal:269-790) is split into stages over
+// SoA path state and compacted queues, so every wave64 works on live paths only:
+//   generate  one thread per (own pixel, sample): primary ray (:270-292) -> ray queue
+//   extend    closest-hit traversal of the ray queue (:314-322)          -> hit records
+//   shade     shade_step per hit (:324-774): updates path state, appends the continuation
+//             ray to the next queue and the NEE shadow ray to the shadow queue
+//   connect   any-hit traversal of the shadow queue (:716-743); unoccluded -> accum += contrib
+//   finish    once fewer than kTailRays paths are alive, one launch runs every remaining path
+//             to completion (trace -> shade -> shadow per thread): the long glass-path tail
+//             costs the longest remaining path instead of one launch per bounce
+//   [extra]   motion-adaptive extra samples (:779-789) as a second generate/iterate pass
+//   resolve   per pixel: sum samples in sample order, average, temporal EMA (:777, :792-819)
+//
+// Queues are split into kShards segments; a block appends to segment blockIdx % 8 with ONE
+// returning atomic per 256 entries (wave ballot + LDS prefix), so no counter word sees more
+// than ~1/2048 of the entries (one word serialises at ~88 atomics/us, MI355X_MICROARCH.md
+// 'dequeue').  Grids are multiples of 8, so segment k only receives chunks c == k (mod 8) and
+// a segment of n/8 + 4096 entries can never overflow.
+//
+// Results are bit-identical to the megakernel: per-path arithmetic is the same shade_step,
+// the accumulation order per path is the reference's (emission of step s, then its shadow
+// contribution, then step s+1), and samples are summed per pixel in sample order.
+#include "rt_shade.h"
+
+namespace rt {
+
+namespace {
+
+constexpr uint32_t kTailRays = 32768;
+
+__device__ __forceinline__ uint32_t lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
+__device__ __forceinline__ uint32_t mbcnt64(unsigned long long m) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+struct BlockAlloc {
+    uint32_t w[kBlock / 64];
+};
+
+// Block-aggregated slot allocation; every thread of the block calls it (converged loop).
+__device__ __forceinline__ uint32_t block_alloc(bool pred, uint32_t* counter, BlockAlloc& sh) {
+    const int wave = threadIdx.x >> 6;
+    unsigned long long m = __ballot(pred);
+    uint32_t prefix = mbcnt64(m);
+    if (lane_id() == 0) sh.w[wave] = (uint32_t)__popcll(m);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t c0 = sh.w[0], c1 = sh.w[1], c2 = sh.w[2], c3 = sh.w[3];
+        uint32_t tot = c0 + c1 + c2 + c3;
+        uint32_t b = tot ? atomicAdd(counter, tot) : 0u;
+        sh.w[0] = b;
+        sh.w[1] = b + c0;
+        sh.w[2] = b + c0 + c1;
+        sh.w[3] = b + c0 + c1 + c2;
+    }
+    __syncthreads();
+    uint32_t r = sh.w[wave] + prefix;
+    __syncthreads();
+    return r;
+}
+
+__device__ __forceinline__ uint32_t compact1by1(uint32_t x) {
+    x &= 0x55555555u;
+    x = (x | (x >> 1)) & 0x33333333u;
+    x = (x | (x >> 2)) & 0x0f0f0f0fu;
+    x = (x | (x >> 4)) & 0x00ff00ffu;
+    x = (x | (x >> 8)) & 0x0000ffffu;
+    return x;
+}
+
+// own pixel index -> image coordinates (tiles tile_id % nranks == rank, Morton order in a tile)
+__device__ __forceinline__ void own_pixel(const FrameParams& P, uint32_t i, int& px, int& py) {
+    const uint32_t T = (uint32_t)P.tile_size, per = T * T;
+    uint32_t k = i / per, r = i % per;
+    int tid = P.rank + (int)k * P.nranks;
+    int tx = tid % P.tiles_x, ty = tid / P.tiles_x;
+    uint32_t lx, ly;
+    if ((T & (T - 1)) == 0) {
+        lx = compact1by1(r);
+        ly = compact1by1(r >> 1);
+    } else {
+        lx = r % T;
+        ly = r / T;
+    }
+    px = tx * (int)T + (int)lx;
+    py = ty * (int)T + (int)ly;
+}
+
+__device__ __forceinline__ uint32_t pack_state(int bounce, int tpass, int step) {
+    return (uint32_t)bounce | ((uint32_t)tpass << 8) | ((uint32_t)step << 16);
+}
+
+struct WfParams {
+    WavefrontBuffers W;
+    uint32_t base_paths;   // own pixels * spp
+    uint32_t own_pixels;
+    uint32_t seg_cap;      // entries per queue segment
+    int spp;
+};
+
+// counts layout: [q*8 + shard] ray queues q = 0, 1; [16 + shard] shadow queue; [24] extra allocator
+constexpr int kCntShadowQ = 16;
+constexpr int kCntExtra = 24;
+
+// dense consumer index g -> entry index of a sharded queue
+__device__ __forceinline__ uint32_t entry_of(const uint32_t* cnt, uint32_t g, uint32_t seg_cap) {
+    uint32_t acc = 0;
+    #pragma unroll
+    for (int k = 0; k < kShards; ++k) {
+        uint32_t c = cnt[k];
+        if (g < acc + c) return (uint32_t)k * seg_cap + (g - acc);
+        acc += c;
+    }
+    return 0xffffffffu;
+}
+
+__device__ __forceinline__ void init_path(const WfParams& Q, uint32_t pid, uint32_t pix, int sample, uint32_t hidx) {
+    Q.W.p_color[pid] = make_float4(1.0f, 1.0f, 1.0f, 0.0f);
+    Q.W.p_accum[pid] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    Q.W.p_meta[pid] = make_uint4(pix, (uint32_t)sample, 0u, hidx);
+}
+
+__device__ __forceinline__ void load_halton(const DevScene& S, HaltonDim* lds) {
+    for (int i = threadIdx.x; i < kHaltonLds; i += kBlock) lds[i] = S.halton[i];
+    __syncthreads();
+}
+
+__device__ __forceinline__ void flush_counters(const FrameParams& P, uint32_t closest, uint32_t shadow, uint32_t paths,
+                                               const TraceCounters& tc, bool count, bool overflow) {
+    unsigned long long c0 = wave_sum(closest), c1 = wave_sum(shadow), c4 = wave_sum(paths);
+    unsigned long long c2 = count ? wave_sum(tc.nodes) : 0ull, c3 = count ? wave_sum(tc.tris) : 0ull;
+    bool of = __ballot(overflow) != 0ull;
+    if (lane_id() == 0) {
+        if (c0) atomicAdd(&P.counters[kCntClosest], c0);
+        if (c1) atomicAdd(&P.counters[kCntShadow], c1);
+        if (c4) atomicAdd(&P.counters[kCntPaths], c4);
+        if (count) {
+            atomicAdd(&P.counters[kCntNodes], c2);
+            atomicAdd(&P.counters[kCntTris], c3);
+        }
+        if (of) atomicAdd(&P.counters[kCntOverflow], 1ull);
+    }
+}
+
+// per-pixel outputs of a shade step (depth / motion / G-buffer, :342-389, :506-515)
+__device__ __forceinline__ void write_pixel_outputs(const FrameParams& P, uint32_t pix, const StepResult& r, bool full) {
+    if (r.primary) {
+        P.depth[pix] = r.depth;
+        P.motion[pix] = make_float2(r.motion.x, r.motion.y);
+    }
+    if (full && r.gbuf && P.gbuffer) {
+        size_t plane = (size_t)P.U.width * P.U.height;
+        P.gbuffer[pix] = r.g0;
+        P.gbuffer[plane + pix] = r.g1;
+        P.gbuffer[2 * plane + pix] = r.g2;
+        P.gbuffer[3 * plane + pix] = r.g3;
+    }
+}
+
+}  // namespace
+
+// ---- generate -------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(kBlock) wf_generate(DevScene S, FrameParams P, WfParams Q) {
+    __shared__ HaltonDim lds_halton[kHaltonLds];
+    __shared__ BlockAlloc ba;
+    load_halton(S, lds_halton);
+    const HaltonTab halton{lds_halton, S.halton};
+    const Uniforms& U = P.U;
+    const int spp = Q.spp;
+    const int maxExtra = (U.enableMotionAdaptiveSampling != 0) ? max(U.motionSamplingMaxExtraSamples, 0) : 0;
+    const int stride = spp + maxExtra;
+    const int shard = blockIdx.x & (kShards - 1);
+    float4* qout = Q.W.q[0] + 2 * (size_t)shard * Q.seg_cap;
+    uint32_t n_paths = 0;
+    const uint32_t total = Q.base_paths;
+    for (uint32_t base = blockIdx.x * kBlock; base < total; base += gridDim.x * kBlock) {
+        uint32_t pid = base + threadIdx.x;
+        bool valid = pid < total;
+        int px = 0, py = 0, s = 0;
+        uint32_t pix = 0;
+        if (valid) {
+            s = (int)(pid % (uint32_t)spp);
+            own_pixel(P, pid / (uint32_t)spp, px, py);
+            valid = px < U.width && py < U.height;
+            pix = (uint32_t)py * (uint32_t)U.width + (uint32_t)px;
+        }
+        f3 o = mk3(0, 0, 0), d = mk3(0, 0, 0);
+        if (valid) {
+            uint32_t offset = P.random[pix];
+            int frameOffset = (int)U.frameIndex * stride + s;
+            int hidx = (int)(offset + (unsigned)frameOffset);
+            init_path(Q, pid, pix, s, (uint32_t)hidx);
+            primary_ray(U, halton, px, py, hidx, o, d);
+            if (s == 0) {  // per-pixel defaults (:252-261)
+                P.depth[pix] = 1.0e8f;
+                P.motion[pix] = make_float2(0.0f, 0.0f);
+                if (P.gbuffer) {
+                    size_t plane = (size_t)U.width * U.height;
+                    float4 z = make_float4(0, 0, 0, 0);
+                    P.gbuffer[pix] = z;
+                    P.gbuffer[plane + pix] = z;
+                    P.gbuffer[2 * plane + pix] = z;
+                    P.gbuffer[3 * plane + pix] = z;
+                }
+            }
+            n_paths++;
+        }
+        bool live = valid && U.maxBounces > 0;
+        uint32_t slot = block_alloc(live, &Q.W.counts[shard], ba);
+        if (live) {
+            qout[2 * slot] = make_float4(o.x, o.y, o.z, __uint_as_float(pid));
+            qout[2 * slot + 1] = make_float4(d.x, d.y, d.z, 0.0f);
+        }
+    }
+    TraceCounters tc{0, 0};
+    flush_counters(P, 0, 0, n_paths, tc, false, false);
+}
+
+// ---- extend: closest hit ----------------------------------------------------------------------------
+template <bool COUNT>
+__global__ void __launch_bounds__(kBlock) wf_extend(DevScene S, FrameParams P, WfParams Q, int cur, uint32_t n) {
+    __shared__ int lds_stack[kStackSize * kBlock];
+    const int next = 1 - cur;
+    if (blockIdx.x == 0 && threadIdx.x < 2 * kShards) {  // reset the queues shade / connect fill
+        uint32_t k = threadIdx.x & (kShards - 1);
+        Q.W.counts[threadIdx.x < kShards ? next * kShards + k : kCntShadowQ + k] = 0;
+    }
+    const uint32_t* cnt = Q.W.counts + cur * kShards;
+    const float4* qin = Q.W.q[cur];
+    int* stack = &lds_stack[threadIdx.x];
+    TraceCounters tc{0, 0};
+    bool overflow = false;
+    uint32_t rays = 0;
+    for (uint32_t base = blockIdx.x * kBlock; base < n; base += gridDim.x * kBlock) {
+        uint32_t g = base + threadIdx.x;
+        if (g < n) {
+            uint32_t e = entry_of(cnt, g, Q.seg_cap);
+            float4 o = qin[2 * (size_t)e], d = qin[2 * (size_t)e + 1];
+            Hit h;
+            trace<false, COUNT>(S, ld3(o), ld3(d), 0.0f, INFINITY, h, stack, tc, overflow);
+            Q.W.hits[e] = make_float4(h.t, __uint_as_float(h.id), h.u, h.v);
+            rays++;
+        }
+    }
+    flush_counters(P, rays, 0, 0, tc, COUNT, overflow);
+}
+
+// ---- shade -------------------------------------------------------------------------------------------
+template <bool FULL>
+__global__ void __launch_bounds__(kBlock) wf_shade(DevScene S, FrameParams P, WfParams Q, int cur, uint32_t n) {
+    __shared__ HaltonDim lds_halton[kHaltonLds];
+    __shared__ BlockAlloc ba_ray, ba_sh;
+    load_halton(S, lds_halton);
+    const HaltonTab halton{lds_halton, S.halton};
+    const Uniforms& U = P.U;
+    const int next = 1 - cur;
+    const int shard = blockIdx.x & (kShards - 1);
+    const uint32_t* cnt = Q.W.counts + cur * kShards;
+    const float4* qin = Q.W.q[cur];
+    float4* qout = Q.W.q[next] + 2 * (size_t)shard * Q.seg_cap;
+    float4* sqout = Q.W.sq + 3 * (size_t)shard * Q.seg_cap;
+    f2 zero2;
+    zero2.x = 0.0f;
+    zero2.y = 0.0f;
+    for (uint32_t base = blockIdx.x * kBlock; base < n; base += gridDim.x * kBlock) {
+        uint32_t g = base + threadIdx.x;
+        StepResult r;
+        r.next = false;
+        r.shadow = false;
+        uint32_t pid = 0;
+        f3 rayO = mk3(0, 0, 0), rayD = mk3(0, 0, 0);
+        if (g < n) {
+            uint32_t e = entry_of(cnt, g, Q.seg_cap);
+            float4 o = qin[2 * (size_t)e], d = qin[2 * (size_t)e + 1];
+            float4 hv = Q.W.hits[e];
+            pid = __float_as_uint(o.w);
+            Hit h;
+            h.t = hv.x;
+            h.id = __float_as_uint(hv.y);
+            h.u = hv.z;
+            h.v = hv.w;
+            if (h.id != 0xffffffffu) {                                           // miss -> path ends (:321-322)
+                uint4 meta = Q.W.p_meta[pid];
+                float4 c = Q.W.p_color[pid], a = Q.W.p_accum[pid];
+                PathRegs p;
+                p.color = mk3(c.x, c.y, c.z);
+                p.accum = mk3(a.x, a.y, a.z);
+                p.bounce = (int)(meta.z & 0xffu);
+                p.tpass = (int)((meta.z >> 8) & 0xffu);
+                p.step = (int)(meta.z >> 16);
+                int sample = (int)meta.y;
+                rayO = ld3(o);
+                rayD = ld3(d);
+                shade_step<FULL>(S, U, halton, (int)meta.w, sample, rayO, rayD, h, p, sample == 0 && p.step == 0,
+                                 zero2, false, zero2, r);
+                write_pixel_outputs(P, meta.x, r, FULL);
+                if (r.next) Q.W.p_color[pid] = make_float4(p.color.x, p.color.y, p.color.z, 0.0f);
+                Q.W.p_accum[pid] = make_float4(p.accum.x, p.accum.y, p.accum.z, 0.0f);
+                if (r.next) Q.W.p_meta[pid] = make_uint4(meta.x, meta.y, pack_state(p.bounce, p.tpass, p.step), meta.w);
+            }
+        }
+        uint32_t ns = block_alloc(r.shadow, &Q.W.counts[kCntShadowQ + shard], ba_sh);
+        if (r.shadow) {
+            sqout[3 * (size_t)ns] = make_float4(r.so.x, r.so.y, r.so.z, __uint_as_float(pid));
+            sqout[3 * (size_t)ns + 1] = make_float4(r.sd.x, r.sd.y, r.sd.z, r.stmax);
+            sqout[3 * (size_t)ns + 2] = make_float4(r.contrib.x, r.contrib.y, r.contrib.z, 0.0f);
+        }
+        uint32_t nr = block_alloc(r.next, &Q.W.counts[next * kShards + shard], ba_ray);
+        if (r.next) {
+            qout[2 * (size_t)nr] = make_float4(rayO.x, rayO.y, rayO.z, __uint_as_float(pid));
+            qout[2 * (size_t)nr + 1] = make_float4(rayD.x, rayD.y, rayD.z, 0.0f);
+        }
+    }
+}
+
+// ---- connect: any-hit shadow rays --------------------------------------------------------------------
+template <bool COUNT>
+__global__ void __launch_bounds__(kBlock) wf_connect(DevScene S, FrameParams P, WfParams Q) {
+    __shared__ int lds_stack[kStackSize * kBlock];
+    int* stack = &lds_stack[threadIdx.x];
+    const uint32_t* cnt = Q.W.counts + kCntShadowQ;
+    uint32_t n = 0;
+    #pragma unroll
+    for (int k = 0; k < kShards; ++k) n += cnt[k];
+    TraceCounters tc{0, 0};
+    bool overflow = false;
+    uint32_t rays = 0;
+    for (uint32_t base = blockIdx.x * kBlock; base < n; base += gridDim.x * kBlock) {
+        uint32_t g = base + threadIdx.x;
+        if (g < n) {
+            uint32_t e = entry_of(cnt, g, Q.seg_cap);
+            float4 o = Q.W.sq[3 * (size_t)e], d = Q.W.sq[3 * (size_t)e + 1];
+            Hit h;
+            rays++;
+            if (!trace<true, COUNT>(S, ld3(o), ld3(d), 0.0f, d.w, h, stack, tc, overflow)) {
+                uint32_t pid = __float_as_uint(o.w);
+                float4 c = Q.W.sq[3 * (size_t)e + 2];
+                float4 a = Q.W.p_accum[pid];
+                Q.W.p_accum[pid] = make_float4(a.x + c.x, a.y + c.y, a.z + c.z, 0.0f);
+            }
+        }
+    }
+    flush_counters(P, 0, rays, 0, tc, COUNT, overflow);
+}
+
+// ---- persistent traversal with per-lane refill (extend: ANY = false, connect: ANY = true) -----------
+// Each wave owns a static contiguous range of the queue and keeps all 64 lanes busy: a lane whose
+// ray is finished takes the next ray of the range at the top of the next iteration, and every
+// iteration advances each lane by exactly one unit of work — one node (two slab tests) or one
+// triangle.  The wave therefore runs ~(total units of its rays)/64 iterations instead of
+// (slowest ray) x (rays per lane) — the divergence cost PMC showed for the one-ray-per-thread
+// loop (SQ_WAIT_ANY 63 %, ~10x more iterations than the mean ray needs).
+// Stack items: node index >= 0, or a leaf range encoded as -1 - (first << 3 | count).
+__device__ __forceinline__ int leaf_item(int child, int count) { return -1 - ((((~child)) << 3) | count); }
+
+template <bool ANY, bool COUNT>
+__global__ void __launch_bounds__(kBlock) wf_trace(DevScene S, FrameParams P, WfParams Q, int cur, uint32_t n_host) {
+    __shared__ int lds_stack[kStackSize * kBlock];
+    int* stack = &lds_stack[threadIdx.x];
+    const uint32_t* cnt = ANY ? Q.W.counts + kCntShadowQ : Q.W.counts + cur * kShards;
+    uint32_t n = n_host;
+    if (ANY) {
+        n = 0;
+        #pragma unroll
+        for (int k = 0; k < kShards; ++k) n += cnt[k];
+    } else if (blockIdx.x == 0 && threadIdx.x < 2 * kShards) {  // reset the queues shade / connect fill
+        const int next = 1 - cur;
+        uint32_t k = threadIdx.x & (kShards - 1);
+        Q.W.counts[threadIdx.x < kShards ? next * kShards + k : kCntShadowQ + k] = 0;
+    }
+    const float4* qin = ANY ? Q.W.sq : Q.W.q[cur];
+    const int qstride = ANY ? 3 : 2;
+    // static wave ranges, contiguous per XCD (blocks b and b+8 share an XCD)
+    const uint32_t nb = gridDim.x, per = nb / 8;
+    uint32_t b = blockIdx.x;
+    if (b < per * 8) b = (b & 7) * per + (b >> 3);
+    const uint32_t waves = nb * (kBlock / 64);
+    const uint32_t wv = b * (kBlock / 64) + (threadIdx.x >> 6);
+    const uint32_t wbeg = (uint32_t)(((uint64_t)n * wv) / waves);
+    const uint32_t wend = (uint32_t)(((uint64_t)n * (wv + 1)) / waves);
+    uint32_t wnext = wbeg;
+
+    TraceCounters tc{0, 0};
+    bool overflow = false;
+    uint32_t rays = 0;
+    bool active = false;
+    uint32_t e = 0;
+    f3 o = mk3(0, 0, 0), d = mk3(0, 0, 0);
+    RayPre pre;
+    pre.kx = pre.ky = pre.kz = 0;
+    pre.Sx = pre.Sy = pre.Sz = 0.0f;
+    float ix = 0, iy = 0, iz = 0, ox = 0, oy = 0, oz = 0;
+    float best = 0.0f, bu = 0.0f, bv = 0.0f;
+    uint32_t best_id = 0xffffffffu;
+    int node = 0, sp = 0, tri = 0, tri_end = 0;
+    bool hit_any = false;
+
+    while (true) {
+        // refill idle lanes from the wave's range
+        unsigned long long idle = __ballot(!active);
+        if (idle != 0ull && wnext < wend) {
+            if (!active) {
+                uint32_t g = wnext + mbcnt64(idle);
+                if (g < wend) {
+                    e = entry_of(cnt, g, Q.seg_cap);
+                    float4 o4 = qin[(size_t)qstride * e], d4 = qin[(size_t)qstride * e + 1];
+                    o = ld3(o4);
+                    d = ld3(d4);
+                    best = ANY ? d4.w : INFINITY;
+                    pre = ray_precompute(d);
+                    auto safe_inv = [](float x) { return 1.0f / (fabsf(x) < 1e-30f ? copysignf(1e-30f, x) : x); };
+                    ix = safe_inv(d.x);
+                    iy = safe_inv(d.y);
+                    iz = safe_inv(d.z);
+                    ox = o.x * ix;
+                    oy = o.y * iy;
+                    oz = o.z * iz;
+                    best_id = 0xffffffffu;
+                    bu = bv = 0.0f;
+                    node = 0;
+                    sp = 0;
+                    tri = tri_end = 0;
+                    hit_any = false;
+                    active = true;
+                    rays++;
+                }
+            }
+            wnext += (uint32_t)__popcll(idle);
+        }
+        if (__ballot(active) == 0ull) break;
+        if (!active) continue;
+
+        bool done = false;
+        if (tri < tri_end) {
+            // ---- one triangle
+            const float4* tp = S.tris + 3 * (size_t)tri;
+            float4 v0 = tp[0], v1 = tp[1], v2 = tp[2];
+            if (COUNT) tc.tris++;
+            float t, u, v;
+            if (intersect_triangle(pre, o, ld3(v0), ld3(v1), ld3(v2), 0.0f, best, &t, &u, &v)) {
+                uint32_t id = __float_as_uint(v0.w);
+                if (ANY) {
+                    hit_any = true;
+                    done = true;
+                } else if (t < best || id < best_id) {
+                    best = t;
+                    best_id = id;
+                    bu = u;
+                    bv = v;
+                }
+            }
+            ++tri;
+            if (!done && tri == tri_end) node = -1;  // pop below
+        } else {
+            // ---- one node: both children's slab tests
+            const float4* np = reinterpret_cast<const float4*>(S.nodes + node);
+            float4 nx = np[0], ny = np[1], nz = np[2];
+            int4 meta = *reinterpret_cast<const int4*>(np + 3);
+            if (COUNT) tc.nodes++;
+            float tf = best * 1.0000004f;
+            float a0 = __builtin_fmaf(nx.x, ix, -ox), b0 = __builtin_fmaf(nx.y, ix, -ox);
+            float a1 = __builtin_fmaf(ny.x, iy, -oy), b1 = __builtin_fmaf(ny.y, iy, -oy);
+            float a2 = __builtin_fmaf(nz.x, iz, -oz), b2 = __builtin_fmaf(nz.y, iz, -oz);
+            float n0 = fmaxf(fmaxf(fminf(a0, b0), fminf(a1, b1)), fmaxf(fminf(a2, b2), 0.0f));
+            float f0 = fminf(fminf(fmaxf(a0, b0), fmaxf(a1, b1)), fminf(fmaxf(a2, b2), tf));
+            float c0 = __builtin_fmaf(nx.z, ix, -ox), d0 = __builtin_fmaf(nx.w, ix, -ox);
+            float c1 = __builtin_fmaf(ny.z, iy, -oy), d1 = __builtin_fmaf(ny.w, iy, -oy);
+            float c2 = __builtin_fmaf(nz.z, iz, -oz), d2 = __builtin_fmaf(nz.w, iz, -oz);
+            float n1 = fmaxf(fmaxf(fminf(c0, d0), fminf(c1, d1)), fmaxf(fminf(c2, d2), 0.0f));
+            float f1 = fminf(fminf(fmaxf(c0, d0), fmaxf(c1, d1)), fminf(fmaxf(c2, d2), tf));
+            bool h0 = n0 <= f0, h1 = n1 <= f1;
+            int i0 = meta.x >= 0 ? meta.x : leaf_item(meta.x, meta.z);
+            int i1 = meta.y >= 0 ? meta.y : leaf_item(meta.y, meta.w);
+            if (h0 && h1) {
+                bool first0 = n0 <= n1;
+                int near = first0 ? i0 : i1, far = first0 ? i1 : i0;
+                if (sp < kStackSize) {
+                    stack[sp * kBlock] = far;
+                    ++sp;
+                } else {
+                    overflow = true;
+                }
+                node = near;
+            } else if (h0) {
+                node = i0;
+            } else if (h1) {
+                node = i1;
+            } else {
+                node = -1;  // pop below
+            }
+            if (node < -1 + 0 && node != -1) {
+                // leaf range item -> triangle units
+                int code = -1 - node;
+                tri = code >> 3;
+                tri_end = tri + (code & 7);
+                node = -2;  // "in leaf" marker; popped when the range ends
+            }
+        }
+        if (!done && node == -1) {
+            if (sp == 0) {
+                done = true;
+            } else {
+                --sp;
+                int item = stack[sp * kBlock];
+                if (item >= 0) {
+                    node = item;
+                } else {
+                    int code = -1 - item;
+                    tri = code >> 3;
+                    tri_end = tri + (code & 7);
+                    node = -2;
+                }
+            }
+        }
+        if (done) {
+            active = false;
+            if (ANY) {
+                if (!hit_any) {
+                    float4 o4 = qin[(size_t)qstride * e];
+                    uint32_t pid = __float_as_uint(o4.w);
+                    float4 c = qin[(size_t)qstride * e + 2];
+                    float4 a = Q.W.p_accum[pid];
+                    Q.W.p_accum[pid] = make_float4(a.x + c.x, a.y + c.y, a.z + c.z, 0.0f);
+                }
+            } else {
+                Q.W.hits[e] = make_float4(best, __uint_as_float(best_id), bu, bv);
+            }
+        }
+    }
+    flush_counters(P, ANY ? 0 : rays, ANY ? rays : 0, 0, tc, COUNT, overflow);
+}
+
+// ---- finish: run the remaining paths to completion --------------------------------------------------
+template <bool COUNT, bool FULL>
+__global__ void __launch_bounds__(kBlock) wf_finish(DevScene S, FrameParams P, WfParams Q, int cur, uint32_t n) {
+    __shared__ int lds_stack[kStackSize * kBlock];
+    __shared__ HaltonDim lds_halton[kHaltonLds];
+    load_halton(S, lds_halton);
+    const HaltonTab halton{lds_halton, S.halton};
+    const Uniforms& U = P.U;
+    const uint32_t* cnt = Q.W.counts + cur * kShards;
+    const float4* qin = Q.W.q[cur];
+    int* stack = &lds_stack[threadIdx.x];
+    TraceCounters tc{0, 0};
+    bool overflow = false;
+    uint32_t n_closest = 0, n_shadow = 0;
+    f2 zero2;
+    zero2.x = 0.0f;
+    zero2.y = 0.0f;
+    for (uint32_t base = blockIdx.x * kBlock; base < n; base += gridDim.x * kBlock) {
+        uint32_t g = base + threadIdx.x;
+        if (g >= n) continue;
+        uint32_t e = entry_of(cnt, g, Q.seg_cap);
+        float4 o = qin[2 * (size_t)e], d = qin[2 * (size_t)e + 1];
+        uint32_t pid = __float_as_uint(o.w);
+        uint4 meta = Q.W.p_meta[pid];
+        float4 c = Q.W.p_color[pid], a = Q.W.p_accum[pid];
+        PathRegs p;
+        p.color = mk3(c.x, c.y, c.z);
+        p.accum = mk3(a.x, a.y, a.z);
+        p.bounce = (int)(meta.z & 0xffu);
+        p.tpass = (int)((meta.z >> 8) & 0xffu);
+        p.step = (int)(meta.z >> 16);
+        const int sample = (int)meta.y;
+        f3 rayO = ld3(o), rayD = ld3(d);
+        while (true) {                                                           // :311 (bounce < max checked)
+            Hit h;
+            n_closest++;
+            if (!trace<false, COUNT>(S, rayO, rayD, 0.0f, INFINITY, h, stack, tc, overflow)) break;
+            StepResult r;
+            shade_step<FULL>(S, U, halton, (int)meta.w, sample, rayO, rayD, h, p, sample == 0 && p.step == 0, zero2,
+                             false, zero2, r);
+            write_pixel_outputs(P, meta.x, r, FULL);
+            if (r.shadow) {
+                Hit sh;
+                n_shadow++;
+                if (!trace<true, COUNT>(S, r.so, r.sd, 0.0f, r.stmax, sh, stack, tc, overflow))
+                    p.accum = p.accum + r.contrib;
+            }
+            if (!r.next) break;
+        }
+        Q.W.p_accum[pid] = make_float4(p.accum.x, p.accum.y, p.accum.z, 0.0f);
+    }
+    flush_counters(P, n_closest, n_shadow, 0, tc, COUNT, overflow);
+}
+
+// ---- motion-adaptive extra samples (:779-789) -----------------------------------------------------------
+__global__ void __launch_bounds__(kBlock) wf_extra(DevScene S, FrameParams P, WfParams Q, int qidx) {
+    __shared__ HaltonDim lds_halton[kHaltonLds];
+    load_halton(S, lds_halton);
+    const HaltonTab halton{lds_halton, S.halton};
+    const Uniforms& U = P.U;
+    const int maxExtra = (U.enableMotionAdaptiveSampling != 0) ? max(U.motionSamplingMaxExtraSamples, 0) : 0;
+    const int stride = Q.spp + maxExtra;
+    const int shard = blockIdx.x & (kShards - 1);
+    float4* qout = Q.W.q[qidx] + 2 * (size_t)shard * Q.seg_cap;
+    uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= Q.own_pixels) return;
+    int px, py;
+    own_pixel(P, i, px, py);
+    uint2 ex = make_uint2(0u, 0u);
+    if (px < U.width && py < U.height) {
+        uint32_t pix = (uint32_t)py * (uint32_t)U.width + (uint32_t)px;
+        float2 mv2 = P.motion[pix], pm2 = Q.W.motion_prev[pix];
+        f2 mv, pm;
+        mv.x = mv2.x;
+        mv.y = mv2.y;
+        pm.x = pm2.x;
+        pm.y = pm2.y;
+        int e = extra_samples(U, maxExtra, mv, pm);
+        if (e > 0) {
+            uint32_t start = atomicAdd(&Q.W.counts[kCntExtra], (uint32_t)e);
+            ex = make_uint2(start, (uint32_t)e);
+            uint32_t offset = P.random[pix];
+            for (int j = 0; j < e; ++j) {
+                int s = Q.spp + j;
+                uint32_t pid = Q.base_paths + start + (uint32_t)j;
+                int hidx = (int)(offset + (unsigned)((int)U.frameIndex * stride + s));
+                init_path(Q, pid, pix, s, (uint32_t)hidx);
+                f3 o, d;
+                primary_ray(U, halton, px, py, hidx, o, d);
+                atomicAdd(&P.counters[kCntPaths], 1ull);
+                if (U.maxBounces > 0) {
+                    uint32_t slot = atomicAdd(&Q.W.counts[qidx * kShards + shard], 1u);
+                    qout[2 * (size_t)slot] = make_float4(o.x, o.y, o.z, __uint_as_float(pid));
+                    qout[2 * (size_t)slot + 1] = make_float4(d.x, d.y, d.z, 0.0f);
+                }
+            }
+        }
+    }
+    Q.W.px_extra[i] = ex;
+}
+
+// ---- resolve (:777, :792-819) -------------------------------------------------------------------------
+__global__ void __launch_bounds__(kBlock) wf_resolve(DevScene S, FrameParams P, WfParams Q, int with_extra) {
+    const Uniforms& U = P.U;
+    uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= Q.own_pixels) return;
+    int px, py;
+    own_pixel(P, i, px, py);
+    if (px >= U.width || py >= U.height) return;
+    size_t pix = (size_t)py * U.width + px;
+    f3 total = mk3(0.0f, 0.0f, 0.0f);
+    for (int s = 0; s < Q.spp; ++s) {
+        float4 a = Q.W.p_accum[(size_t)i * Q.spp + s];
+        total = total + mk3(a.x, a.y, a.z);
+    }
+    int nsamp = Q.spp;
+    if (with_extra) {
+        uint2 ex = Q.W.px_extra[i];
+        for (uint32_t j = 0; j < ex.y; ++j) {
+            float4 a = Q.W.p_accum[Q.base_paths + ex.x + j];
+            total = total + mk3(a.x, a.y, a.z);
+        }
+        nsamp += (int)ex.y;
+    }
+    float2 mv2 = P.motion[pix], pm2 = Q.W.motion_prev[pix];
+    f2 mv, pm;
+    mv.x = mv2.x;
+    mv.y = mv2.y;
+    pm.x = pm2.x;
+    pm.y = pm2.y;
+    f3 c = resolve_pixel(U, total, nsamp, mv, pm, P.accum_in, pix);
+    P.accum_out[pix] = make_float4(c.x, c.y, c.z, 1.0f);
+}
+
+size_t wavefront_queue_entries(size_t paths) { return (size_t)kShards * (paths / kShards + 4096); }
+
+static unsigned grid_for(uint32_t n, unsigned cap) {
+    unsigned g = (unsigned)((n + kBlock - 1) / kBlock);
+    if (g > cap) g = cap;
+    g = (g + kShards - 1) / kShards * kShards;  // multiple of 8: segment bound (see header)
+    return g == 0 ? kShards : g;
+}
+
+#define WF_CHECK(expr)                    \
+    do {                                  \
+        hipError_t e_ = (expr);           \
+        if (e_ != hipSuccess) {           \
+            *err = hipGetErrorString(e_); \
+            return false;                 \
+        }                                 \
+    } while (0)
+
+// resident blocks of the persistent traversal kernel (CUs x blocks per CU), queried once
+static unsigned trace_grid_cap() {
+    static unsigned cap = 0;
+    if (!cap) {
+        int dev = 0, cus = 256, per = 0;
+        if (hipGetDevice(&dev) == hipSuccess) hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, wf_trace<false, false>, kBlock, 0) != hipSuccess || per < 1)
+            per = 4;
+        cap = (unsigned)(cus * per);
+    }
+    return cap;
+}
+
+static uint32_t queue_total(const uint32_t* h, int q) {
+    uint32_t s = 0;
+    for (int k = 0; k < kShards; ++k) s += h[q * kShards + k];
+    return s;
+}
+
+static bool iterate(const DevScene& S, const FrameParams& P, WfParams& Q, int& cur, uint32_t n, bool count, bool full,
+                    hipStream_t stream, float* stage_ms, int* iterations, const char** err) {
+    const int max_it = P.U.maxBounces * (P.U.maxBounces + 1) + 2;
+    WavefrontBuffers& W = Q.W;
+    for (int it = 0; it < max_it && n > 0; ++it) {
+        if (n < kTailRays) {
+            // run the tail to completion in one launch
+            WF_CHECK(hipEventRecord(W.ev[0], stream));
+            unsigned g = grid_for(n, 1u << 20);
+            if (count) {
+                if (full) hipLaunchKernelGGL((wf_finish<true, true>), dim3(g), dim3(kBlock), 0, stream, S, P, Q, cur, n);
+                else hipLaunchKernelGGL((wf_finish<true, false>), dim3(g), dim3(kBlock), 0, stream, S, P, Q, cur, n);
+            } else {
+                if (full) hipLaunchKernelGGL((wf_finish<false, true>), dim3(g), dim3(kBlock), 0, stream, S, P, Q, cur, n);
+                else hipLaunchKernelGGL((wf_finish<false, false>), dim3(g), dim3(kBlock), 0, stream, S, P, Q, cur, n);
+            }
+            WF_CHECK(hipGetLastError());
+            WF_CHECK(hipEventRecord(W.ev[1], stream));
+            WF_CHECK(hipStreamSynchronize(stream));
+            float a = 0;
+            WF_CHECK(hipEventElapsedTime(&a, W.ev[0], W.ev[1]));
+            stage_ms[5] += a;
+            ++*iterations;
+            return true;
+        }
+        int next = 1 - cur;
+        WF_CHECK(hipEventRecord(W.ev[0], stream));
+        unsigned g = grid_for(n, 8192);
+        unsigned gt = grid_for(n, trace_grid_cap());
+        if (count) hipLaunchKernelGGL((wf_trace<false, true>), dim3(gt), dim3(kBlock), 0, stream, S, P, Q, cur, n);
+        else hipLaunchKernelGGL((wf_trace<false, false>), dim3(gt), dim3(kBlock), 0, stream, S, P, Q, cur, n);
+        WF_CHECK(hipEventRecord(W.ev[1], stream));
+        if (full) hipLaunchKernelGGL(wf_shade<true>, dim3(g), dim3(kBlock), 0, stream, S, P, Q, cur, n);
+        else hipLaunchKernelGGL(wf_shade<false>, dim3(g), dim3(kBlock), 0, stream, S, P, Q, cur, n);
+        WF_CHECK(hipEventRecord(W.ev[2], stream));
+        if (count) hipLaunchKernelGGL((wf_trace<true, true>), dim3(gt), dim3(kBlock), 0, stream, S, P, Q, cur, n);
+        else hipLaunchKernelGGL((wf_trace<true, false>), dim3(gt), dim3(kBlock), 0, stream, S, P, Q, cur, n);
+        WF_CHECK(hipGetLastError());
+        WF_CHECK(hipEventRecord(W.ev[3], stream));
+        WF_CHECK(hipMemcpyAsync(W.h_counts, W.counts, kWfCountWords * sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
+        WF_CHECK(hipStreamSynchronize(stream));
+        float a = 0, b = 0, c = 0;
+        WF_CHECK(hipEventElapsedTime(&a, W.ev[0], W.ev[1]));
+        WF_CHECK(hipEventElapsedTime(&b, W.ev[1], W.ev[2]));
+        WF_CHECK(hipEventElapsedTime(&c, W.ev[2], W.ev[3]));
+        stage_ms[1] += a;
+        stage_ms[2] += b;
+        stage_ms[3] += c;
+        n = queue_total(W.h_counts, next);
+        cur = next;
+        ++*iterations;
+    }
+    return true;
+}
+
+bool run_wavefront(const DevScene& S, const FrameParams& P, WavefrontBuffers& W, int own_tiles, bool count,
+                   hipStream_t stream, float* stage_ms, int* iterations, const char** err) {
+    WfParams Q;
+    Q.W = W;
+    Q.spp = max(P.U.samplesPerPixel, 1);
+    Q.own_pixels = (uint32_t)own_tiles * (uint32_t)P.tile_size * (uint32_t)P.tile_size;
+    Q.base_paths = Q.own_pixels * (uint32_t)Q.spp;
+    Q.seg_cap = (uint32_t)(W.queue_entries / kShards);
+    *iterations = 0;
+    for (int k = 0; k < 7; ++k) stage_ms[k] = 0.0f;
+    const bool full = needs_full(P.U);
+    const int maxExtra = (P.U.enableMotionAdaptiveSampling != 0) ? max(P.U.motionSamplingMaxExtraSamples, 0) : 0;
+    size_t npix = (size_t)P.U.width * P.U.height;
+
+    WF_CHECK(hipEventRecord(W.ev[0], stream));
+    WF_CHECK(hipMemsetAsync(W.counts, 0, kWfCountWords * sizeof(uint32_t), stream));
+    WF_CHECK(hipMemcpyAsync(W.motion_prev, P.motion, npix * sizeof(float2), hipMemcpyDeviceToDevice, stream));
+    hipLaunchKernelGGL(wf_generate, dim3(grid_for(Q.base_paths, 16384)), dim3(kBlock), 0, stream, S, P, Q);
+    WF_CHECK(hipGetLastError());
+    WF_CHECK(hipEventRecord(W.ev[1], stream));
+    WF_CHECK(hipMemcpyAsync(W.h_counts, W.counts, kWfCountWords * sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
+    WF_CHECK(hipStreamSynchronize(stream));
+    float ms = 0;
+    WF_CHECK(hipEventElapsedTime(&ms, W.ev[0], W.ev[1]));
+    stage_ms[0] += ms;
+    int cur = 0;
+    if (!iterate(S, P, Q, cur, queue_total(W.h_counts, 0), count, full, stream, stage_ms, iterations, err)) return false;
+
+    WF_CHECK(hipEventRecord(W.ev[0], stream));
+    if (maxExtra > 0) {
+        // the extra-sample pass appends primary rays to queue `cur` (reset here)
+        WF_CHECK(hipMemsetAsync(W.counts + cur * kShards, 0, kShards * sizeof(uint32_t), stream));
+        hipLaunchKernelGGL(wf_extra, dim3(grid_for(Q.own_pixels, 1u << 30)), dim3(kBlock), 0, stream, S, P, Q, cur);
+        WF_CHECK(hipGetLastError());
+        WF_CHECK(hipMemcpyAsync(W.h_counts, W.counts, kWfCountWords * sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
+        WF_CHECK(hipStreamSynchronize(stream));
+        uint32_t n_extra = queue_total(W.h_counts, cur);
+        if (n_extra > 0) {
+            if (!iterate(S, P, Q, cur, n_extra, count, full, stream, stage_ms, iterations, err)) return false;
+        }
+    }
+    hipLaunchKernelGGL(wf_resolve, dim3(grid_for(Q.own_pixels, 1u << 30)), dim3(kBlock), 0, stream, S, P, Q,
+                       maxExtra > 0 ? 1 : 0);
+    WF_CHECK(hipGetLastError());
+    WF_CHECK(hipEventRecord(W.ev[1], stream));
+    WF_CHECK(hipStreamSynchronize(stream));
+    WF_CHECK(hipEventElapsedTime(&ms, W.ev[0], W.ev[1]));
+    stage_ms[4] += ms;
+    return true;
+}
+
+}  // namespace rt

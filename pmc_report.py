@@ -1,0 +1,18 @@
+import csv, collections, glob, sys
+agg=collections.defaultdict(lambda: collections.defaultdict(float))
+for f in sorted(glob.glob('gpurun_out/pmc/p*/run_counter_collection.csv')):
+    for r in csv.DictReader(open(f)):
+        k=r['Kernel_Name'].split('(')[0].replace('void ','')
+        if 'rocclr' in k: continue
+        agg[k][r['Counter_Name']]+=float(r['Counter_Value'])
+flt = sys.argv[1] if len(sys.argv)>1 else ''
+for k,v in agg.items():
+    if flt not in k: continue
+    print(k)
+    for c,x in sorted(v.items()): print('   %-34s %.4g'%(c,x))
+    g=lambda n: v.get(n,0)
+    if g('SQ_WAVE_CYCLES'):
+        print('   -> wait_any %.2f wait_inst %.2f valu %.2f'%(g('SQ_WAIT_ANY')/g('SQ_WAVE_CYCLES'), g('SQ_WAIT_INST_ANY')/g('SQ_WAVE_CYCLES'), g('SQ_ACTIVE_INST_VALU')/g('SQ_WAVE_CYCLES')))
+    if g('SQ_ACTIVE_INST_VALU') and g('SQ_THREAD_CYCLES_VALU'): print('   -> lane util %.3f'%(g('SQ_THREAD_CYCLES_VALU')/(64*g('SQ_ACTIVE_INST_VALU'))))
+    if g('TCP_TCC_READ_REQ_sum'): print('   -> avg L2 read latency %.1f cyc'%(g('TCP_TCC_READ_REQ_LATENCY_sum')/g('TCP_TCC_READ_REQ_sum')))
+    if g('SQ_CYCLES'): print('   -> avg waves resident %.1f (per SE?)'%(g('SQ_LEVEL_WAVES')/g('SQ_CYCLES')))

@@ -1,0 +1,63 @@
+"""Regenerate the golden fixtures from the CPU oracle (oracle/rt_oracle.c).
+
+The reference cannot run in this container (Swift/Metal absent), so these
+fixtures are the oracle's own outputs for fixed seeds: they pin the oracle against silent
+changes (tests/test_oracle_kat.py) and give the GPU path a second, independent anchor.
+Run from the repo root:  python tests/golden/make_golden.py
+"""
+import importlib
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, ROOT)
+
+CASES = {
+    # name: (preset, W, H, knobs, frames)
+    "c1_pbr_b1": ("c1", 64, 64, dict(samplesPerPixel=1, maxBounces=1), 1),
+    "c1_pbr_b4": ("c1", 64, 64, dict(samplesPerPixel=2, maxBounces=4), 1),
+    "c1_legacy_b3": ("c1", 64, 48, dict(samplesPerPixel=1, maxBounces=3, shadingMode=1), 1),
+    "c1_ema_f3": ("c1", 48, 48, dict(samplesPerPixel=1, maxBounces=2), 3),
+    "c3g_small_b8": ("c3g", 64, 36, dict(samplesPerPixel=1, maxBounces=8), 1),
+    "c2_small_b4": ("c2", 64, 36, dict(samplesPerPixel=1, maxBounces=4), 1),
+}
+SEED = 11
+
+
+def render_case(rt, oracle, preset, W, H, knobs, frames, assets):
+    scene = rt.Scene.preset(preset, assets)
+    osc = oracle.OracleScene(scene.desc())
+    rnd = rt.random_offsets(SEED, W, H)
+    prev, motion = None, None
+    for f in range(frames):
+        u = rt.uniforms_default(W, H, scene.light_count)
+        for k, v in knobs.items():
+            setattr(u, k, v)
+        u.frameIndex = f
+        out = osc.render(u, rnd, accum_in=prev, motion_in=motion)
+        prev, motion = out["radiance"], out["motion"]
+    return out
+
+
+def main():
+    rt = importlib.import_module("metal4-raytracing_amd")
+    import oracle
+    assets = os.path.join(ROOT, "assets")
+    meta = {}
+    for name, (preset, W, H, knobs, frames) in CASES.items():
+        out = render_case(rt, oracle, preset, W, H, knobs, frames, assets)
+        np.savez_compressed(os.path.join(ROOT, "tests", "golden", name + ".npz"), radiance=out["radiance"][..., :3],
+                            depth=out["depth"], motion=out["motion"],
+                            counts=np.array([out["closest_rays"], out["shadow_rays"], out["paths"]], np.uint64))
+        meta[name] = dict(preset=preset, width=W, height=H, knobs=knobs, frames=frames, seed=SEED,
+                          closest_rays=int(out["closest_rays"]), shadow_rays=int(out["shadow_rays"]))
+        print(name, meta[name])
+    with open(os.path.join(ROOT, "tests", "golden", "cases.json"), "w") as f:
+        json.dump(meta, f, indent=1, sort_keys=True)
+
+
+if __name__ == "__main__":
+    main()

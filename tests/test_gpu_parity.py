@@ -11,9 +11,12 @@ from helpers import REL_L2_TOL, parity_report
 pytestmark = pytest.mark.gpu
 
 
-def _render_pair(rt, orc, preset, W, H, assets, frames=1, seed=7, **knobs):
+PIPELINES = ["megakernel", "wavefront"]
+
+
+def _render_pair(rt, orc, preset, W, H, assets, frames=1, seed=7, pipeline="megakernel", **knobs):
     scene = rt.Scene.preset(preset, assets)
-    R = rt.Renderer(scene, W, H, seed=seed)
+    R = rt.Renderer(scene, W, H, seed=seed, pipeline=pipeline)
     for k, v in knobs.items():
         setattr(R, k, v)
     osc = orc.OracleScene(scene.desc())
@@ -33,15 +36,16 @@ def _render_pair(rt, orc, preset, W, H, assets, frames=1, seed=7, **knobs):
     return out
 
 
+@pytest.mark.parametrize("pipeline", PIPELINES)
 @pytest.mark.parametrize("preset,W,H,spp,bounces,mode", [
     ("c1", 64, 64, 1, 1, 0),          # config 1 (plumbing case), small
     ("c1", 256, 256, 1, 1, 0),        # config 1 at its full size
     ("c1", 96, 64, 2, 4, 0),          # more bounces, non-square
     ("c1", 64, 48, 2, 3, 1),          # legacy shading (ShadingModeLegacy)
 ])
-def test_c1_parity(rt, orc, assets, preset, W, H, spp, bounces, mode):
+def test_c1_parity(rt, orc, assets, preset, W, H, spp, bounces, mode, pipeline):
     (g, gd, gm, st, o), = _render_pair(rt, orc, preset, W, H, assets, samplesPerPixel=spp, maxBounces=bounces,
-                                       shadingMode=mode)
+                                       shadingMode=mode, pipeline=pipeline)
     rep = parity_report(g, o["radiance"])
     print(rep, st.closest_rays, o["closest_rays"], st.shadow_rays, o["shadow_rays"])
     assert rep["n_bad"] == 0, rep
@@ -51,38 +55,46 @@ def test_c1_parity(rt, orc, assets, preset, W, H, spp, bounces, mode):
     assert st.paths == o["paths"]
 
 
-def test_glass_dragon_parity(rt, orc, assets):
+@pytest.mark.parametrize("pipeline", PIPELINES)
+def test_glass_dragon_parity(rt, orc, assets, pipeline):
     """C3g scene (glass dragon stand-in, 871k tris) at reduced resolution, 8 bounces."""
-    (g, gd, gm, st, o), = _render_pair(rt, orc, "c3g", 96, 54, assets, samplesPerPixel=2, maxBounces=8)
+    (g, gd, gm, st, o), = _render_pair(rt, orc, "c3g", 96, 54, assets, samplesPerPixel=2, maxBounces=8,
+                                       pipeline=pipeline)
     rep = parity_report(g, o["radiance"])
     print(rep)
     assert rep["n_bad"] == 0, rep
     assert st.closest_rays == o["closest_rays"] and st.shadow_rays == o["shadow_rays"]
 
 
-def test_bunny_parity(rt, orc, assets):
-    (g, gd, gm, st, o), = _render_pair(rt, orc, "c2", 80, 45, assets, samplesPerPixel=2, maxBounces=4)
+@pytest.mark.parametrize("pipeline", PIPELINES)
+def test_bunny_parity(rt, orc, assets, pipeline):
+    (g, gd, gm, st, o), = _render_pair(rt, orc, "c2", 80, 45, assets, samplesPerPixel=2, maxBounces=4,
+                                       pipeline=pipeline)
     rep = parity_report(g, o["radiance"])
     assert rep["n_bad"] == 0, rep
 
 
-def test_temporal_accumulation(rt, orc, assets):
+@pytest.mark.parametrize("pipeline", PIPELINES)
+def test_temporal_accumulation(rt, orc, assets, pipeline):
     """frameIndex > 0: EMA with the history target (Raytracing.metal:796-817), 3 frames."""
-    frames = _render_pair(rt, orc, "c1", 48, 48, assets, frames=3, samplesPerPixel=1, maxBounces=2)
+    frames = _render_pair(rt, orc, "c1", 48, 48, assets, frames=3, samplesPerPixel=1, maxBounces=2,
+                          pipeline=pipeline)
     for g, gd, gm, st, o in frames:
         rep = parity_report(g, o["radiance"])
         assert rep["n_bad"] == 0, rep
 
 
+@pytest.mark.parametrize("pipeline", PIPELINES)
 @pytest.mark.parametrize("mode", range(1, 8))
-def test_debug_modes(rt, orc, assets, mode):
-    (g, gd, gm, st, o), = _render_pair(rt, orc, "c1", 32, 32, assets, debugTextureMode=mode)
+def test_debug_modes(rt, orc, assets, mode, pipeline):
+    (g, gd, gm, st, o), = _render_pair(rt, orc, "c1", 32, 32, assets, debugTextureMode=mode, pipeline=pipeline)
     assert parity_report(g, o["radiance"])["n_bad"] == 0
 
 
-def test_gbuffer(rt, orc, assets):
+@pytest.mark.parametrize("pipeline", PIPELINES)
+def test_gbuffer(rt, orc, assets, pipeline):
     scene = rt.Scene.preset("c1", assets)
-    R = rt.Renderer(scene, 40, 30, seed=3)
+    R = rt.Renderer(scene, 40, 30, seed=3, pipeline=pipeline)
     R.useTemporalDenoiser = True
     u = R.draw()
     _, _, gb = R.aux(gbuffer=True)
@@ -90,19 +102,20 @@ def test_gbuffer(rt, orc, assets):
     assert np.array_equal(gb, o["gbuffer"])
 
 
-def test_tiles_bitwise(rt, assets):
+@pytest.mark.parametrize("pipeline", PIPELINES)
+def test_tiles_bitwise(rt, assets, pipeline):
     """Tile-split rendering is bitwise identical to the full-image render."""
     import torch
     scene = rt.Scene.preset("c1", assets)
     W, H, T = 200, 136, 64
-    full = rt.Renderer(scene, W, H, seed=5)
+    full = rt.Renderer(scene, W, H, seed=5, pipeline=pipeline)
     full.maxBounces = 3
     full.draw()
     ref = full.radiance()
     n = 3
     canvas = np.zeros_like(ref)
     for rank in range(n):
-        R = rt.Renderer(scene, W, H, seed=5)
+        R = rt.Renderer(scene, W, H, seed=5, pipeline=pipeline)
         R.maxBounces = 3
         R.draw(tiles=(T, rank, n))
         cnt = R.tile_count(T, rank, n)
@@ -133,3 +146,45 @@ def test_counting_frame_matches(rt, assets):
     st = R2.stats()
     assert np.array_equal(a, b)
     assert st.node_visits > st.closest_rays and st.tri_tests > 0
+
+
+def test_pipelines_agree_full_frame(rt, assets):
+    """Wavefront and megakernel produce bit-identical frames on the headline scene (reduced size)."""
+    scene = rt.Scene.preset("c3g", assets)
+    imgs = []
+    counts = []
+    for pl in PIPELINES:
+        R = rt.Renderer(scene, 320, 180, seed=3, pipeline=pl)
+        R.samplesPerPixel = 4
+        R.maxBounces = 8
+        R.draw()
+        imgs.append(R.radiance())
+        st = R.stats()
+        counts.append((st.closest_rays, st.shadow_rays, st.paths))
+    assert counts[0] == counts[1]
+    assert np.array_equal(imgs[0], imgs[1])
+
+
+@pytest.mark.parametrize("pipeline", PIPELINES)
+@pytest.mark.parametrize("name", ["c1_pbr_b1", "c1_pbr_b4", "c1_legacy_b3", "c1_ema_f3", "c3g_small_b8", "c2_small_b4"])
+def test_gpu_matches_golden_fixtures(rt, assets, name, pipeline):
+    """The HIP path against the committed fixtures (tests/golden, oracle-generated, seed 11)."""
+    import json
+    import os
+    from conftest import ROOT
+    gdir = os.path.join(ROOT, "tests", "golden")
+    meta = json.load(open(os.path.join(gdir, "cases.json")))[name]
+    g = np.load(os.path.join(gdir, name + ".npz"))
+    scene = rt.Scene.preset(meta["preset"], assets)
+    R = rt.Renderer(scene, meta["width"], meta["height"], seed=meta["seed"], pipeline=pipeline)
+    for k, v in meta["knobs"].items():
+        setattr(R, k, v)
+    for _ in range(meta["frames"]):
+        R.draw()
+    img = R.radiance()[..., :3]
+    depth, motion, _ = R.aux()
+    st = R.stats()
+    rep = parity_report(img, g["radiance"])
+    assert rep["n_bad"] == 0, rep
+    assert np.array_equal(depth, g["depth"])
+    assert [st.closest_rays, st.shadow_rays] == g["counts"].tolist()[:2]
