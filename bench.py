@@ -31,7 +31,7 @@ HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: 8.0 TB/s spec
 # + 3x16 B normals + 48 B instance transform; per pixel 4 B offset + 16 B history read +
 # 16 B accumulation write + 4 B depth + 8+8 B motion read/write.
 B_RAY = 48
-B_NODE = 64
+B_NODE = 80  # compressed 8-wide node (Bvh8Node)
 B_TRI = 48
 B_HIT = 16 + 48 + 48
 B_PIXEL = 4 + 16 + 16 + 4 + 16

@@ -167,6 +167,15 @@ rt_status rt_get_stats(rt_ctx* ctx, rt_stats* out);
 /* Library build identification (kernel code object arch etc). */
 const char* rt_version(void);
 
+/* Test hook (host only, no device): build the library's BVH for `scene` and trace `n` rays
+ * (6 floats each: origin, direction) with the traversal code the kernels use, compiled for the
+ * host.  any = 0: closest hit, 1: any hit; tmax per ray or NULL (= infinity).  Outputs per ray:
+ * t (inf on miss), original triangle id (0xffffffff on miss), barycentrics u/v, BVH nodes
+ * fetched and triangles tested (u, v, nodes, tris may be NULL). */
+rt_status rt_debug_trace_host(const rt_scene_desc* scene, const float* rays, const float* tmax, uint32_t n,
+                              int32_t any, float* t, uint32_t* id, float* u, float* v, uint32_t* nodes,
+                              uint32_t* tris);
+
 #ifdef __cplusplus
 }
 #endif

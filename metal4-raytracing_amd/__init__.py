@@ -81,6 +81,25 @@ def random_offsets(seed, width, height):
     return out
 
 
+def debug_trace_host(scene, origins, dirs, tmax=None, any_hit=False):
+    """Test hook: trace rays through the library's own BVH + traversal code on the host.
+    Returns dict(t, id, u, v, nodes, tris) arrays."""
+    o = np.ascontiguousarray(origins, np.float32).reshape(-1, 3)
+    d = np.ascontiguousarray(dirs, np.float32).reshape(-1, 3)
+    n = o.shape[0]
+    rays = np.ascontiguousarray(np.concatenate([o, d], axis=1), np.float32)
+    tm = None if tmax is None else np.ascontiguousarray(np.broadcast_to(tmax, (n,)), np.float32)
+    out = dict(t=np.empty(n, np.float32), id=np.empty(n, np.uint32), u=np.empty(n, np.float32),
+               v=np.empty(n, np.float32), nodes=np.empty(n, np.uint32), tris=np.empty(n, np.uint32))
+    FP, UP = C.POINTER(C.c_float), C.POINTER(C.c_uint32)
+    d_ = scene.desc()
+    _check(lib().rt_debug_trace_host(C.byref(d_), rays.ctypes.data_as(FP), tm.ctypes.data_as(FP) if tm is not None else None,
+                                     n, 1 if any_hit else 0, out["t"].ctypes.data_as(FP), out["id"].ctypes.data_as(UP),
+                                     out["u"].ctypes.data_as(FP), out["v"].ctypes.data_as(FP),
+                                     out["nodes"].ctypes.data_as(UP), out["tris"].ctypes.data_as(UP)))
+    return out
+
+
 def glass_override():
     o = MaterialOverride()
     lib().rt_material_override_glass(C.byref(o))

@@ -174,7 +174,7 @@ EXPORTED_SYMBOLS = [
     "rt_create", "rt_destroy", "rt_last_error", "rt_set_stream", "rt_scene_upload", "rt_bvh_build",
     "rt_bvh_refit", "rt_set_instance_transforms", "rt_skin", "rt_resize", "rt_render_frame", "rt_wait",
     "rt_read_radiance", "rt_read_aux", "rt_tile_count", "rt_pack_tiles", "rt_unpack_tiles",
-    "rt_set_counting", "rt_get_stats", "rt_version",
+    "rt_set_counting", "rt_get_stats", "rt_version", "rt_debug_trace_host",
     # rt_scene.h
     "rt_material_override_glass", "rt_scene_new", "rt_scene_free", "rt_scene_last_error",
     "rt_scene_add_obj", "rt_scene_add_procedural", "rt_scene_set_lights", "rt_scene_set_light_intensity",
@@ -209,6 +209,8 @@ def declare(lib):
         "rt_set_counting": (st, [vp, C.c_int32]),
         "rt_get_stats": (st, [vp, P(Stats)]),
         "rt_version": (C.c_char_p, []),
+        "rt_debug_trace_host": (st, [P(SceneDesc), P(C.c_float), P(C.c_float), C.c_uint32, C.c_int32, P(C.c_float),
+                                     P(C.c_uint32), P(C.c_float), P(C.c_float), P(C.c_uint32), P(C.c_uint32)]),
         "rt_material_override_glass": (None, [P(MaterialOverride)]),
         "rt_scene_new": (st, [P(vp)]),
         "rt_scene_free": (st, [vp]),

@@ -55,13 +55,14 @@ struct rt_ctx {
 
     // BVH
     BvhResult bvh;
+    Bvh8Result bvh8;
     std::vector<uint32_t> level_nodes;
     std::vector<uint32_t> level_off;
 
     // device buffers
     DevBuf d_pos, d_prev_pos, d_nrm, d_rest_pos, d_rest_nrm, d_jidx, d_jw, d_joints;
     DevBuf d_tri_info, d_inst, d_prev_inst, d_mat, d_lights, d_halton;
-    DevBuf d_tris, d_nodes, d_slot_to_tri, d_levels;
+    DevBuf d_tris, d_nodes, d_node_box, d_slot_to_tri, d_levels;
     DevBuf d_random, d_accum[2], d_depth, d_motion, d_gbuffer, d_counters;
     int width = 0, height = 0;
     int read_idx = 0;   // accum[read_idx] = history (TextureIndexAccumulation)
@@ -145,7 +146,7 @@ static void xform_host(const float* m, const float4& p, float* out) {
 static size_t ctx_bytes(const rt_ctx* c) {
     const DevBuf* all[] = {&c->d_pos, &c->d_prev_pos, &c->d_nrm, &c->d_rest_pos, &c->d_rest_nrm, &c->d_jidx, &c->d_jw,
                            &c->d_joints, &c->d_tri_info, &c->d_inst, &c->d_prev_inst, &c->d_mat, &c->d_lights,
-                           &c->d_halton, &c->d_tris, &c->d_nodes, &c->d_slot_to_tri, &c->d_levels, &c->d_random,
+                           &c->d_halton, &c->d_tris, &c->d_nodes, &c->d_node_box, &c->d_slot_to_tri, &c->d_levels, &c->d_random,
                            &c->d_accum[0], &c->d_accum[1], &c->d_depth, &c->d_motion, &c->d_gbuffer, &c->d_counters,
                            &c->d_wf_color, &c->d_wf_accum, &c->d_wf_meta, &c->d_wf_q0, &c->d_wf_q1, &c->d_wf_hits,
                            &c->d_wf_sq, &c->d_wf_counts, &c->d_wf_mprev, &c->d_wf_extra};
@@ -250,7 +251,7 @@ rt_status rt_destroy(rt_ctx* c) {
     if (c->stream) hipStreamSynchronize(c->stream);
     DevBuf* all[] = {&c->d_pos, &c->d_prev_pos, &c->d_nrm, &c->d_rest_pos, &c->d_rest_nrm, &c->d_jidx, &c->d_jw,
                      &c->d_joints, &c->d_tri_info, &c->d_inst, &c->d_prev_inst, &c->d_mat, &c->d_lights, &c->d_halton,
-                     &c->d_tris, &c->d_nodes, &c->d_slot_to_tri, &c->d_levels, &c->d_random, &c->d_accum[0],
+                     &c->d_tris, &c->d_nodes, &c->d_node_box, &c->d_slot_to_tri, &c->d_levels, &c->d_random, &c->d_accum[0],
                      &c->d_accum[1], &c->d_depth, &c->d_motion, &c->d_gbuffer, &c->d_counters,
                      &c->d_wf_color, &c->d_wf_accum, &c->d_wf_meta, &c->d_wf_q0, &c->d_wf_q1, &c->d_wf_hits,
                      &c->d_wf_sq, &c->d_wf_counts, &c->d_wf_mprev, &c->d_wf_extra};
@@ -403,36 +404,39 @@ rt_status rt_bvh_build(rt_ctx* c) {
         c->world_dirty = false;
     }
     c->bvh = build_bvh2(c->h_world.data(), c->num_tris, 4, kStackSize - 2);
-    if (c->bvh.max_depth > kStackSize) FAIL(c, RT_ERR_STATE, "BVH deeper than traversal stack");
+    c->bvh8 = collapse_bvh8(c->bvh);
+    if (c->bvh8.max_depth > kStackSize) FAIL(c, RT_ERR_STATE, "BVH deeper than traversal stack");
+    if (c->bvh8.nodes.size() >= (1u << 23)) FAIL(c, RT_ERR_UNSUPPORTED, "BVH too large (2^23 nodes)");
     const uint32_t n = c->num_tris;
     std::vector<float4> tris(3 * (size_t)n);
     for (uint32_t k = 0; k < n; ++k) {
-        uint32_t id = c->bvh.tri_order[k];
+        uint32_t id = c->bvh8.tri_order[k];
         const float* w = &c->h_world[9 * (size_t)id];
-        uint32_t idb = id;
         float idf;
-        std::memcpy(&idf, &idb, 4);
+        std::memcpy(&idf, &id, 4);
         tris[3 * k + 0] = make_float4(w[0], w[1], w[2], idf);
         tris[3 * k + 1] = make_float4(w[3], w[4], w[5], 0.0f);
         tris[3 * k + 2] = make_float4(w[6], w[7], w[8], 0.0f);
     }
-    // nodes grouped by depth for the level-synchronous refit
-    std::vector<int> depth(c->bvh.nodes.size(), 0);
+    // nodes grouped by depth for the level-synchronous refit (BFS order: parent < child)
+    const size_t nn = c->bvh8.nodes.size();
+    std::vector<int> depth(nn, 0);
     int maxd = 0;
-    for (size_t k = 1; k < c->bvh.nodes.size(); ++k) {
-        depth[k] = depth[c->bvh.parent[k]] + 1;
+    for (size_t k = 1; k < nn; ++k) {
+        depth[k] = depth[c->bvh8.parent[k]] + 1;
         maxd = std::max(maxd, depth[k]);
     }
     c->level_off.assign(maxd + 2, 0);
     for (int d : depth) c->level_off[d + 1]++;
     for (int d = 0; d <= maxd; ++d) c->level_off[d + 1] += c->level_off[d];
-    c->level_nodes.assign(c->bvh.nodes.size(), 0);
+    c->level_nodes.assign(nn, 0);
     std::vector<uint32_t> fill(c->level_off.begin(), c->level_off.end() - 1);
-    for (size_t k = 0; k < depth.size(); ++k) c->level_nodes[fill[depth[k]]++] = (uint32_t)k;
+    for (size_t k = 0; k < nn; ++k) c->level_nodes[fill[depth[k]]++] = (uint32_t)k;
     rt_status st;
     if ((st = dev_upload(c, c->d_tris, tris.data(), tris.size() * 16))) return st;
-    if ((st = dev_upload(c, c->d_nodes, c->bvh.nodes.data(), c->bvh.nodes.size() * sizeof(Bvh2Node)))) return st;
-    if ((st = dev_upload(c, c->d_slot_to_tri, c->bvh.tri_order.data(), (size_t)n * 4))) return st;
+    if ((st = dev_upload(c, c->d_nodes, c->bvh8.nodes.data(), nn * sizeof(Bvh8Node)))) return st;
+    if ((st = dev_upload(c, c->d_node_box, c->bvh8.node_box.data(), c->bvh8.node_box.size() * 4))) return st;
+    if ((st = dev_upload(c, c->d_slot_to_tri, c->bvh8.tri_order.data(), (size_t)n * 4))) return st;
     if ((st = dev_upload(c, c->d_levels, c->level_nodes.data(), c->level_nodes.size() * 4))) return st;
     HIPC(c, hipStreamSynchronize(c->stream));
     c->bvh_ready = true;
@@ -447,8 +451,8 @@ rt_status rt_bvh_refit(rt_ctx* c) {
                    (const float*)c->d_inst.p, (float4*)c->d_tris.p, c->num_tris, c->stream);
     for (int d = (int)c->level_off.size() - 2; d >= 0; --d) {
         uint32_t off = c->level_off[d], cnt = c->level_off[d + 1] - off;
-        launch_refit_level((Bvh2Node*)c->d_nodes.p, (const float4*)c->d_tris.p, (const uint32_t*)c->d_levels.p + off,
-                           cnt, c->bvh.pad, c->stream);
+        launch_refit8_level((Bvh8Node*)c->d_nodes.p, (float*)c->d_node_box.p, (const float4*)c->d_tris.p,
+                            (const uint32_t*)c->d_levels.p + off, cnt, c->bvh8.pad, c->stream);
     }
     HIPC(c, hipGetLastError());
     return RT_OK;
@@ -550,7 +554,8 @@ rt_status rt_render_frame(rt_ctx* c, const Uniforms* U, const rt_tile_set* tiles
     }
     DevScene S;
     S.tris = (const float4*)c->d_tris.p;
-    S.nodes = (const Bvh2Node*)c->d_nodes.p;
+    S.nodes = nullptr;
+    S.nodes8 = (const Bvh8Node*)c->d_nodes.p;
     S.tri_info = (const uint4*)c->d_tri_info.p;
     S.pos = (const float4*)c->d_pos.p;
     S.prev_pos = (const float4*)c->d_prev_pos.p;
@@ -686,10 +691,69 @@ rt_status rt_get_stats(rt_ctx* c, rt_stats* out) {
     if (!c || !out) FAIL(c, RT_ERR_INVALID_ARG, "null argument");
     rt_status st = rt_wait(c);
     if (st) return st;
-    c->stats.bvh_nodes = c->bvh.nodes.size();
+    c->stats.bvh_nodes = c->bvh8.nodes.size();
     c->stats.triangles = c->num_tris;
     c->stats.device_bytes = ctx_bytes(c);
     *out = c->stats;
+    return RT_OK;
+}
+
+rt_status rt_debug_trace_host(const rt_scene_desc* sd, const float* rays, const float* tmax, uint32_t n, int32_t any,
+                              float* t_out, uint32_t* id_out, float* u_out, float* v_out, uint32_t* nodes_out,
+                              uint32_t* tris_out) {
+    if (!sd || !rays || (n && (!t_out || !id_out))) FAIL((rt_ctx*)nullptr, RT_ERR_INVALID_ARG, "null argument");
+    // world-space triangles in the original order (same arithmetic as rt_scene_upload)
+    std::vector<float> world;
+    for (uint32_t m = 0; m < sd->mesh_count; ++m) {
+        const rt_mesh_desc& md = sd->meshes[m];
+        float M[12];
+        std::memcpy(M, &md.transform, 48);
+        for (uint32_t s = 0; s < md.submesh_count; ++s) {
+            const rt_submesh_desc& sm = md.submeshes[s];
+            for (uint32_t i = 0; i < sm.index_count; ++i) {
+                const rt_float3& p = md.positions[sm.indices[i]];
+                float w[3];
+                xform_host(M, make_float4(p.x, p.y, p.z, 0.0f), w);
+                world.insert(world.end(), w, w + 3);
+            }
+        }
+    }
+    uint32_t nt = (uint32_t)(world.size() / 9);
+    BvhResult bvh2 = build_bvh2(world.data(), nt, 4, kStackSize - 2);
+    Bvh8Result bvh = collapse_bvh8(bvh2);
+    std::vector<float4> tris(3 * (size_t)nt);
+    for (uint32_t k = 0; k < nt; ++k) {
+        uint32_t id = bvh.tri_order[k];
+        const float* w = &world[9 * (size_t)id];
+        float idf;
+        std::memcpy(&idf, &id, 4);
+        tris[3 * k] = make_float4(w[0], w[1], w[2], idf);
+        tris[3 * k + 1] = make_float4(w[3], w[4], w[5], 0.0f);
+        tris[3 * k + 2] = make_float4(w[6], w[7], w[8], 0.0f);
+    }
+    DevScene S;
+    std::memset(&S, 0, sizeof S);
+    S.tris = tris.data();
+    S.nodes8 = bvh.nodes.data();
+    S.num_tris = (int)nt;
+    std::vector<int> stack((size_t)kStackSize * kBlock);
+    for (uint32_t r = 0; r < n; ++r) {
+        const float* q = rays + 6 * (size_t)r;
+        f3 o = mk3(q[0], q[1], q[2]), d = mk3(q[3], q[4], q[5]);
+        float tm = tmax ? tmax[r] : INFINITY;
+        Hit h;
+        TraceCounters tc{0, 0};
+        bool overflow = false;
+        bool hit = any ? trace8<true, true>(S, o, d, 0.0f, tm, h, stack.data(), tc, overflow)
+                       : trace8<false, true>(S, o, d, 0.0f, tm, h, stack.data(), tc, overflow);
+        if (overflow) FAIL((rt_ctx*)nullptr, RT_ERR_STATE, "traversal stack overflow");
+        t_out[r] = hit ? h.t : INFINITY;
+        id_out[r] = hit ? h.id : 0xffffffffu;
+        if (u_out) u_out[r] = hit ? h.u : 0.0f;
+        if (v_out) v_out[r] = hit ? h.v : 0.0f;
+        if (nodes_out) nodes_out[r] = tc.nodes;
+        if (tris_out) tris_out[r] = tc.tris;
+    }
     return RT_OK;
 }
 

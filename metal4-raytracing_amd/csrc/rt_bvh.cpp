@@ -262,3 +262,147 @@ void refit_bvh2(BvhResult& bvh, const float* v) {
 }
 
 }  // namespace rt
+
+// ---- compressed 8-wide collapse ------------------------------------------------------------------
+namespace rt {
+
+namespace {
+struct WItem {
+    float lo[3], hi[3];
+    bool leaf;
+    int node;            // BVH2 node (internal)
+    uint32_t start, count;  // leaf range in BVH2 triangle order
+};
+
+float item_area(const WItem& it) {
+    float d0 = it.hi[0] - it.lo[0], d1 = it.hi[1] - it.lo[1], d2 = it.hi[2] - it.lo[2];
+    return 2.0f * (d0 * d1 + d1 * d2 + d2 * d0);
+}
+
+void bvh2_children(const BvhResult& b2, int k, std::vector<WItem>& out) {
+    const Bvh2Node& n = b2.nodes[k];
+    for (int s = 0; s < 2; ++s) {
+        if (n.child[s] < 0 && n.count[s] == 0) continue;  // empty slot
+        WItem it;
+        it.lo[0] = n.lx[2 * s]; it.hi[0] = n.lx[2 * s + 1];
+        it.lo[1] = n.ly[2 * s]; it.hi[1] = n.ly[2 * s + 1];
+        it.lo[2] = n.lz[2 * s]; it.hi[2] = n.lz[2 * s + 1];
+        it.leaf = n.child[s] < 0;
+        it.node = it.leaf ? -1 : n.child[s];
+        it.start = it.leaf ? (uint32_t)~n.child[s] : 0u;
+        it.count = it.leaf ? (uint32_t)n.count[s] : 0u;
+        out.push_back(it);
+    }
+}
+}  // namespace
+
+void quantize_bvh8_node(Bvh8Node& nd, const float clo[8][3], const float chi[8][3], const bool used[8]) {
+    double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (int c = 0; c < 8; ++c)
+        if (used[c])
+            for (int a = 0; a < 3; ++a) { lo[a] = std::min(lo[a], (double)clo[c][a]); hi[a] = std::max(hi[a], (double)chi[c][a]); }
+    for (int a = 0; a < 3; ++a) {
+        if (!(lo[a] <= hi[a])) { lo[a] = 0.0; hi[a] = 0.0; }
+        nd.p[a] = (float)lo[a];
+        if ((double)nd.p[a] > lo[a]) nd.p[a] = std::nextafter(nd.p[a], -INFINITY);  // p <= every child lo
+        double ext = hi[a] - (double)nd.p[a];
+        int e = -100;
+        if (ext > 0.0) {
+            e = (int)std::ceil(std::log2(ext / 255.0));
+            while (std::ldexp(255.0, e) < ext) ++e;
+        }
+        e = std::max(-126, std::min(127, e));
+        nd.e[a] = (uint8_t)(e + 127);
+        double inv = std::ldexp(1.0, -e);
+        for (int c = 0; c < 8; ++c) {
+            uint8_t ql = 255, qh = 0;
+            if (used[c]) {
+                double fl = std::floor(((double)clo[c][a] - (double)nd.p[a]) * inv);
+                double fh = std::ceil(((double)chi[c][a] - (double)nd.p[a]) * inv);
+                ql = (uint8_t)std::max(0.0, std::min(255.0, fl));
+                qh = (uint8_t)std::max(0.0, std::min(255.0, fh));
+            }
+            nd.q[16 * a + c] = ql;
+            nd.q[16 * a + 8 + c] = qh;
+        }
+    }
+}
+
+Bvh8Result collapse_bvh8(const BvhResult& b2) {
+    Bvh8Result out;
+    out.pad = b2.pad;
+    struct Job { int b2node; uint32_t b8node; int depth; };
+    std::vector<Job> queue;
+    out.nodes.emplace_back();
+    out.parent.push_back(-1);
+    queue.push_back({0, 0u, 0});
+    for (size_t qi = 0; qi < queue.size(); ++qi) {
+        Job job = queue[qi];
+        out.max_depth = std::max(out.max_depth, job.depth + 1);
+        std::vector<WItem> items;
+        bvh2_children(b2, job.b2node, items);
+        while (items.size() < 8) {
+            int best = -1;
+            float ba = -1.0f;
+            for (size_t i = 0; i < items.size(); ++i)
+                if (!items[i].leaf && item_area(items[i]) > ba) { ba = item_area(items[i]); best = (int)i; }
+            if (best < 0) break;
+            std::vector<WItem> kids;
+            bvh2_children(b2, items[best].node, kids);
+            if (items.size() - 1 + kids.size() > 8) break;
+            items.erase(items.begin() + best);
+            items.insert(items.end(), kids.begin(), kids.end());
+        }
+        // slot order: centroid along the longest axis of the node box
+        float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+        for (auto& it : items)
+            for (int a = 0; a < 3; ++a) { lo[a] = std::min(lo[a], it.lo[a]); hi[a] = std::max(hi[a], it.hi[a]); }
+        int axis = 0;
+        for (int a = 1; a < 3; ++a) if (hi[a] - lo[a] > hi[axis] - lo[axis]) axis = a;
+        std::stable_sort(items.begin(), items.end(), [&](const WItem& x, const WItem& y) {
+            return x.lo[axis] + x.hi[axis] < y.lo[axis] + y.hi[axis];
+        });
+        Bvh8Node nd;
+        std::memset(&nd, 0, sizeof nd);
+        nd.axis = (uint8_t)axis;
+        uint32_t n_internal = 0, n_tris = 0;
+        for (auto& it : items) { if (!it.leaf) ++n_internal; else n_tris += it.count; }
+        nd.child_base = (uint32_t)out.nodes.size();
+        nd.tri_base = (uint32_t)out.tri_order.size();
+        float clo[8][3], chi[8][3];
+        bool used[8] = {false, false, false, false, false, false, false, false};
+        uint32_t rank = 0, toff = 0;
+        for (size_t c = 0; c < items.size(); ++c) {
+            const WItem& it = items[c];
+            used[c] = true;
+            for (int a = 0; a < 3; ++a) { clo[c][a] = it.lo[a]; chi[c][a] = it.hi[a]; }
+            if (!it.leaf) {
+                nd.meta[c] = (uint8_t)(0x80 | rank);
+                uint32_t child = nd.child_base + rank;
+                ++rank;
+                queue.push_back({it.node, child, job.depth + 1});
+            } else {
+                nd.meta[c] = (uint8_t)(((it.count - 1) << 5) | toff);
+                for (uint32_t t = 0; t < it.count; ++t) out.tri_order.push_back(b2.tri_order[it.start + t]);
+                toff += it.count;
+            }
+        }
+        (void)n_tris;
+        quantize_bvh8_node(nd, clo, chi, used);
+        out.nodes[job.b8node] = nd;
+        for (uint32_t r = 0; r < n_internal; ++r) {
+            out.nodes.emplace_back();
+            out.parent.push_back((int32_t)job.b8node);
+        }
+        // node box (for refit / diagnostics)
+        if (out.node_box.size() < 6 * out.nodes.size()) out.node_box.resize(6 * out.nodes.size(), 0.0f);
+        for (int a = 0; a < 3; ++a) {
+            out.node_box[6 * job.b8node + a] = lo[a];
+            out.node_box[6 * job.b8node + 3 + a] = hi[a];
+        }
+    }
+    out.node_box.resize(6 * out.nodes.size());
+    return out;
+}
+
+}  // namespace rt

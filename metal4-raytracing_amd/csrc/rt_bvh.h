@@ -34,6 +34,44 @@ struct BvhResult {
     float pad = 0.0f;                  // absolute box padding used
 };
 
+// Compressed 8-wide node (80 B = five 16-byte loads; after Ylitie, Karras, Laine, HPG 2017).
+// Child boxes are quantized to 8 bits per plane against the node's origin p and per-axis
+// power-of-two scale 2^e, rounded outward, so the dequantized box p + q * 2^e always encloses
+// the (padded) BVH2 box it came from: traversal stays conservative and exact.
+//   meta[c]: 0x80 | rank  — internal child, node index = child_base + rank (slot order)
+//            (count-1) << 5 | offset — leaf with `count` (1..4) triangles at tri_base + offset
+//            0 with an empty box (qlo = 255 > qhi = 0) — unused slot
+//   axis: children are sorted by centroid along `axis`; rays with d[axis] < 0 visit them in
+//   reverse slot order (approximate front-to-back order for closest-hit culling).
+// Byte order of q: [qlo.x 0..7][qhi.x 0..7][qlo.y ..][qhi.y ..][qlo.z ..][qhi.z ..].
+struct alignas(16) Bvh8Node {
+    float p[3];
+    uint8_t e[3];   // biased exponents (e + 127): scale = 2^(e - 127)
+    uint8_t axis;
+    uint32_t child_base;
+    uint32_t tri_base;
+    uint8_t meta[8];
+    uint8_t q[48];
+};
+static_assert(sizeof(Bvh8Node) == 80, "wide node is 80 B");
+
+struct Bvh8Result {
+    std::vector<Bvh8Node> nodes;
+    std::vector<uint32_t> tri_order;   // BVH8 triangle slot -> original triangle id
+    std::vector<int32_t> parent;       // node -> parent node (-1 root)
+    std::vector<float> node_box;       // 6 floats per node: lo xyz, hi xyz (padded), for refit
+    int max_depth = 0;
+    float pad = 0.0f;
+};
+
+// Collapse a BVH2 into the compressed 8-wide layout (greedy: repeatedly open the internal child
+// with the largest surface area until a node has 8 children).
+Bvh8Result collapse_bvh8(const BvhResult& b2);
+
+// Re-quantize node n from its children's boxes (children: node_box of internal children, leaf
+// triangle bounds from tri_verts in BVH8 triangle order, padded).  Host mirror of the refit kernel.
+void quantize_bvh8_node(Bvh8Node& node, const float child_lo[8][3], const float child_hi[8][3], const bool used[8]);
+
 // tri_verts: 9 floats per triangle (v0, v1, v2 world space), n triangles.
 // max_depth_limit: the traversal stack bound; the builder falls back to median splits near it.
 BvhResult build_bvh2(const float* tri_verts, uint32_t n, int max_leaf, int max_depth_limit);

@@ -23,6 +23,7 @@ constexpr int kBlock = 256;      // threads per block for the traversal kernels
 struct DevScene {
     const float4* tris;
     const Bvh2Node* nodes;
+    const Bvh8Node* nodes8;
     const uint4* tri_info;
     const float4* pos;
     const float4* prev_pos;
@@ -42,10 +43,10 @@ struct Hit {
     float u, v;
 };
 
-__device__ __forceinline__ f3 ld3(const float4& v) { return mk3(v.x, v.y, v.z); }
+__host__ __device__ __forceinline__ f3 ld3(const float4& v) { return mk3(v.x, v.y, v.z); }
 
 // Object->world with the instance's packed 4x3 (columns c0..c3): ((c0*x + c1*y) + c2*z) + c3*w
-__device__ __forceinline__ f3 xform(const float* m, f3 p, float w) {
+__host__ __device__ __forceinline__ f3 xform(const float* m, f3 p, float w) {
     f3 c0 = mk3(m[0], m[1], m[2]), c1 = mk3(m[3], m[4], m[5]), c2 = mk3(m[6], m[7], m[8]), c3 = mk3(m[9], m[10], m[11]);
     return ((c0 * p.x + c1 * p.y) + c2 * p.z) + c3 * w;
 }
@@ -58,7 +59,7 @@ struct TraceCounters {
 // Closest-hit (ANY=false) or any-hit (ANY=true) traversal with a per-thread LDS stack.
 // stack: this thread's column of a [kStackSize][kBlock] LDS array (stride kBlock words).
 template <bool ANY, bool COUNT>
-__device__ __forceinline__ bool trace(const DevScene& S, f3 o, f3 d, float tmin, float tmax, Hit& hit,
+__host__ __device__ __forceinline__ bool trace(const DevScene& S, f3 o, f3 d, float tmin, float tmax, Hit& hit,
                                       int* stack, TraceCounters& cnt, bool& overflow) {
     RayPre pre = ray_precompute(d);
     // conservative slab test (boxes are padded at build time; see rt_bvh.h)
@@ -105,7 +106,7 @@ __device__ __forceinline__ bool trace(const DevScene& S, f3 o, f3 d, float tmin,
                     if (COUNT) cnt.tris++;
                     float t, u, v;
                     if (intersect_triangle(pre, o, ld3(v0), ld3(v1), ld3(v2), tmin, best, &t, &u, &v)) {
-                        uint32_t id = __float_as_uint(v0.w);
+                        uint32_t id = __builtin_bit_cast(uint32_t, v0.w);
                         if (ANY) { hit.t = t; hit.id = id; hit.u = u; hit.v = v; return true; }
                         if (t < best || id < best_id) { best = t; best_id = id; bu = u; bv = v; }
                     }
@@ -127,6 +128,148 @@ __device__ __forceinline__ bool trace(const DevScene& S, f3 o, f3 d, float tmin,
             --sp;
             node = stack[sp * kBlock];
         }
+    }
+    hit.t = best; hit.id = best_id; hit.u = bu; hit.v = bv;
+    return best_id != 0xffffffffu;
+}
+
+// ---- compressed 8-wide BVH traversal (rt_bvh.h Bvh8Node) --------------------------------------
+struct RaySetup {
+    f3 o, d;
+    RayPre pre;
+    float ix, iy, iz;   // 1 / d (safe)
+    float ox, oy, oz;   // o * (1 / d)
+};
+
+__host__ __device__ __forceinline__ RaySetup ray_setup(f3 o, f3 d) {
+    RaySetup R;
+    R.o = o;
+    R.d = d;
+    R.pre = ray_precompute(d);
+    auto safe_inv = [](float x) { return 1.0f / (fabsf(x) < 1e-30f ? copysignf(1e-30f, x) : x); };
+    R.ix = safe_inv(d.x);
+    R.iy = safe_inv(d.y);
+    R.iz = safe_inv(d.z);
+    R.ox = o.x * R.ix;
+    R.oy = o.y * R.iy;
+    R.oz = o.z * R.iz;
+    return R;
+}
+
+__host__ __device__ __forceinline__ float byte_f(uint32_t w, int b) { return (float)((w >> (8 * b)) & 0xffu); }
+
+// Slab-test the 8 children of node `ni` (five 16-byte loads).  Returns the internal children hit
+// (bit r = internal rank r), the triangles to test (bit k = triangle tri_base + k), and the
+// traversal direction of the node's slot order.
+__host__ __device__ __forceinline__ void test_node8(const Bvh8Node* nodes, uint32_t ni, const RaySetup& R, float tmin,
+                                                    float tmax, uint32_t& ihits, uint32_t& tmask,
+                                                    uint32_t& child_base, uint32_t& tri_base, bool& flip) {
+    const float4* np = reinterpret_cast<const float4*>(nodes + ni);
+    const float4 h0 = np[0];
+    const uint4 h1 = *reinterpret_cast<const uint4*>(np + 1);
+    const uint4 qx = *reinterpret_cast<const uint4*>(np + 2);
+    const uint4 qy = *reinterpret_cast<const uint4*>(np + 3);
+    const uint4 qz = *reinterpret_cast<const uint4*>(np + 4);
+    const uint32_t ew = __builtin_bit_cast(uint32_t, h0.w);
+    const float sx = __builtin_bit_cast(float, (ew & 0xffu) << 23);
+    const float sy = __builtin_bit_cast(float, ((ew >> 8) & 0xffu) << 23);
+    const float sz = __builtin_bit_cast(float, ((ew >> 16) & 0xffu) << 23);
+    const int axis = (int)((ew >> 24) & 3u);
+    const float ax = sx * R.ix, ay = sy * R.iy, az = sz * R.iz;
+    const float bx = __builtin_fmaf(h0.x, R.ix, -R.ox);
+    const float by = __builtin_fmaf(h0.y, R.iy, -R.oy);
+    const float bz = __builtin_fmaf(h0.z, R.iz, -R.oz);
+    // near / far planes by direction sign
+    const uint32_t nx0 = R.ix >= 0.0f ? qx.x : qx.z, nx1 = R.ix >= 0.0f ? qx.y : qx.w;
+    const uint32_t fx0 = R.ix >= 0.0f ? qx.z : qx.x, fx1 = R.ix >= 0.0f ? qx.w : qx.y;
+    const uint32_t ny0 = R.iy >= 0.0f ? qy.x : qy.z, ny1 = R.iy >= 0.0f ? qy.y : qy.w;
+    const uint32_t fy0 = R.iy >= 0.0f ? qy.z : qy.x, fy1 = R.iy >= 0.0f ? qy.w : qy.y;
+    const uint32_t nz0 = R.iz >= 0.0f ? qz.x : qz.z, nz1 = R.iz >= 0.0f ? qz.y : qz.w;
+    const uint32_t fz0 = R.iz >= 0.0f ? qz.z : qz.x, fz1 = R.iz >= 0.0f ? qz.w : qz.y;
+    const float tf_max = tmax * 1.0000004f;
+    uint32_t ih = 0, tm = 0;
+    #pragma unroll
+    for (int c = 0; c < 8; ++c) {
+        const int b = c & 3;
+        const uint32_t wnx = c < 4 ? nx0 : nx1, wfx = c < 4 ? fx0 : fx1;
+        const uint32_t wny = c < 4 ? ny0 : ny1, wfy = c < 4 ? fy0 : fy1;
+        const uint32_t wnz = c < 4 ? nz0 : nz1, wfz = c < 4 ? fz0 : fz1;
+        const float tnx = __builtin_fmaf(byte_f(wnx, b), ax, bx), tfx = __builtin_fmaf(byte_f(wfx, b), ax, bx);
+        const float tny = __builtin_fmaf(byte_f(wny, b), ay, by), tfy = __builtin_fmaf(byte_f(wfy, b), ay, by);
+        const float tnz = __builtin_fmaf(byte_f(wnz, b), az, bz), tfz = __builtin_fmaf(byte_f(wfz, b), az, bz);
+        const float tn = fmaxf(fmaxf(tnx, tny), fmaxf(tnz, tmin));
+        const float tf = fminf(fminf(tfx, tfy), fminf(tfz, tf_max));
+        if (tn <= tf) {
+            const uint32_t m = ((c < 4 ? h1.z : h1.w) >> (8 * b)) & 0xffu;
+            if (m & 0x80u) ih |= 1u << (m & 7u);
+            else tm |= ((1u << ((m >> 5) + 1u)) - 1u) << (m & 31u);
+        }
+    }
+    ihits = ih;
+    tmask = tm;
+    child_base = h1.x;
+    tri_base = h1.y;
+    const float dax = axis == 0 ? R.d.x : (axis == 1 ? R.d.y : R.d.z);
+    flip = dax < 0.0f;
+}
+
+__host__ __device__ __forceinline__ int lowest_bit(uint32_t m) { return __builtin_ctz(m); }
+__host__ __device__ __forceinline__ int highest_bit(uint32_t m) { return 31 - __builtin_clz(m); }
+
+// Stack entry of a node group: child_base << 9 | flip << 8 | remaining internal hits.
+__host__ __device__ __forceinline__ uint32_t pack_group(uint32_t base, bool flip, uint32_t hits) {
+    return (base << 9) | ((uint32_t)flip << 8) | hits;
+}
+
+// Closest-hit (ANY=false) / any-hit (ANY=true) traversal of the 8-wide BVH. Triangles found by a
+// node test are intersected before the next node is fetched (they shrink `best` first).
+template <bool ANY, bool COUNT>
+__host__ __device__ __forceinline__ bool trace8(const DevScene& S, f3 o, f3 d, float tmin, float tmax, Hit& hit,
+                                                int* stack, TraceCounters& cnt, bool& overflow) {
+    const RaySetup R = ray_setup(o, d);
+    float best = tmax, bu = 0.0f, bv = 0.0f;
+    uint32_t best_id = 0xffffffffu;
+    uint32_t g_base = 0, g_hits = 1, t_base = 0, t_mask = 0;  // virtual group holding the root
+    bool g_flip = false;
+    int sp = 0;
+    while (true) {
+        if (t_mask) {
+            const int k = lowest_bit(t_mask);
+            t_mask &= t_mask - 1u;
+            const float4* tp = S.tris + 3 * (size_t)(t_base + (uint32_t)k);
+            const float4 v0 = tp[0], v1 = tp[1], v2 = tp[2];
+            if (COUNT) cnt.tris++;
+            float t, u, v;
+            if (intersect_triangle(R.pre, o, ld3(v0), ld3(v1), ld3(v2), tmin, best, &t, &u, &v)) {
+                const uint32_t id = __builtin_bit_cast(uint32_t, v0.w);
+                if (ANY) {
+                    hit.t = t; hit.id = id; hit.u = u; hit.v = v;
+                    return true;
+                }
+                if (t < best || id < best_id) { best = t; best_id = id; bu = u; bv = v; }
+            }
+            continue;
+        }
+        if (!g_hits) {
+            if (sp == 0) break;
+            --sp;
+            const uint32_t e = (uint32_t)stack[sp * kBlock];
+            g_base = e >> 9;
+            g_flip = (e >> 8) & 1u;
+            g_hits = e & 0xffu;
+        }
+        const int r = g_flip ? highest_bit(g_hits) : lowest_bit(g_hits);
+        g_hits &= ~(1u << r);
+        if (g_hits) {
+            if (sp < kStackSize) {
+                stack[sp * kBlock] = (int)pack_group(g_base, g_flip, g_hits);
+                ++sp;
+            } else {
+                overflow = true;
+            }
+        }
+        if (COUNT) cnt.nodes++;
+        test_node8(S.nodes8, g_base + (uint32_t)r, R, tmin, best, g_hits, t_mask, g_base, t_base, g_flip);
     }
     hit.t = best; hit.id = best_id; hit.u = bu; hit.v = bv;
     return best_id != 0xffffffffu;

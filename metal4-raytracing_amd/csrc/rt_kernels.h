@@ -67,7 +67,7 @@ void launch_skin(const float4* rest_pos, const float4* rest_nrm, const ushort4* 
                  const float* joints, float4* out_pos, float4* out_nrm, uint32_t n, hipStream_t s);
 void launch_flatten(const uint4* tri_info, const uint32_t* slot_to_tri, const float4* pos, const float* inst,
                     float4* tris, uint32_t n, hipStream_t s);
-void launch_refit_level(Bvh2Node* nodes, const float4* tris, const uint32_t* level_nodes, uint32_t count, float pad,
-                        hipStream_t s);
+void launch_refit8_level(Bvh8Node* nodes, float* node_box, const float4* tris, const uint32_t* level_nodes,
+                         uint32_t count, float pad, hipStream_t s);
 
 }  // namespace rt

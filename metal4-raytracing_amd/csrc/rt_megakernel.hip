@@ -75,7 +75,7 @@ megakernel(DevScene S, FrameParams P) {
             while (p.bounce < U.maxBounces) {                                        // :311
                 Hit h;
                 n_closest++;
-                if (!trace<false, COUNT>(S, rayO, rayD, 0.0f, INFINITY, h, stack, tc, overflow)) break;  // :318-322
+                if (!trace8<false, COUNT>(S, rayO, rayD, 0.0f, INFINITY, h, stack, tc, overflow)) break;  // :318-322
                 StepResult r;
                 shade_step<FULL>(S, U, halton, hidx, sampleIndex, rayO, rayD, h, p, !wroteGBuffer, prevMotion,
                            hadPrimaryHit, motionVector, r);
@@ -91,7 +91,7 @@ megakernel(DevScene S, FrameParams P) {
                 if (r.shadow) {                                                       // :716-743
                     Hit sh;
                     n_shadow++;
-                    if (!trace<true, COUNT>(S, r.so, r.sd, 0.0f, r.stmax, sh, stack, tc, overflow))
+                    if (!trace8<true, COUNT>(S, r.so, r.sd, 0.0f, r.stmax, sh, stack, tc, overflow))
                         p.accum = p.accum + r.contrib;
                 }
                 if (!r.next) break;

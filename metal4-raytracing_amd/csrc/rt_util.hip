@@ -109,45 +109,82 @@ void launch_flatten(const uint4* tri_info, const uint32_t* slot_to_tri, const fl
     hipLaunchKernelGGL(flatten_k, dim3((n + 255) / 256), dim3(256), 0, s, tri_info, slot_to_tri, pos, inst, tris, n);
 }
 
-// ---- level-synchronous refit: one launch per tree level, deepest first ------------------------
-__global__ void refit_level_k(Bvh2Node* __restrict__ nodes, const float4* __restrict__ tris,
-                              const uint32_t* __restrict__ level_nodes, uint32_t count, float pad) {
+// ---- level-synchronous refit of the 8-wide BVH: one launch per level, deepest first -------------
+// Each node recomputes its children's boxes (internal: the child's stored box; leaf: bounds of its
+// triangles + pad), re-quantizes them exactly as quantize_bvh8_node does on the host (double
+// precision, outward rounding), and stores its own box for its parent.
+__global__ void refit8_level_k(Bvh8Node* __restrict__ nodes, float* __restrict__ node_box,
+                               const float4* __restrict__ tris, const uint32_t* __restrict__ level_nodes,
+                               uint32_t count, float pad) {
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= count) return;
-    Bvh2Node nd = nodes[level_nodes[i]];
-    #pragma unroll
-    for (int s = 0; s < 2; ++s) {
-        float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
-        if (nd.child[s] >= 0) {
-            const Bvh2Node& c = nodes[nd.child[s]];
-            for (int cs = 0; cs < 2; ++cs) {
-                if (c.child[cs] < 0 && c.count[cs] == 0) continue;
-                lo[0] = fminf(lo[0], c.lx[2 * cs]); hi[0] = fmaxf(hi[0], c.lx[2 * cs + 1]);
-                lo[1] = fminf(lo[1], c.ly[2 * cs]); hi[1] = fmaxf(hi[1], c.ly[2 * cs + 1]);
-                lo[2] = fminf(lo[2], c.lz[2 * cs]); hi[2] = fmaxf(hi[2], c.lz[2 * cs + 1]);
-            }
+    const uint32_t ni = level_nodes[i];
+    Bvh8Node nd = nodes[ni];
+    float clo[8][3], chi[8][3];
+    bool used[8];
+    double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (int c = 0; c < 8; ++c) {
+        // unused slots carry an empty quantized box (qlo = 255 > qhi = 0 on x)
+        used[c] = !(nd.q[c] == 255 && nd.q[8 + c] == 0);
+        if (!used[c]) continue;
+        const uint32_t m = nd.meta[c];
+        float l[3] = {INFINITY, INFINITY, INFINITY}, h[3] = {-INFINITY, -INFINITY, -INFINITY};
+        if (m & 0x80u) {
+            const float* b = node_box + 6 * (size_t)(nd.child_base + (m & 7u));
+            for (int a = 0; a < 3; ++a) { l[a] = b[a]; h[a] = b[3 + a]; }
         } else {
-            if (nd.count[s] == 0) continue;
-            int first = ~nd.child[s];
-            for (int t = 0; t < nd.count[s]; ++t)
+            const uint32_t first = nd.tri_base + (m & 31u), n = (m >> 5) + 1u;
+            for (uint32_t t = 0; t < n; ++t)
                 for (int q = 0; q < 3; ++q) {
-                    float4 v = tris[3 * (first + t) + q];
-                    lo[0] = fminf(lo[0], v.x); hi[0] = fmaxf(hi[0], v.x);
-                    lo[1] = fminf(lo[1], v.y); hi[1] = fmaxf(hi[1], v.y);
-                    lo[2] = fminf(lo[2], v.z); hi[2] = fmaxf(hi[2], v.z);
+                    float4 v = tris[3 * (size_t)(first + t) + q];
+                    l[0] = fminf(l[0], v.x); h[0] = fmaxf(h[0], v.x);
+                    l[1] = fminf(l[1], v.y); h[1] = fmaxf(h[1], v.y);
+                    l[2] = fminf(l[2], v.z); h[2] = fmaxf(h[2], v.z);
                 }
-            for (int a = 0; a < 3; ++a) { lo[a] -= pad; hi[a] += pad; }
+            for (int a = 0; a < 3; ++a) { l[a] -= pad; h[a] += pad; }
         }
-        nd.lx[2 * s] = lo[0]; nd.lx[2 * s + 1] = hi[0];
-        nd.ly[2 * s] = lo[1]; nd.ly[2 * s + 1] = hi[1];
-        nd.lz[2 * s] = lo[2]; nd.lz[2 * s + 1] = hi[2];
+        for (int a = 0; a < 3; ++a) {
+            clo[c][a] = l[a];
+            chi[c][a] = h[a];
+            lo[a] = fmin(lo[a], (double)l[a]);
+            hi[a] = fmax(hi[a], (double)h[a]);
+        }
     }
-    nodes[level_nodes[i]] = nd;
+    for (int a = 0; a < 3; ++a) {
+        if (!(lo[a] <= hi[a])) { lo[a] = 0.0; hi[a] = 0.0; }
+        float p = (float)lo[a];
+        if ((double)p > lo[a]) p = nextafterf(p, -INFINITY);
+        nd.p[a] = p;
+        double ext = hi[a] - (double)p;
+        int e = -100;
+        if (ext > 0.0) {
+            e = (int)ceil(log2(ext / 255.0));
+            while (ldexp(255.0, e) < ext) ++e;
+        }
+        e = max(-126, min(127, e));
+        nd.e[a] = (uint8_t)(e + 127);
+        const double inv = ldexp(1.0, -e);
+        for (int c = 0; c < 8; ++c) {
+            uint8_t ql = 255, qh = 0;
+            if (used[c]) {
+                double fl = floor(((double)clo[c][a] - (double)p) * inv);
+                double fh = ceil(((double)chi[c][a] - (double)p) * inv);
+                ql = (uint8_t)fmax(0.0, fmin(255.0, fl));
+                qh = (uint8_t)fmax(0.0, fmin(255.0, fh));
+            }
+            nd.q[16 * a + c] = ql;
+            nd.q[16 * a + 8 + c] = qh;
+        }
+        node_box[6 * (size_t)ni + a] = (float)lo[a];
+        node_box[6 * (size_t)ni + 3 + a] = (float)hi[a];
+    }
+    nodes[ni] = nd;
 }
-void launch_refit_level(Bvh2Node* nodes, const float4* tris, const uint32_t* level_nodes, uint32_t count, float pad,
-                        hipStream_t s) {
+void launch_refit8_level(Bvh8Node* nodes, float* node_box, const float4* tris, const uint32_t* level_nodes,
+                         uint32_t count, float pad, hipStream_t s) {
     if (!count) return;
-    hipLaunchKernelGGL(refit_level_k, dim3((count + 255) / 256), dim3(256), 0, s, nodes, tris, level_nodes, count, pad);
+    hipLaunchKernelGGL(refit8_level_k, dim3((count + 127) / 128), dim3(128), 0, s, nodes, node_box, tris, level_nodes,
+                       count, pad);
 }
 
 }  // namespace rt

@@ -28,7 +28,11 @@ namespace rt {
 
 namespace {
 
-constexpr uint32_t kTailRays = 32768;
+constexpr uint32_t kTailRaysDefault = 32768;
+static uint32_t tail_rays() {  // RT_TAIL_RAYS overrides (tuning experiments)
+    static uint32_t v = [] { const char* e = getenv("RT_TAIL_RAYS"); return e ? (uint32_t)atol(e) : kTailRaysDefault; }();
+    return v;
+}
 
 __device__ __forceinline__ uint32_t lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
 __device__ __forceinline__ uint32_t mbcnt64(unsigned long long m) {
@@ -218,35 +222,6 @@ __global__ void __launch_bounds__(kBlock) wf_generate(DevScene S, FrameParams P,
     flush_counters(P, 0, 0, n_paths, tc, false, false);
 }
 
-// ---- extend: closest hit ----------------------------------------------------------------------------
-template <bool COUNT>
-__global__ void __launch_bounds__(kBlock) wf_extend(DevScene S, FrameParams P, WfParams Q, int cur, uint32_t n) {
-    __shared__ int lds_stack[kStackSize * kBlock];
-    const int next = 1 - cur;
-    if (blockIdx.x == 0 && threadIdx.x < 2 * kShards) {  // reset the queues shade / connect fill
-        uint32_t k = threadIdx.x & (kShards - 1);
-        Q.W.counts[threadIdx.x < kShards ? next * kShards + k : kCntShadowQ + k] = 0;
-    }
-    const uint32_t* cnt = Q.W.counts + cur * kShards;
-    const float4* qin = Q.W.q[cur];
-    int* stack = &lds_stack[threadIdx.x];
-    TraceCounters tc{0, 0};
-    bool overflow = false;
-    uint32_t rays = 0;
-    for (uint32_t base = blockIdx.x * kBlock; base < n; base += gridDim.x * kBlock) {
-        uint32_t g = base + threadIdx.x;
-        if (g < n) {
-            uint32_t e = entry_of(cnt, g, Q.seg_cap);
-            float4 o = qin[2 * (size_t)e], d = qin[2 * (size_t)e + 1];
-            Hit h;
-            trace<false, COUNT>(S, ld3(o), ld3(d), 0.0f, INFINITY, h, stack, tc, overflow);
-            Q.W.hits[e] = make_float4(h.t, __uint_as_float(h.id), h.u, h.v);
-            rays++;
-        }
-    }
-    flush_counters(P, rays, 0, 0, tc, COUNT, overflow);
-}
-
 // ---- shade -------------------------------------------------------------------------------------------
 template <bool FULL>
 __global__ void __launch_bounds__(kBlock) wf_shade(DevScene S, FrameParams P, WfParams Q, int cur, uint32_t n) {
@@ -315,46 +290,12 @@ __global__ void __launch_bounds__(kBlock) wf_shade(DevScene S, FrameParams P, Wf
     }
 }
 
-// ---- connect: any-hit shadow rays --------------------------------------------------------------------
-template <bool COUNT>
-__global__ void __launch_bounds__(kBlock) wf_connect(DevScene S, FrameParams P, WfParams Q) {
-    __shared__ int lds_stack[kStackSize * kBlock];
-    int* stack = &lds_stack[threadIdx.x];
-    const uint32_t* cnt = Q.W.counts + kCntShadowQ;
-    uint32_t n = 0;
-    #pragma unroll
-    for (int k = 0; k < kShards; ++k) n += cnt[k];
-    TraceCounters tc{0, 0};
-    bool overflow = false;
-    uint32_t rays = 0;
-    for (uint32_t base = blockIdx.x * kBlock; base < n; base += gridDim.x * kBlock) {
-        uint32_t g = base + threadIdx.x;
-        if (g < n) {
-            uint32_t e = entry_of(cnt, g, Q.seg_cap);
-            float4 o = Q.W.sq[3 * (size_t)e], d = Q.W.sq[3 * (size_t)e + 1];
-            Hit h;
-            rays++;
-            if (!trace<true, COUNT>(S, ld3(o), ld3(d), 0.0f, d.w, h, stack, tc, overflow)) {
-                uint32_t pid = __float_as_uint(o.w);
-                float4 c = Q.W.sq[3 * (size_t)e + 2];
-                float4 a = Q.W.p_accum[pid];
-                Q.W.p_accum[pid] = make_float4(a.x + c.x, a.y + c.y, a.z + c.z, 0.0f);
-            }
-        }
-    }
-    flush_counters(P, 0, rays, 0, tc, COUNT, overflow);
-}
-
 // ---- persistent traversal with per-lane refill (extend: ANY = false, connect: ANY = true) -----------
 // Each wave owns a static contiguous range of the queue and keeps all 64 lanes busy: a lane whose
 // ray is finished takes the next ray of the range at the top of the next iteration, and every
-// iteration advances each lane by exactly one unit of work — one node (two slab tests) or one
+// iteration advances each lane by exactly one unit of work — one 8-wide node test or one
 // triangle.  The wave therefore runs ~(total units of its rays)/64 iterations instead of
-// (slowest ray) x (rays per lane) — the divergence cost PMC showed for the one-ray-per-thread
-// loop (SQ_WAIT_ANY 63 %, ~10x more iterations than the mean ray needs).
-// Stack items: node index >= 0, or a leaf range encoded as -1 - (first << 3 | count).
-__device__ __forceinline__ int leaf_item(int child, int count) { return -1 - ((((~child)) << 3) | count); }
-
+// (slowest ray) x (rays per lane).
 template <bool ANY, bool COUNT>
 __global__ void __launch_bounds__(kBlock) wf_trace(DevScene S, FrameParams P, WfParams Q, int cur, uint32_t n_host) {
     __shared__ int lds_stack[kStackSize * kBlock];
@@ -385,17 +326,12 @@ __global__ void __launch_bounds__(kBlock) wf_trace(DevScene S, FrameParams P, Wf
     TraceCounters tc{0, 0};
     bool overflow = false;
     uint32_t rays = 0;
-    bool active = false;
+    bool active = false, hit_any = false, g_flip = false;
     uint32_t e = 0;
-    f3 o = mk3(0, 0, 0), d = mk3(0, 0, 0);
-    RayPre pre;
-    pre.kx = pre.ky = pre.kz = 0;
-    pre.Sx = pre.Sy = pre.Sz = 0.0f;
-    float ix = 0, iy = 0, iz = 0, ox = 0, oy = 0, oz = 0;
+    RaySetup R = ray_setup(mk3(0, 0, 0), mk3(1, 0, 0));
     float best = 0.0f, bu = 0.0f, bv = 0.0f;
-    uint32_t best_id = 0xffffffffu;
-    int node = 0, sp = 0, tri = 0, tri_end = 0;
-    bool hit_any = false;
+    uint32_t best_id = 0xffffffffu, g_base = 0, g_hits = 0, t_base = 0, t_mask = 0;
+    int sp = 0;
 
     while (true) {
         // refill idle lanes from the wave's range
@@ -406,22 +342,15 @@ __global__ void __launch_bounds__(kBlock) wf_trace(DevScene S, FrameParams P, Wf
                 if (g < wend) {
                     e = entry_of(cnt, g, Q.seg_cap);
                     float4 o4 = qin[(size_t)qstride * e], d4 = qin[(size_t)qstride * e + 1];
-                    o = ld3(o4);
-                    d = ld3(d4);
+                    R = ray_setup(ld3(o4), ld3(d4));
                     best = ANY ? d4.w : INFINITY;
-                    pre = ray_precompute(d);
-                    auto safe_inv = [](float x) { return 1.0f / (fabsf(x) < 1e-30f ? copysignf(1e-30f, x) : x); };
-                    ix = safe_inv(d.x);
-                    iy = safe_inv(d.y);
-                    iz = safe_inv(d.z);
-                    ox = o.x * ix;
-                    oy = o.y * iy;
-                    oz = o.z * iz;
                     best_id = 0xffffffffu;
                     bu = bv = 0.0f;
-                    node = 0;
+                    g_base = 0;
+                    g_hits = 1;   // virtual group holding the root
+                    g_flip = false;
+                    t_mask = 0;
                     sp = 0;
-                    tri = tri_end = 0;
                     hit_any = false;
                     active = true;
                     rays++;
@@ -433,14 +362,16 @@ __global__ void __launch_bounds__(kBlock) wf_trace(DevScene S, FrameParams P, Wf
         if (!active) continue;
 
         bool done = false;
-        if (tri < tri_end) {
+        if (t_mask) {
             // ---- one triangle
-            const float4* tp = S.tris + 3 * (size_t)tri;
-            float4 v0 = tp[0], v1 = tp[1], v2 = tp[2];
+            const int k = lowest_bit(t_mask);
+            t_mask &= t_mask - 1u;
+            const float4* tp = S.tris + 3 * (size_t)(t_base + (uint32_t)k);
+            const float4 v0 = tp[0], v1 = tp[1], v2 = tp[2];
             if (COUNT) tc.tris++;
             float t, u, v;
-            if (intersect_triangle(pre, o, ld3(v0), ld3(v1), ld3(v2), 0.0f, best, &t, &u, &v)) {
-                uint32_t id = __float_as_uint(v0.w);
+            if (intersect_triangle(R.pre, R.o, ld3(v0), ld3(v1), ld3(v2), 0.0f, best, &t, &u, &v)) {
+                const uint32_t id = __float_as_uint(v0.w);
                 if (ANY) {
                     hit_any = true;
                     done = true;
@@ -451,69 +382,29 @@ __global__ void __launch_bounds__(kBlock) wf_trace(DevScene S, FrameParams P, Wf
                     bv = v;
                 }
             }
-            ++tri;
-            if (!done && tri == tri_end) node = -1;  // pop below
         } else {
-            // ---- one node: both children's slab tests
-            const float4* np = reinterpret_cast<const float4*>(S.nodes + node);
-            float4 nx = np[0], ny = np[1], nz = np[2];
-            int4 meta = *reinterpret_cast<const int4*>(np + 3);
-            if (COUNT) tc.nodes++;
-            float tf = best * 1.0000004f;
-            float a0 = __builtin_fmaf(nx.x, ix, -ox), b0 = __builtin_fmaf(nx.y, ix, -ox);
-            float a1 = __builtin_fmaf(ny.x, iy, -oy), b1 = __builtin_fmaf(ny.y, iy, -oy);
-            float a2 = __builtin_fmaf(nz.x, iz, -oz), b2 = __builtin_fmaf(nz.y, iz, -oz);
-            float n0 = fmaxf(fmaxf(fminf(a0, b0), fminf(a1, b1)), fmaxf(fminf(a2, b2), 0.0f));
-            float f0 = fminf(fminf(fmaxf(a0, b0), fmaxf(a1, b1)), fminf(fmaxf(a2, b2), tf));
-            float c0 = __builtin_fmaf(nx.z, ix, -ox), d0 = __builtin_fmaf(nx.w, ix, -ox);
-            float c1 = __builtin_fmaf(ny.z, iy, -oy), d1 = __builtin_fmaf(ny.w, iy, -oy);
-            float c2 = __builtin_fmaf(nz.z, iz, -oz), d2 = __builtin_fmaf(nz.w, iz, -oz);
-            float n1 = fmaxf(fmaxf(fminf(c0, d0), fminf(c1, d1)), fmaxf(fminf(c2, d2), 0.0f));
-            float f1 = fminf(fminf(fmaxf(c0, d0), fmaxf(c1, d1)), fminf(fmaxf(c2, d2), tf));
-            bool h0 = n0 <= f0, h1 = n1 <= f1;
-            int i0 = meta.x >= 0 ? meta.x : leaf_item(meta.x, meta.z);
-            int i1 = meta.y >= 0 ? meta.y : leaf_item(meta.y, meta.w);
-            if (h0 && h1) {
-                bool first0 = n0 <= n1;
-                int near = first0 ? i0 : i1, far = first0 ? i1 : i0;
+            // ---- one 8-wide node
+            if (!g_hits) {  // sp > 0 here (checked at the end of the previous iteration)
+                --sp;
+                const uint32_t ent = (uint32_t)stack[sp * kBlock];
+                g_base = ent >> 9;
+                g_flip = (ent >> 8) & 1u;
+                g_hits = ent & 0xffu;
+            }
+            const int r = g_flip ? highest_bit(g_hits) : lowest_bit(g_hits);
+            g_hits &= ~(1u << r);
+            if (g_hits) {
                 if (sp < kStackSize) {
-                    stack[sp * kBlock] = far;
+                    stack[sp * kBlock] = (int)pack_group(g_base, g_flip, g_hits);
                     ++sp;
                 } else {
                     overflow = true;
                 }
-                node = near;
-            } else if (h0) {
-                node = i0;
-            } else if (h1) {
-                node = i1;
-            } else {
-                node = -1;  // pop below
             }
-            if (node < -1 + 0 && node != -1) {
-                // leaf range item -> triangle units
-                int code = -1 - node;
-                tri = code >> 3;
-                tri_end = tri + (code & 7);
-                node = -2;  // "in leaf" marker; popped when the range ends
-            }
+            if (COUNT) tc.nodes++;
+            test_node8(S.nodes8, g_base + (uint32_t)r, R, 0.0f, best, g_hits, t_mask, g_base, t_base, g_flip);
         }
-        if (!done && node == -1) {
-            if (sp == 0) {
-                done = true;
-            } else {
-                --sp;
-                int item = stack[sp * kBlock];
-                if (item >= 0) {
-                    node = item;
-                } else {
-                    int code = -1 - item;
-                    tri = code >> 3;
-                    tri_end = tri + (code & 7);
-                    node = -2;
-                }
-            }
-        }
+        if (!done && !t_mask && !g_hits && sp == 0) done = true;
         if (done) {
             active = false;
             if (ANY) {
@@ -568,7 +459,7 @@ __global__ void __launch_bounds__(kBlock) wf_finish(DevScene S, FrameParams P, W
         while (true) {                                                           // :311 (bounce < max checked)
             Hit h;
             n_closest++;
-            if (!trace<false, COUNT>(S, rayO, rayD, 0.0f, INFINITY, h, stack, tc, overflow)) break;
+            if (!trace8<false, COUNT>(S, rayO, rayD, 0.0f, INFINITY, h, stack, tc, overflow)) break;
             StepResult r;
             shade_step<FULL>(S, U, halton, (int)meta.w, sample, rayO, rayD, h, p, sample == 0 && p.step == 0, zero2,
                              false, zero2, r);
@@ -576,7 +467,7 @@ __global__ void __launch_bounds__(kBlock) wf_finish(DevScene S, FrameParams P, W
             if (r.shadow) {
                 Hit sh;
                 n_shadow++;
-                if (!trace<true, COUNT>(S, r.so, r.sd, 0.0f, r.stmax, sh, stack, tc, overflow))
+                if (!trace8<true, COUNT>(S, r.so, r.sd, 0.0f, r.stmax, sh, stack, tc, overflow))
                     p.accum = p.accum + r.contrib;
             }
             if (!r.next) break;
@@ -708,7 +599,7 @@ static bool iterate(const DevScene& S, const FrameParams& P, WfParams& Q, int& c
     const int max_it = P.U.maxBounces * (P.U.maxBounces + 1) + 2;
     WavefrontBuffers& W = Q.W;
     for (int it = 0; it < max_it && n > 0; ++it) {
-        if (n < kTailRays) {
+        if (n < tail_rays()) {
             // run the tail to completion in one launch
             WF_CHECK(hipEventRecord(W.ev[0], stream));
             unsigned g = grid_for(n, 1u << 20);
