@@ -16,6 +16,7 @@ import argparse
 import importlib
 import json
 import os
+import re
 import sys
 import time
 
@@ -35,6 +36,9 @@ B_NODE = 80  # compressed 8-wide node (Bvh8Node)
 B_TRI = 48
 B_HIT = 16 + 48 + 48
 B_PIXEL = 4 + 16 + 16 + 4 + 16
+B_QRAY = 48  # wf_trace queue entry: extend 32 B ray in + 16 B hit out; connect 48 B shadow entry in
+TRAFFIC_JSON_REL = "profiles/r01_traffic_wf_trace.json"
+TRAFFIC_JSON = os.path.join(os.path.dirname(os.path.abspath(__file__)), TRAFFIC_JSON_REL)
 
 
 def parse():
@@ -76,26 +80,19 @@ def main():
     R.samplesPerPixel = a.spp
     R.maxBounces = a.bounces
     tiles = (a.tile, rank, n) if n > 1 else None
-    own = R.tile_count(a.tile, rank, n)
-    max_own = max(R.tile_count(a.tile, r, n) for r in range(n))
     T = a.tile
     dev = torch.device("cuda", local)
-    packed = torch.zeros((max_own, T, T, 4), dtype=torch.float32, device=dev) if n > 1 else None
-    gather_list = [torch.empty_like(packed) for _ in range(n)] if (n > 1 and rank == 0) else None
+    gather = None
+    if n > 1:
+        tiles_mod = importlib.import_module("metal4-raytracing_amd.tiles")
+        gather = tiles_mod.TileGather(a.width, a.height, T, rank, n, dev, renderer=R)
 
     def frame():
         R.draw(tiles=tiles)
         R.wait()
         st = R.stats()
-        if n > 1:
-            R.pack_tiles(T, rank, n, packed.data_ptr())
-            R.wait()
-            dist.gather(packed, gather_list, dst=0)
-            if rank == 0:
-                torch.cuda.current_stream().synchronize()
-                for r in range(1, n):
-                    R.unpack_tiles(T, r, n, gather_list[r].data_ptr())
-                R.wait()
+        if gather is not None:
+            gather.gather()   # packed tiles -> rank 0 over RCCL, unpacked into its radiance target
         return st
 
     def barrier():
@@ -111,6 +108,9 @@ def main():
     rays_c = cst.closest_rays + cst.shadow_rays
     nodes_per_ray = cst.node_visits / max(rays_c, 1)
     tris_per_ray = cst.tri_tests / max(rays_c, 1)
+    # the queue traversal kernel alone (wavefront): its own node / triangle visits per traced ray
+    q_nodes_per_ray = cst.trace_nodes / max(cst.trace_rays, 1)
+    q_tris_per_ray = cst.trace_tris / max(cst.trace_rays, 1)
     R.samplesPerPixel = a.spp  # resets frameIndex (didSet)
 
     for _ in range(a.warmup):
@@ -121,10 +121,14 @@ def main():
     kernel_ms = []
     stage_ms = np.zeros(7)
     closest = 0
+    trace_rays, trace_launches, trace_ms = 0, 0, 0.0
     for _ in range(a.steps):
         st = frame()
         rays += st.closest_rays + st.shadow_rays
         closest += st.closest_rays
+        trace_rays += st.trace_rays
+        trace_launches += st.trace_launches
+        trace_ms += st.trace_ms
         kernel_ms.append(st.last_frame_ms)
         stage_ms += np.array(list(st.kernel_ms))
         last_st = st
@@ -146,16 +150,36 @@ def main():
 
     value = rays / dt / 1e9
     ms_per_step = dt / a.steps * 1e3
-    # roofline of the dominant (only) kernel, per launch
-    rays_per_launch = rays / a.steps / n
-    closest_per_launch = closest / a.steps / n
-    pixels_per_launch = a.width * a.height / n
-    bytes_per_launch = (rays_per_launch * (B_RAY + nodes_per_ray * B_NODE + tris_per_ray * B_TRI)
-                        + closest_per_launch * B_HIT + pixels_per_launch * B_PIXEL)
-    achieved = bytes_per_launch / (kms * 1e-3) / 1e9
-    traffic = None
-    if a.traffic_csv and os.path.exists(a.traffic_csv):
-        traffic = read_traffic(a.traffic_csv)
+    if last_st.pipeline == 1 and trace_launches > 0:
+        # dominant kernel: wf_trace (extend + connect launches), per launch.  Algorithmic bytes per
+        # traced ray: 48 B queue entry in (+ hit record out) + 80 B per 8-wide node fetched + 48 B
+        # per triangle tested (DESIGN.md 'Roofline').
+        kernel = "rt::wf_trace<{false,true}, false> (extend + connect)"
+        rays_per_launch = trace_rays / trace_launches
+        launch_ms = trace_ms / trace_launches
+        bytes_per_launch = rays_per_launch * (B_QRAY + q_nodes_per_ray * B_NODE + q_tris_per_ray * B_TRI)
+        npr, tpr = q_nodes_per_ray, q_tris_per_ray
+    else:
+        # megakernel: the whole frame is one launch
+        kernel = "rt::megakernel<false, false>"
+        rays_per_launch = rays / a.steps / n
+        closest_per_launch = closest / a.steps / n
+        pixels_per_launch = a.width * a.height / n
+        launch_ms = kms
+        bytes_per_launch = (rays_per_launch * (B_RAY + nodes_per_ray * B_NODE + tris_per_ray * B_TRI)
+                            + closest_per_launch * B_HIT + pixels_per_launch * B_PIXEL)
+        npr, tpr = nodes_per_ray, tris_per_ray
+    achieved = bytes_per_launch / (launch_ms * 1e-3) / 1e9
+    traffic, traffic_src = None, None
+    if a.traffic_csv:
+        traffic = read_traffic(a.traffic_csv.split(","), r"wf_trace<(true|false),false>"
+                               if last_st.pipeline == 1 else r"megakernel<false,")
+        traffic_src = "live: " + a.traffic_csv
+    elif os.path.exists(TRAFFIC_JSON):
+        with open(TRAFFIC_JSON) as f:
+            tj = json.load(f)
+        if tj.get("kernel") == kernel and tj.get("config") == [a.scene, a.width, a.height, a.spp, a.bounces]:
+            traffic, traffic_src = tj["bytes_per_launch"], TRAFFIC_JSON_REL + " (" + tj.get("source", "") + ")"
 
     cpu = None
     if not a.no_cpu and n == 1:
@@ -188,10 +212,9 @@ def main():
         },
         "roofline": {
             "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-            "kernel": "rt::megakernel<false>" if a.pipeline == "megakernel" else "wavefront",
-            "bytes_per_launch": int(bytes_per_launch), "nodes_per_ray": round(nodes_per_ray, 2),
-            "tris_per_ray": round(tris_per_ray, 2),
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": traffic_src,
+            "kernel": kernel, "launch_ms": round(launch_ms, 4), "bytes_per_launch": int(bytes_per_launch),
+            "rays_per_launch": int(rays_per_launch), "nodes_per_ray": round(npr, 3), "tris_per_ray": round(tpr, 3),
         },
         "cpu_baseline": cpu,
     }
@@ -200,25 +223,31 @@ def main():
         dist.destroy_process_group()
 
 
-def read_traffic(path):
-    """Per-launch HBM bytes from a rocprofv3 --pmc FETCH_SIZE/WRITE_SIZE CSV (KB units; gfx950
-    FETCH_SIZE reports half of wide reads -> x2, MI355X_MICROARCH.md §HBM)."""
+def read_traffic(paths, kernel_key):
+    """Per-launch HBM bytes of the dominant kernel from rocprofv3 --pmc counter_collection CSVs
+    (FETCH_SIZE and WRITE_SIZE come from separate passes; KB units; gfx950 FETCH_SIZE reports half
+    of wide reads -> x2, MI355X_MICROARCH.md 'HBM').  COUNT=true instantiations are excluded."""
     import csv
-    fetch, write, n = 0.0, 0.0, 0
-    with open(path) as f:
-        for row in csv.DictReader(f):
-            if "megakernel" not in row.get("Kernel_Name", "") and "wavefront" not in row.get("Kernel_Name", ""):
-                continue
-            name = row.get("Counter_Name", "")
-            v = float(row.get("Counter_Value", 0))
-            if name == "FETCH_SIZE":
-                fetch += v
-                n += 1
-            elif name == "WRITE_SIZE":
-                write += v
-    if n == 0:
+    fetch, write, nf, nw = 0.0, 0.0, 0, 0
+    for path in paths:
+        if not os.path.exists(path):
+            continue
+        with open(path) as f:
+            for row in csv.DictReader(f):
+                k = row.get("Kernel_Name", "").split("(")[0].replace(" ", "")
+                if not re.search(kernel_key, k):
+                    continue
+                name = row.get("Counter_Name", "")
+                v = float(row.get("Counter_Value", 0))
+                if name == "FETCH_SIZE":
+                    fetch += v
+                    nf += 1
+                elif name == "WRITE_SIZE":
+                    write += v
+                    nw += 1
+    if nf == 0 or nw == 0:
         return None
-    return int((2 * fetch + write) * 1024 / n)
+    return int((2 * fetch / nf + write / nw) * 1024)
 
 
 def cpu_baseline(rt, scene, R, a):

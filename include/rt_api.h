@@ -122,6 +122,12 @@ typedef struct rt_stats {
                                wavefront [0] generate [1] extend [2] shade [3] connect [4] resolve */
     int32_t pipeline;       /* RT_PIPELINE_* that rendered the last frame */
     int32_t iterations;     /* wavefront: extend/shade/connect rounds of the last frame */
+    /* wavefront: the queue traversal kernel (extend + connect launches; the finish tail excluded) */
+    uint64_t trace_rays;    /* rays it traced */
+    uint64_t trace_nodes;   /* nodes it fetched (counting frames only) */
+    uint64_t trace_tris;    /* triangles it tested (counting frames only) */
+    int32_t trace_launches; /* its launches */
+    float trace_ms;         /* its summed device time (HIP events on the render stream) */
 } rt_stats;
 
 rt_status rt_create(const rt_opts* opts, rt_ctx** out);
@@ -158,6 +164,12 @@ rt_status rt_read_aux(rt_ctx* ctx, float* depth, float* motion, float* gbuffer);
 int32_t rt_tile_count(int32_t width, int32_t height, const rt_tile_set* tiles);
 rt_status rt_pack_tiles(rt_ctx* ctx, const rt_tile_set* tiles, void* device_dst);
 rt_status rt_unpack_tiles(rt_ctx* ctx, const rt_tile_set* tiles, const void* device_src);
+/* Host-memory forms of the same layout (RGBA fp32 images of width x height), for gathers that
+ * land in host memory and for tests of the tile protocol without a device. */
+rt_status rt_pack_tiles_host(int32_t width, int32_t height, const rt_tile_set* tiles, const float* src_rgba,
+                             float* dst_packed);
+rt_status rt_unpack_tiles_host(int32_t width, int32_t height, const rt_tile_set* tiles, const float* src_packed,
+                               float* dst_rgba);
 
 /* Device ray/node counters: when enabled, frames also count BVH node visits / triangle tests
  * (a few percent slower). Ray counts are always collected. */

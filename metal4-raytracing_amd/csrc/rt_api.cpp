@@ -72,7 +72,7 @@ struct rt_ctx {
     // wavefront pipeline state
     WavefrontBuffers wf;
     DevBuf d_wf_color, d_wf_accum, d_wf_meta, d_wf_q0, d_wf_q1, d_wf_hits, d_wf_sq, d_wf_counts, d_wf_mprev, d_wf_extra;
-    int wf_iterations = 0;
+    WfFrameStats wfs{};
     bool last_wavefront = false;
 };
 
@@ -138,6 +138,17 @@ static std::vector<HaltonDim> halton_table() {
     return t;
 }
 
+// SAH build + 8-wide collapse whose group-stack depth fits the kStackSize LDS stack: the binned-SAH
+// builder falls back to median splits past its depth limit, so tighter limits bound the depth.
+static bool build_bvh8_fit(const float* world, uint32_t n, BvhResult& b2, Bvh8Result& b8) {
+    for (int limit : {64, 48, 40, 32, 28, 24, 21}) {
+        b2 = build_bvh2(world, n, 4, limit);
+        b8 = collapse_bvh8(b2);
+        if (b8.max_depth <= kStackSize) return true;
+    }
+    return false;
+}
+
 // host object->world, identical arithmetic to rt::xform on the device
 static void xform_host(const float* m, const float4& p, float* out) {
     for (int r = 0; r < 3; ++r) out[r] = ((m[0 + r] * p.x + m[3 + r] * p.y) + m[6 + r] * p.z) + m[9 + r] * 1.0f;
@@ -161,8 +172,8 @@ static rt_status ensure_wavefront(rt_ctx* c, size_t own_px, int spp, int max_ext
     size_t npix = (size_t)c->width * c->height;
     if (paths >= (1ull << 32)) FAIL(c, RT_ERR_UNSUPPORTED, "too many paths for one frame");
     rt_status st;
-    if (W.cap_paths < paths) {
-        size_t qe = wavefront_queue_entries(paths);
+    if (W.cap_paths < paths || W.queue_entries < wavefront_queue_entries(paths, max_extra)) {
+        size_t qe = wavefront_queue_entries(paths, max_extra);
         if ((st = dev_alloc(c, c->d_wf_color, paths * 16))) return st;
         if ((st = dev_alloc(c, c->d_wf_accum, paths * 16))) return st;
         if ((st = dev_alloc(c, c->d_wf_meta, paths * 16))) return st;
@@ -225,7 +236,7 @@ rt_status rt_create(const rt_opts* opts, rt_ctx** out) {
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipEventCreate(&c->ev0);
     if (e == hipSuccess) e = hipEventCreate(&c->ev1);
-    if (e == hipSuccess) e = hipHostMalloc((void**)&c->h_counters, sizeof(unsigned long long) * kCntSlots, 0);
+    if (e == hipSuccess) e = hipHostMalloc((void**)&c->h_counters, sizeof(unsigned long long) * kCounterWords, 0);
     if (e != hipSuccess) {
         g_err = std::string("HIP init: ") + hipGetErrorString(e);
         delete c;
@@ -234,7 +245,7 @@ rt_status rt_create(const rt_opts* opts, rt_ctx** out) {
     c->stream = c->own_stream;
     auto tab = halton_table();
     rt_status st = dev_upload(c, c->d_halton, tab.data(), tab.size() * sizeof(HaltonDim));
-    if (!st) st = dev_alloc(c, c->d_counters, sizeof(unsigned long long) * kCntSlots);
+    if (!st) st = dev_alloc(c, c->d_counters, sizeof(unsigned long long) * kCounterWords);
     if (!st && hipStreamSynchronize(c->stream) != hipSuccess) st = RT_ERR_HIP;
     if (st) {
         g_err = c->err;
@@ -403,9 +414,8 @@ rt_status rt_bvh_build(rt_ctx* c) {
         }
         c->world_dirty = false;
     }
-    c->bvh = build_bvh2(c->h_world.data(), c->num_tris, 4, kStackSize - 2);
-    c->bvh8 = collapse_bvh8(c->bvh);
-    if (c->bvh8.max_depth > kStackSize) FAIL(c, RT_ERR_STATE, "BVH deeper than traversal stack");
+    if (!build_bvh8_fit(c->h_world.data(), c->num_tris, c->bvh, c->bvh8))
+        FAIL(c, RT_ERR_UNSUPPORTED, "BVH deeper than the traversal stack at every depth limit");
     if (c->bvh8.nodes.size() >= (1u << 23)) FAIL(c, RT_ERR_UNSUPPORTED, "BVH too large (2^23 nodes)");
     const uint32_t n = c->num_tris;
     std::vector<float4> tris(3 * (size_t)n);
@@ -554,7 +564,6 @@ rt_status rt_render_frame(rt_ctx* c, const Uniforms* U, const rt_tile_set* tiles
     }
     DevScene S;
     S.tris = (const float4*)c->d_tris.p;
-    S.nodes = nullptr;
     S.nodes8 = (const Bvh8Node*)c->d_nodes.p;
     S.tri_info = (const uint4*)c->d_tri_info.p;
     S.pos = (const float4*)c->d_pos.p;
@@ -580,7 +589,7 @@ rt_status rt_render_frame(rt_ctx* c, const Uniforms* U, const rt_tile_set* tiles
     P.rank = rank;
     P.nranks = nranks;
     P.tiles_x = tiles_x;
-    HIPC(c, hipMemsetAsync(c->d_counters.p, 0, sizeof(unsigned long long) * kCntSlots, c->stream));
+    HIPC(c, hipMemsetAsync(c->d_counters.p, 0, sizeof(unsigned long long) * kCounterWords, c->stream));
     // DebugTextureModeMotion reads sample 0's motion from later samples of the same pixel
     // (Raytracing.metal:483): only the per-pixel kernel orders samples that way.
     bool wavefront = c->pipeline == RT_PIPELINE_WAVEFRONT && U->debugTextureMode != DebugTextureModeMotion;
@@ -593,8 +602,10 @@ rt_status rt_render_frame(rt_ctx* c, const Uniforms* U, const rt_tile_set* tiles
     for (float& k : c->stats.kernel_ms) k = 0.0f;
     if (wavefront) {
         const char* err = nullptr;
-        if (own > 0 && !run_wavefront(S, P, c->wf, own, c->counting, c->stream, c->stats.kernel_ms, &c->wf_iterations, &err))
+        c->wfs = WfFrameStats{};
+        if (own > 0 && !run_wavefront(S, P, c->wf, own, c->counting, c->stream, &c->wfs, &err))
             FAIL(c, RT_ERR_HIP, std::string("wavefront: ") + (err ? err : "?"));
+        std::memcpy(c->stats.kernel_ms, c->wfs.stage_ms, sizeof c->stats.kernel_ms);
     } else {
         int nblocks = own * (ts / 16) * (ts / 16);
         if (nblocks > 0) launch_megakernel(S, P, nblocks, c->counting, c->stream);
@@ -602,7 +613,7 @@ rt_status rt_render_frame(rt_ctx* c, const Uniforms* U, const rt_tile_set* tiles
     HIPC(c, hipGetLastError());
     HIPC(c, hipEventRecord(c->ev1, c->stream));
     c->last_wavefront = wavefront;
-    HIPC(c, hipMemcpyAsync(c->h_counters, c->d_counters.p, sizeof(unsigned long long) * kCntSlots,
+    HIPC(c, hipMemcpyAsync(c->h_counters, c->d_counters.p, sizeof(unsigned long long) * kCounterWords,
                            hipMemcpyDeviceToHost, c->stream));
     c->read_idx = 1 - c->read_idx;  // swap accumulationTargets (Renderer.swift:1492-1494)
     c->frame_pending = true;
@@ -619,14 +630,24 @@ rt_status rt_wait(rt_ctx* c) {
         c->stats.last_frame_ms = ms;
         if (!c->last_wavefront) c->stats.kernel_ms[0] = ms;
         c->stats.pipeline = c->last_wavefront ? RT_PIPELINE_WAVEFRONT : RT_PIPELINE_MEGAKERNEL;
-        c->stats.iterations = c->last_wavefront ? c->wf_iterations : 0;
-        c->stats.closest_rays = c->h_counters[kCntClosest];
-        c->stats.shadow_rays = c->h_counters[kCntShadow];
-        c->stats.node_visits = c->h_counters[kCntNodes];
-        c->stats.tri_tests = c->h_counters[kCntTris];
-        c->stats.paths = c->h_counters[kCntPaths];
+        c->stats.iterations = c->last_wavefront ? c->wfs.iterations : 0;
+        c->stats.trace_rays = c->last_wavefront ? c->wfs.trace_rays : 0;
+        c->stats.trace_launches = c->last_wavefront ? c->wfs.trace_launches : 0;
+        c->stats.trace_ms = c->last_wavefront ? c->wfs.trace_ms : 0.0f;
+        auto total = [c](int slot) {
+            unsigned long long t = 0;
+            for (int r = 0; r < kCntReplicas; ++r) t += c->h_counters[cnt_word(slot, r)];
+            return t;
+        };
+        c->stats.closest_rays = total(kCntClosest);
+        c->stats.shadow_rays = total(kCntShadow);
+        c->stats.node_visits = total(kCntNodes);
+        c->stats.tri_tests = total(kCntTris);
+        c->stats.paths = total(kCntPaths);
+        c->stats.trace_nodes = c->last_wavefront ? total(kCntTraceNodes) : 0;
+        c->stats.trace_tris = c->last_wavefront ? total(kCntTraceTris) : 0;
         c->frame_pending = false;
-        if (c->h_counters[kCntOverflow]) FAIL(c, RT_ERR_STATE, "traversal stack overflow");
+        if (total(kCntOverflow)) FAIL(c, RT_ERR_STATE, "traversal stack overflow");
     }
     return RT_OK;
 }
@@ -681,6 +702,44 @@ rt_status rt_unpack_tiles(rt_ctx* c, const rt_tile_set* t, const void* src) {
     return RT_OK;
 }
 
+static rt_status host_tiles(int32_t w, int32_t h, const rt_tile_set* t, int& ts, int& rank, int& nranks, int& tiles_x,
+                            int& own) {
+    ts = (t && t->tile_size > 0) ? t->tile_size : 64;
+    nranks = (t && t->nranks > 0) ? t->nranks : 1;
+    rank = (t && t->nranks > 0) ? t->rank : 0;
+    if (w <= 0 || h <= 0 || rank < 0 || rank >= nranks) FAIL((rt_ctx*)nullptr, RT_ERR_INVALID_ARG, "bad tile set");
+    tiles_x = (w + ts - 1) / ts;
+    own = rt_tile_count(w, h, t);
+    return RT_OK;
+}
+
+rt_status rt_pack_tiles_host(int32_t w, int32_t h, const rt_tile_set* t, const float* src, float* dst) {
+    if (!src || !dst) FAIL((rt_ctx*)nullptr, RT_ERR_INVALID_ARG, "null argument");
+    int ts, rank, nranks, tiles_x, own;
+    rt_status st = host_tiles(w, h, t, ts, rank, nranks, tiles_x, own);
+    if (st) return st;
+    for (size_t i = 0; i < (size_t)ts * ts * own; ++i) {
+        int x, y;
+        tile_pixel(i, ts, rank, nranks, tiles_x, x, y);
+        for (int q = 0; q < 4; ++q) dst[4 * i + q] = (x < w && y < h) ? src[4 * ((size_t)y * w + x) + q] : 0.0f;
+    }
+    return RT_OK;
+}
+
+rt_status rt_unpack_tiles_host(int32_t w, int32_t h, const rt_tile_set* t, const float* src, float* dst) {
+    if (!src || !dst) FAIL((rt_ctx*)nullptr, RT_ERR_INVALID_ARG, "null argument");
+    int ts, rank, nranks, tiles_x, own;
+    rt_status st = host_tiles(w, h, t, ts, rank, nranks, tiles_x, own);
+    if (st) return st;
+    for (size_t i = 0; i < (size_t)ts * ts * own; ++i) {
+        int x, y;
+        tile_pixel(i, ts, rank, nranks, tiles_x, x, y);
+        if (x < w && y < h)
+            for (int q = 0; q < 4; ++q) dst[4 * ((size_t)y * w + x) + q] = src[4 * i + q];
+    }
+    return RT_OK;
+}
+
 rt_status rt_set_counting(rt_ctx* c, int32_t enabled) {
     if (!c) FAIL(c, RT_ERR_INVALID_ARG, "null ctx");
     c->counting = enabled != 0;
@@ -719,8 +778,9 @@ rt_status rt_debug_trace_host(const rt_scene_desc* sd, const float* rays, const 
         }
     }
     uint32_t nt = (uint32_t)(world.size() / 9);
-    BvhResult bvh2 = build_bvh2(world.data(), nt, 4, kStackSize - 2);
-    Bvh8Result bvh = collapse_bvh8(bvh2);
+    BvhResult bvh2;
+    Bvh8Result bvh;
+    if (!build_bvh8_fit(world.data(), nt, bvh2, bvh)) FAIL((rt_ctx*)nullptr, RT_ERR_UNSUPPORTED, "BVH too deep");
     std::vector<float4> tris(3 * (size_t)nt);
     for (uint32_t k = 0; k < nt; ++k) {
         uint32_t id = bvh.tri_order[k];

@@ -17,12 +17,11 @@
 
 namespace rt {
 
-constexpr int kStackSize = 32;   // per-thread traversal stack entries (LDS)
+constexpr int kStackSize = 16;   // per-thread traversal stack entries (LDS): node groups of the 8-wide BVH
 constexpr int kBlock = 256;      // threads per block for the traversal kernels
 
 struct DevScene {
     const float4* tris;
-    const Bvh2Node* nodes;
     const Bvh8Node* nodes8;
     const uint4* tri_info;
     const float4* pos;
@@ -56,89 +55,13 @@ struct TraceCounters {
     uint32_t tris;
 };
 
-// Closest-hit (ANY=false) or any-hit (ANY=true) traversal with a per-thread LDS stack.
-// stack: this thread's column of a [kStackSize][kBlock] LDS array (stride kBlock words).
-template <bool ANY, bool COUNT>
-__host__ __device__ __forceinline__ bool trace(const DevScene& S, f3 o, f3 d, float tmin, float tmax, Hit& hit,
-                                      int* stack, TraceCounters& cnt, bool& overflow) {
-    RayPre pre = ray_precompute(d);
-    // conservative slab test (boxes are padded at build time; see rt_bvh.h)
-    auto safe_inv = [](float x) {
-        float ax = fabsf(x);
-        return 1.0f / (ax < 1e-30f ? copysignf(1e-30f, x) : x);
-    };
-    const float ix = safe_inv(d.x), iy = safe_inv(d.y), iz = safe_inv(d.z);
-    const float ox = o.x * ix, oy = o.y * iy, oz = o.z * iz;
-    float best = tmax;
-    uint32_t best_id = 0xffffffffu;
-    float bu = 0.0f, bv = 0.0f;
-    int sp = 0;
-    int node = 0;
-    const float4* tris = S.tris;
-    while (true) {
-        const float4* np = reinterpret_cast<const float4*>(S.nodes + node);
-        float4 nx = np[0], ny = np[1], nz = np[2];
-        int4 meta = *reinterpret_cast<const int4*>(np + 3);
-        if (COUNT) cnt.nodes++;
-        float tf = best * 1.0000004f;
-        float a0 = __builtin_fmaf(nx.x, ix, -ox), b0 = __builtin_fmaf(nx.y, ix, -ox);
-        float a1 = __builtin_fmaf(ny.x, iy, -oy), b1 = __builtin_fmaf(ny.y, iy, -oy);
-        float a2 = __builtin_fmaf(nz.x, iz, -oz), b2 = __builtin_fmaf(nz.y, iz, -oz);
-        float n0 = fmaxf(fmaxf(fminf(a0, b0), fminf(a1, b1)), fmaxf(fminf(a2, b2), tmin));
-        float f0 = fminf(fminf(fmaxf(a0, b0), fmaxf(a1, b1)), fminf(fmaxf(a2, b2), tf));
-        float c0 = __builtin_fmaf(nx.z, ix, -ox), d0 = __builtin_fmaf(nx.w, ix, -ox);
-        float c1 = __builtin_fmaf(ny.z, iy, -oy), d1 = __builtin_fmaf(ny.w, iy, -oy);
-        float c2 = __builtin_fmaf(nz.z, iz, -oz), d2 = __builtin_fmaf(nz.w, iz, -oz);
-        float n1 = fmaxf(fmaxf(fminf(c0, d0), fminf(c1, d1)), fmaxf(fminf(c2, d2), tmin));
-        float f1 = fminf(fminf(fmaxf(c0, d0), fmaxf(c1, d1)), fminf(fmaxf(c2, d2), tf));
-        bool h0 = n0 <= f0, h1 = n1 <= f1;
-        // leaves are intersected in place
-        #pragma unroll
-        for (int s = 0; s < 2; ++s) {
-            bool hs = s == 0 ? h0 : h1;
-            int ch = s == 0 ? meta.x : meta.y;
-            int cnt_s = s == 0 ? meta.z : meta.w;
-            if (hs && ch < 0) {
-                int first = ~ch;
-                for (int k = 0; k < cnt_s; ++k) {
-                    const float4* tp = tris + 3 * (first + k);
-                    float4 v0 = tp[0], v1 = tp[1], v2 = tp[2];
-                    if (COUNT) cnt.tris++;
-                    float t, u, v;
-                    if (intersect_triangle(pre, o, ld3(v0), ld3(v1), ld3(v2), tmin, best, &t, &u, &v)) {
-                        uint32_t id = __builtin_bit_cast(uint32_t, v0.w);
-                        if (ANY) { hit.t = t; hit.id = id; hit.u = u; hit.v = v; return true; }
-                        if (t < best || id < best_id) { best = t; best_id = id; bu = u; bv = v; }
-                    }
-                }
-                if (s == 0) h0 = false; else h1 = false;
-            }
-        }
-        if (h0 && h1) {
-            int near = n0 <= n1 ? meta.x : meta.y;
-            int far = n0 <= n1 ? meta.y : meta.x;
-            if (sp < kStackSize) { stack[sp * kBlock] = far; ++sp; } else { overflow = true; }
-            node = near;
-        } else if (h0) {
-            node = meta.x;
-        } else if (h1) {
-            node = meta.y;
-        } else {
-            if (sp == 0) break;
-            --sp;
-            node = stack[sp * kBlock];
-        }
-    }
-    hit.t = best; hit.id = best_id; hit.u = bu; hit.v = bv;
-    return best_id != 0xffffffffu;
-}
-
 // ---- compressed 8-wide BVH traversal (rt_bvh.h Bvh8Node) --------------------------------------
 struct RaySetup {
     f3 o, d;
     RayPre pre;
     float ix, iy, iz;   // 1 / d (safe)
     float ox, oy, oz;   // o * (1 / d)
+    uint32_t dneg;      // bit a = (d[a] < 0)
 };
 
 __host__ __device__ __forceinline__ RaySetup ray_setup(f3 o, f3 d) {
@@ -146,13 +69,23 @@ __host__ __device__ __forceinline__ RaySetup ray_setup(f3 o, f3 d) {
     R.o = o;
     R.d = d;
     R.pre = ray_precompute(d);
-    auto safe_inv = [](float x) { return 1.0f / (fabsf(x) < 1e-30f ? copysignf(1e-30f, x) : x); };
+    // slab reciprocals only steer the (conservative, padded) box tests: the 1-ulp hardware
+    // reciprocal is enough on the device; triangle tests use the exact RayPre divisions.
+    auto safe_inv = [](float x) {
+        x = fabsf(x) < 1e-30f ? copysignf(1e-30f, x) : x;
+#if defined(__HIP_DEVICE_COMPILE__)
+        return __builtin_amdgcn_rcpf(x);
+#else
+        return 1.0f / x;
+#endif
+    };
     R.ix = safe_inv(d.x);
     R.iy = safe_inv(d.y);
     R.iz = safe_inv(d.z);
     R.ox = o.x * R.ix;
     R.oy = o.y * R.iy;
     R.oz = o.z * R.iz;
+    R.dneg = (d.x < 0.0f ? 1u : 0u) | (d.y < 0.0f ? 2u : 0u) | (d.z < 0.0f ? 4u : 0u);
     return R;
 }
 
@@ -209,8 +142,7 @@ __host__ __device__ __forceinline__ void test_node8(const Bvh8Node* nodes, uint3
     tmask = tm;
     child_base = h1.x;
     tri_base = h1.y;
-    const float dax = axis == 0 ? R.d.x : (axis == 1 ? R.d.y : R.d.z);
-    flip = dax < 0.0f;
+    flip = (R.dneg >> axis) & 1u;   // bit select: a dynamic pick of R.d lowers to a scratch access
 }
 
 __host__ __device__ __forceinline__ int lowest_bit(uint32_t m) { return __builtin_ctz(m); }

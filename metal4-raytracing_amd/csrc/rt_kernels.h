@@ -7,7 +7,11 @@ namespace rt {
 
 constexpr int kHaltonLds = 64;   // first Halton dimensions staged in LDS per block
 
-enum CounterSlot { kCntClosest = 0, kCntShadow = 1, kCntNodes = 2, kCntTris = 3, kCntPaths = 4, kCntOverflow = 5, kCntSlots = 8 };
+// kCntTraceNodes / kCntTraceTris: the share of node / triangle visits made by wf_trace launches
+enum CounterSlot {
+    kCntClosest = 0, kCntShadow = 1, kCntNodes = 2, kCntTris = 3, kCntPaths = 4, kCntOverflow = 5,
+    kCntTraceNodes = 6, kCntTraceTris = 7, kCntSlots = 8
+};
 
 struct FrameParams {
     Uniforms U;
@@ -28,6 +32,40 @@ __device__ __forceinline__ unsigned long long wave_sum(uint32_t v) {
     return s;
 }
 
+// Statistics counters: every (slot, replica) word sits on a 128-B line of its own and a block adds
+// to replica blockIdx % 8 once per slot, so no line sees more than ~1/8 of the blocks' atomics
+// (device-scope atomics on one line serialise at ~88/us).  The host sums the replicas.
+constexpr int kCntReplicas = 8;
+constexpr int kCntLineU64 = 16;
+constexpr int kCounterWords = kCntSlots * kCntReplicas * kCntLineU64;
+__host__ __device__ constexpr uint32_t cnt_word(int slot, int rep) {
+    return ((uint32_t)slot * kCntReplicas + (uint32_t)rep) * kCntLineU64;
+}
+
+// Block-wide flush of the per-thread statistics; every thread of the block must call it.
+// trace_kernel: the node / triangle visits are also added to the kCntTrace* slots.
+__device__ __forceinline__ void block_flush_counters(unsigned long long* counters, uint32_t closest, uint32_t shadow,
+                                                     uint32_t nodes, uint32_t tris, uint32_t paths, bool overflow,
+                                                     bool trace_kernel = false) {
+    __shared__ unsigned long long red[kBlock / 64][kCntSlots];
+    const unsigned long long n = wave_sum(nodes), t = wave_sum(tris);
+    const unsigned long long v[kCntSlots] = {wave_sum(closest), wave_sum(shadow), n, t, wave_sum(paths),
+                                             __ballot(overflow) != 0ull ? 1ull : 0ull,
+                                             trace_kernel ? n : 0ull, trace_kernel ? t : 0ull};
+    const int wave = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) {
+        #pragma unroll
+        for (int k = 0; k < kCntSlots; ++k) red[wave][k] = v[k];
+    }
+    __syncthreads();
+    if (threadIdx.x < kCntSlots) {
+        unsigned long long s = 0;
+        #pragma unroll
+        for (int w = 0; w < kBlock / 64; ++w) s += red[w][threadIdx.x];
+        if (s) atomicAdd(&counters[cnt_word(threadIdx.x, blockIdx.x & (kCntReplicas - 1))], s);
+    }
+}
+
 void launch_megakernel(const DevScene& S, const FrameParams& P, int nblocks, bool count, hipStream_t stream);
 
 // Wavefront pipeline (rt_wavefront.hip): path state SoA indexed by path id
@@ -35,7 +73,11 @@ void launch_megakernel(const DevScene& S, const FrameParams& P, int nblocks, boo
 // {float4 o (w = path id), float4 d}, hit records {t, tri id, u, v}, shadow queue of
 // {float4 o (w = path id), float4 d (w = tmax), float4 contribution}.
 constexpr int kShards = 8;        // queue segments (one allocation counter each)
-constexpr int kWfCountWords = 32; // [0..7] queue 0, [8..15] queue 1, [16..23] shadow, [24] extra allocator
+// Counter slots: [0..7] queue 0, [8..15] queue 1, [16..23] shadow, [24] extra allocator; each slot on a
+// 128-B line of its own (cslot), so the per-XCD shards never contend for one line's atomics.
+constexpr int kCntStride = 32;
+constexpr int kWfCountWords = 32 * kCntStride;
+__host__ __device__ constexpr uint32_t cslot(int c) { return (uint32_t)c * kCntStride; }
 struct WavefrontBuffers {
     size_t queue_entries = 0;     // kShards segments of queue_entries / kShards
     float4* p_color = nullptr;
@@ -44,7 +86,7 @@ struct WavefrontBuffers {
     float4* q[2] = {nullptr, nullptr};
     float4* hits = nullptr;
     float4* sq = nullptr;
-    uint32_t* counts = nullptr;   // device: [0],[1] ray queues, [2] shadow queue, [3] extra-path allocator
+    uint32_t* counts = nullptr;   // device counter slots (see cslot)
     uint32_t* h_counts = nullptr; // pinned host mirror
     float2* motion_prev = nullptr;
     uint2* px_extra = nullptr;    // per own pixel: (first extra path - base_paths, count)
@@ -52,11 +94,30 @@ struct WavefrontBuffers {
     size_t cap_pixels = 0;
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
 };
-// Runs one frame; returns false on a HIP error (message in *err). stage_ms: [0] generate,
-// [1] extend, [2] shade, [3] connect, [4] resolve (+extra-sample bookkeeping).
+// Per-frame measurements of the wavefront pipeline. stage_ms: [0] generate, [1] extend,
+// [2] shade, [3] connect, [4] resolve (+extra-sample bookkeeping), [5] finish.
+struct WfFrameStats {
+    float stage_ms[7];
+    int iterations;
+    unsigned long long trace_rays;  // rays traced by wf_trace launches (extend + connect)
+    int trace_launches;
+    float trace_ms;                 // their summed device time
+};
+// Runs one frame; returns false on a HIP error (message in *err).
 bool run_wavefront(const DevScene& S, const FrameParams& P, WavefrontBuffers& W, int own_tiles, bool count,
-                   hipStream_t stream, float* stage_ms, int* iterations, const char** err);
-size_t wavefront_queue_entries(size_t paths);
+                   hipStream_t stream, WfFrameStats* fs, const char** err);
+size_t wavefront_queue_entries(size_t paths, int max_extra);
+
+// Packed-tile layout of the multi-GPU gather: element i of a rank's packed buffer is pixel
+// (i % T, (i / T) % T) of its (i / T^2)-th own tile; own tile k is tile id rank + k * nranks.
+__host__ __device__ __forceinline__ void tile_pixel(size_t i, int tile, int rank, int nranks, int tiles_x, int& x,
+                                                    int& y) {
+    const size_t per = (size_t)tile * tile;
+    const int k = (int)(i / per), r = (int)(i % per);
+    const int tid = rank + k * nranks;
+    x = (tid % tiles_x) * tile + r % tile;
+    y = (tid / tiles_x) * tile + r / tile;
+}
 
 // Utility kernels (rt_util.hip)
 void launch_pack_tiles(const float4* src, float4* dst, int width, int height, int tile, int rank, int nranks,

@@ -112,20 +112,7 @@ megakernel(DevScene S, FrameParams P) {
             P.gbuffer[3 * plane + pix] = g3;
         }
     }
-    // counters: one atomic per wave
-    unsigned long long c0 = wave_sum(n_closest), c1 = wave_sum(n_shadow), c4 = wave_sum(n_paths);
-    unsigned long long c2 = COUNT ? wave_sum(tc.nodes) : 0ull, c3 = COUNT ? wave_sum(tc.tris) : 0ull;
-    bool of = __ballot(overflow) != 0ull;
-    if (lane == 0) {
-        atomicAdd(&P.counters[kCntClosest], c0);
-        atomicAdd(&P.counters[kCntShadow], c1);
-        if (COUNT) {
-            atomicAdd(&P.counters[kCntNodes], c2);
-            atomicAdd(&P.counters[kCntTris], c3);
-        }
-        atomicAdd(&P.counters[kCntPaths], c4);
-        if (of) atomicAdd(&P.counters[kCntOverflow], 1ull);
-    }
+    block_flush_counters(P.counters, n_closest, n_shadow, COUNT ? tc.nodes : 0u, COUNT ? tc.tris : 0u, n_paths, overflow);
 }
 
 void launch_megakernel(const DevScene& S, const FrameParams& P, int nblocks, bool count, hipStream_t stream) {

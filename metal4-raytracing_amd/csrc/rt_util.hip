@@ -10,22 +10,18 @@ namespace rt {
 // ---- tiles ----------------------------------------------------------------------------------
 __global__ void pack_tiles_k(const float4* __restrict__ src, float4* __restrict__ dst, int width, int height, int tile,
                              int rank, int nranks, int tiles_x, int own) {
-    size_t per = (size_t)tile * tile;
     size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= per * own) return;
-    int k = (int)(i / per), r = (int)(i % per);
-    int tid = rank + k * nranks;
-    int x = (tid % tiles_x) * tile + r % tile, y = (tid / tiles_x) * tile + r / tile;
+    if (i >= (size_t)tile * tile * own) return;
+    int x, y;
+    tile_pixel(i, tile, rank, nranks, tiles_x, x, y);
     dst[i] = (x < width && y < height) ? src[(size_t)y * width + x] : make_float4(0, 0, 0, 0);
 }
 __global__ void unpack_tiles_k(const float4* __restrict__ src, float4* __restrict__ dst, int width, int height, int tile,
                                int rank, int nranks, int tiles_x, int own) {
-    size_t per = (size_t)tile * tile;
     size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= per * own) return;
-    int k = (int)(i / per), r = (int)(i % per);
-    int tid = rank + k * nranks;
-    int x = (tid % tiles_x) * tile + r % tile, y = (tid / tiles_x) * tile + r / tile;
+    if (i >= (size_t)tile * tile * own) return;
+    int x, y;
+    tile_pixel(i, tile, rank, nranks, tiles_x, x, y);
     if (x < width && y < height) dst[(size_t)y * width + x] = src[i];
 }
 void launch_pack_tiles(const float4* src, float4* dst, int width, int height, int tile, int rank, int nranks,

@@ -17,7 +17,7 @@
 // returning atomic per 256 entries (wave ballot + LDS prefix), so no counter word sees more
 // than ~1/2048 of the entries (one word serialises at ~88 atomics/us, MI355X_MICROARCH.md
 // 'dequeue').  Grids are multiples of 8, so segment k only receives chunks c == k (mod 8) and
-// a segment of n/8 + 4096 entries can never overflow.
+// a segment of n/8 + 4096 (+ 256 per extra sample) entries can never overflow.
 //
 // Results are bit-identical to the megakernel: per-path arithmetic is the same shade_step,
 // the accumulation order per path is the reference's (emission of step s, then its shadow
@@ -31,6 +31,11 @@ namespace {
 constexpr uint32_t kTailRaysDefault = 32768;
 static uint32_t tail_rays() {  // RT_TAIL_RAYS overrides (tuning experiments)
     static uint32_t v = [] { const char* e = getenv("RT_TAIL_RAYS"); return e ? (uint32_t)atol(e) : kTailRaysDefault; }();
+    return v;
+}
+
+static int refill_min() {  // RT_REFILL_MIN overrides (tuning experiments)
+    static int v = [] { const char* e = getenv("RT_REFILL_MIN"); return e ? atoi(e) : 8; }();
     return v;
 }
 
@@ -61,6 +66,33 @@ __device__ __forceinline__ uint32_t block_alloc(bool pred, uint32_t* counter, Bl
     }
     __syncthreads();
     uint32_t r = sh.w[wave] + prefix;
+    __syncthreads();
+    return r;
+}
+
+// Block-aggregated allocation of v slots per thread (wave scan + LDS prefix, one atomic per block).
+__device__ __forceinline__ uint32_t block_alloc_n(uint32_t v, uint32_t* counter, BlockAlloc& sh) {
+    const int wave = threadIdx.x >> 6;
+    const uint32_t lane = lane_id();
+    uint32_t incl = v;
+    #pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        uint32_t t = __shfl_up(incl, off, 64);
+        if (lane >= (uint32_t)off) incl += t;
+    }
+    if (lane == 63) sh.w[wave] = incl;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t c0 = sh.w[0], c1 = sh.w[1], c2 = sh.w[2], c3 = sh.w[3];
+        uint32_t tot = c0 + c1 + c2 + c3;
+        uint32_t b = tot ? atomicAdd(counter, tot) : 0u;
+        sh.w[0] = b;
+        sh.w[1] = b + c0;
+        sh.w[2] = b + c0 + c1;
+        sh.w[3] = b + c0 + c1 + c2;
+    }
+    __syncthreads();
+    uint32_t r = sh.w[wave] + incl - v;
     __syncthreads();
     return r;
 }
@@ -102,22 +134,38 @@ struct WfParams {
     uint32_t own_pixels;
     uint32_t seg_cap;      // entries per queue segment
     int spp;
+    int refill_min;        // wf_trace refills once at least this many lanes of a wave are idle
 };
 
-// counts layout: [q*8 + shard] ray queues q = 0, 1; [16 + shard] shadow queue; [24] extra allocator
+// counter slots (cslot): [q*8 + shard] ray queues q = 0, 1; [16 + shard] shadow queue; [24] extra allocator
 constexpr int kCntShadowQ = 16;
 constexpr int kCntExtra = 24;
 
-// dense consumer index g -> entry index of a sharded queue
-__device__ __forceinline__ uint32_t entry_of(const uint32_t* cnt, uint32_t g, uint32_t seg_cap) {
+// Inclusive prefix of a sharded queue's segment counts, loaded once per kernel (uniform, so the
+// loads are scalar and the lookups below stay in registers).
+struct ShardPrefix {
+    uint32_t end[kShards];
+};
+__device__ __forceinline__ ShardPrefix load_prefix(const uint32_t* cnt) {
+    ShardPrefix p;
     uint32_t acc = 0;
     #pragma unroll
     for (int k = 0; k < kShards; ++k) {
-        uint32_t c = cnt[k];
-        if (g < acc + c) return (uint32_t)k * seg_cap + (g - acc);
-        acc += c;
+        acc += __builtin_amdgcn_readfirstlane(cnt[cslot(k)]);
+        p.end[k] = acc;
     }
-    return 0xffffffffu;
+    return p;
+}
+// dense consumer index g (< p.end[kShards - 1]) -> entry index of the sharded queue
+__device__ __forceinline__ uint32_t entry_of(const ShardPrefix& p, uint32_t g, uint32_t seg_cap) {
+    uint32_t k = 0, start = 0;
+    #pragma unroll
+    for (int j = 0; j < kShards - 1; ++j) {
+        const bool past = g >= p.end[j];
+        k = past ? (uint32_t)(j + 1) : k;
+        start = past ? p.end[j] : start;
+    }
+    return k * seg_cap + (g - start);
 }
 
 __device__ __forceinline__ void init_path(const WfParams& Q, uint32_t pid, uint32_t pix, int sample, uint32_t hidx) {
@@ -132,20 +180,10 @@ __device__ __forceinline__ void load_halton(const DevScene& S, HaltonDim* lds) {
 }
 
 __device__ __forceinline__ void flush_counters(const FrameParams& P, uint32_t closest, uint32_t shadow, uint32_t paths,
-                                               const TraceCounters& tc, bool count, bool overflow) {
-    unsigned long long c0 = wave_sum(closest), c1 = wave_sum(shadow), c4 = wave_sum(paths);
-    unsigned long long c2 = count ? wave_sum(tc.nodes) : 0ull, c3 = count ? wave_sum(tc.tris) : 0ull;
-    bool of = __ballot(overflow) != 0ull;
-    if (lane_id() == 0) {
-        if (c0) atomicAdd(&P.counters[kCntClosest], c0);
-        if (c1) atomicAdd(&P.counters[kCntShadow], c1);
-        if (c4) atomicAdd(&P.counters[kCntPaths], c4);
-        if (count) {
-            atomicAdd(&P.counters[kCntNodes], c2);
-            atomicAdd(&P.counters[kCntTris], c3);
-        }
-        if (of) atomicAdd(&P.counters[kCntOverflow], 1ull);
-    }
+                                               const TraceCounters& tc, bool count, bool overflow,
+                                               bool trace_kernel = false) {
+    block_flush_counters(P.counters, closest, shadow, count ? tc.nodes : 0u, count ? tc.tris : 0u, paths, overflow,
+                         trace_kernel);
 }
 
 // per-pixel outputs of a shade step (depth / motion / G-buffer, :342-389, :506-515)
@@ -212,7 +250,7 @@ __global__ void __launch_bounds__(kBlock) wf_generate(DevScene S, FrameParams P,
             n_paths++;
         }
         bool live = valid && U.maxBounces > 0;
-        uint32_t slot = block_alloc(live, &Q.W.counts[shard], ba);
+        uint32_t slot = block_alloc(live, &Q.W.counts[cslot(shard)], ba);
         if (live) {
             qout[2 * slot] = make_float4(o.x, o.y, o.z, __uint_as_float(pid));
             qout[2 * slot + 1] = make_float4(d.x, d.y, d.z, 0.0f);
@@ -232,7 +270,7 @@ __global__ void __launch_bounds__(kBlock) wf_shade(DevScene S, FrameParams P, Wf
     const Uniforms& U = P.U;
     const int next = 1 - cur;
     const int shard = blockIdx.x & (kShards - 1);
-    const uint32_t* cnt = Q.W.counts + cur * kShards;
+    const ShardPrefix cnt = load_prefix(Q.W.counts + cslot(cur * kShards));
     const float4* qin = Q.W.q[cur];
     float4* qout = Q.W.q[next] + 2 * (size_t)shard * Q.seg_cap;
     float4* sqout = Q.W.sq + 3 * (size_t)shard * Q.seg_cap;
@@ -276,13 +314,13 @@ __global__ void __launch_bounds__(kBlock) wf_shade(DevScene S, FrameParams P, Wf
                 if (r.next) Q.W.p_meta[pid] = make_uint4(meta.x, meta.y, pack_state(p.bounce, p.tpass, p.step), meta.w);
             }
         }
-        uint32_t ns = block_alloc(r.shadow, &Q.W.counts[kCntShadowQ + shard], ba_sh);
+        uint32_t ns = block_alloc(r.shadow, &Q.W.counts[cslot(kCntShadowQ + shard)], ba_sh);
         if (r.shadow) {
             sqout[3 * (size_t)ns] = make_float4(r.so.x, r.so.y, r.so.z, __uint_as_float(pid));
             sqout[3 * (size_t)ns + 1] = make_float4(r.sd.x, r.sd.y, r.sd.z, r.stmax);
             sqout[3 * (size_t)ns + 2] = make_float4(r.contrib.x, r.contrib.y, r.contrib.z, 0.0f);
         }
-        uint32_t nr = block_alloc(r.next, &Q.W.counts[next * kShards + shard], ba_ray);
+        uint32_t nr = block_alloc(r.next, &Q.W.counts[cslot(next * kShards + shard)], ba_ray);
         if (r.next) {
             qout[2 * (size_t)nr] = make_float4(rayO.x, rayO.y, rayO.z, __uint_as_float(pid));
             qout[2 * (size_t)nr + 1] = make_float4(rayD.x, rayD.y, rayD.z, 0.0f);
@@ -300,16 +338,14 @@ template <bool ANY, bool COUNT>
 __global__ void __launch_bounds__(kBlock) wf_trace(DevScene S, FrameParams P, WfParams Q, int cur, uint32_t n_host) {
     __shared__ int lds_stack[kStackSize * kBlock];
     int* stack = &lds_stack[threadIdx.x];
-    const uint32_t* cnt = ANY ? Q.W.counts + kCntShadowQ : Q.W.counts + cur * kShards;
+    const ShardPrefix cnt = load_prefix(ANY ? Q.W.counts + cslot(kCntShadowQ) : Q.W.counts + cslot(cur * kShards));
     uint32_t n = n_host;
     if (ANY) {
-        n = 0;
-        #pragma unroll
-        for (int k = 0; k < kShards; ++k) n += cnt[k];
+        n = cnt.end[kShards - 1];
     } else if (blockIdx.x == 0 && threadIdx.x < 2 * kShards) {  // reset the queues shade / connect fill
         const int next = 1 - cur;
         uint32_t k = threadIdx.x & (kShards - 1);
-        Q.W.counts[threadIdx.x < kShards ? next * kShards + k : kCntShadowQ + k] = 0;
+        Q.W.counts[cslot(threadIdx.x < kShards ? next * kShards + k : kCntShadowQ + k)] = 0;
     }
     const float4* qin = ANY ? Q.W.sq : Q.W.q[cur];
     const int qstride = ANY ? 3 : 2;
@@ -336,7 +372,7 @@ __global__ void __launch_bounds__(kBlock) wf_trace(DevScene S, FrameParams P, Wf
     while (true) {
         // refill idle lanes from the wave's range
         unsigned long long idle = __ballot(!active);
-        if (idle != 0ull && wnext < wend) {
+        if (idle != 0ull && wnext < wend && (__popcll(idle) >= Q.refill_min || idle == ~0ull)) {
             if (!active) {
                 uint32_t g = wnext + mbcnt64(idle);
                 if (g < wend) {
@@ -420,7 +456,7 @@ __global__ void __launch_bounds__(kBlock) wf_trace(DevScene S, FrameParams P, Wf
             }
         }
     }
-    flush_counters(P, ANY ? 0 : rays, ANY ? rays : 0, 0, tc, COUNT, overflow);
+    flush_counters(P, ANY ? 0 : rays, ANY ? rays : 0, 0, tc, COUNT, overflow, true);
 }
 
 // ---- finish: run the remaining paths to completion --------------------------------------------------
@@ -431,7 +467,7 @@ __global__ void __launch_bounds__(kBlock) wf_finish(DevScene S, FrameParams P, W
     load_halton(S, lds_halton);
     const HaltonTab halton{lds_halton, S.halton};
     const Uniforms& U = P.U;
-    const uint32_t* cnt = Q.W.counts + cur * kShards;
+    const ShardPrefix cnt = load_prefix(Q.W.counts + cslot(cur * kShards));
     const float4* qin = Q.W.q[cur];
     int* stack = &lds_stack[threadIdx.x];
     TraceCounters tc{0, 0};
@@ -487,41 +523,45 @@ __global__ void __launch_bounds__(kBlock) wf_extra(DevScene S, FrameParams P, Wf
     const int stride = Q.spp + maxExtra;
     const int shard = blockIdx.x & (kShards - 1);
     float4* qout = Q.W.q[qidx] + 2 * (size_t)shard * Q.seg_cap;
-    uint32_t i = blockIdx.x * kBlock + threadIdx.x;
-    if (i >= Q.own_pixels) return;
-    int px, py;
-    own_pixel(P, i, px, py);
-    uint2 ex = make_uint2(0u, 0u);
-    if (px < U.width && py < U.height) {
-        uint32_t pix = (uint32_t)py * (uint32_t)U.width + (uint32_t)px;
-        float2 mv2 = P.motion[pix], pm2 = Q.W.motion_prev[pix];
-        f2 mv, pm;
-        mv.x = mv2.x;
-        mv.y = mv2.y;
-        pm.x = pm2.x;
-        pm.y = pm2.y;
-        int e = extra_samples(U, maxExtra, mv, pm);
-        if (e > 0) {
-            uint32_t start = atomicAdd(&Q.W.counts[kCntExtra], (uint32_t)e);
-            ex = make_uint2(start, (uint32_t)e);
-            uint32_t offset = P.random[pix];
-            for (int j = 0; j < e; ++j) {
-                int s = Q.spp + j;
-                uint32_t pid = Q.base_paths + start + (uint32_t)j;
-                int hidx = (int)(offset + (unsigned)((int)U.frameIndex * stride + s));
-                init_path(Q, pid, pix, s, (uint32_t)hidx);
-                f3 o, d;
-                primary_ray(U, halton, px, py, hidx, o, d);
-                atomicAdd(&P.counters[kCntPaths], 1ull);
-                if (U.maxBounces > 0) {
-                    uint32_t slot = atomicAdd(&Q.W.counts[qidx * kShards + shard], 1u);
-                    qout[2 * (size_t)slot] = make_float4(o.x, o.y, o.z, __uint_as_float(pid));
-                    qout[2 * (size_t)slot + 1] = make_float4(d.x, d.y, d.z, 0.0f);
-                }
+    __shared__ BlockAlloc ba;
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    int px = 0, py = 0, e = 0;
+    uint32_t pix = 0;
+    if (i < Q.own_pixels) {
+        own_pixel(P, i, px, py);
+        if (px < U.width && py < U.height) {
+            pix = (uint32_t)py * (uint32_t)U.width + (uint32_t)px;
+            float2 mv2 = P.motion[pix], pm2 = Q.W.motion_prev[pix];
+            f2 mv, pm;
+            mv.x = mv2.x;
+            mv.y = mv2.y;
+            pm.x = pm2.x;
+            pm.y = pm2.y;
+            e = extra_samples(U, maxExtra, mv, pm);
+        }
+    }
+    const uint32_t start = block_alloc_n((uint32_t)e, &Q.W.counts[cslot(kCntExtra)], ba);
+    const uint32_t slot0 =
+        block_alloc_n(U.maxBounces > 0 ? (uint32_t)e : 0u, &Q.W.counts[cslot(qidx * kShards + shard)], ba);
+    if (e > 0) {
+        const uint32_t offset = P.random[pix];
+        for (int j = 0; j < e; ++j) {
+            int s = Q.spp + j;
+            uint32_t pid = Q.base_paths + start + (uint32_t)j;
+            int hidx = (int)(offset + (unsigned)((int)U.frameIndex * stride + s));
+            init_path(Q, pid, pix, s, (uint32_t)hidx);
+            f3 o, d;
+            primary_ray(U, halton, px, py, hidx, o, d);
+            if (U.maxBounces > 0) {
+                const uint32_t slot = slot0 + (uint32_t)j;
+                qout[2 * (size_t)slot] = make_float4(o.x, o.y, o.z, __uint_as_float(pid));
+                qout[2 * (size_t)slot + 1] = make_float4(d.x, d.y, d.z, 0.0f);
             }
         }
     }
-    Q.W.px_extra[i] = ex;
+    if (i < Q.own_pixels) Q.W.px_extra[i] = make_uint2(start, (uint32_t)e);
+    TraceCounters tc{0, 0};
+    flush_counters(P, 0, 0, (uint32_t)e, tc, false, false);
 }
 
 // ---- resolve (:777, :792-819) -------------------------------------------------------------------------
@@ -557,7 +597,11 @@ __global__ void __launch_bounds__(kBlock) wf_resolve(DevScene S, FrameParams P, 
     P.accum_out[pix] = make_float4(c.x, c.y, c.z, 1.0f);
 }
 
-size_t wavefront_queue_entries(size_t paths) { return (size_t)kShards * (paths / kShards + 4096); }
+// Segment k only receives entries from blocks b == k (mod 8): at most n/8 + 256 per pass over n
+// inputs, and (own pixels/8 + 256) * maxExtra from the extra-sample pass.
+size_t wavefront_queue_entries(size_t paths, int max_extra) {
+    return (size_t)kShards * (paths / kShards + 4096 + 256 * (size_t)max_extra);
+}
 
 static unsigned grid_for(uint32_t n, unsigned cap) {
     unsigned g = (unsigned)((n + kBlock - 1) / kBlock);
@@ -590,12 +634,13 @@ static unsigned trace_grid_cap() {
 
 static uint32_t queue_total(const uint32_t* h, int q) {
     uint32_t s = 0;
-    for (int k = 0; k < kShards; ++k) s += h[q * kShards + k];
+    for (int k = 0; k < kShards; ++k) s += h[cslot(q * kShards + k)];
     return s;
 }
 
 static bool iterate(const DevScene& S, const FrameParams& P, WfParams& Q, int& cur, uint32_t n, bool count, bool full,
-                    hipStream_t stream, float* stage_ms, int* iterations, const char** err) {
+                    hipStream_t stream, WfFrameStats* fs, const char** err) {
+    float* stage_ms = fs->stage_ms;
     const int max_it = P.U.maxBounces * (P.U.maxBounces + 1) + 2;
     WavefrontBuffers& W = Q.W;
     for (int it = 0; it < max_it && n > 0; ++it) {
@@ -616,7 +661,7 @@ static bool iterate(const DevScene& S, const FrameParams& P, WfParams& Q, int& c
             float a = 0;
             WF_CHECK(hipEventElapsedTime(&a, W.ev[0], W.ev[1]));
             stage_ms[5] += a;
-            ++*iterations;
+            ++fs->iterations;
             return true;
         }
         int next = 1 - cur;
@@ -642,23 +687,27 @@ static bool iterate(const DevScene& S, const FrameParams& P, WfParams& Q, int& c
         stage_ms[1] += a;
         stage_ms[2] += b;
         stage_ms[3] += c;
+        fs->trace_rays += (unsigned long long)n + queue_total(W.h_counts, 2);  // extend + connect rays
+        fs->trace_launches += 2;
+        fs->trace_ms += a + c;
         n = queue_total(W.h_counts, next);
         cur = next;
-        ++*iterations;
+        ++fs->iterations;
     }
     return true;
 }
 
 bool run_wavefront(const DevScene& S, const FrameParams& P, WavefrontBuffers& W, int own_tiles, bool count,
-                   hipStream_t stream, float* stage_ms, int* iterations, const char** err) {
+                   hipStream_t stream, WfFrameStats* fs, const char** err) {
     WfParams Q;
     Q.W = W;
     Q.spp = max(P.U.samplesPerPixel, 1);
     Q.own_pixels = (uint32_t)own_tiles * (uint32_t)P.tile_size * (uint32_t)P.tile_size;
     Q.base_paths = Q.own_pixels * (uint32_t)Q.spp;
     Q.seg_cap = (uint32_t)(W.queue_entries / kShards);
-    *iterations = 0;
-    for (int k = 0; k < 7; ++k) stage_ms[k] = 0.0f;
+    Q.refill_min = refill_min();
+    *fs = WfFrameStats{};
+    float* stage_ms = fs->stage_ms;
     const bool full = needs_full(P.U);
     const int maxExtra = (P.U.enableMotionAdaptiveSampling != 0) ? max(P.U.motionSamplingMaxExtraSamples, 0) : 0;
     size_t npix = (size_t)P.U.width * P.U.height;
@@ -675,19 +724,19 @@ bool run_wavefront(const DevScene& S, const FrameParams& P, WavefrontBuffers& W,
     WF_CHECK(hipEventElapsedTime(&ms, W.ev[0], W.ev[1]));
     stage_ms[0] += ms;
     int cur = 0;
-    if (!iterate(S, P, Q, cur, queue_total(W.h_counts, 0), count, full, stream, stage_ms, iterations, err)) return false;
+    if (!iterate(S, P, Q, cur, queue_total(W.h_counts, 0), count, full, stream, fs, err)) return false;
 
     WF_CHECK(hipEventRecord(W.ev[0], stream));
     if (maxExtra > 0) {
         // the extra-sample pass appends primary rays to queue `cur` (reset here)
-        WF_CHECK(hipMemsetAsync(W.counts + cur * kShards, 0, kShards * sizeof(uint32_t), stream));
+        WF_CHECK(hipMemsetAsync(W.counts + cslot(cur * kShards), 0, cslot(kShards) * sizeof(uint32_t), stream));
         hipLaunchKernelGGL(wf_extra, dim3(grid_for(Q.own_pixels, 1u << 30)), dim3(kBlock), 0, stream, S, P, Q, cur);
         WF_CHECK(hipGetLastError());
         WF_CHECK(hipMemcpyAsync(W.h_counts, W.counts, kWfCountWords * sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
         WF_CHECK(hipStreamSynchronize(stream));
         uint32_t n_extra = queue_total(W.h_counts, cur);
         if (n_extra > 0) {
-            if (!iterate(S, P, Q, cur, n_extra, count, full, stream, stage_ms, iterations, err)) return false;
+            if (!iterate(S, P, Q, cur, n_extra, count, full, stream, fs, err)) return false;
         }
     }
     hipLaunchKernelGGL(wf_resolve, dim3(grid_for(Q.own_pixels, 1u << 30)), dim3(kBlock), 0, stream, S, P, Q,
