@@ -1,7 +1,7 @@
 #!/bin/bash
 # usage: gpurun_cmp.sh  -> GPU tests + bench of both pipelines
 mkdir -p gpurun_out
-timeout -k 10 400 python -m pytest tests/test_gpu_parity.py -x -q -m gpu > gpurun_out/t.log 2>&1
+timeout -k 10 400 python -m pytest tests -x -q -m gpu > gpurun_out/t.log 2>&1
 rc=$?; echo "TEST rc=$rc"; tail -4 gpurun_out/t.log
 if [ $rc -gt 1 ]; then echo "tests crashed/timed out; stopping"; exit $rc; fi
 for p in wavefront megakernel; do

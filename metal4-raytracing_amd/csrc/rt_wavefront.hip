@@ -39,6 +39,11 @@ static int refill_min() {  // RT_REFILL_MIN overrides (tuning experiments)
     return v;
 }
 
+static int tri_vote() {  // RT_TRI_VOTE overrides (tuning experiments)
+    static int v = [] { const char* e = getenv("RT_TRI_VOTE"); return e ? atoi(e) : 0; }();
+    return v;
+}
+
 __device__ __forceinline__ uint32_t lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
 __device__ __forceinline__ uint32_t mbcnt64(unsigned long long m) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
@@ -135,6 +140,7 @@ struct WfParams {
     uint32_t seg_cap;      // entries per queue segment
     int spp;
     int refill_min;        // wf_trace refills once at least this many lanes of a wave are idle
+    int tri_vote;          // wf_trace phase vote threshold (lanes with triangle work), 0 = off
 };
 
 // counter slots (cslot): [q*8 + shard] ray queues q = 0, 1; [16 + shard] shadow queue; [24] extra allocator
@@ -335,7 +341,7 @@ __global__ void __launch_bounds__(kBlock) wf_shade(DevScene S, FrameParams P, Wf
 // triangle.  The wave therefore runs ~(total units of its rays)/64 iterations instead of
 // (slowest ray) x (rays per lane).
 template <bool ANY, bool COUNT>
-__global__ void __launch_bounds__(kBlock) wf_trace(DevScene S, FrameParams P, WfParams Q, int cur, uint32_t n_host) {
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) wf_trace(DevScene S, FrameParams P, WfParams Q, int cur, uint32_t n_host) {
     __shared__ int lds_stack[kStackSize * kBlock];
     int* stack = &lds_stack[threadIdx.x];
     const ShardPrefix cnt = load_prefix(ANY ? Q.W.counts + cslot(kCntShadowQ) : Q.W.counts + cslot(cur * kShards));
@@ -398,16 +404,32 @@ __global__ void __launch_bounds__(kBlock) wf_trace(DevScene S, FrameParams P, Wf
         if (!active) continue;
 
         bool done = false;
-        if (t_mask) {
-            // ---- one triangle
-            const int k = lowest_bit(t_mask);
+        // Phase vote: a wave runs EITHER a triangle step OR a node step per iteration, so the
+        // two code paths are never both issued; triangles wait until at least tri_vote lanes
+        // have some (or no lane has node work).  tri_vote == 0: per-lane choice (both issued).
+        bool do_tri = t_mask != 0u, do_node = t_mask == 0u;
+        if (Q.tri_vote > 0) {
+            const unsigned long long bt = __ballot(do_tri), bn = __ballot(do_node);
+            const bool tri_phase = __popcll(bt) >= Q.tri_vote || bn == 0ull;
+            do_tri = do_tri && tri_phase;
+            do_node = do_node && !tri_phase;
+        }
+        if (do_tri) {
+            // ---- up to two triangles: both fetched before either is tested (one memory
+            // latency), tested in mask order so closest-hit updates are those of the serial loop
+            const int k0 = lowest_bit(t_mask);
             t_mask &= t_mask - 1u;
-            const float4* tp = S.tris + 3 * (size_t)(t_base + (uint32_t)k);
-            const float4 v0 = tp[0], v1 = tp[1], v2 = tp[2];
-            if (COUNT) tc.tris++;
+            const bool two = t_mask != 0u;
+            const int k1 = two ? lowest_bit(t_mask) : k0;
+            if (two) t_mask &= t_mask - 1u;
+            const float4* tp0 = S.tris + 3 * (size_t)(t_base + (uint32_t)k0);
+            const float4* tp1 = S.tris + 3 * (size_t)(t_base + (uint32_t)k1);
+            const float4 a0 = tp0[0], a1 = tp0[1], a2 = tp0[2];
+            const float4 b0 = tp1[0], b1 = tp1[1], b2 = tp1[2];
+            if (COUNT) tc.tris += two ? 2u : 1u;
             float t, u, v;
-            if (intersect_triangle(R.pre, R.o, ld3(v0), ld3(v1), ld3(v2), 0.0f, best, &t, &u, &v)) {
-                const uint32_t id = __float_as_uint(v0.w);
+            if (intersect_triangle(R.pre, R.o, ld3(a0), ld3(a1), ld3(a2), 0.0f, best, &t, &u, &v)) {
+                const uint32_t id = __float_as_uint(a0.w);
                 if (ANY) {
                     hit_any = true;
                     done = true;
@@ -418,7 +440,19 @@ __global__ void __launch_bounds__(kBlock) wf_trace(DevScene S, FrameParams P, Wf
                     bv = v;
                 }
             }
-        } else {
+            if (two && !done && intersect_triangle(R.pre, R.o, ld3(b0), ld3(b1), ld3(b2), 0.0f, best, &t, &u, &v)) {
+                const uint32_t id = __float_as_uint(b0.w);
+                if (ANY) {
+                    hit_any = true;
+                    done = true;
+                } else if (t < best || id < best_id) {
+                    best = t;
+                    best_id = id;
+                    bu = u;
+                    bv = v;
+                }
+            }
+        } else if (do_node) {
             // ---- one 8-wide node
             if (!g_hits) {  // sp > 0 here (checked at the end of the previous iteration)
                 --sp;
@@ -706,6 +740,7 @@ bool run_wavefront(const DevScene& S, const FrameParams& P, WavefrontBuffers& W,
     Q.base_paths = Q.own_pixels * (uint32_t)Q.spp;
     Q.seg_cap = (uint32_t)(W.queue_entries / kShards);
     Q.refill_min = refill_min();
+    Q.tri_vote = tri_vote();
     *fs = WfFrameStats{};
     float* stage_ms = fs->stage_ms;
     const bool full = needs_full(P.U);

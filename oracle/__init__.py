@@ -71,6 +71,8 @@ def lib():
             f.restype = C.c_int
         L.rt_oracle_skin.argtypes = [vp, vp, vp, vp, vp, vp, vp, C.c_uint32]
         L.rt_oracle_skin.restype = None
+        L.rt_oracle_scene_set_previous.argtypes = [vp, C.c_uint32, vp, vp]
+        L.rt_oracle_scene_set_previous.restype = C.c_int
         _lib = L
     return _lib
 
@@ -111,6 +113,14 @@ class OracleScene:
         if not hit:
             return None
         return (t.value, i.value, u.value, v.value)
+
+    def set_previous(self, mesh, prev_positions=None, prev_transform=None):
+        """Motion-vector history of one mesh: positions (n,4) f32 before the last skinning tick
+        and/or the previous (4,3) packed transform. The arrays must outlive the scene."""
+        pp = None if prev_positions is None else prev_positions.ctypes.data
+        pt = None if prev_transform is None else np.ascontiguousarray(prev_transform, np.float32).ctypes.data
+        if lib().rt_oracle_scene_set_previous(self._h, mesh, pp, pt) != 0:
+            raise RuntimeError("set_previous failed")
 
     def render(self, uniforms, random, accum_in=None, motion_in=None, gbuffer=False, row_start=0, row_step=1,
                threads=None):

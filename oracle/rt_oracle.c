@@ -241,6 +241,17 @@ int rt_oracle_scene_create(const rt_scene_desc* d, rt_oracle_scene** out) {
     return 0;
 }
 
+/* Previous-frame state of mesh m for motion vectors (Raytracing.metal:342-389): the positions
+ * before the last skinning tick (Renderer.swift:1290-1303) and/or the previous instance
+ * transform (Renderer.swift:939-944).  NULL keeps the current value. */
+int rt_oracle_scene_set_previous(rt_oracle_scene* s, uint32_t m, const rt_float3* prev_positions,
+                                 const float* prev_transform) {
+    if (!s || m >= s->nmesh) return 1;
+    if (prev_positions) s->prev_pos[m] = prev_positions;
+    if (prev_transform) memcpy(s->prev_xf[m], prev_transform, 48);
+    return 0;
+}
+
 void rt_oracle_scene_destroy(rt_oracle_scene* s) {
     if (!s) return;
     for (uint32_t m = 0; m < s->nmesh; ++m) free(s->mats[m]);

@@ -49,6 +49,9 @@ typedef struct rt_oracle_frame {
 
 int rt_oracle_scene_create(const rt_scene_desc* desc, rt_oracle_scene** out);
 void rt_oracle_scene_destroy(rt_oracle_scene* s);
+/* previous-frame positions / instance transform of mesh m for motion vectors; NULL keeps */
+int rt_oracle_scene_set_previous(rt_oracle_scene* s, uint32_t mesh, const rt_float3* prev_positions,
+                                 const float* prev_transform);
 uint32_t rt_oracle_scene_triangles(const rt_oracle_scene* s);
 
 int rt_oracle_render(const rt_oracle_scene* s, rt_oracle_frame* f);
