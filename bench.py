@@ -52,7 +52,7 @@ def parse():
     p.add_argument("--spp", type=int, default=4)
     p.add_argument("--bounces", type=int, default=8)
     p.add_argument("--tile", type=int, default=64)
-    p.add_argument("--pipeline", default="megakernel")
+    p.add_argument("--pipeline", default="wavefront", choices=["wavefront", "megakernel"])
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample time")
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--traffic-csv", default=None, help="rocprofv3 --pmc counter_collection.csv for traffic")

@@ -212,7 +212,7 @@ class Renderer:
     draw() = updateUniforms + raytracingKernel dispatch + accumulation swap.
     """
 
-    def __init__(self, scene, width, height, device=0, pipeline="megakernel", seed=1, stream=None):
+    def __init__(self, scene, width, height, device=0, pipeline="wavefront", seed=1, stream=None):
         object.__setattr__(self, "_ctx", None)
         self.scene = scene
         self.width, self.height = int(width), int(height)

@@ -576,6 +576,7 @@ rt_status rt_render_frame(rt_ctx* c, const Uniforms* U, const rt_tile_set* tiles
     S.halton = (const HaltonDim*)c->d_halton.p;
     S.max_submeshes = c->max_sub;
     S.num_tris = (int)c->num_tris;
+    S.num_nodes8 = (int)c->bvh8.nodes.size();
     FrameParams P;
     P.U = *U;
     P.random = (const uint32_t*)c->d_random.p;
@@ -796,6 +797,7 @@ rt_status rt_debug_trace_host(const rt_scene_desc* sd, const float* rays, const 
     S.tris = tris.data();
     S.nodes8 = bvh.nodes.data();
     S.num_tris = (int)nt;
+    S.num_nodes8 = (int)bvh.nodes.size();
     std::vector<int> stack((size_t)kStackSize * kBlock);
     for (uint32_t r = 0; r < n; ++r) {
         const float* q = rays + 6 * (size_t)r;

@@ -19,6 +19,7 @@ namespace rt {
 
 constexpr int kStackSize = 16;   // per-thread traversal stack entries (LDS): node groups of the 8-wide BVH
 constexpr int kBlock = 256;      // threads per block for the traversal kernels
+constexpr int kTopNodes = 32;    // first BFS nodes of the 8-wide BVH staged in LDS by wf_trace
 
 struct DevScene {
     const float4* tris;
@@ -34,6 +35,7 @@ struct DevScene {
     const HaltonDim* halton;
     int max_submeshes;
     int num_tris;
+    int num_nodes8;
 };
 
 struct Hit {
@@ -94,15 +96,27 @@ __host__ __device__ __forceinline__ float byte_f(uint32_t w, int b) { return (fl
 // Slab-test the 8 children of node `ni` (five 16-byte loads).  Returns the internal children hit
 // (bit r = internal rank r), the triangles to test (bit k = triangle tri_base + k), and the
 // traversal direction of the node's slot order.
-__host__ __device__ __forceinline__ void test_node8(const Bvh8Node* nodes, uint32_t ni, const RaySetup& R, float tmin,
-                                                    float tmax, uint32_t& ihits, uint32_t& tmask,
-                                                    uint32_t& child_base, uint32_t& tri_base, bool& flip) {
-    const float4* np = reinterpret_cast<const float4*>(nodes + ni);
-    const float4 h0 = np[0];
-    const uint4 h1 = *reinterpret_cast<const uint4*>(np + 1);
-    const uint4 qx = *reinterpret_cast<const uint4*>(np + 2);
-    const uint4 qy = *reinterpret_cast<const uint4*>(np + 3);
-    const uint4 qz = *reinterpret_cast<const uint4*>(np + 4);
+// The five 16-byte words of a node (from global memory or an LDS copy).
+struct NodeWords {
+    float4 h0;
+    uint4 h1, qx, qy, qz;
+};
+__host__ __device__ __forceinline__ NodeWords load_node8(const Bvh8Node* nodes, uint32_t ni) {
+    const uint4* np = reinterpret_cast<const uint4*>(nodes + ni);
+    NodeWords w;
+    w.h0 = *reinterpret_cast<const float4*>(np);
+    w.h1 = np[1];
+    w.qx = np[2];
+    w.qy = np[3];
+    w.qz = np[4];
+    return w;
+}
+
+__host__ __device__ __forceinline__ void test_node8_words(const NodeWords& W, const RaySetup& R, float tmin, float tmax,
+                                                          uint32_t& ihits, uint32_t& tmask, uint32_t& child_base,
+                                                          uint32_t& tri_base, bool& flip) {
+    const float4 h0 = W.h0;
+    const uint4 h1 = W.h1, qx = W.qx, qy = W.qy, qz = W.qz;
     const uint32_t ew = __builtin_bit_cast(uint32_t, h0.w);
     const float sx = __builtin_bit_cast(float, (ew & 0xffu) << 23);
     const float sy = __builtin_bit_cast(float, ((ew >> 8) & 0xffu) << 23);
@@ -143,6 +157,12 @@ __host__ __device__ __forceinline__ void test_node8(const Bvh8Node* nodes, uint3
     child_base = h1.x;
     tri_base = h1.y;
     flip = (R.dneg >> axis) & 1u;   // bit select: a dynamic pick of R.d lowers to a scratch access
+}
+
+__host__ __device__ __forceinline__ void test_node8(const Bvh8Node* nodes, uint32_t ni, const RaySetup& R, float tmin,
+                                                    float tmax, uint32_t& ihits, uint32_t& tmask,
+                                                    uint32_t& child_base, uint32_t& tri_base, bool& flip) {
+    test_node8_words(load_node8(nodes, ni), R, tmin, tmax, ihits, tmask, child_base, tri_base, flip);
 }
 
 __host__ __device__ __forceinline__ int lowest_bit(uint32_t m) { return __builtin_ctz(m); }

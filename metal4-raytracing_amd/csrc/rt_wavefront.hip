@@ -24,11 +24,14 @@
 // contribution, then step s+1), and samples are summed per pixel in sample order.
 #include "rt_shade.h"
 
+#include <cstdio>
+#include <vector>
+
 namespace rt {
 
 namespace {
 
-constexpr uint32_t kTailRaysDefault = 32768;
+constexpr uint32_t kTailRaysDefault = 524288;
 static uint32_t tail_rays() {  // RT_TAIL_RAYS overrides (tuning experiments)
     static uint32_t v = [] { const char* e = getenv("RT_TAIL_RAYS"); return e ? (uint32_t)atol(e) : kTailRaysDefault; }();
     return v;
@@ -343,7 +346,12 @@ __global__ void __launch_bounds__(kBlock) wf_shade(DevScene S, FrameParams P, Wf
 template <bool ANY, bool COUNT>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) wf_trace(DevScene S, FrameParams P, WfParams Q, int cur, uint32_t n_host) {
     __shared__ int lds_stack[kStackSize * kBlock];
+    __shared__ uint4 lds_top[kTopNodes * 5];   // BVH top levels (BFS order: root, its children, ...)
     int* stack = &lds_stack[threadIdx.x];
+    const uint32_t n_top = (uint32_t)min(S.num_nodes8, kTopNodes);
+    for (uint32_t i = threadIdx.x; i < n_top * 5; i += kBlock)
+        lds_top[i] = reinterpret_cast<const uint4*>(S.nodes8)[i];
+    __syncthreads();
     const ShardPrefix cnt = load_prefix(ANY ? Q.W.counts + cslot(kCntShadowQ) : Q.W.counts + cslot(cur * kShards));
     uint32_t n = n_host;
     if (ANY) {
@@ -472,7 +480,19 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 
                 }
             }
             if (COUNT) tc.nodes++;
-            test_node8(S.nodes8, g_base + (uint32_t)r, R, 0.0f, best, g_hits, t_mask, g_base, t_base, g_flip);
+            const uint32_t ni = g_base + (uint32_t)r;
+            NodeWords w;
+            if (ni < n_top) {
+                const uint4* l = lds_top + 5 * ni;
+                w.h0 = __builtin_bit_cast(float4, l[0]);
+                w.h1 = l[1];
+                w.qx = l[2];
+                w.qy = l[3];
+                w.qz = l[4];
+            } else {
+                w = load_node8(S.nodes8, ni);
+            }
+            test_node8_words(w, R, 0.0f, best, g_hits, t_mask, g_base, t_base, g_flip);
         }
         if (!done && !t_mask && !g_hits && sp == 0) done = true;
         if (done) {
@@ -672,6 +692,27 @@ static uint32_t queue_total(const uint32_t* h, int q) {
     return s;
 }
 
+// Diagnostics (RT_WF_DUMP=<prefix>): the ray queue of every extend round written to
+// <prefix>_it<k>.bin as n x 8 floats (o.xyz, path id bits, d.xyz, 0), dense order.
+static void dump_queue(const WfParams& Q, int cur, int it, hipStream_t stream) {
+    static const char* prefix = getenv("RT_WF_DUMP");
+    if (!prefix) return;
+    char name[512];
+    snprintf(name, sizeof name, "%s_it%02d.bin", prefix, it);
+    FILE* f = fopen(name, "wb");
+    if (!f) return;
+    std::vector<float4> buf;
+    for (int k = 0; k < kShards; ++k) {
+        const uint32_t c = Q.W.h_counts[cslot(cur * kShards + k)];
+        buf.resize(2 * (size_t)c);
+        if (c && hipMemcpyAsync(buf.data(), Q.W.q[cur] + 2 * (size_t)k * Q.seg_cap, 32 * (size_t)c,
+                                hipMemcpyDeviceToHost, stream) == hipSuccess &&
+            hipStreamSynchronize(stream) == hipSuccess)
+            fwrite(buf.data(), 32, c, f);
+    }
+    fclose(f);
+}
+
 static bool iterate(const DevScene& S, const FrameParams& P, WfParams& Q, int& cur, uint32_t n, bool count, bool full,
                     hipStream_t stream, WfFrameStats* fs, const char** err) {
     float* stage_ms = fs->stage_ms;
@@ -699,6 +740,7 @@ static bool iterate(const DevScene& S, const FrameParams& P, WfParams& Q, int& c
             return true;
         }
         int next = 1 - cur;
+        dump_queue(Q, cur, fs->iterations, stream);
         WF_CHECK(hipEventRecord(W.ev[0], stream));
         unsigned g = grid_for(n, 8192);
         unsigned gt = grid_for(n, trace_grid_cap());

@@ -12,5 +12,5 @@ while read -r set; do
   rc=$?
   echo "pass $i rc=$rc"
   [ $rc -ne 0 ] && exit $rc
-done < $R/${SETS:-pmc_sets.txt}
+done < $R/${SETS:-tools/pmc_sets.txt}
 exit 0
