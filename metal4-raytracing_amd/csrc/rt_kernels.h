@@ -73,10 +73,11 @@ void launch_megakernel(const DevScene& S, const FrameParams& P, int nblocks, boo
 // {float4 o (w = path id), float4 d}, hit records {t, tri id, u, v}, shadow queue of
 // {float4 o (w = path id), float4 d (w = tmax), float4 contribution}.
 constexpr int kShards = 8;        // queue segments (one allocation counter each)
-// Counter slots: [0..7] queue 0, [8..15] queue 1, [16..23] shadow, [24] extra allocator; each slot on a
+// Counter slots: [0..7] queue 0, [8..15] queue 1, [16..23] shadow, [24] extra allocator,
+// [32..39] / [40..47] per-XCD chunk counters of the extend / connect launches; each slot on a
 // 128-B line of its own (cslot), so the per-XCD shards never contend for one line's atomics.
 constexpr int kCntStride = 32;
-constexpr int kWfCountWords = 32 * kCntStride;
+constexpr int kWfCountWords = 48 * kCntStride;
 __host__ __device__ constexpr uint32_t cslot(int c) { return (uint32_t)c * kCntStride; }
 struct WavefrontBuffers {
     size_t queue_entries = 0;     // kShards segments of queue_entries / kShards

@@ -42,6 +42,11 @@ static int refill_min() {  // RT_REFILL_MIN overrides (tuning experiments)
     return v;
 }
 
+static int chunk_size() {  // RT_CHUNK overrides (tuning experiments)
+    static int v = [] { const char* e = getenv("RT_CHUNK"); return e ? atoi(e) : 64; }();
+    return v;
+}
+
 static int tri_vote() {  // RT_TRI_VOTE overrides (tuning experiments)
     static int v = [] { const char* e = getenv("RT_TRI_VOTE"); return e ? atoi(e) : 0; }();
     return v;
@@ -144,11 +149,14 @@ struct WfParams {
     int spp;
     int refill_min;        // wf_trace refills once at least this many lanes of a wave are idle
     int tri_vote;          // wf_trace phase vote threshold (lanes with triangle work), 0 = off
+    int chunk;             // wf_trace dynamic chunk size (rays per grab), 0 = static wave ranges
 };
 
 // counter slots (cslot): [q*8 + shard] ray queues q = 0, 1; [16 + shard] shadow queue; [24] extra allocator
 constexpr int kCntShadowQ = 16;
 constexpr int kCntExtra = 24;
+constexpr int kCntChunkExtend = 32;   // 8 per-XCD chunk counters each
+constexpr int kCntChunkConnect = 40;
 
 // Inclusive prefix of a sharded queue's segment counts, loaded once per kernel (uniform, so the
 // loads are scalar and the lookups below stay in registers).
@@ -361,6 +369,10 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 
         uint32_t k = threadIdx.x & (kShards - 1);
         Q.W.counts[cslot(threadIdx.x < kShards ? next * kShards + k : kCntShadowQ + k)] = 0;
     }
+    // chunk counters of the OTHER traversal kind are reset here for its next launch (extend and
+    // connect alternate; the frame start zeroes both)
+    if (blockIdx.x == 0 && threadIdx.x < kShards)
+        Q.W.counts[cslot((ANY ? kCntChunkExtend : kCntChunkConnect) + threadIdx.x)] = 0;
     const float4* qin = ANY ? Q.W.sq : Q.W.q[cur];
     const int qstride = ANY ? 3 : 2;
     // static wave ranges, contiguous per XCD (blocks b and b+8 share an XCD)
@@ -369,9 +381,19 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 
     if (b < per * 8) b = (b & 7) * per + (b >> 3);
     const uint32_t waves = nb * (kBlock / 64);
     const uint32_t wv = b * (kBlock / 64) + (threadIdx.x >> 6);
-    const uint32_t wbeg = (uint32_t)(((uint64_t)n * wv) / waves);
-    const uint32_t wend = (uint32_t)(((uint64_t)n * (wv + 1)) / waves);
-    uint32_t wnext = wbeg;
+    // static: this wave's range; dynamic (Q.chunk > 0): chunks of this XCD's eighth of the queue,
+    // grabbed with one atomic per chunk when the current one runs out
+    uint32_t wnext, wend;
+    const uint32_t xcd = blockIdx.x & 7u;
+    const uint32_t xbeg = (uint32_t)(((uint64_t)n * xcd) / 8), xend = (uint32_t)(((uint64_t)n * (xcd + 1)) / 8);
+    uint32_t* chunk_ctr = Q.W.counts + cslot((ANY ? kCntChunkConnect : kCntChunkExtend) + (int)xcd);
+    bool exhausted = false;
+    if (Q.chunk > 0) {
+        wnext = wend = 0;
+    } else {
+        wnext = (uint32_t)(((uint64_t)n * wv) / waves);
+        wend = (uint32_t)(((uint64_t)n * (wv + 1)) / waves);
+    }
 
     TraceCounters tc{0, 0};
     bool overflow = false;
@@ -386,6 +408,17 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 
     while (true) {
         // refill idle lanes from the wave's range
         unsigned long long idle = __ballot(!active);
+        if (Q.chunk > 0 && wnext >= wend && !exhausted && (__popcll(idle) >= Q.refill_min || idle == ~0ull)) {
+            uint32_t base = 0;
+            if (lane_id() == 0) base = atomicAdd(chunk_ctr, (uint32_t)Q.chunk);
+            base = xbeg + __builtin_amdgcn_readfirstlane(base);
+            if (base >= xend) {
+                exhausted = true;
+            } else {
+                wnext = base;
+                wend = min(base + (uint32_t)Q.chunk, xend);
+            }
+        }
         if (idle != 0ull && wnext < wend && (__popcll(idle) >= Q.refill_min || idle == ~0ull)) {
             if (!active) {
                 uint32_t g = wnext + mbcnt64(idle);
@@ -783,6 +816,7 @@ bool run_wavefront(const DevScene& S, const FrameParams& P, WavefrontBuffers& W,
     Q.seg_cap = (uint32_t)(W.queue_entries / kShards);
     Q.refill_min = refill_min();
     Q.tri_vote = tri_vote();
+    Q.chunk = chunk_size();
     *fs = WfFrameStats{};
     float* stage_ms = fs->stage_ms;
     const bool full = needs_full(P.U);
