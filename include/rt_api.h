@@ -95,7 +95,9 @@ typedef struct rt_scene_desc {
 typedef struct rt_opts {
     int32_t device;     /* HIP device ordinal */
     int32_t pipeline;   /* RT_PIPELINE_* */
-    int32_t reserved[6];
+    int32_t tail_paths; /* wavefront: below this many live paths the rest of the frame runs in the
+                           persistent finish kernel; 0 = default (524288), 1 = never */
+    int32_t reserved[5];
 } rt_opts;
 
 /* Image-space tile partition for multi-GPU rendering: the image is cut into

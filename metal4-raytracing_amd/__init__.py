@@ -212,13 +212,14 @@ class Renderer:
     draw() = updateUniforms + raytracingKernel dispatch + accumulation swap.
     """
 
-    def __init__(self, scene, width, height, device=0, pipeline="wavefront", seed=1, stream=None):
+    def __init__(self, scene, width, height, device=0, pipeline="wavefront", seed=1, stream=None, tail_paths=0):
         object.__setattr__(self, "_ctx", None)
         self.scene = scene
         self.width, self.height = int(width), int(height)
         opts = _abi.Opts()
         opts.device = device
         opts.pipeline = {"megakernel": 0, "wavefront": 1}[pipeline]
+        opts.tail_paths = int(tail_paths)
         ctx = C.c_void_p()
         _check(lib().rt_create(C.byref(opts), C.byref(ctx)))
         object.__setattr__(self, "_ctx", ctx)

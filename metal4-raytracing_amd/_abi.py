@@ -116,7 +116,7 @@ class SceneDesc(C.Structure):
 
 
 class Opts(C.Structure):
-    _fields_ = [("device", C.c_int32), ("pipeline", C.c_int32), ("reserved", C.c_int32 * 6)]
+    _fields_ = [("device", C.c_int32), ("pipeline", C.c_int32), ("tail_paths", C.c_int32), ("reserved", C.c_int32 * 5)]
 
 
 class TileSet(C.Structure):

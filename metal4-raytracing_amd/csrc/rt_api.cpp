@@ -34,6 +34,7 @@ struct MeshInfo {
 struct rt_ctx {
     int device = 0;
     int pipeline = RT_PIPELINE_MEGAKERNEL;
+    int tail_paths = 0;
     hipStream_t own_stream = nullptr, stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     std::string err;
@@ -226,6 +227,7 @@ rt_status rt_create(const rt_opts* opts, rt_ctx** out) {
     if (opts) {
         c->device = opts->device;
         c->pipeline = opts->pipeline;
+        c->tail_paths = opts->tail_paths;
     }
     if (c->device < 0 || c->device >= ndev) { delete c; FAIL((rt_ctx*)nullptr, RT_ERR_INVALID_ARG, "bad device ordinal"); }
     if (c->pipeline != RT_PIPELINE_MEGAKERNEL && c->pipeline != RT_PIPELINE_WAVEFRONT) {
@@ -604,7 +606,7 @@ rt_status rt_render_frame(rt_ctx* c, const Uniforms* U, const rt_tile_set* tiles
     if (wavefront) {
         const char* err = nullptr;
         c->wfs = WfFrameStats{};
-        if (own > 0 && !run_wavefront(S, P, c->wf, own, c->counting, c->stream, &c->wfs, &err))
+        if (own > 0 && !run_wavefront(S, P, c->wf, own, c->counting, c->tail_paths, c->stream, &c->wfs, &err))
             FAIL(c, RT_ERR_HIP, std::string("wavefront: ") + (err ? err : "?"));
         std::memcpy(c->stats.kernel_ms, c->wfs.stage_ms, sizeof c->stats.kernel_ms);
     } else {

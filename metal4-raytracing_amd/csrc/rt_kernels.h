@@ -105,8 +105,9 @@ struct WfFrameStats {
     float trace_ms;                 // their summed device time
 };
 // Runs one frame; returns false on a HIP error (message in *err).
+// tail_paths: finish-kernel threshold (0 = default / RT_TAIL_RAYS).
 bool run_wavefront(const DevScene& S, const FrameParams& P, WavefrontBuffers& W, int own_tiles, bool count,
-                   hipStream_t stream, WfFrameStats* fs, const char** err);
+                   int tail_paths, hipStream_t stream, WfFrameStats* fs, const char** err);
 size_t wavefront_queue_entries(size_t paths, int max_extra);
 
 // Packed-tile layout of the multi-GPU gather: element i of a rank's packed buffer is pixel

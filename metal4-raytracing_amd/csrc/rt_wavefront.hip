@@ -150,11 +150,13 @@ struct WfParams {
     int refill_min;        // wf_trace refills once at least this many lanes of a wave are idle
     int tri_vote;          // wf_trace phase vote threshold (lanes with triangle work), 0 = off
     int chunk;             // wf_trace dynamic chunk size (rays per grab), 0 = static wave ranges
+    uint32_t tail;         // live paths below which wf_finish runs the rest
 };
 
 // counter slots (cslot): [q*8 + shard] ray queues q = 0, 1; [16 + shard] shadow queue; [24] extra allocator
 constexpr int kCntShadowQ = 16;
 constexpr int kCntExtra = 24;
+constexpr int kCntChunkFinish = 25;
 constexpr int kCntChunkExtend = 32;   // 8 per-XCD chunk counters each
 constexpr int kCntChunkConnect = 40;
 
@@ -549,6 +551,9 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 
 // ---- finish: run the remaining paths to completion --------------------------------------------------
 template <bool COUNT, bool FULL>
 __global__ void __launch_bounds__(kBlock) wf_finish(DevScene S, FrameParams P, WfParams Q, int cur, uint32_t n) {
+    // Persistent: every lane runs ONE path segment (closest hit, shade, shadow ray) per iteration
+    // and picks up the next remaining path as soon as its own ends, so a wave waits for its
+    // slowest segment, not for its slowest path.  Paths come in chunks of 64 from one counter.
     __shared__ int lds_stack[kStackSize * kBlock];
     __shared__ HaltonDim lds_halton[kHaltonLds];
     load_halton(S, lds_halton);
@@ -557,32 +562,64 @@ __global__ void __launch_bounds__(kBlock) wf_finish(DevScene S, FrameParams P, W
     const ShardPrefix cnt = load_prefix(Q.W.counts + cslot(cur * kShards));
     const float4* qin = Q.W.q[cur];
     int* stack = &lds_stack[threadIdx.x];
+    uint32_t* chunk_ctr = Q.W.counts + cslot(kCntChunkFinish);
+    constexpr uint32_t kChunk = 64;
     TraceCounters tc{0, 0};
     bool overflow = false;
     uint32_t n_closest = 0, n_shadow = 0;
     f2 zero2;
     zero2.x = 0.0f;
     zero2.y = 0.0f;
-    for (uint32_t base = blockIdx.x * kBlock; base < n; base += gridDim.x * kBlock) {
-        uint32_t g = base + threadIdx.x;
-        if (g >= n) continue;
-        uint32_t e = entry_of(cnt, g, Q.seg_cap);
-        float4 o = qin[2 * (size_t)e], d = qin[2 * (size_t)e + 1];
-        uint32_t pid = __float_as_uint(o.w);
-        uint4 meta = Q.W.p_meta[pid];
-        float4 c = Q.W.p_color[pid], a = Q.W.p_accum[pid];
-        PathRegs p;
-        p.color = mk3(c.x, c.y, c.z);
-        p.accum = mk3(a.x, a.y, a.z);
-        p.bounce = (int)(meta.z & 0xffu);
-        p.tpass = (int)((meta.z >> 8) & 0xffu);
-        p.step = (int)(meta.z >> 16);
-        const int sample = (int)meta.y;
-        f3 rayO = ld3(o), rayD = ld3(d);
-        while (true) {                                                           // :311 (bounce < max checked)
-            Hit h;
-            n_closest++;
-            if (!trace8<false, COUNT>(S, rayO, rayD, 0.0f, INFINITY, h, stack, tc, overflow)) break;
+    uint32_t wnext = 0, wend = 0;
+    bool exhausted = false, active = false;
+    uint32_t pid = 0;
+    uint4 meta = make_uint4(0, 0, 0, 0);
+    PathRegs p;
+    p.color = p.accum = mk3(0, 0, 0);
+    p.bounce = p.tpass = p.step = 0;
+    f3 rayO = mk3(0, 0, 0), rayD = mk3(0, 0, 0);
+    while (true) {
+        unsigned long long idle = __ballot(!active);
+        if (wnext >= wend && !exhausted && (__popcll(idle) >= 8 || idle == ~0ull)) {
+            uint32_t base = 0;
+            if (lane_id() == 0) base = atomicAdd(chunk_ctr, kChunk);
+            base = __builtin_amdgcn_readfirstlane(base);
+            if (base >= n) {
+                exhausted = true;
+            } else {
+                wnext = base;
+                wend = min(base + kChunk, n);
+            }
+        }
+        if (idle != 0ull && wnext < wend) {
+            if (!active) {
+                const uint32_t g = wnext + mbcnt64(idle);
+                if (g < wend) {
+                    const uint32_t e = entry_of(cnt, g, Q.seg_cap);
+                    const float4 o = qin[2 * (size_t)e], d = qin[2 * (size_t)e + 1];
+                    pid = __float_as_uint(o.w);
+                    meta = Q.W.p_meta[pid];
+                    const float4 c = Q.W.p_color[pid], a = Q.W.p_accum[pid];
+                    p.color = mk3(c.x, c.y, c.z);
+                    p.accum = mk3(a.x, a.y, a.z);
+                    p.bounce = (int)(meta.z & 0xffu);
+                    p.tpass = (int)((meta.z >> 8) & 0xffu);
+                    p.step = (int)(meta.z >> 16);
+                    rayO = ld3(o);
+                    rayD = ld3(d);
+                    active = true;
+                }
+            }
+            wnext += (uint32_t)__popcll(idle);
+        }
+        if (__ballot(active) == 0ull) break;
+        if (!active) continue;
+        // one segment of the path (:311-774)
+        bool ends = true;
+        Hit h;
+        n_closest++;
+        if (trace8<false, COUNT>(S, rayO, rayD, 0.0f, INFINITY, h, stack, tc, overflow)) {
+            const int sample = (int)meta.y;
             StepResult r;
             shade_step<FULL>(S, U, halton, (int)meta.w, sample, rayO, rayD, h, p, sample == 0 && p.step == 0, zero2,
                              false, zero2, r);
@@ -593,9 +630,12 @@ __global__ void __launch_bounds__(kBlock) wf_finish(DevScene S, FrameParams P, W
                 if (!trace8<true, COUNT>(S, r.so, r.sd, 0.0f, r.stmax, sh, stack, tc, overflow))
                     p.accum = p.accum + r.contrib;
             }
-            if (!r.next) break;
+            ends = !r.next;
         }
-        Q.W.p_accum[pid] = make_float4(p.accum.x, p.accum.y, p.accum.z, 0.0f);
+        if (ends) {
+            Q.W.p_accum[pid] = make_float4(p.accum.x, p.accum.y, p.accum.z, 0.0f);
+            active = false;
+        }
     }
     flush_counters(P, n_closest, n_shadow, 0, tc, COUNT, overflow);
 }
@@ -719,6 +759,23 @@ static unsigned trace_grid_cap() {
     return cap;
 }
 
+// resident blocks of the persistent finish kernel instantiation in use
+static unsigned finish_grid_cap(bool count, bool full) {
+    static unsigned cap[4] = {0, 0, 0, 0};
+    const int k = (count ? 2 : 0) + (full ? 1 : 0);
+    if (!cap[k]) {
+        int dev = 0, cus = 256, per = 0;
+        if (hipGetDevice(&dev) == hipSuccess) hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        hipError_t e = count ? (full ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, wf_finish<true, true>, kBlock, 0)
+                                     : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, wf_finish<true, false>, kBlock, 0))
+                             : (full ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, wf_finish<false, true>, kBlock, 0)
+                                     : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, wf_finish<false, false>, kBlock, 0));
+        if (e != hipSuccess || per < 1) per = 2;
+        cap[k] = (unsigned)(cus * per);
+    }
+    return cap[k];
+}
+
 static uint32_t queue_total(const uint32_t* h, int q) {
     uint32_t s = 0;
     for (int k = 0; k < kShards; ++k) s += h[cslot(q * kShards + k)];
@@ -752,10 +809,11 @@ static bool iterate(const DevScene& S, const FrameParams& P, WfParams& Q, int& c
     const int max_it = P.U.maxBounces * (P.U.maxBounces + 1) + 2;
     WavefrontBuffers& W = Q.W;
     for (int it = 0; it < max_it && n > 0; ++it) {
-        if (n < tail_rays()) {
+        if (n < Q.tail) {
             // run the tail to completion in one launch
             WF_CHECK(hipEventRecord(W.ev[0], stream));
-            unsigned g = grid_for(n, 1u << 20);
+            WF_CHECK(hipMemsetAsync(W.counts + cslot(kCntChunkFinish), 0, sizeof(uint32_t), stream));
+            unsigned g = grid_for(n, finish_grid_cap(count, full));
             if (count) {
                 if (full) hipLaunchKernelGGL((wf_finish<true, true>), dim3(g), dim3(kBlock), 0, stream, S, P, Q, cur, n);
                 else hipLaunchKernelGGL((wf_finish<true, false>), dim3(g), dim3(kBlock), 0, stream, S, P, Q, cur, n);
@@ -807,7 +865,7 @@ static bool iterate(const DevScene& S, const FrameParams& P, WfParams& Q, int& c
 }
 
 bool run_wavefront(const DevScene& S, const FrameParams& P, WavefrontBuffers& W, int own_tiles, bool count,
-                   hipStream_t stream, WfFrameStats* fs, const char** err) {
+                   int tail_paths, hipStream_t stream, WfFrameStats* fs, const char** err) {
     WfParams Q;
     Q.W = W;
     Q.spp = max(P.U.samplesPerPixel, 1);
@@ -817,6 +875,7 @@ bool run_wavefront(const DevScene& S, const FrameParams& P, WavefrontBuffers& W,
     Q.refill_min = refill_min();
     Q.tri_vote = tri_vote();
     Q.chunk = chunk_size();
+    Q.tail = tail_paths > 0 ? (uint32_t)tail_paths : tail_rays();
     *fs = WfFrameStats{};
     float* stage_ms = fs->stage_ms;
     const bool full = needs_full(P.U);

@@ -18,3 +18,17 @@ def parity_report(gpu, ref):
     e = rel_l2_per_pixel(gpu, ref)
     exact = np.mean(np.all(np.asarray(gpu)[..., :3] == np.asarray(ref)[..., :3], axis=-1))
     return dict(max_rel=float(e.max()), n_bad=int((e > REL_L2_TOL).sum()), frac_bitwise=float(exact))
+
+
+# Pipeline variants of the GPU tests: the per-pixel megakernel, and the wavefront pipeline with
+# the default finish threshold (small frames run almost entirely in the persistent finish
+# kernel), with no finish kernel at all (every bounce through extend / shade / connect) and
+# with a small threshold (bulk rounds, then finish).
+PIPELINES = ["megakernel", "wavefront", "wavefront-bulk", "wavefront-mixed"]
+_VARIANTS = {"megakernel": ("megakernel", 0), "wavefront": ("wavefront", 0),
+             "wavefront-bulk": ("wavefront", 1), "wavefront-mixed": ("wavefront", 2048)}
+
+
+def make_renderer(rt, scene, W, H, pipeline="wavefront", **kw):
+    pl, tail = _VARIANTS[pipeline]
+    return rt.Renderer(scene, W, H, pipeline=pl, tail_paths=tail, **kw)

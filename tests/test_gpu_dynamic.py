@@ -10,11 +10,10 @@ import ctypes as C
 import numpy as np
 import pytest
 
-from helpers import parity_report
+from helpers import PIPELINES, make_renderer, parity_report
 
 pytestmark = pytest.mark.gpu
 
-PIPELINES = ["megakernel", "wavefront"]
 
 
 def _f4(ptr, n):
@@ -76,7 +75,7 @@ def test_skinning_refit_parity(rt, orc, assets, pipeline, rebuild):
     ji = np.ctypeslib.as_array(md.joint_indices, shape=(n, 4)).copy()
     jw = np.ctypeslib.as_array(md.joint_weights, shape=(n, 4)).copy()
     J = sc.joint_matrices(m, 0.35)
-    R = rt.Renderer(sc, W, H, seed=5, pipeline=pipeline)
+    R = make_renderer(rt, sc, W, H, pipeline, seed=5)
     R.samplesPerPixel = 2
     R.maxBounces = 2
     R.skin(m, J)
@@ -101,7 +100,7 @@ def test_instance_motion_and_extra_samples(rt, orc, assets, pipeline):
     W, H = 96, 64
     sc = rt.Scene.preset("c2", assets)
     desc = sc.desc()
-    R = rt.Renderer(sc, W, H, seed=9, pipeline=pipeline)
+    R = make_renderer(rt, sc, W, H, pipeline, seed=9)
     R.samplesPerPixel = 1
     R.maxBounces = 2
     assert R.useMotionAdaptiveSampling
