@@ -96,7 +96,7 @@ typedef struct rt_opts {
     int32_t device;     /* HIP device ordinal */
     int32_t pipeline;   /* RT_PIPELINE_* */
     int32_t tail_paths; /* wavefront: below this many live paths the rest of the frame runs in the
-                           persistent finish kernel; 0 = default (524288), 1 = never */
+                           persistent finish kernel; 0 = default (1048576), 1 = never */
     int32_t reserved[5];
 } rt_opts;
 

@@ -63,7 +63,7 @@ struct rt_ctx {
     // device buffers
     DevBuf d_pos, d_prev_pos, d_nrm, d_rest_pos, d_rest_nrm, d_jidx, d_jw, d_joints;
     DevBuf d_tri_info, d_inst, d_prev_inst, d_mat, d_lights, d_halton;
-    DevBuf d_tris, d_nodes, d_node_box, d_slot_to_tri, d_levels;
+    DevBuf d_tris, d_nodes, d_node_box, d_slot_to_tri, d_levels, d_maxabs;
     DevBuf d_random, d_accum[2], d_depth, d_motion, d_gbuffer, d_counters;
     int width = 0, height = 0;
     int read_idx = 0;   // accum[read_idx] = history (TextureIndexAccumulation)
@@ -158,7 +158,7 @@ static void xform_host(const float* m, const float4& p, float* out) {
 static size_t ctx_bytes(const rt_ctx* c) {
     const DevBuf* all[] = {&c->d_pos, &c->d_prev_pos, &c->d_nrm, &c->d_rest_pos, &c->d_rest_nrm, &c->d_jidx, &c->d_jw,
                            &c->d_joints, &c->d_tri_info, &c->d_inst, &c->d_prev_inst, &c->d_mat, &c->d_lights,
-                           &c->d_halton, &c->d_tris, &c->d_nodes, &c->d_node_box, &c->d_slot_to_tri, &c->d_levels, &c->d_random,
+                           &c->d_halton, &c->d_tris, &c->d_nodes, &c->d_node_box, &c->d_slot_to_tri, &c->d_levels, &c->d_maxabs, &c->d_random,
                            &c->d_accum[0], &c->d_accum[1], &c->d_depth, &c->d_motion, &c->d_gbuffer, &c->d_counters,
                            &c->d_wf_color, &c->d_wf_accum, &c->d_wf_meta, &c->d_wf_q0, &c->d_wf_q1, &c->d_wf_hits,
                            &c->d_wf_sq, &c->d_wf_counts, &c->d_wf_mprev, &c->d_wf_extra};
@@ -264,7 +264,7 @@ rt_status rt_destroy(rt_ctx* c) {
     if (c->stream) hipStreamSynchronize(c->stream);
     DevBuf* all[] = {&c->d_pos, &c->d_prev_pos, &c->d_nrm, &c->d_rest_pos, &c->d_rest_nrm, &c->d_jidx, &c->d_jw,
                      &c->d_joints, &c->d_tri_info, &c->d_inst, &c->d_prev_inst, &c->d_mat, &c->d_lights, &c->d_halton,
-                     &c->d_tris, &c->d_nodes, &c->d_node_box, &c->d_slot_to_tri, &c->d_levels, &c->d_random, &c->d_accum[0],
+                     &c->d_tris, &c->d_nodes, &c->d_node_box, &c->d_slot_to_tri, &c->d_levels, &c->d_maxabs, &c->d_random, &c->d_accum[0],
                      &c->d_accum[1], &c->d_depth, &c->d_motion, &c->d_gbuffer, &c->d_counters,
                      &c->d_wf_color, &c->d_wf_accum, &c->d_wf_meta, &c->d_wf_q0, &c->d_wf_q1, &c->d_wf_hits,
                      &c->d_wf_sq, &c->d_wf_counts, &c->d_wf_mprev, &c->d_wf_extra};
@@ -459,12 +459,16 @@ rt_status rt_bvh_refit(rt_ctx* c) {
     if (!c) FAIL(c, RT_ERR_INVALID_ARG, "null ctx");
     if (!c->bvh_ready) FAIL(c, RT_ERR_STATE, "rt_bvh_refit before rt_bvh_build");
     HIPC(c, hipSetDevice(c->device));
+    rt_status st = dev_alloc(c, c->d_maxabs, 4);
+    if (st) return st;
+    HIPC(c, hipMemsetAsync(c->d_maxabs.p, 0, 4, c->stream));
     launch_flatten((const uint4*)c->d_tri_info.p, (const uint32_t*)c->d_slot_to_tri.p, (const float4*)c->d_pos.p,
-                   (const float*)c->d_inst.p, (float4*)c->d_tris.p, c->num_tris, c->stream);
+                   (const float*)c->d_inst.p, (float4*)c->d_tris.p, c->num_tris, (unsigned*)c->d_maxabs.p, c->stream);
     for (int d = (int)c->level_off.size() - 2; d >= 0; --d) {
         uint32_t off = c->level_off[d], cnt = c->level_off[d + 1] - off;
         launch_refit8_level((Bvh8Node*)c->d_nodes.p, (float*)c->d_node_box.p, (const float4*)c->d_tris.p,
-                            (const uint32_t*)c->d_levels.p + off, cnt, c->bvh8.pad, c->stream);
+                            (const uint32_t*)c->d_levels.p + off, cnt, c->bvh8.pad, (const unsigned*)c->d_maxabs.p,
+                            c->stream);
     }
     HIPC(c, hipGetLastError());
     return RT_OK;

@@ -128,9 +128,11 @@ void launch_unpack_tiles(const float4* src, float4* dst, int width, int height, 
                          int tiles_x, int own, hipStream_t s);
 void launch_skin(const float4* rest_pos, const float4* rest_nrm, const ushort4* jidx, const float4* jw,
                  const float* joints, float4* out_pos, float4* out_nrm, uint32_t n, hipStream_t s);
+// flatten also reduces max |world coordinate| into *maxabs_bits (float bits; zero it first)
 void launch_flatten(const uint4* tri_info, const uint32_t* slot_to_tri, const float4* pos, const float* inst,
-                    float4* tris, uint32_t n, hipStream_t s);
+                    float4* tris, uint32_t n, unsigned* maxabs_bits, hipStream_t s);
+// pad = max(pad_min, 4e-6 * max |coordinate|) as the builder pads (rt_bvh.cpp)
 void launch_refit8_level(Bvh8Node* nodes, float* node_box, const float4* tris, const uint32_t* level_nodes,
-                         uint32_t count, float pad, hipStream_t s);
+                         uint32_t count, float pad_min, const unsigned* maxabs_bits, hipStream_t s);
 
 }  // namespace rt

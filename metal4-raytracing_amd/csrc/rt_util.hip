@@ -86,23 +86,35 @@ void launch_skin(const float4* rest_pos, const float4* rest_nrm, const ushort4* 
 // ---- flatten world-space triangles into BVH slot order ----------------------------------------
 __global__ void flatten_k(const uint4* __restrict__ tri_info, const uint32_t* __restrict__ slot_to_tri,
                           const float4* __restrict__ pos, const float* __restrict__ inst, float4* __restrict__ tris,
-                          uint32_t n) {
+                          uint32_t n, unsigned* __restrict__ maxabs_bits) {
+    __shared__ float red[4];
     uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= n) return;
-    uint32_t id = slot_to_tri[k];
-    uint4 ti = tri_info[id];
-    const float* M = inst + 12 * (ti.w >> 8);
-    uint32_t vi[3] = {ti.x, ti.y, ti.z};
-    #pragma unroll
-    for (int q = 0; q < 3; ++q) {
-        f3 w = xform(M, ld3(pos[vi[q]]), 1.0f);
-        tris[3 * k + q] = make_float4(w.x, w.y, w.z, q == 0 ? __uint_as_float(id) : 0.0f);
+    float m = 0.0f;
+    if (k < n) {
+        uint32_t id = slot_to_tri[k];
+        uint4 ti = tri_info[id];
+        const float* M = inst + 12 * (ti.w >> 8);
+        uint32_t vi[3] = {ti.x, ti.y, ti.z};
+        #pragma unroll
+        for (int q = 0; q < 3; ++q) {
+            f3 w = xform(M, ld3(pos[vi[q]]), 1.0f);
+            tris[3 * k + q] = make_float4(w.x, w.y, w.z, q == 0 ? __uint_as_float(id) : 0.0f);
+            m = fmaxf(m, fmaxf(fabsf(w.x), fmaxf(fabsf(w.y), fabsf(w.z))));
+        }
     }
+    // block max of |coordinate| -> one atomic per block (non-negative floats order as their bits)
+    #pragma unroll
+    for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off, 64));
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0 && maxabs_bits)
+        atomicMax(maxabs_bits, __float_as_uint(fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]))));
 }
 void launch_flatten(const uint4* tri_info, const uint32_t* slot_to_tri, const float4* pos, const float* inst,
-                    float4* tris, uint32_t n, hipStream_t s) {
+                    float4* tris, uint32_t n, unsigned* maxabs_bits, hipStream_t s) {
     if (!n) return;
-    hipLaunchKernelGGL(flatten_k, dim3((n + 255) / 256), dim3(256), 0, s, tri_info, slot_to_tri, pos, inst, tris, n);
+    hipLaunchKernelGGL(flatten_k, dim3((n + 255) / 256), dim3(256), 0, s, tri_info, slot_to_tri, pos, inst, tris, n,
+                       maxabs_bits);
 }
 
 // ---- level-synchronous refit of the 8-wide BVH: one launch per level, deepest first -------------
@@ -111,9 +123,11 @@ void launch_flatten(const uint4* tri_info, const uint32_t* slot_to_tri, const fl
 // precision, outward rounding), and stores its own box for its parent.
 __global__ void refit8_level_k(Bvh8Node* __restrict__ nodes, float* __restrict__ node_box,
                                const float4* __restrict__ tris, const uint32_t* __restrict__ level_nodes,
-                               uint32_t count, float pad) {
+                               uint32_t count, float pad_min, const unsigned* __restrict__ maxabs_bits) {
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= count) return;
+    // the builder's padding rule (4e-6 * max |coordinate|) on the refitted geometry
+    const float pad = fmaxf(pad_min, 4e-6f * __uint_as_float(*maxabs_bits));
     const uint32_t ni = level_nodes[i];
     Bvh8Node nd = nodes[ni];
     float clo[8][3], chi[8][3];
@@ -177,10 +191,10 @@ __global__ void refit8_level_k(Bvh8Node* __restrict__ nodes, float* __restrict__
     nodes[ni] = nd;
 }
 void launch_refit8_level(Bvh8Node* nodes, float* node_box, const float4* tris, const uint32_t* level_nodes,
-                         uint32_t count, float pad, hipStream_t s) {
+                         uint32_t count, float pad_min, const unsigned* maxabs_bits, hipStream_t s) {
     if (!count) return;
     hipLaunchKernelGGL(refit8_level_k, dim3((count + 127) / 128), dim3(128), 0, s, nodes, node_box, tris, level_nodes,
-                       count, pad);
+                       count, pad_min, maxabs_bits);
 }
 
 }  // namespace rt

@@ -31,7 +31,7 @@ namespace rt {
 
 namespace {
 
-constexpr uint32_t kTailRaysDefault = 524288;
+constexpr uint32_t kTailRaysDefault = 1048576;
 static uint32_t tail_rays() {  // RT_TAIL_RAYS overrides (tuning experiments)
     static uint32_t v = [] { const char* e = getenv("RT_TAIL_RAYS"); return e ? (uint32_t)atol(e) : kTailRaysDefault; }();
     return v;
