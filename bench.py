@@ -170,7 +170,7 @@ def main():
                             + closest_per_launch * B_HIT + pixels_per_launch * B_PIXEL)
         npr, tpr = nodes_per_ray, tris_per_ray
     achieved = bytes_per_launch / (launch_ms * 1e-3) / 1e9
-    traffic, traffic_src = None, None
+    traffic, traffic_src, l2_hit = None, None, None
     if a.traffic_csv:
         traffic = read_traffic(a.traffic_csv.split(","), r"wf_trace<(true|false),false>"
                                if last_st.pipeline == 1 else r"megakernel<false,")
@@ -180,6 +180,9 @@ def main():
             tj = json.load(f)
         if tj.get("kernel") == kernel and tj.get("config") == [a.scene, a.width, a.height, a.spp, a.bounces]:
             traffic, traffic_src = tj["bytes_per_launch"], TRAFFIC_JSON_REL + " (" + tj.get("source", "") + ")"
+            # TCC hit rates (rocprofv3 TCC_HIT/TCC_MISS pass) of the traversal and shade kernels
+            hits = tj.get("l2_hit") or {}
+            l2_hit = {k: v for k, v in hits.items() if re.search(r"wf_(trace|shade|finish)<", k)} or None
 
     cpu = None
     if not a.no_cpu and n == 1:
@@ -213,6 +216,7 @@ def main():
         "roofline": {
             "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": traffic_src,
+            "l2_hit": l2_hit,
             "kernel": kernel, "launch_ms": round(launch_ms, 4), "bytes_per_launch": int(bytes_per_launch),
             "rays_per_launch": int(rays_per_launch), "nodes_per_ray": round(npr, 3), "tris_per_ray": round(tpr, 3),
         },
@@ -263,13 +267,17 @@ def cpu_baseline(rt, scene, R, a):
     t_probe = time.perf_counter() - t0
     step = max(1, int(probe_step * t_probe / max(a.cpu_seconds, 0.1)))
     step = min(step, probe_step)
-    t0 = time.perf_counter()
-    o = osc.render(u, R.random, row_start=0, row_step=step, threads=threads)
-    t = time.perf_counter() - t0
-    rays = o["closest_rays"] + o["shadow_rays"]
+    # a whole frame shorter than the target: repeat it so the sample still spans ~cpu_seconds
+    reps = 1 if step > 1 else max(1, int(round(a.cpu_seconds / max(t_probe * probe_step, 1e-3))))
+    rays, t = 0, 0.0
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        o = osc.render(u, R.random, row_start=0, row_step=step, threads=threads)
+        t += time.perf_counter() - t0
+        rays += o["closest_rays"] + o["shadow_rays"]
     return {"value": round(rays / t / 1e9, 6), "unit": "Grays/s", "cores": threads, "kind": "port",
             "sample": f"every {step}th row of frame 0 ({(a.height + step - 1) // step} rows x {a.width} px x "
-                      f"{a.spp} spp), {rays} rays in {t:.1f} s"}
+                      f"{a.spp} spp) x {reps}, {rays} rays in {t:.1f} s"}
 
 
 if __name__ == "__main__":

@@ -2,7 +2,7 @@
 # Round artefacts (run from the repo root on the GPU box):
 #   1. the default bench line (with the CPU baseline)           -> gpurun_out/${TAG}_bench.json
 #   2. rocprofv3 --kernel-trace --stats of a bench run            -> gpurun_out/${TAG}_kernel_stats.csv
-#   3. two --pmc passes (FETCH_SIZE, WRITE_SIZE) of the same run  -> gpurun_out/${TAG}_traffic_wf_trace.json
+#   3. three --pmc passes (FETCH_SIZE, WRITE_SIZE, TCC_HIT+TCC_MISS) -> gpurun_out/${TAG}_traffic_wf_trace.json gpurun_out/${TAG}_pmc_TCC_HIT_sum/run_counter_collection.csv
 TAG=${TAG:-r01}
 R=$PWD
 mkdir -p gpurun_out
@@ -12,8 +12,9 @@ cat gpurun_out/${TAG}_bench.json
 cd /tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/${TAG}_prof -o run --output-format csv -- python3 $R/bench.py --no-cpu > $R/gpurun_out/${TAG}_prof.log 2>&1 || { echo "kernel trace failed"; exit 1; }
 cp $R/gpurun_out/${TAG}_prof/run_kernel_stats.csv $R/gpurun_out/${TAG}_kernel_stats.csv
-for c in FETCH_SIZE WRITE_SIZE; do
-  timeout -k 10 300 rocprofv3 --pmc $c --output-format csv -d $R/gpurun_out/${TAG}_pmc_$c -o run -- python3 $R/bench.py --no-cpu > $R/gpurun_out/${TAG}_pmc_$c.log 2>&1 || { echo "pmc $c failed"; exit 1; }
+for c in FETCH_SIZE WRITE_SIZE "TCC_HIT_sum TCC_MISS_sum"; do
+  n=${c%% *}
+  timeout -k 10 300 rocprofv3 --pmc $c --output-format csv -d $R/gpurun_out/${TAG}_pmc_$n -o run -- python3 $R/bench.py --no-cpu > $R/gpurun_out/${TAG}_pmc_$n.log 2>&1 || { echo "pmc $n failed"; exit 1; }
 done
 cd $R
-python3 tools/traffic_json.py gpurun_out/${TAG}_pmc_FETCH_SIZE/run_counter_collection.csv,gpurun_out/${TAG}_pmc_WRITE_SIZE/run_counter_collection.csv gpurun_out/${TAG}_bench.json gpurun_out/${TAG}_traffic_wf_trace.json
+python3 tools/traffic_json.py gpurun_out/${TAG}_pmc_FETCH_SIZE/run_counter_collection.csv,gpurun_out/${TAG}_pmc_WRITE_SIZE/run_counter_collection.csv gpurun_out/${TAG}_bench.json gpurun_out/${TAG}_traffic_wf_trace.json gpurun_out/${TAG}_pmc_TCC_HIT_sum/run_counter_collection.csv
