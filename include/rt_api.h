@@ -96,8 +96,11 @@ typedef struct rt_opts {
     int32_t device;     /* HIP device ordinal */
     int32_t pipeline;   /* RT_PIPELINE_* */
     int32_t tail_paths; /* wavefront: below this many live paths the rest of the frame runs in the
-                           persistent finish kernel; 0 = default (1048576), 1 = never */
-    int32_t reserved[5];
+                           persistent finish kernel; 0 = default (4194304), 1 = never */
+    int32_t sort_bins;  /* wavefront: hits are sorted into this many bins of BVH leaf order between
+                           extend and shade (a power of two in [1024, 4096]); 0 = default (no
+                           sort), < 0 = no sort.  Never changes the image, only memory locality. */
+    int32_t reserved[4];
 } rt_opts;
 
 /* Image-space tile partition for multi-GPU rendering: the image is cut into
@@ -121,7 +124,8 @@ typedef struct rt_stats {
     uint64_t device_bytes;  /* device memory held by the context */
     float last_frame_ms;    /* device time of the last rt_render_frame (HIP events) */
     float kernel_ms[7];     /* per-stage device time of the last frame: megakernel [0];
-                               wavefront [0] generate [1] extend [2] shade [3] connect [4] resolve */
+                               wavefront [0] generate [1] extend [2] shade [3] connect [4] resolve
+                               [5] finish (tail) [6] hit sort */
     int32_t pipeline;       /* RT_PIPELINE_* that rendered the last frame */
     int32_t iterations;     /* wavefront: extend/shade/connect rounds of the last frame */
     /* wavefront: the queue traversal kernel (extend + connect launches; the finish tail excluded) */

@@ -212,7 +212,8 @@ class Renderer:
     draw() = updateUniforms + raytracingKernel dispatch + accumulation swap.
     """
 
-    def __init__(self, scene, width, height, device=0, pipeline="wavefront", seed=1, stream=None, tail_paths=0):
+    def __init__(self, scene, width, height, device=0, pipeline="wavefront", seed=1, stream=None, tail_paths=0,
+                 sort_bins=0):
         object.__setattr__(self, "_ctx", None)
         self.scene = scene
         self.width, self.height = int(width), int(height)
@@ -220,6 +221,7 @@ class Renderer:
         opts.device = device
         opts.pipeline = {"megakernel": 0, "wavefront": 1}[pipeline]
         opts.tail_paths = int(tail_paths)
+        opts.sort_bins = int(sort_bins)   # 0 = default hit sort, < 0 = none
         ctx = C.c_void_p()
         _check(lib().rt_create(C.byref(opts), C.byref(ctx)))
         object.__setattr__(self, "_ctx", ctx)

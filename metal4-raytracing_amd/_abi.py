@@ -116,7 +116,8 @@ class SceneDesc(C.Structure):
 
 
 class Opts(C.Structure):
-    _fields_ = [("device", C.c_int32), ("pipeline", C.c_int32), ("tail_paths", C.c_int32), ("reserved", C.c_int32 * 5)]
+    _fields_ = [("device", C.c_int32), ("pipeline", C.c_int32), ("tail_paths", C.c_int32), ("sort_bins", C.c_int32),
+                ("reserved", C.c_int32 * 4)]
 
 
 class TileSet(C.Structure):

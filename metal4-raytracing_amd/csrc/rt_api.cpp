@@ -35,6 +35,7 @@ struct rt_ctx {
     int device = 0;
     int pipeline = RT_PIPELINE_MEGAKERNEL;
     int tail_paths = 0;
+    int sort_bins = kSortBinsDefault;   // 0 = no hit sort
     hipStream_t own_stream = nullptr, stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     std::string err;
@@ -63,7 +64,7 @@ struct rt_ctx {
     // device buffers
     DevBuf d_pos, d_prev_pos, d_nrm, d_rest_pos, d_rest_nrm, d_jidx, d_jw, d_joints;
     DevBuf d_tri_info, d_inst, d_prev_inst, d_mat, d_lights, d_halton;
-    DevBuf d_tris, d_nodes, d_node_box, d_slot_to_tri, d_levels, d_maxabs;
+    DevBuf d_tris, d_nodes, d_node_box, d_slot_to_tri, d_levels, d_maxabs, d_tri_bin;
     DevBuf d_random, d_accum[2], d_depth, d_motion, d_gbuffer, d_counters;
     int width = 0, height = 0;
     int read_idx = 0;   // accum[read_idx] = history (TextureIndexAccumulation)
@@ -73,6 +74,7 @@ struct rt_ctx {
     // wavefront pipeline state
     WavefrontBuffers wf;
     DevBuf d_wf_color, d_wf_accum, d_wf_meta, d_wf_q0, d_wf_q1, d_wf_hits, d_wf_sq, d_wf_counts, d_wf_mprev, d_wf_extra;
+    DevBuf d_wf_sorted, d_wf_sort_table, d_wf_sort_total;
     WfFrameStats wfs{};
     bool last_wavefront = false;
 };
@@ -161,7 +163,8 @@ static size_t ctx_bytes(const rt_ctx* c) {
                            &c->d_halton, &c->d_tris, &c->d_nodes, &c->d_node_box, &c->d_slot_to_tri, &c->d_levels, &c->d_maxabs, &c->d_random,
                            &c->d_accum[0], &c->d_accum[1], &c->d_depth, &c->d_motion, &c->d_gbuffer, &c->d_counters,
                            &c->d_wf_color, &c->d_wf_accum, &c->d_wf_meta, &c->d_wf_q0, &c->d_wf_q1, &c->d_wf_hits,
-                           &c->d_wf_sq, &c->d_wf_counts, &c->d_wf_mprev, &c->d_wf_extra};
+                           &c->d_wf_sq, &c->d_wf_counts, &c->d_wf_mprev, &c->d_wf_extra,
+                           &c->d_wf_sorted, &c->d_wf_sort_table, &c->d_wf_sort_total, &c->d_tri_bin};
     size_t s = 0;
     for (auto* b : all) s += b->bytes;
     return s;
@@ -182,6 +185,9 @@ static rt_status ensure_wavefront(rt_ctx* c, size_t own_px, int spp, int max_ext
         if ((st = dev_alloc(c, c->d_wf_q1, qe * 32))) return st;
         if ((st = dev_alloc(c, c->d_wf_hits, qe * 16))) return st;
         if ((st = dev_alloc(c, c->d_wf_sq, qe * 48))) return st;
+        if (c->sort_bins) {
+            if ((st = dev_alloc(c, c->d_wf_sorted, qe * 48))) return st;
+        }
         W.cap_paths = paths;
         W.queue_entries = qe;
     }
@@ -190,6 +196,10 @@ static rt_status ensure_wavefront(rt_ctx* c, size_t own_px, int spp, int max_ext
         if ((st = dev_alloc(c, c->d_wf_mprev, px * 8))) return st;
         if ((st = dev_alloc(c, c->d_wf_extra, px * 8))) return st;
         W.cap_pixels = px;
+    }
+    if (c->sort_bins && !c->d_wf_sort_table.p) {
+        if ((st = dev_alloc(c, c->d_wf_sort_table, (size_t)kSortMaxBins * kSortBlocks * 4))) return st;
+        if ((st = dev_alloc(c, c->d_wf_sort_total, (size_t)kSortMaxBins * 4))) return st;
     }
     if (!c->d_wf_counts.p) {
         if ((st = dev_alloc(c, c->d_wf_counts, kWfCountWords * 4))) return st;
@@ -206,6 +216,9 @@ static rt_status ensure_wavefront(rt_ctx* c, size_t own_px, int spp, int max_ext
     W.counts = (uint32_t*)c->d_wf_counts.p;
     W.motion_prev = (float2*)c->d_wf_mprev.p;
     W.px_extra = (uint2*)c->d_wf_extra.p;
+    W.sorted = (float4*)c->d_wf_sorted.p;
+    W.sort_table = (uint32_t*)c->d_wf_sort_table.p;
+    W.sort_total = (uint32_t*)c->d_wf_sort_total.p;
     return RT_OK;
 }
 
@@ -228,11 +241,18 @@ rt_status rt_create(const rt_opts* opts, rt_ctx** out) {
         c->device = opts->device;
         c->pipeline = opts->pipeline;
         c->tail_paths = opts->tail_paths;
+        c->sort_bins = opts->sort_bins == 0 ? kSortBinsDefault : std::max(opts->sort_bins, 0);
     }
+    if (const char* e = getenv("RT_SORT_BINS")) c->sort_bins = std::max(0, atoi(e));  // tuning experiments
     if (c->device < 0 || c->device >= ndev) { delete c; FAIL((rt_ctx*)nullptr, RT_ERR_INVALID_ARG, "bad device ordinal"); }
     if (c->pipeline != RT_PIPELINE_MEGAKERNEL && c->pipeline != RT_PIPELINE_WAVEFRONT) {
         delete c;
         FAIL((rt_ctx*)nullptr, RT_ERR_INVALID_ARG, "bad pipeline");
+    }
+    if (c->sort_bins && (c->sort_bins < kSortMinBins || c->sort_bins > kSortMaxBins ||
+                         (c->sort_bins & (c->sort_bins - 1)))) {
+        delete c;
+        FAIL((rt_ctx*)nullptr, RT_ERR_INVALID_ARG, "sort_bins must be a power of two in [1024, 4096]");
     }
     hipError_t e = hipSetDevice(c->device);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking);
@@ -267,7 +287,8 @@ rt_status rt_destroy(rt_ctx* c) {
                      &c->d_tris, &c->d_nodes, &c->d_node_box, &c->d_slot_to_tri, &c->d_levels, &c->d_maxabs, &c->d_random, &c->d_accum[0],
                      &c->d_accum[1], &c->d_depth, &c->d_motion, &c->d_gbuffer, &c->d_counters,
                      &c->d_wf_color, &c->d_wf_accum, &c->d_wf_meta, &c->d_wf_q0, &c->d_wf_q1, &c->d_wf_hits,
-                     &c->d_wf_sq, &c->d_wf_counts, &c->d_wf_mprev, &c->d_wf_extra};
+                     &c->d_wf_sq, &c->d_wf_counts, &c->d_wf_mprev, &c->d_wf_extra,
+                     &c->d_wf_sorted, &c->d_wf_sort_table, &c->d_wf_sort_total, &c->d_tri_bin};
     for (auto* b : all) dev_free(*b);
     if (c->h_counters) hipHostFree(c->h_counters);
     if (c->wf.h_counts) hipHostFree(c->wf.h_counts);
@@ -450,6 +471,10 @@ rt_status rt_bvh_build(rt_ctx* c) {
     if ((st = dev_upload(c, c->d_node_box, c->bvh8.node_box.data(), c->bvh8.node_box.size() * 4))) return st;
     if ((st = dev_upload(c, c->d_slot_to_tri, c->bvh8.tri_order.data(), (size_t)n * 4))) return st;
     if ((st = dev_upload(c, c->d_levels, c->level_nodes.data(), c->level_nodes.size() * 4))) return st;
+    // hit-sort keys: the leaf-order bin of every triangle (DevScene::tri_bin)
+    std::vector<uint16_t> tri_bin(n);
+    for (uint32_t k = 0; k < n; ++k) tri_bin[c->bvh8.tri_order[k]] = (uint16_t)(((uint64_t)k * kSortMaxBins) / n);
+    if ((st = dev_upload(c, c->d_tri_bin, tri_bin.data(), (size_t)n * 2))) return st;
     HIPC(c, hipStreamSynchronize(c->stream));
     c->bvh_ready = true;
     return RT_OK;
@@ -580,6 +605,7 @@ rt_status rt_render_frame(rt_ctx* c, const Uniforms* U, const rt_tile_set* tiles
     S.materials = (const Material*)c->d_mat.p;
     S.lights = (const Light*)c->d_lights.p;
     S.halton = (const HaltonDim*)c->d_halton.p;
+    S.tri_bin = (const uint16_t*)c->d_tri_bin.p;
     S.max_submeshes = c->max_sub;
     S.num_tris = (int)c->num_tris;
     S.num_nodes8 = (int)c->bvh8.nodes.size();
@@ -610,7 +636,7 @@ rt_status rt_render_frame(rt_ctx* c, const Uniforms* U, const rt_tile_set* tiles
     if (wavefront) {
         const char* err = nullptr;
         c->wfs = WfFrameStats{};
-        if (own > 0 && !run_wavefront(S, P, c->wf, own, c->counting, c->tail_paths, c->stream, &c->wfs, &err))
+        if (own > 0 && !run_wavefront(S, P, c->wf, own, c->counting, c->tail_paths, c->sort_bins, c->stream, &c->wfs, &err))
             FAIL(c, RT_ERR_HIP, std::string("wavefront: ") + (err ? err : "?"));
         std::memcpy(c->stats.kernel_ms, c->wfs.stage_ms, sizeof c->stats.kernel_ms);
     } else {

@@ -33,6 +33,7 @@ struct DevScene {
     const Material* materials;
     const Light* lights;
     const HaltonDim* halton;
+    const uint16_t* tri_bin;   // per original triangle: its BVH leaf slot * kSortMaxBins / num_tris
     int max_submeshes;
     int num_tris;
     int num_nodes8;

@@ -91,12 +91,24 @@ struct WavefrontBuffers {
     uint32_t* h_counts = nullptr; // pinned host mirror
     float2* motion_prev = nullptr;
     uint2* px_extra = nullptr;    // per own pixel: (first extra path - base_paths, count)
+    // per-bounce hit sort (wf_sort_*): the hits reordered by key as {o, d, hit} float4 triples,
+    // per-(bin, block) counts, per-bin totals
+    float4* sorted = nullptr;
+    uint32_t* sort_table = nullptr;
+    uint32_t* sort_total = nullptr;
     size_t cap_paths = 0;         // base + extra paths
     size_t cap_pixels = 0;
-    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+    hipEvent_t ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
 };
+// Hit sort: kSortBlocks blocks of kSortThreads share one partition of the queue in the histogram
+// and scatter kernels; bins are a power of two in [kSortMinBins, kSortMaxBins].
+constexpr int kSortBlocks = 256;
+constexpr int kSortThreads = 1024;
+constexpr int kSortMinBins = 1024;
+constexpr int kSortMaxBins = 4096;
+constexpr int kSortBinsDefault = 0;   // off: measured slower on C3g (DESIGN.md §3 'Hit sort')
 // Per-frame measurements of the wavefront pipeline. stage_ms: [0] generate, [1] extend,
-// [2] shade, [3] connect, [4] resolve (+extra-sample bookkeeping), [5] finish.
+// [2] shade, [3] connect, [4] resolve (+extra-sample bookkeeping), [5] finish, [6] hit sort.
 struct WfFrameStats {
     float stage_ms[7];
     int iterations;
@@ -106,8 +118,9 @@ struct WfFrameStats {
 };
 // Runs one frame; returns false on a HIP error (message in *err).
 // tail_paths: finish-kernel threshold (0 = default / RT_TAIL_RAYS).
+// sort_bins: hit-sort bins (0 = no sort).
 bool run_wavefront(const DevScene& S, const FrameParams& P, WavefrontBuffers& W, int own_tiles, bool count,
-                   int tail_paths, hipStream_t stream, WfFrameStats* fs, const char** err);
+                   int tail_paths, int sort_bins, hipStream_t stream, WfFrameStats* fs, const char** err);
 size_t wavefront_queue_entries(size_t paths, int max_extra);
 
 // Packed-tile layout of the multi-GPU gather: element i of a rank's packed buffer is pixel

@@ -31,7 +31,7 @@ namespace rt {
 
 namespace {
 
-constexpr uint32_t kTailRaysDefault = 1048576;
+constexpr uint32_t kTailRaysDefault = 4194304;
 static uint32_t tail_rays() {  // RT_TAIL_RAYS overrides (tuning experiments)
     static uint32_t v = [] { const char* e = getenv("RT_TAIL_RAYS"); return e ? (uint32_t)atol(e) : kTailRaysDefault; }();
     return v;
@@ -44,6 +44,16 @@ static int refill_min() {  // RT_REFILL_MIN overrides (tuning experiments)
 
 static int chunk_size() {  // RT_CHUNK overrides (tuning experiments)
     static int v = [] { const char* e = getenv("RT_CHUNK"); return e ? atoi(e) : 64; }();
+    return v;
+}
+
+static int env_int(const char* name, int dflt) {  // tuning experiments
+    const char* e = getenv(name);
+    return e ? atoi(e) : dflt;
+}
+
+static bool wf_log() {  // RT_WF_LOG=1: per-iteration queue sizes and stage times on stderr
+    static const bool v = env_int("RT_WF_LOG", 0) != 0;
     return v;
 }
 
@@ -151,12 +161,21 @@ struct WfParams {
     int tri_vote;          // wf_trace phase vote threshold (lanes with triangle work), 0 = off
     int chunk;             // wf_trace dynamic chunk size (rays per grab), 0 = static wave ranges
     uint32_t tail;         // live paths below which wf_finish runs the rest
+    uint32_t sort_bins;    // hit-sort bins (0 = shade reads the extend queue unsorted)
+    int sort_xcd;          // sorted shade: XCD k shades the k-th eighth of the sorted hits
+    int steal;             // wf_trace: a wave whose XCD's eighth ran dry takes chunks of the others
+    int diag;              // wf_finish: record the diagnostics slots (RT_WF_LOG)
+    int finish_step;       // tail: wf_finish_step (1) or the per-segment wf_finish (0)
+    int shade_min;         // wf_finish_step: shade once this many lanes wait (or none traverses)
 };
 
 // counter slots (cslot): [q*8 + shard] ray queues q = 0, 1; [16 + shard] shadow queue; [24] extra allocator
 constexpr int kCntShadowQ = 16;
 constexpr int kCntExtra = 24;
 constexpr int kCntChunkFinish = 25;
+constexpr int kCntSorted = 26;
+constexpr uint32_t kNoKey = 0xffffffffu;
+constexpr int kCntDiagSegs = 27, kCntDiagIters = 28, kCntDiagTime = 29;   // wf_finish diagnostics   // sort key of a miss (dropped by the sort)         // hits the sort kept (misses dropped) = shade's input size
 constexpr int kCntChunkExtend = 32;   // 8 per-XCD chunk counters each
 constexpr int kCntChunkConnect = 40;
 
@@ -280,7 +299,11 @@ __global__ void __launch_bounds__(kBlock) wf_generate(DevScene S, FrameParams P,
 }
 
 // ---- shade -------------------------------------------------------------------------------------------
-template <bool FULL>
+// SORTED: the input is the hit-sorted array (wf_sort_scatter; misses already dropped) and the
+// blocks of XCD k (blockIdx % 8) shade the k-th eighth of it, so one XCD's L2 serves one scene
+// region and the rays / shadow rays it appends to its queue shard stay grouped by region for
+// the next extend / connect launches (which hand shard k's range to XCD k).
+template <bool FULL, bool SORTED>
 __global__ void __launch_bounds__(kBlock) wf_shade(DevScene S, FrameParams P, WfParams Q, int cur, uint32_t n) {
     __shared__ HaltonDim lds_halton[kHaltonLds];
     __shared__ BlockAlloc ba_ray, ba_sh;
@@ -296,17 +319,34 @@ __global__ void __launch_bounds__(kBlock) wf_shade(DevScene S, FrameParams P, Wf
     f2 zero2;
     zero2.x = 0.0f;
     zero2.y = 0.0f;
-    for (uint32_t base = blockIdx.x * kBlock; base < n; base += gridDim.x * kBlock) {
+    uint32_t beg = blockIdx.x * kBlock, end = n, stride = gridDim.x * kBlock;
+    if (SORTED) n = __builtin_amdgcn_readfirstlane(Q.W.counts[cslot(kCntSorted)]);
+    end = n;
+    if (SORTED && Q.sort_xcd) {   // grid is a multiple of 8 (grid_for)
+        beg = (uint32_t)(((uint64_t)n * (uint32_t)shard) / kShards);
+        end = (uint32_t)(((uint64_t)n * (uint32_t)(shard + 1)) / kShards);
+        beg += (blockIdx.x >> 3) * kBlock;
+        stride = (gridDim.x >> 3) * kBlock;
+    }
+    for (uint32_t base = beg; base < end; base += stride) {
         uint32_t g = base + threadIdx.x;
         StepResult r;
         r.next = false;
         r.shadow = false;
         uint32_t pid = 0;
         f3 rayO = mk3(0, 0, 0), rayD = mk3(0, 0, 0);
-        if (g < n) {
-            uint32_t e = entry_of(cnt, g, Q.seg_cap);
-            float4 o = qin[2 * (size_t)e], d = qin[2 * (size_t)e + 1];
-            float4 hv = Q.W.hits[e];
+        if (g < end) {
+            float4 o, d, hv;
+            if (SORTED) {
+                o = Q.W.sorted[3 * (size_t)g];
+                d = Q.W.sorted[3 * (size_t)g + 1];
+                hv = Q.W.sorted[3 * (size_t)g + 2];
+            } else {
+                uint32_t e = entry_of(cnt, g, Q.seg_cap);
+                o = qin[2 * (size_t)e];
+                d = qin[2 * (size_t)e + 1];
+                hv = Q.W.hits[e];
+            }
             pid = __float_as_uint(o.w);
             Hit h;
             h.t = hv.x;
@@ -344,6 +384,108 @@ __global__ void __launch_bounds__(kBlock) wf_shade(DevScene S, FrameParams P, Wf
             qout[2 * (size_t)nr] = make_float4(rayO.x, rayO.y, rayO.z, __uint_as_float(pid));
             qout[2 * (size_t)nr + 1] = make_float4(rayD.x, rayD.y, rayD.z, 0.0f);
         }
+    }
+}
+
+// ---- hit sort (between extend and shade) -------------------------------------------------------------
+// A counting sort of the extend queue's hits by key (the bin of the hit triangle's BVH leaf slot,
+// S.tri_bin; leaf order is spatially coherent, so a bin is one scene region), in three launches: per-block histograms, a scan of each bin's row of block counts, and a
+// scatter that writes {o, d, hit} of every hit to its bin's range.  Misses are dropped (their
+// paths end, :321-322).  The order inside a bin is arbitrary; per-path results do not depend on
+// the order paths are shaded in, so the output stays bit-identical.
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
+    const uint32_t lane = lane_id();
+    #pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t t = __shfl_up(v, off, 64);
+        if (lane >= (uint32_t)off) v += t;
+    }
+    return v;
+}
+
+// block b's share of the dense queue index range (the same in hist and scatter)
+__device__ __forceinline__ void sort_range(uint32_t n, uint32_t& beg, uint32_t& end) {
+    beg = (uint32_t)(((uint64_t)n * blockIdx.x) / kSortBlocks);
+    end = (uint32_t)(((uint64_t)n * (blockIdx.x + 1)) / kSortBlocks);
+}
+
+// sort key of queue entry e: kNoKey for a miss, else the leaf bin at Q.sort_bins resolution
+__device__ __forceinline__ uint32_t sort_key(const DevScene& S, const WfParams& Q, uint32_t e, uint32_t shift) {
+    const uint32_t id = __float_as_uint(Q.W.hits[e].y);
+    return id == 0xffffffffu ? kNoKey : ((uint32_t)S.tri_bin[id] >> shift);
+}
+
+__global__ void __launch_bounds__(kSortThreads) wf_sort_hist(DevScene S, WfParams Q, int cur) {
+    __shared__ uint32_t h[kSortMaxBins];
+    const uint32_t shift = __builtin_ctz(kSortMaxBins) - __builtin_ctz(Q.sort_bins);
+    const uint32_t K = Q.sort_bins;
+    const ShardPrefix cnt = load_prefix(Q.W.counts + cslot(cur * kShards));
+    for (uint32_t k = threadIdx.x; k < K; k += kSortThreads) h[k] = 0;
+    __syncthreads();
+    uint32_t beg, end;
+    sort_range(cnt.end[kShards - 1], beg, end);
+    for (uint32_t g = beg + threadIdx.x; g < end; g += kSortThreads) {
+        const uint32_t k = sort_key(S, Q, entry_of(cnt, g, Q.seg_cap), shift);
+        if (k != kNoKey) atomicAdd(&h[k], 1u);
+    }
+    __syncthreads();
+    for (uint32_t k = threadIdx.x; k < K; k += kSortThreads) Q.W.sort_table[(size_t)k * kSortBlocks + blockIdx.x] = h[k];
+}
+
+// one block per bin: exclusive scan of the bin's kSortBlocks block counts (in place) + bin total
+__global__ void __launch_bounds__(kSortBlocks) wf_sort_rowscan(WfParams Q) {
+    __shared__ uint32_t w[kSortBlocks / 64];
+    uint32_t* row = Q.W.sort_table + (size_t)blockIdx.x * kSortBlocks;
+    const uint32_t v = row[threadIdx.x];
+    const uint32_t incl = wave_incl_scan(v);
+    const int wave = threadIdx.x >> 6;
+    if (lane_id() == 63) w[wave] = incl;
+    __syncthreads();
+    uint32_t base = 0;
+    for (int i = 0; i < wave; ++i) base += w[i];
+    row[threadIdx.x] = base + incl - v;
+    if (threadIdx.x == kSortBlocks - 1) Q.W.sort_total[blockIdx.x] = base + incl;
+}
+
+__global__ void __launch_bounds__(kSortThreads) wf_sort_scatter(DevScene S, WfParams Q, int cur) {
+    __shared__ uint32_t off[kSortMaxBins];
+    const uint32_t shift = __builtin_ctz(kSortMaxBins) - __builtin_ctz(Q.sort_bins);
+    __shared__ uint32_t w[kSortThreads / 64];
+    const uint32_t K = Q.sort_bins, per = K / kSortThreads;   // 1, 2 or 4 bins per thread
+    const ShardPrefix cnt = load_prefix(Q.W.counts + cslot(cur * kShards));
+    // bin starts: exclusive scan of the bin totals, plus this block's offset inside each bin
+    uint32_t loc[kSortMaxBins / kSortThreads];
+    uint32_t s = 0;
+    for (uint32_t i = 0; i < per; ++i) {
+        loc[i] = s;
+        s += Q.W.sort_total[threadIdx.x * per + i];
+    }
+    const uint32_t incl = wave_incl_scan(s);
+    const int wave = threadIdx.x >> 6;
+    if (lane_id() == 63) w[wave] = incl;
+    __syncthreads();
+    uint32_t base = 0;
+    for (int i = 0; i < wave; ++i) base += w[i];
+    const uint32_t excl = base + incl - s;
+    for (uint32_t i = 0; i < per; ++i) {
+        const uint32_t k = threadIdx.x * per + i;
+        off[k] = excl + loc[i] + Q.W.sort_table[(size_t)k * kSortBlocks + blockIdx.x];
+    }
+    if (blockIdx.x == 0 && threadIdx.x == kSortThreads - 1) Q.W.counts[cslot(kCntSorted)] = excl + s;
+    __syncthreads();
+    const float4* qin = Q.W.q[cur];
+    uint32_t beg, end;
+    sort_range(cnt.end[kShards - 1], beg, end);
+    for (uint32_t g = beg + threadIdx.x; g < end; g += kSortThreads) {
+        const uint32_t e = entry_of(cnt, g, Q.seg_cap);
+        const float4 hv = Q.W.hits[e];
+        const uint32_t id = __float_as_uint(hv.y);
+        if (id == 0xffffffffu) continue;
+        const uint32_t pos = atomicAdd(&off[(uint32_t)S.tri_bin[id] >> shift], 1u);
+        const float4 o = qin[2 * (size_t)e], d = qin[2 * (size_t)e + 1];
+        Q.W.sorted[3 * (size_t)pos] = o;
+        Q.W.sorted[3 * (size_t)pos + 1] = d;
+        Q.W.sorted[3 * (size_t)pos + 2] = hv;
     }
 }
 
@@ -387,9 +529,10 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 
     // grabbed with one atomic per chunk when the current one runs out
     uint32_t wnext, wend;
     const uint32_t xcd = blockIdx.x & 7u;
-    const uint32_t xbeg = (uint32_t)(((uint64_t)n * xcd) / 8), xend = (uint32_t)(((uint64_t)n * (xcd + 1)) / 8);
-    uint32_t* chunk_ctr = Q.W.counts + cslot((ANY ? kCntChunkConnect : kCntChunkExtend) + (int)xcd);
-    bool exhausted = false;
+    uint32_t* const chunk_ctr0 = Q.W.counts + cslot(ANY ? kCntChunkConnect : kCntChunkExtend);
+    // eighth the wave grabs from: its own XCD's, then (Q.steal) the following XCDs' once that one
+    // ran dry, so one slow region cannot hold the launch; 8 = nothing left
+    uint32_t stolen = 0;
     if (Q.chunk > 0) {
         wnext = wend = 0;
     } else {
@@ -410,12 +553,14 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 
     while (true) {
         // refill idle lanes from the wave's range
         unsigned long long idle = __ballot(!active);
-        if (Q.chunk > 0 && wnext >= wend && !exhausted && (__popcll(idle) >= Q.refill_min || idle == ~0ull)) {
+        if (Q.chunk > 0 && wnext >= wend && stolen < 8 && (__popcll(idle) >= Q.refill_min || idle == ~0ull)) {
+            const uint32_t xc = (xcd + stolen) & 7u;
+            const uint32_t xbeg = (uint32_t)(((uint64_t)n * xc) / 8), xend = (uint32_t)(((uint64_t)n * (xc + 1)) / 8);
             uint32_t base = 0;
-            if (lane_id() == 0) base = atomicAdd(chunk_ctr, (uint32_t)Q.chunk);
+            if (lane_id() == 0) base = atomicAdd(chunk_ctr0 + cslot((int)xc), (uint32_t)Q.chunk);
             base = xbeg + __builtin_amdgcn_readfirstlane(base);
             if (base >= xend) {
-                exhausted = true;
+                stolen = Q.steal ? stolen + 1 : 8;
             } else {
                 wnext = base;
                 wend = min(base + (uint32_t)Q.chunk, xend);
@@ -578,6 +723,10 @@ __global__ void __launch_bounds__(kBlock) wf_finish(DevScene S, FrameParams P, W
     p.color = p.accum = mk3(0, 0, 0);
     p.bounce = p.tpass = p.step = 0;
     f3 rayO = mk3(0, 0, 0), rayD = mk3(0, 0, 0);
+    // diagnostics (Q.diag, RT_WF_LOG): segments of the longest path, loop iterations and wall
+    // time (s_memrealtime, 100 MHz) of the slowest wave
+    uint32_t segs = 0, max_segs = 0, iters = 0;
+    const uint64_t t_start = Q.diag ? __builtin_amdgcn_s_memrealtime() : 0;
     while (true) {
         unsigned long long idle = __ballot(!active);
         if (wnext >= wend && !exhausted && (__popcll(idle) >= 8 || idle == ~0ull)) {
@@ -613,9 +762,11 @@ __global__ void __launch_bounds__(kBlock) wf_finish(DevScene S, FrameParams P, W
             wnext += (uint32_t)__popcll(idle);
         }
         if (__ballot(active) == 0ull) break;
+        ++iters;
         if (!active) continue;
         // one segment of the path (:311-774)
         bool ends = true;
+        ++segs;
         Hit h;
         n_closest++;
         if (trace8<false, COUNT>(S, rayO, rayD, 0.0f, INFINITY, h, stack, tc, overflow)) {
@@ -635,6 +786,268 @@ __global__ void __launch_bounds__(kBlock) wf_finish(DevScene S, FrameParams P, W
         if (ends) {
             Q.W.p_accum[pid] = make_float4(p.accum.x, p.accum.y, p.accum.z, 0.0f);
             active = false;
+            max_segs = max(max_segs, segs);
+            segs = 0;
+        }
+    }
+    if (Q.diag) {
+        const uint32_t dt = (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_start);
+        for (int off = 32; off > 0; off >>= 1) max_segs = max(max_segs, (uint32_t)__shfl_xor((int)max_segs, off, 64));
+        if (lane_id() == 0) {
+            atomicMax(&Q.W.counts[cslot(kCntDiagSegs)], max_segs);
+            atomicMax(&Q.W.counts[cslot(kCntDiagIters)], iters);
+            atomicMax(&Q.W.counts[cslot(kCntDiagTime)], dt);
+        }
+    }
+    flush_counters(P, n_closest, n_shadow, 0, tc, COUNT, overflow);
+}
+
+// ---- finish, step-interleaved ------------------------------------------------------------------------
+// Same work as wf_finish, but every lane advances by ONE traversal step per iteration (one 8-wide
+// node or up to two triangles, closest-hit or shadow any-hit), as in wf_trace.  A lane whose
+// closest-hit traversal ended waits in kReady; the wave shades all waiting lanes together once
+// at least Q.shade_min of them wait (or no lane is traversing), then each continues with its
+// shadow ray, its next ray, or the next path of the queue.  A wave therefore costs the sum of its
+// own lanes' steps, not the sum over segments of the slowest lane's traversal: the glass paths
+// left at the tail (up to ~20 segments) no longer wait for their wave's worst ray every segment.
+template <bool COUNT, bool FULL, int WAVES>
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES, WAVES)))
+wf_finish_step(DevScene S, FrameParams P, WfParams Q, int cur, uint32_t n) {
+    __shared__ int lds_stack[kStackSize * kBlock];
+    __shared__ uint4 lds_top[kTopNodes * 5];
+    __shared__ HaltonDim lds_halton[kHaltonLds];
+    int* stack = &lds_stack[threadIdx.x];
+    const uint32_t n_top = (uint32_t)min(S.num_nodes8, kTopNodes);
+    for (uint32_t i = threadIdx.x; i < n_top * 5; i += kBlock) lds_top[i] = reinterpret_cast<const uint4*>(S.nodes8)[i];
+    load_halton(S, lds_halton);   // ends with a block barrier
+    const HaltonTab halton{lds_halton, S.halton};
+    const Uniforms& U = P.U;
+    const ShardPrefix cnt = load_prefix(Q.W.counts + cslot(cur * kShards));
+    const float4* qin = Q.W.q[cur];
+    uint32_t* chunk_ctr = Q.W.counts + cslot(kCntChunkFinish);
+    constexpr uint32_t kChunk = 64;
+    constexpr int kIdle = 0, kClosest = 1, kShadow = 2, kReady = 3;
+    TraceCounters tc{0, 0};
+    bool overflow = false;
+    uint32_t n_closest = 0, n_shadow = 0;
+    f2 zero2;
+    zero2.x = 0.0f;
+    zero2.y = 0.0f;
+    uint32_t wnext = 0, wend = 0;
+    bool exhausted = false;
+    int mode = kIdle;
+    // path
+    uint32_t pid = 0;
+    uint4 meta = make_uint4(0, 0, 0, 0);
+    PathRegs p;
+    p.color = p.accum = mk3(0, 0, 0);
+    p.bounce = p.tpass = p.step = 0;
+    f3 rayO = mk3(0, 0, 0), rayD = mk3(0, 0, 0), contrib = mk3(0, 0, 0);
+    bool next = false, hit_any = false;
+    // traversal
+    RaySetup R = ray_setup(mk3(0, 0, 0), mk3(1, 0, 0));
+    float best = 0.0f, bu = 0.0f, bv = 0.0f;
+    uint32_t best_id = 0xffffffffu, g_base = 0, g_hits = 0, t_base = 0, t_mask = 0;
+    bool g_flip = false;
+    int sp = 0;
+    auto start_trace = [&](f3 o, f3 d, float tmax) {
+        R = ray_setup(o, d);
+        best = tmax;
+        best_id = 0xffffffffu;
+        bu = bv = 0.0f;
+        g_base = 0;
+        g_hits = 1;   // virtual group holding the root
+        g_flip = false;
+        t_mask = 0;
+        sp = 0;
+        hit_any = false;
+    };
+    // diagnostics (Q.diag, RT_WF_LOG): segments of the longest path, loop iterations and wall
+    // time (s_memrealtime, 100 MHz) of the slowest wave
+    uint32_t segs = 0, max_segs = 0, iters = 0;
+    const uint64_t t_start = Q.diag ? __builtin_amdgcn_s_memrealtime() : 0;
+    auto end_path = [&]() {
+        Q.W.p_accum[pid] = make_float4(p.accum.x, p.accum.y, p.accum.z, 0.0f);
+        mode = kIdle;
+        max_segs = max(max_segs, segs);
+        segs = 0;
+    };
+
+    while (true) {
+        // ---- refill idle lanes with the next remaining paths (chunks of 64 from one counter)
+        const unsigned long long idle = __ballot(mode == kIdle);
+        const bool refill = __popcll(idle) >= Q.refill_min || idle == ~0ull;
+        if (wnext >= wend && !exhausted && refill) {
+            uint32_t base = 0;
+            if (lane_id() == 0) base = atomicAdd(chunk_ctr, kChunk);
+            base = __builtin_amdgcn_readfirstlane(base);
+            if (base >= n) {
+                exhausted = true;
+            } else {
+                wnext = base;
+                wend = min(base + kChunk, n);
+            }
+        }
+        if (idle != 0ull && wnext < wend && refill) {
+            if (mode == kIdle) {
+                const uint32_t g = wnext + mbcnt64(idle);
+                if (g < wend) {
+                    const uint32_t e = entry_of(cnt, g, Q.seg_cap);
+                    const float4 o = qin[2 * (size_t)e], d = qin[2 * (size_t)e + 1];
+                    pid = __float_as_uint(o.w);
+                    meta = Q.W.p_meta[pid];
+                    const float4 c = Q.W.p_color[pid], a = Q.W.p_accum[pid];
+                    p.color = mk3(c.x, c.y, c.z);
+                    p.accum = mk3(a.x, a.y, a.z);
+                    p.bounce = (int)(meta.z & 0xffu);
+                    p.tpass = (int)((meta.z >> 8) & 0xffu);
+                    p.step = (int)(meta.z >> 16);
+                    rayO = ld3(o);
+                    rayD = ld3(d);
+                    start_trace(rayO, rayD, INFINITY);
+                    mode = kClosest;
+                    n_closest++;
+                    segs++;
+                }
+            }
+            wnext += (uint32_t)__popcll(idle);
+        }
+        if (__ballot(mode != kIdle) == 0ull) break;   // idle everywhere => refill found nothing
+        ++iters;
+
+        // ---- one traversal step (closest hit or shadow any-hit)
+        if (mode == kClosest || mode == kShadow) {
+            const bool any = mode == kShadow;
+            bool tdone = false;
+            if (t_mask) {
+                // up to two triangles, both fetched before either is tested, tested in mask order
+                const int k0 = lowest_bit(t_mask);
+                t_mask &= t_mask - 1u;
+                const bool two = t_mask != 0u;
+                const int k1 = two ? lowest_bit(t_mask) : k0;
+                if (two) t_mask &= t_mask - 1u;
+                const float4* tp0 = S.tris + 3 * (size_t)(t_base + (uint32_t)k0);
+                const float4* tp1 = S.tris + 3 * (size_t)(t_base + (uint32_t)k1);
+                const float4 a0 = tp0[0], a1 = tp0[1], a2 = tp0[2];
+                const float4 b0 = tp1[0], b1 = tp1[1], b2 = tp1[2];
+                if (COUNT) tc.tris += two ? 2u : 1u;
+                float t, u, v;
+                if (intersect_triangle(R.pre, R.o, ld3(a0), ld3(a1), ld3(a2), 0.0f, best, &t, &u, &v)) {
+                    const uint32_t id = __float_as_uint(a0.w);
+                    if (any) {
+                        hit_any = true;
+                        tdone = true;
+                    } else if (t < best || id < best_id) {
+                        best = t;
+                        best_id = id;
+                        bu = u;
+                        bv = v;
+                    }
+                }
+                if (two && !tdone && intersect_triangle(R.pre, R.o, ld3(b0), ld3(b1), ld3(b2), 0.0f, best, &t, &u, &v)) {
+                    const uint32_t id = __float_as_uint(b0.w);
+                    if (any) {
+                        hit_any = true;
+                        tdone = true;
+                    } else if (t < best || id < best_id) {
+                        best = t;
+                        best_id = id;
+                        bu = u;
+                        bv = v;
+                    }
+                }
+            } else {
+                if (!g_hits) {   // sp > 0 here (checked at the end of the previous step)
+                    --sp;
+                    const uint32_t ent = (uint32_t)stack[sp * kBlock];
+                    g_base = ent >> 9;
+                    g_flip = (ent >> 8) & 1u;
+                    g_hits = ent & 0xffu;
+                }
+                const int r = g_flip ? highest_bit(g_hits) : lowest_bit(g_hits);
+                g_hits &= ~(1u << r);
+                if (g_hits) {
+                    if (sp < kStackSize) {
+                        stack[sp * kBlock] = (int)pack_group(g_base, g_flip, g_hits);
+                        ++sp;
+                    } else {
+                        overflow = true;
+                    }
+                }
+                if (COUNT) tc.nodes++;
+                const uint32_t ni = g_base + (uint32_t)r;
+                NodeWords w;
+                if (ni < n_top) {
+                    const uint4* l = lds_top + 5 * ni;
+                    w.h0 = __builtin_bit_cast(float4, l[0]);
+                    w.h1 = l[1];
+                    w.qx = l[2];
+                    w.qy = l[3];
+                    w.qz = l[4];
+                } else {
+                    w = load_node8(S.nodes8, ni);
+                }
+                test_node8_words(w, R, 0.0f, best, g_hits, t_mask, g_base, t_base, g_flip);
+            }
+            if (!tdone && !t_mask && !g_hits && sp == 0) tdone = true;
+            if (tdone) {
+                if (any) {   // shadow ray done: unoccluded -> add its contribution (:741-743)
+                    if (!hit_any) p.accum = p.accum + contrib;
+                    if (next) {
+                        start_trace(rayO, rayD, INFINITY);
+                        mode = kClosest;
+                        n_closest++;
+                        segs++;
+                    } else {
+                        end_path();
+                    }
+                } else if (best_id == 0xffffffffu) {   // miss -> path ends (:321-322)
+                    end_path();
+                } else {
+                    mode = kReady;
+                }
+            }
+        }
+
+        // ---- shade the waiting lanes together (:324-774)
+        const unsigned long long ready = __ballot(mode == kReady);
+        if (ready != 0ull &&
+            (__popcll(ready) >= Q.shade_min || __ballot(mode == kClosest || mode == kShadow) == 0ull)) {
+            if (mode == kReady) {
+                Hit h;
+                h.t = best;
+                h.id = best_id;
+                h.u = bu;
+                h.v = bv;
+                const int sample = (int)meta.y;
+                StepResult r;
+                shade_step<FULL>(S, U, halton, (int)meta.w, sample, rayO, rayD, h, p, sample == 0 && p.step == 0,
+                                 zero2, false, zero2, r);
+                write_pixel_outputs(P, meta.x, r, FULL);
+                next = r.next;
+                if (r.shadow) {
+                    contrib = r.contrib;
+                    start_trace(r.so, r.sd, r.stmax);
+                    mode = kShadow;
+                    n_shadow++;
+                } else if (r.next) {
+                    start_trace(rayO, rayD, INFINITY);
+                    mode = kClosest;
+                    n_closest++;
+                    segs++;
+                } else {
+                    end_path();
+                }
+            }
+        }
+    }
+    if (Q.diag) {
+        const uint32_t dt = (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_start);
+        for (int off = 32; off > 0; off >>= 1) max_segs = max(max_segs, (uint32_t)__shfl_xor((int)max_segs, off, 64));
+        if (lane_id() == 0) {
+            atomicMax(&Q.W.counts[cslot(kCntDiagSegs)], max_segs);
+            atomicMax(&Q.W.counts[cslot(kCntDiagIters)], iters);
+            atomicMax(&Q.W.counts[cslot(kCntDiagTime)], dt);
         }
     }
     flush_counters(P, n_closest, n_shadow, 0, tc, COUNT, overflow);
@@ -759,21 +1172,31 @@ static unsigned trace_grid_cap() {
     return cap;
 }
 
-// resident blocks of the persistent finish kernel instantiation in use
-static unsigned finish_grid_cap(bool count, bool full) {
-    static unsigned cap[4] = {0, 0, 0, 0};
-    const int k = (count ? 2 : 0) + (full ? 1 : 0);
-    if (!cap[k]) {
-        int dev = 0, cus = 256, per = 0;
-        if (hipGetDevice(&dev) == hipSuccess) hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        hipError_t e = count ? (full ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, wf_finish<true, true>, kBlock, 0)
-                                     : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, wf_finish<true, false>, kBlock, 0))
-                             : (full ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, wf_finish<false, true>, kBlock, 0)
-                                     : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, wf_finish<false, false>, kBlock, 0));
-        if (e != hipSuccess || per < 1) per = 2;
-        cap[k] = (unsigned)(cus * per);
+// resident blocks (CUs x blocks per CU) of a persistent kernel
+template <typename K>
+static unsigned resident_grid(K kernel, int fallback_per_cu) {
+    int dev = 0, cus = 256, per = 0;
+    if (hipGetDevice(&dev) == hipSuccess) hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, kBlock, 0) != hipSuccess || per < 1)
+        per = fallback_per_cu;
+    return (unsigned)(cus * per);
+}
+
+// the finish launch: step-interleaved (STEP, default) or per-segment kernel, grid = resident blocks
+template <bool STEP, bool COUNT, bool FULL>
+static void launch_finish(const DevScene& S, const FrameParams& P, const WfParams& Q, int cur, uint32_t n,
+                          hipStream_t stream) {
+    static const int waves = env_int("RT_FINISH_WAVES", 4);
+    if (STEP && waves == 3) {
+        static const unsigned cap = resident_grid(wf_finish_step<COUNT, FULL, 3>, 2);
+        hipLaunchKernelGGL((wf_finish_step<COUNT, FULL, 3>), dim3(grid_for(n, cap)), dim3(kBlock), 0, stream, S, P, Q, cur, n);
+    } else if (STEP) {
+        static const unsigned cap = resident_grid(wf_finish_step<COUNT, FULL, 4>, 2);
+        hipLaunchKernelGGL((wf_finish_step<COUNT, FULL, 4>), dim3(grid_for(n, cap)), dim3(kBlock), 0, stream, S, P, Q, cur, n);
+    } else {
+        static const unsigned cap = resident_grid(wf_finish<COUNT, FULL>, 2);
+        hipLaunchKernelGGL((wf_finish<COUNT, FULL>), dim3(grid_for(n, cap)), dim3(kBlock), 0, stream, S, P, Q, cur, n);
     }
-    return cap[k];
 }
 
 static uint32_t queue_total(const uint32_t* h, int q) {
@@ -813,13 +1236,16 @@ static bool iterate(const DevScene& S, const FrameParams& P, WfParams& Q, int& c
             // run the tail to completion in one launch
             WF_CHECK(hipEventRecord(W.ev[0], stream));
             WF_CHECK(hipMemsetAsync(W.counts + cslot(kCntChunkFinish), 0, sizeof(uint32_t), stream));
-            unsigned g = grid_for(n, finish_grid_cap(count, full));
-            if (count) {
-                if (full) hipLaunchKernelGGL((wf_finish<true, true>), dim3(g), dim3(kBlock), 0, stream, S, P, Q, cur, n);
-                else hipLaunchKernelGGL((wf_finish<true, false>), dim3(g), dim3(kBlock), 0, stream, S, P, Q, cur, n);
+            if (Q.finish_step) {
+                if (count) full ? launch_finish<true, true, true>(S, P, Q, cur, n, stream)
+                                : launch_finish<true, true, false>(S, P, Q, cur, n, stream);
+                else full ? launch_finish<true, false, true>(S, P, Q, cur, n, stream)
+                          : launch_finish<true, false, false>(S, P, Q, cur, n, stream);
             } else {
-                if (full) hipLaunchKernelGGL((wf_finish<false, true>), dim3(g), dim3(kBlock), 0, stream, S, P, Q, cur, n);
-                else hipLaunchKernelGGL((wf_finish<false, false>), dim3(g), dim3(kBlock), 0, stream, S, P, Q, cur, n);
+                if (count) full ? launch_finish<false, true, true>(S, P, Q, cur, n, stream)
+                                : launch_finish<false, true, false>(S, P, Q, cur, n, stream);
+                else full ? launch_finish<false, false, true>(S, P, Q, cur, n, stream)
+                          : launch_finish<false, false, false>(S, P, Q, cur, n, stream);
             }
             WF_CHECK(hipGetLastError());
             WF_CHECK(hipEventRecord(W.ev[1], stream));
@@ -828,6 +1254,12 @@ static bool iterate(const DevScene& S, const FrameParams& P, WfParams& Q, int& c
             WF_CHECK(hipEventElapsedTime(&a, W.ev[0], W.ev[1]));
             stage_ms[5] += a;
             ++fs->iterations;
+            if (wf_log()) {
+                WF_CHECK(hipMemcpy(W.h_counts, W.counts, kWfCountWords * sizeof(uint32_t), hipMemcpyDeviceToHost));
+                fprintf(stderr, "[wf] it %d finish paths %u  %.3f ms; longest path %u segments, slowest wave %u "
+                        "iterations in %.3f ms\n", it, n, a, W.h_counts[cslot(kCntDiagSegs)],
+                        W.h_counts[cslot(kCntDiagIters)], W.h_counts[cslot(kCntDiagTime)] * 1e-5);
+            }
             return true;
         }
         int next = 1 - cur;
@@ -838,8 +1270,20 @@ static bool iterate(const DevScene& S, const FrameParams& P, WfParams& Q, int& c
         if (count) hipLaunchKernelGGL((wf_trace<false, true>), dim3(gt), dim3(kBlock), 0, stream, S, P, Q, cur, n);
         else hipLaunchKernelGGL((wf_trace<false, false>), dim3(gt), dim3(kBlock), 0, stream, S, P, Q, cur, n);
         WF_CHECK(hipEventRecord(W.ev[1], stream));
-        if (full) hipLaunchKernelGGL(wf_shade<true>, dim3(g), dim3(kBlock), 0, stream, S, P, Q, cur, n);
-        else hipLaunchKernelGGL(wf_shade<false>, dim3(g), dim3(kBlock), 0, stream, S, P, Q, cur, n);
+        const bool sort = Q.sort_bins != 0;
+        if (sort) {
+            hipLaunchKernelGGL(wf_sort_hist, dim3(kSortBlocks), dim3(kSortThreads), 0, stream, S, Q, cur);
+            hipLaunchKernelGGL(wf_sort_rowscan, dim3(Q.sort_bins), dim3(kSortBlocks), 0, stream, Q);
+            hipLaunchKernelGGL(wf_sort_scatter, dim3(kSortBlocks), dim3(kSortThreads), 0, stream, S, Q, cur);
+        }
+        WF_CHECK(hipEventRecord(W.ev[4], stream));
+        if (full) {
+            if (sort) hipLaunchKernelGGL((wf_shade<true, true>), dim3(g), dim3(kBlock), 0, stream, S, P, Q, cur, n);
+            else hipLaunchKernelGGL((wf_shade<true, false>), dim3(g), dim3(kBlock), 0, stream, S, P, Q, cur, n);
+        } else {
+            if (sort) hipLaunchKernelGGL((wf_shade<false, true>), dim3(g), dim3(kBlock), 0, stream, S, P, Q, cur, n);
+            else hipLaunchKernelGGL((wf_shade<false, false>), dim3(g), dim3(kBlock), 0, stream, S, P, Q, cur, n);
+        }
         WF_CHECK(hipEventRecord(W.ev[2], stream));
         if (count) hipLaunchKernelGGL((wf_trace<true, true>), dim3(gt), dim3(kBlock), 0, stream, S, P, Q, cur, n);
         else hipLaunchKernelGGL((wf_trace<true, false>), dim3(gt), dim3(kBlock), 0, stream, S, P, Q, cur, n);
@@ -847,16 +1291,21 @@ static bool iterate(const DevScene& S, const FrameParams& P, WfParams& Q, int& c
         WF_CHECK(hipEventRecord(W.ev[3], stream));
         WF_CHECK(hipMemcpyAsync(W.h_counts, W.counts, kWfCountWords * sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
         WF_CHECK(hipStreamSynchronize(stream));
-        float a = 0, b = 0, c = 0;
+        float a = 0, b = 0, c = 0, srt = 0;
         WF_CHECK(hipEventElapsedTime(&a, W.ev[0], W.ev[1]));
-        WF_CHECK(hipEventElapsedTime(&b, W.ev[1], W.ev[2]));
+        WF_CHECK(hipEventElapsedTime(&srt, W.ev[1], W.ev[4]));
+        WF_CHECK(hipEventElapsedTime(&b, W.ev[4], W.ev[2]));
         WF_CHECK(hipEventElapsedTime(&c, W.ev[2], W.ev[3]));
         stage_ms[1] += a;
+        stage_ms[6] += srt;
         stage_ms[2] += b;
         stage_ms[3] += c;
         fs->trace_rays += (unsigned long long)n + queue_total(W.h_counts, 2);  // extend + connect rays
         fs->trace_launches += 2;
         fs->trace_ms += a + c;
+        if (wf_log())
+            fprintf(stderr, "[wf] it %d rays %u shadow %u  extend %.3f sort %.3f shade %.3f connect %.3f ms\n", it, n,
+                    queue_total(W.h_counts, 2), a, srt, b, c);
         n = queue_total(W.h_counts, next);
         cur = next;
         ++fs->iterations;
@@ -865,7 +1314,7 @@ static bool iterate(const DevScene& S, const FrameParams& P, WfParams& Q, int& c
 }
 
 bool run_wavefront(const DevScene& S, const FrameParams& P, WavefrontBuffers& W, int own_tiles, bool count,
-                   int tail_paths, hipStream_t stream, WfFrameStats* fs, const char** err) {
+                   int tail_paths, int sort_bins, hipStream_t stream, WfFrameStats* fs, const char** err) {
     WfParams Q;
     Q.W = W;
     Q.spp = max(P.U.samplesPerPixel, 1);
@@ -876,6 +1325,19 @@ bool run_wavefront(const DevScene& S, const FrameParams& P, WavefrontBuffers& W,
     Q.tri_vote = tri_vote();
     Q.chunk = chunk_size();
     Q.tail = tail_paths > 0 ? (uint32_t)tail_paths : tail_rays();
+    Q.sort_bins = (uint32_t)sort_bins;
+    static const int sort_xcd = env_int("RT_SORT_XCD", 1), steal = env_int("RT_STEAL", 0);
+    Q.sort_xcd = sort_xcd;
+    Q.steal = steal;
+    Q.diag = wf_log() ? 1 : 0;
+    static const int finish_step = env_int("RT_FINISH_STEP", 1), shade_min = env_int("RT_SHADE_MIN", 16);
+    Q.finish_step = finish_step;
+    Q.shade_min = shade_min;
+    if (sort_bins && (sort_bins < kSortMinBins || sort_bins > kSortMaxBins || (sort_bins & (sort_bins - 1)) ||
+                      !S.tri_bin || !W.sorted)) {
+        *err = "bad hit-sort configuration";
+        return false;
+    }
     *fs = WfFrameStats{};
     float* stage_ms = fs->stage_ms;
     const bool full = needs_full(P.U);

@@ -23,12 +23,14 @@ def parity_report(gpu, ref):
 # Pipeline variants of the GPU tests: the per-pixel megakernel, and the wavefront pipeline with
 # the default finish threshold (small frames run almost entirely in the persistent finish
 # kernel), with no finish kernel at all (every bounce through extend / shade / connect) and
-# with a small threshold (bulk rounds, then finish).
-PIPELINES = ["megakernel", "wavefront", "wavefront-bulk", "wavefront-mixed"]
-_VARIANTS = {"megakernel": ("megakernel", 0), "wavefront": ("wavefront", 0),
-             "wavefront-bulk": ("wavefront", 1), "wavefront-mixed": ("wavefront", 2048)}
+# with a small threshold (bulk rounds, then finish).  "wavefront-bulk-sort" and the mixed variant
+# also sort hits by BVH leaf bin between extend and shade (off by default).
+PIPELINES = ["megakernel", "wavefront", "wavefront-bulk", "wavefront-mixed", "wavefront-bulk-sort"]
+_VARIANTS = {"megakernel": ("megakernel", 0, 0), "wavefront": ("wavefront", 0, 0),
+             "wavefront-bulk": ("wavefront", 1, 0), "wavefront-mixed": ("wavefront", 2048, 4096),
+             "wavefront-bulk-sort": ("wavefront", 1, 2048)}
 
 
 def make_renderer(rt, scene, W, H, pipeline="wavefront", **kw):
-    pl, tail = _VARIANTS[pipeline]
-    return rt.Renderer(scene, W, H, pipeline=pl, tail_paths=tail, **kw)
+    pl, tail, sort_bins = _VARIANTS[pipeline]
+    return rt.Renderer(scene, W, H, pipeline=pl, tail_paths=tail, sort_bins=sort_bins, **kw)
