@@ -607,6 +607,7 @@ rt_status rt_render_frame(rt_ctx* c, const Uniforms* U, const rt_tile_set* tiles
     S.halton = (const HaltonDim*)c->d_halton.p;
     S.tri_bin = (const uint16_t*)c->d_tri_bin.p;
     S.max_submeshes = c->max_sub;
+    S.num_materials = (int)c->h_mat.size();
     S.num_tris = (int)c->num_tris;
     S.num_nodes8 = (int)c->bvh8.nodes.size();
     FrameParams P;

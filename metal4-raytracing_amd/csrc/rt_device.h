@@ -35,6 +35,7 @@ struct DevScene {
     const HaltonDim* halton;
     const uint16_t* tri_bin;   // per original triangle: its BVH leaf slot * kSortMaxBins / num_tris
     int max_submeshes;
+    int num_materials;         // instances * max_submeshes
     int num_tris;
     int num_nodes8;
 };

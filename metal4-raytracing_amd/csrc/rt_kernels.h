@@ -77,7 +77,9 @@ constexpr int kShards = 8;        // queue segments (one allocation counter each
 // [32..39] / [40..47] per-XCD chunk counters of the extend / connect launches; each slot on a
 // 128-B line of its own (cslot), so the per-XCD shards never contend for one line's atomics.
 constexpr int kCntStride = 32;
-constexpr int kWfCountWords = 48 * kCntStride;
+constexpr int kWfDiagHist = 48 * kCntStride;        // 64 words: wf_finish wave end-time histogram (50 us bins)
+constexpr int kWfDiagSteps = kWfDiagHist + 64;        // 66 words: wf_trace steps-per-ray histograms + max
+constexpr int kWfCountWords = 48 * kCntStride + 64 + 66;
 __host__ __device__ constexpr uint32_t cslot(int c) { return (uint32_t)c * kCntStride; }
 struct WavefrontBuffers {
     size_t queue_entries = 0;     // kShards segments of queue_entries / kShards

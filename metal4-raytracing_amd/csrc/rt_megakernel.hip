@@ -15,9 +15,8 @@ __global__ void __launch_bounds__(kBlock)
 megakernel(DevScene S, FrameParams P) {
     __shared__ int lds_stack[kStackSize * kBlock];
     __shared__ HaltonDim lds_halton[kHaltonLds];
-    for (int i = threadIdx.x; i < kHaltonLds; i += kBlock) lds_halton[i] = S.halton[i];
-    __syncthreads();
-    const HaltonTab halton{lds_halton, S.halton};
+    __shared__ MatRec lds_mat[kMatLds];
+    const ShadeTabs halton = load_tabs(S, lds_halton, lds_mat);
 
     const Uniforms& U = P.U;
     // block -> tile mapping (XCD-contiguous), 16x16 pixels per block

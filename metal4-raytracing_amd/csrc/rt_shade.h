@@ -11,13 +11,48 @@
 
 namespace rt {
 
-struct HaltonTab {
+// The fields of a Material the kernel reads (Raytracing.metal:399-453), packed for LDS:
+// base = (baseColor, opacity), emis = (emission, refractionIndex).
+struct MatRec {
+    float4 base;
+    float4 emis;
+};
+constexpr int kMatLds = 128;   // material records staged in LDS per block (4 KB)
+
+// Per-block lookup tables of the shading code: the first Halton dimensions and the scene's
+// material records in LDS (global memory beyond what was staged).
+struct ShadeTabs {
     const HaltonDim* lds;
     const HaltonDim* glob;
+    const MatRec* mat_lds;
+    const Material* mat_glob;
+    int n_mat_lds;             // = number of materials when they fit in LDS, else 0
     __device__ __forceinline__ float operator()(int i, int d) const {
         return halton_fast(i, d < kHaltonLds ? lds[d] : glob[d]);
     }
+    __device__ __forceinline__ MatRec material(int slot) const {
+        if (slot < n_mat_lds) return mat_lds[slot];
+        const Material& m = mat_glob[slot];
+        MatRec r;
+        r.base = make_float4(m.baseColor.x, m.baseColor.y, m.baseColor.z, m.opacity);
+        r.emis = make_float4(m.emission.x, m.emission.y, m.emission.z, m.refractionIndex);
+        return r;
+    }
 };
+
+// Stages the Halton dimensions and the material records of the scene in LDS; every thread of
+// the block calls it (ends with a barrier).
+__device__ __forceinline__ ShadeTabs load_tabs(const DevScene& S, HaltonDim* lds_halton, MatRec* lds_mat) {
+    for (int i = threadIdx.x; i < kHaltonLds; i += blockDim.x) lds_halton[i] = S.halton[i];
+    const int n_mat = (lds_mat && S.num_materials <= kMatLds) ? S.num_materials : 0;
+    for (int i = threadIdx.x; i < n_mat; i += blockDim.x) {
+        const Material& m = S.materials[i];
+        lds_mat[i].base = make_float4(m.baseColor.x, m.baseColor.y, m.baseColor.z, m.opacity);
+        lds_mat[i].emis = make_float4(m.emission.x, m.emission.y, m.emission.z, m.refractionIndex);
+    }
+    __syncthreads();
+    return ShadeTabs{lds_halton, S.halton, lds_mat, S.materials, n_mat};
+}
 
 struct PathRegs {
     f3 color;
@@ -47,7 +82,7 @@ __host__ __device__ __forceinline__ bool needs_full(const Uniforms& U) {
 // FULL = false compiles out the debug-visualisation and G-buffer branches (the caller selects
 // FULL = true whenever uniforms.debugTextureMode != 0 or enableDenoiseGBuffer != 0).
 template <bool FULL>
-__device__ __forceinline__ void shade_step(const DevScene& S, const Uniforms& U, const HaltonTab& halton, int hidx,
+__device__ __forceinline__ void shade_step(const DevScene& S, const Uniforms& U, const ShadeTabs& halton, int hidx,
                                            int sampleIndex, f3& rayO, f3& rayD, const Hit& h, PathRegs& p,
                                            bool gbuf_pending, f2 prevMotion, bool hadPrimaryHit, f2 motionVector,
                                            StepResult& r) {
@@ -60,7 +95,7 @@ __device__ __forceinline__ void shade_step(const DevScene& S, const Uniforms& U,
     int geometryIndex = (int)(ti.w & 0xffu);
     const float* M = S.inst + 12 * instanceIndex;                                       // :329-333
     f3 P_ = rayO + rayD * h.t;                                                          // :336
-    const Material& mat = S.materials[instanceIndex * S.max_submeshes + geometryIndex]; // :337-339
+    const MatRec mat = halton.material(instanceIndex * S.max_submeshes + geometryIndex); // :337-339 (LDS)
     float bu = h.u, bv = h.v, bw = (1.0f - bu) - bv;                                    // :63-65
     const Camera& cam = U.camera;
     f3 cright = ldf3(cam.right), cup = ldf3(cam.up), cfwd = ldf3(cam.forward);
@@ -97,11 +132,11 @@ __device__ __forceinline__ void shade_step(const DevScene& S, const Uniforms& U,
     f3 Ng = normalize(xform(M, objN, 0.0f));                                          // :392-393
     if (length(objN) < 1e-10f) Ng = -rayD;                                            // :395-397
 
-    f3 albedo = ldf3(mat.baseColor);                                                  // :399
+    f3 albedo = ld3(mat.base);                                                        // :399
     // textureFlags == 0 for every uploaded material (rt_scene_upload rejects others)
     const float roughness = 1.0f, metallic = 0.0f, ao = 1.0f;                         // :431-446
-    float opacity = clampf(mat.opacity, 0.0f, 1.0f);                                  // :448
-    f3 emission = ldf3(mat.emission);                                                 // :453
+    float opacity = clampf(mat.base.w, 0.0f, 1.0f);                                   // :448
+    f3 emission = ld3(mat.emis);                                                      // :453
 
     if (FULL && U.debugTextureMode != DebugTextureModeNone) {                         // :459-490
         f3 dc = mk3(0.0f, 0.0f, 0.0f);
@@ -137,7 +172,7 @@ __device__ __forceinline__ void shade_step(const DevScene& S, const Uniforms& U,
     }
 
     float clampedOpacity = clampf(opacity, 0.0f, 1.0f);                              // :517-576
-    float ior = fmaxf(mat.refractionIndex, 1.0f);
+    float ior = fmaxf(mat.emis.w, 1.0f);
     if (clampedOpacity < 0.999f || ior > 1.01f) {
         f3 N = shadingNormal, I = rayD;
         float cosi = clampf(dot(-I, N), -1.0f, 1.0f);
@@ -296,7 +331,7 @@ __device__ __forceinline__ void shade_step(const DevScene& S, const Uniforms& U,
 }
 
 // Primary ray for (pixel, sample) (Raytracing.metal:270-292).
-__device__ __forceinline__ void primary_ray(const Uniforms& U, const HaltonTab& halton, int px, int py, int hidx,
+__device__ __forceinline__ void primary_ray(const Uniforms& U, const ShadeTabs& halton, int px, int py, int hidx,
                                             f3& o, f3& d) {
     float rx = halton(hidx, 0), ry = halton(hidx, 1);
     float spx = (float)px + rx, spy = (float)py + ry;

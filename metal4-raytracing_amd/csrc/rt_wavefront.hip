@@ -57,6 +57,11 @@ static bool wf_log() {  // RT_WF_LOG=1: per-iteration queue sizes and stage time
     return v;
 }
 
+static uint32_t drain_paths() {  // RT_DRAIN_PATHS: finish rounds with fewer paths never drain
+    static const uint32_t v = (uint32_t)env_int("RT_DRAIN_PATHS", 65536);
+    return v;
+}
+
 static int tri_vote() {  // RT_TRI_VOTE overrides (tuning experiments)
     static int v = [] { const char* e = getenv("RT_TRI_VOTE"); return e ? atoi(e) : 0; }();
     return v;
@@ -167,15 +172,16 @@ struct WfParams {
     int diag;              // wf_finish: record the diagnostics slots (RT_WF_LOG)
     int finish_step;       // tail: wf_finish_step (1) or the per-segment wf_finish (0)
     int shade_min;         // wf_finish_step: shade once this many lanes wait (or none traverses)
+    int drain_min;         // wf_finish_step: hand paths back to the next round below this many busy lanes
 };
 
 // counter slots (cslot): [q*8 + shard] ray queues q = 0, 1; [16 + shard] shadow queue; [24] extra allocator
 constexpr int kCntShadowQ = 16;
 constexpr int kCntExtra = 24;
 constexpr int kCntChunkFinish = 25;
-constexpr int kCntSorted = 26;
-constexpr uint32_t kNoKey = 0xffffffffu;
-constexpr int kCntDiagSegs = 27, kCntDiagIters = 28, kCntDiagTime = 29;   // wf_finish diagnostics   // sort key of a miss (dropped by the sort)         // hits the sort kept (misses dropped) = shade's input size
+constexpr int kCntSorted = 26;                 // hits the sort kept (misses dropped) = shade's input size
+constexpr uint32_t kNoKey = 0xffffffffu;       // sort key of a miss (dropped by the sort)
+constexpr int kCntDiagSegs = 27, kCntDiagIters = 28, kCntDiagTime = 29;   // wf_finish diagnostics
 constexpr int kCntChunkExtend = 32;   // 8 per-XCD chunk counters each
 constexpr int kCntChunkConnect = 40;
 
@@ -212,10 +218,6 @@ __device__ __forceinline__ void init_path(const WfParams& Q, uint32_t pid, uint3
     Q.W.p_meta[pid] = make_uint4(pix, (uint32_t)sample, 0u, hidx);
 }
 
-__device__ __forceinline__ void load_halton(const DevScene& S, HaltonDim* lds) {
-    for (int i = threadIdx.x; i < kHaltonLds; i += kBlock) lds[i] = S.halton[i];
-    __syncthreads();
-}
 
 __device__ __forceinline__ void flush_counters(const FrameParams& P, uint32_t closest, uint32_t shadow, uint32_t paths,
                                                const TraceCounters& tc, bool count, bool overflow,
@@ -245,8 +247,7 @@ __device__ __forceinline__ void write_pixel_outputs(const FrameParams& P, uint32
 __global__ void __launch_bounds__(kBlock) wf_generate(DevScene S, FrameParams P, WfParams Q) {
     __shared__ HaltonDim lds_halton[kHaltonLds];
     __shared__ BlockAlloc ba;
-    load_halton(S, lds_halton);
-    const HaltonTab halton{lds_halton, S.halton};
+    const ShadeTabs halton = load_tabs(S, lds_halton, nullptr);   // no shading: Halton only
     const Uniforms& U = P.U;
     const int spp = Q.spp;
     const int maxExtra = (U.enableMotionAdaptiveSampling != 0) ? max(U.motionSamplingMaxExtraSamples, 0) : 0;
@@ -306,9 +307,9 @@ __global__ void __launch_bounds__(kBlock) wf_generate(DevScene S, FrameParams P,
 template <bool FULL, bool SORTED>
 __global__ void __launch_bounds__(kBlock) wf_shade(DevScene S, FrameParams P, WfParams Q, int cur, uint32_t n) {
     __shared__ HaltonDim lds_halton[kHaltonLds];
+    __shared__ MatRec lds_mat[kMatLds];
     __shared__ BlockAlloc ba_ray, ba_sh;
-    load_halton(S, lds_halton);
-    const HaltonTab halton{lds_halton, S.halton};
+    const ShadeTabs halton = load_tabs(S, lds_halton, lds_mat);
     const Uniforms& U = P.U;
     const int next = 1 - cur;
     const int shard = blockIdx.x & (kShards - 1);
@@ -549,6 +550,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 
     float best = 0.0f, bu = 0.0f, bv = 0.0f;
     uint32_t best_id = 0xffffffffu, g_base = 0, g_hits = 0, t_base = 0, t_mask = 0;
     int sp = 0;
+    uint32_t steps = 0;   // COUNT: iterations the current ray has taken
 
     while (true) {
         // refill idle lanes from the wave's range
@@ -584,12 +586,14 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 
                     hit_any = false;
                     active = true;
                     rays++;
+                    if (COUNT) steps = 0;
                 }
             }
             wnext += (uint32_t)__popcll(idle);
         }
         if (__ballot(active) == 0ull) break;
         if (!active) continue;
+        if (COUNT) ++steps;
 
         bool done = false;
         // Phase vote: a wave runs EITHER a triangle step OR a node step per iteration, so the
@@ -677,6 +681,10 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 
         if (!done && !t_mask && !g_hits && sp == 0) done = true;
         if (done) {
             active = false;
+            if (COUNT && Q.diag) {   // steps-per-ray histogram (log2 bins) of the counting frame
+                atomicAdd(&Q.W.counts[kWfDiagSteps + (ANY ? 32 : 0) + (31 - __builtin_clz(steps))], 1u);
+                atomicMax(&Q.W.counts[kWfDiagSteps + 64 + (ANY ? 1 : 0)], steps);
+            }
             if (ANY) {
                 if (!hit_any) {
                     float4 o4 = qin[(size_t)qstride * e];
@@ -701,8 +709,8 @@ __global__ void __launch_bounds__(kBlock) wf_finish(DevScene S, FrameParams P, W
     // slowest segment, not for its slowest path.  Paths come in chunks of 64 from one counter.
     __shared__ int lds_stack[kStackSize * kBlock];
     __shared__ HaltonDim lds_halton[kHaltonLds];
-    load_halton(S, lds_halton);
-    const HaltonTab halton{lds_halton, S.halton};
+    __shared__ MatRec lds_mat[kMatLds];
+    const ShadeTabs halton = load_tabs(S, lds_halton, lds_mat);
     const Uniforms& U = P.U;
     const ShardPrefix cnt = load_prefix(Q.W.counts + cslot(cur * kShards));
     const float4* qin = Q.W.q[cur];
@@ -797,6 +805,7 @@ __global__ void __launch_bounds__(kBlock) wf_finish(DevScene S, FrameParams P, W
             atomicMax(&Q.W.counts[cslot(kCntDiagSegs)], max_segs);
             atomicMax(&Q.W.counts[cslot(kCntDiagIters)], iters);
             atomicMax(&Q.W.counts[cslot(kCntDiagTime)], dt);
+            atomicAdd(&Q.W.counts[kWfDiagHist + min(dt / 5000u, 63u)], 1u);
         }
     }
     flush_counters(P, n_closest, n_shadow, 0, tc, COUNT, overflow);
@@ -816,11 +825,11 @@ wf_finish_step(DevScene S, FrameParams P, WfParams Q, int cur, uint32_t n) {
     __shared__ int lds_stack[kStackSize * kBlock];
     __shared__ uint4 lds_top[kTopNodes * 5];
     __shared__ HaltonDim lds_halton[kHaltonLds];
+    __shared__ MatRec lds_mat[kMatLds];
     int* stack = &lds_stack[threadIdx.x];
     const uint32_t n_top = (uint32_t)min(S.num_nodes8, kTopNodes);
     for (uint32_t i = threadIdx.x; i < n_top * 5; i += kBlock) lds_top[i] = reinterpret_cast<const uint4*>(S.nodes8)[i];
-    load_halton(S, lds_halton);   // ends with a block barrier
-    const HaltonTab halton{lds_halton, S.halton};
+    const ShadeTabs halton = load_tabs(S, lds_halton, lds_mat);   // ends with a block barrier
     const Uniforms& U = P.U;
     const ShardPrefix cnt = load_prefix(Q.W.counts + cslot(cur * kShards));
     const float4* qin = Q.W.q[cur];
@@ -843,7 +852,9 @@ wf_finish_step(DevScene S, FrameParams P, WfParams Q, int cur, uint32_t n) {
     p.color = p.accum = mk3(0, 0, 0);
     p.bounce = p.tpass = p.step = 0;
     f3 rayO = mk3(0, 0, 0), rayD = mk3(0, 0, 0), contrib = mk3(0, 0, 0);
-    bool next = false, hit_any = false;
+    bool next = false, hit_any = false, draining = false;
+    float4* qout = Q.W.q[1 - cur] + 2 * (size_t)(blockIdx.x & (kShards - 1)) * Q.seg_cap;
+    uint32_t* qout_cnt = Q.W.counts + cslot((1 - cur) * kShards + (int)(blockIdx.x & (kShards - 1)));
     // traversal
     RaySetup R = ray_setup(mk3(0, 0, 0), mk3(1, 0, 0));
     float best = 0.0f, bu = 0.0f, bv = 0.0f;
@@ -914,6 +925,35 @@ wf_finish_step(DevScene S, FrameParams P, WfParams Q, int cur, uint32_t n) {
         }
         if (__ballot(mode != kIdle) == 0ull) break;   // idle everywhere => refill found nothing
         ++iters;
+
+        // ---- drain (Q.drain_min > 0): once the queue is exhausted and fewer than drain_min lanes
+        // of this wave are busy, paths at a closest-hit query are handed back as rays of the next
+        // round (queue 1 - cur; the query restarts there, so the result is unchanged), lanes in a
+        // shadow query finish it first.  The next launch packs the survivors into dense waves
+        // instead of this wave running its few long paths alone.
+        if (!draining && Q.drain_min > 0 && exhausted && wnext >= wend &&
+            __popcll(__ballot(mode != kIdle)) < Q.drain_min)
+            draining = true;
+        if (draining) {
+            const bool spill = mode == kClosest || mode == kReady;
+            const unsigned long long sm = __ballot(spill);
+            if (sm != 0ull) {
+                uint32_t base = 0;
+                if (lane_id() == 0) base = atomicAdd(qout_cnt, (uint32_t)__popcll(sm));
+                base = __builtin_amdgcn_readfirstlane(base);
+                if (spill) {
+                    const uint32_t slot = base + mbcnt64(sm);
+                    qout[2 * (size_t)slot] = make_float4(rayO.x, rayO.y, rayO.z, __uint_as_float(pid));
+                    qout[2 * (size_t)slot + 1] = make_float4(rayD.x, rayD.y, rayD.z, 0.0f);
+                    Q.W.p_color[pid] = make_float4(p.color.x, p.color.y, p.color.z, 0.0f);
+                    Q.W.p_accum[pid] = make_float4(p.accum.x, p.accum.y, p.accum.z, 0.0f);
+                    Q.W.p_meta[pid] = make_uint4(meta.x, meta.y, pack_state(p.bounce, p.tpass, p.step), meta.w);
+                    n_closest--;   // traced again (and counted) by the next round
+                    mode = kIdle;
+                }
+            }
+            if (__ballot(mode != kIdle) == 0ull) break;
+        }
 
         // ---- one traversal step (closest hit or shadow any-hit)
         if (mode == kClosest || mode == kShadow) {
@@ -1048,6 +1088,7 @@ wf_finish_step(DevScene S, FrameParams P, WfParams Q, int cur, uint32_t n) {
             atomicMax(&Q.W.counts[cslot(kCntDiagSegs)], max_segs);
             atomicMax(&Q.W.counts[cslot(kCntDiagIters)], iters);
             atomicMax(&Q.W.counts[cslot(kCntDiagTime)], dt);
+            atomicAdd(&Q.W.counts[kWfDiagHist + min(dt / 5000u, 63u)], 1u);
         }
     }
     flush_counters(P, n_closest, n_shadow, 0, tc, COUNT, overflow);
@@ -1056,8 +1097,7 @@ wf_finish_step(DevScene S, FrameParams P, WfParams Q, int cur, uint32_t n) {
 // ---- motion-adaptive extra samples (:779-789) -----------------------------------------------------------
 __global__ void __launch_bounds__(kBlock) wf_extra(DevScene S, FrameParams P, WfParams Q, int qidx) {
     __shared__ HaltonDim lds_halton[kHaltonLds];
-    load_halton(S, lds_halton);
-    const HaltonTab halton{lds_halton, S.halton};
+    const ShadeTabs halton = load_tabs(S, lds_halton, nullptr);   // no shading: Halton only
     const Uniforms& U = P.U;
     const int maxExtra = (U.enableMotionAdaptiveSampling != 0) ? max(U.motionSamplingMaxExtraSamples, 0) : 0;
     const int stride = Q.spp + maxExtra;
@@ -1233,33 +1273,54 @@ static bool iterate(const DevScene& S, const FrameParams& P, WfParams& Q, int& c
     WavefrontBuffers& W = Q.W;
     for (int it = 0; it < max_it && n > 0; ++it) {
         if (n < Q.tail) {
-            // run the tail to completion in one launch
-            WF_CHECK(hipEventRecord(W.ev[0], stream));
-            WF_CHECK(hipMemsetAsync(W.counts + cslot(kCntChunkFinish), 0, sizeof(uint32_t), stream));
-            if (Q.finish_step) {
-                if (count) full ? launch_finish<true, true, true>(S, P, Q, cur, n, stream)
-                                : launch_finish<true, true, false>(S, P, Q, cur, n, stream);
-                else full ? launch_finish<true, false, true>(S, P, Q, cur, n, stream)
-                          : launch_finish<true, false, false>(S, P, Q, cur, n, stream);
-            } else {
-                if (count) full ? launch_finish<false, true, true>(S, P, Q, cur, n, stream)
-                                : launch_finish<false, true, false>(S, P, Q, cur, n, stream);
-                else full ? launch_finish<false, false, true>(S, P, Q, cur, n, stream)
-                          : launch_finish<false, false, false>(S, P, Q, cur, n, stream);
+            // run the tail in persistent finish launches; with draining (wf_finish_step), each
+            // round hands the paths still alive at its end to the next round in queue 1 - cur
+            // Small rounds run to completion (no drain): a few paths in one wave would otherwise be
+            // handed on round after round; the round count is capped as well.
+            const int drain_min = Q.drain_min;
+            for (int round = 0; n > 0; ++round) {
+                Q.drain_min = (n >= drain_paths() && round < 32) ? drain_min : 0;
+                WF_CHECK(hipEventRecord(W.ev[0], stream));
+                WF_CHECK(hipMemsetAsync(W.counts + cslot(kCntChunkFinish), 0, sizeof(uint32_t), stream));
+                for (int k = 0; k < kShards; ++k)
+                    WF_CHECK(hipMemsetAsync(W.counts + cslot((1 - cur) * kShards + k), 0, sizeof(uint32_t), stream));
+                if (wf_log()) WF_CHECK(hipMemsetAsync(W.counts + kWfDiagHist, 0, 64 * sizeof(uint32_t), stream));
+                if (Q.finish_step) {
+                    if (count) full ? launch_finish<true, true, true>(S, P, Q, cur, n, stream)
+                                    : launch_finish<true, true, false>(S, P, Q, cur, n, stream);
+                    else full ? launch_finish<true, false, true>(S, P, Q, cur, n, stream)
+                              : launch_finish<true, false, false>(S, P, Q, cur, n, stream);
+                } else {
+                    if (count) full ? launch_finish<false, true, true>(S, P, Q, cur, n, stream)
+                                    : launch_finish<false, true, false>(S, P, Q, cur, n, stream);
+                    else full ? launch_finish<false, false, true>(S, P, Q, cur, n, stream)
+                              : launch_finish<false, false, false>(S, P, Q, cur, n, stream);
+                }
+                WF_CHECK(hipGetLastError());
+                WF_CHECK(hipEventRecord(W.ev[1], stream));
+                WF_CHECK(hipMemcpyAsync(W.h_counts, W.counts, kWfCountWords * sizeof(uint32_t), hipMemcpyDeviceToHost,
+                                        stream));
+                WF_CHECK(hipStreamSynchronize(stream));
+                float a = 0;
+                WF_CHECK(hipEventElapsedTime(&a, W.ev[0], W.ev[1]));
+                stage_ms[5] += a;
+                ++fs->iterations;
+                const uint32_t n_next = Q.drain_min > 0 ? queue_total(W.h_counts, 1 - cur) : 0u;
+                if (wf_log()) {
+                    fprintf(stderr, "[wf] it %d finish paths %u -> %u handed on  %.3f ms; longest path %u segments, "
+                            "slowest wave %u iterations in %.3f ms\n", it, n, n_next, a,
+                            W.h_counts[cslot(kCntDiagSegs)], W.h_counts[cslot(kCntDiagIters)],
+                            W.h_counts[cslot(kCntDiagTime)] * 1e-5);
+                    fprintf(stderr, "[wf] finish wave end times (50 us bins):");
+                    for (int b = 0; b < 64; ++b)
+                        if (W.h_counts[kWfDiagHist + b]) fprintf(stderr, " %d:%u", b, W.h_counts[kWfDiagHist + b]);
+                    fprintf(stderr, "\n");
+                }
+                n = n_next;
+                cur = 1 - cur;
+                ++it;
             }
-            WF_CHECK(hipGetLastError());
-            WF_CHECK(hipEventRecord(W.ev[1], stream));
-            WF_CHECK(hipStreamSynchronize(stream));
-            float a = 0;
-            WF_CHECK(hipEventElapsedTime(&a, W.ev[0], W.ev[1]));
-            stage_ms[5] += a;
-            ++fs->iterations;
-            if (wf_log()) {
-                WF_CHECK(hipMemcpy(W.h_counts, W.counts, kWfCountWords * sizeof(uint32_t), hipMemcpyDeviceToHost));
-                fprintf(stderr, "[wf] it %d finish paths %u  %.3f ms; longest path %u segments, slowest wave %u "
-                        "iterations in %.3f ms\n", it, n, a, W.h_counts[cslot(kCntDiagSegs)],
-                        W.h_counts[cslot(kCntDiagIters)], W.h_counts[cslot(kCntDiagTime)] * 1e-5);
-            }
+            Q.drain_min = drain_min;
             return true;
         }
         int next = 1 - cur;
@@ -1303,9 +1364,21 @@ static bool iterate(const DevScene& S, const FrameParams& P, WfParams& Q, int& c
         fs->trace_rays += (unsigned long long)n + queue_total(W.h_counts, 2);  // extend + connect rays
         fs->trace_launches += 2;
         fs->trace_ms += a + c;
-        if (wf_log())
+        if (wf_log()) {
             fprintf(stderr, "[wf] it %d rays %u shadow %u  extend %.3f sort %.3f shade %.3f connect %.3f ms\n", it, n,
                     queue_total(W.h_counts, 2), a, srt, b, c);
+            if (count) {
+                for (int any = 0; any < 2; ++any) {
+                    fprintf(stderr, "[wf]   %s steps/ray log2 bins (max %u):", any ? "connect" : "extend",
+                            W.h_counts[kWfDiagSteps + 64 + any]);
+                    for (int b2 = 0; b2 < 32; ++b2)
+                        if (W.h_counts[kWfDiagSteps + 32 * any + b2])
+                            fprintf(stderr, " %d:%u", b2, W.h_counts[kWfDiagSteps + 32 * any + b2]);
+                    fprintf(stderr, "\n");
+                }
+                WF_CHECK(hipMemsetAsync(W.counts + kWfDiagSteps, 0, 66 * sizeof(uint32_t), stream));
+            }
+        }
         n = queue_total(W.h_counts, next);
         cur = next;
         ++fs->iterations;
@@ -1333,6 +1406,8 @@ bool run_wavefront(const DevScene& S, const FrameParams& P, WavefrontBuffers& W,
     static const int finish_step = env_int("RT_FINISH_STEP", 1), shade_min = env_int("RT_SHADE_MIN", 16);
     Q.finish_step = finish_step;
     Q.shade_min = shade_min;
+    static const int drain_min = env_int("RT_DRAIN", 0);   // measured slower on C3g: off
+    Q.drain_min = Q.finish_step ? drain_min : 0;
     if (sort_bins && (sort_bins < kSortMinBins || sort_bins > kSortMaxBins || (sort_bins & (sort_bins - 1)) ||
                       !S.tri_bin || !W.sorted)) {
         *err = "bad hit-sort configuration";
