@@ -76,7 +76,12 @@ struct rt_ctx {
     DevBuf d_wf_color, d_wf_accum, d_wf_meta, d_wf_q0, d_wf_q1, d_wf_hits, d_wf_sq, d_wf_counts, d_wf_mprev, d_wf_extra;
     DevBuf d_wf_sorted, d_wf_sort_table, d_wf_sort_total;
     WfFrameStats wfs{};
+    WfTimeline wft;
     bool last_wavefront = false;
+
+    // motion bookkeeping for the extra-sample pass: motion vectors are exactly zero unless the
+    // camera, an instance transform or skinned positions differ from their previous copies
+    bool inst_moved = false, skin_moved = false, last_moving = false;
 };
 
 #define FAIL(ctx, code, msg)                 \
@@ -205,6 +210,7 @@ static rt_status ensure_wavefront(rt_ctx* c, size_t own_px, int spp, int max_ext
         if ((st = dev_alloc(c, c->d_wf_counts, kWfCountWords * 4))) return st;
         HIPC(c, hipHostMalloc((void**)&W.h_counts, kWfCountWords * 4, 0));
         for (auto& e : W.ev) HIPC(c, hipEventCreate(&e));
+        for (auto& e : c->wft.ev) HIPC(c, hipEventCreate(&e));
     }
     W.p_color = (float4*)c->d_wf_color.p;
     W.p_accum = (float4*)c->d_wf_accum.p;
@@ -293,6 +299,8 @@ rt_status rt_destroy(rt_ctx* c) {
     if (c->h_counters) hipHostFree(c->h_counters);
     if (c->wf.h_counts) hipHostFree(c->wf.h_counts);
     for (auto& e : c->wf.ev)
+        if (e) hipEventDestroy(e);
+    for (auto& e : c->wft.ev)
         if (e) hipEventDestroy(e);
     if (c->ev0) hipEventDestroy(c->ev0);
     if (c->ev1) hipEventDestroy(c->ev1);
@@ -417,6 +425,7 @@ rt_status rt_scene_upload(rt_ctx* c, const rt_scene_desc* sd) {
     HIPC(c, hipStreamSynchronize(c->stream));
     c->scene_ready = true;
     c->bvh_ready = false;
+    c->inst_moved = c->skin_moved = c->last_moving = false;
     return RT_OK;
 }
 
@@ -505,6 +514,7 @@ rt_status rt_set_instance_transforms(rt_ctx* c, const rt_packed_float4x3* t, uin
     HIPC(c, hipSetDevice(c->device));
     // prev <- cur (Renderer.swift:939-944), then the new transforms
     HIPC(c, hipMemcpyAsync(c->d_prev_inst.p, c->d_inst.p, c->h_inst.size() * 4, hipMemcpyDeviceToDevice, c->stream));
+    c->inst_moved = std::memcmp(c->h_inst.data(), t, (size_t)count * 48) != 0;
     std::memcpy(c->h_inst.data(), t, (size_t)count * 48);
     HIPC(c, hipMemcpyAsync(c->d_inst.p, c->h_inst.data(), c->h_inst.size() * 4, hipMemcpyHostToDevice, c->stream));
     HIPC(c, hipStreamSynchronize(c->stream));
@@ -529,6 +539,7 @@ rt_status rt_skin(rt_ctx* c, uint32_t mesh_index, const float* joints, uint32_t 
     HIPC(c, hipGetLastError());
     HIPC(c, hipStreamSynchronize(c->stream));  // joint upload buffer is reused next call
     c->world_dirty = true;
+    c->skin_moved = true;   // conservative: positions may now differ from previousPositions
     return RT_OK;
 }
 
@@ -552,6 +563,7 @@ rt_status rt_resize(rt_ctx* c, int32_t w, int32_t h, const uint32_t* offsets) {
     c->width = w;
     c->height = h;
     c->read_idx = 0;
+    c->last_moving = false;   // motion target cleared
     return RT_OK;
 }
 
@@ -632,14 +644,20 @@ rt_status rt_render_frame(rt_ctx* c, const Uniforms* U, const rt_tile_set* tiles
         int max_extra = U->enableMotionAdaptiveSampling ? std::max(U->motionSamplingMaxExtraSamples, 0) : 0;
         if ((st = ensure_wavefront(c, (size_t)own * ts * ts, spp, max_extra))) return st;
     }
+    // extra samples can only be non-zero when something moved in this frame or the previous one
+    const bool moving = c->inst_moved || c->skin_moved ||
+                        std::memcmp(&U->camera, &U->previousCamera, sizeof(Camera)) != 0;
+    const bool extra_pass = moving || c->last_moving;
+    c->last_moving = moving;
     HIPC(c, hipEventRecord(c->ev0, c->stream));
     for (float& k : c->stats.kernel_ms) k = 0.0f;
+    c->wft.pending = false;
     if (wavefront) {
         const char* err = nullptr;
         c->wfs = WfFrameStats{};
-        if (own > 0 && !run_wavefront(S, P, c->wf, own, c->counting, c->tail_paths, c->sort_bins, c->stream, &c->wfs, &err))
+        if (own > 0 && !run_wavefront(S, P, c->wf, own, c->counting, c->tail_paths, c->sort_bins, extra_pass, c->stream,
+                                      &c->wft, &c->wfs, &err))
             FAIL(c, RT_ERR_HIP, std::string("wavefront: ") + (err ? err : "?"));
-        std::memcpy(c->stats.kernel_ms, c->wfs.stage_ms, sizeof c->stats.kernel_ms);
     } else {
         int nblocks = own * (ts / 16) * (ts / 16);
         if (nblocks > 0) launch_megakernel(S, P, nblocks, c->counting, c->stream);
@@ -662,7 +680,14 @@ rt_status rt_wait(rt_ctx* c) {
         float ms = 0.0f;
         HIPC(c, hipEventElapsedTime(&ms, c->ev0, c->ev1));
         c->stats.last_frame_ms = ms;
-        if (!c->last_wavefront) c->stats.kernel_ms[0] = ms;
+        if (c->last_wavefront) {
+            const char* err = nullptr;
+            if (!wavefront_collect(c->wf, c->wft, &c->wfs, &err))
+                FAIL(c, RT_ERR_HIP, std::string("wavefront stats: ") + (err ? err : "?"));
+            std::memcpy(c->stats.kernel_ms, c->wfs.stage_ms, sizeof c->stats.kernel_ms);
+        } else {
+            c->stats.kernel_ms[0] = ms;
+        }
         c->stats.pipeline = c->last_wavefront ? RT_PIPELINE_WAVEFRONT : RT_PIPELINE_MEGAKERNEL;
         c->stats.iterations = c->last_wavefront ? c->wfs.iterations : 0;
         c->stats.trace_rays = c->last_wavefront ? c->wfs.trace_rays : 0;

@@ -79,7 +79,9 @@ constexpr int kShards = 8;        // queue segments (one allocation counter each
 constexpr int kCntStride = 32;
 constexpr int kWfDiagHist = 48 * kCntStride;        // 64 words: wf_finish wave end-time histogram (50 us bins)
 constexpr int kWfDiagSteps = kWfDiagHist + 64;        // 66 words: wf_trace steps-per-ray histograms + max
-constexpr int kWfCountWords = 48 * kCntStride + 64 + 66;
+constexpr int kWfStat = kWfDiagSteps + 66;              // 3 words: rounds, wf_trace launches, their rays
+constexpr int kStatRounds = 0, kStatTraceLaunches = 1, kStatTraceRays = 2;
+constexpr int kWfCountWords = 48 * kCntStride + 64 + 66 + 3;
 __host__ __device__ constexpr uint32_t cslot(int c) { return (uint32_t)c * kCntStride; }
 struct WavefrontBuffers {
     size_t queue_entries = 0;     // kShards segments of queue_entries / kShards
@@ -120,9 +122,28 @@ struct WfFrameStats {
 };
 // Runs one frame; returns false on a HIP error (message in *err).
 // tail_paths: finish-kernel threshold (0 = default / RT_TAIL_RAYS).
-// sort_bins: hit-sort bins (0 = no sort).
+// Host-side record of a frame enqueued with device-side control: events between the launches and
+// which stage each interval belongs to; collected once the frame is done (wavefront_collect).
+struct WfTimeline {
+    static constexpr int kMaxEv = 160;
+    struct Span {
+        int stage, a, b;
+    };
+    hipEvent_t ev[kMaxEv] = {};
+    Span spans[kMaxEv];
+    int n_ev = 0, n_spans = 0;
+    bool pending = false;
+};
+// Runs (host-driven: queue sizes read back every round; with RT_WF_LOG / RT_WF_DUMP /
+// RT_WF_HOST=1) or enqueues (device-driven, the default: `tl` receives the timeline, stats come
+// from wavefront_collect after the stream finished) one frame; false on a HIP error (*err).
+// sort_bins: hit-sort bins (0 = no sort).  extra_pass: the motion-adaptive extra samples can be
+// non-zero this frame (something moved in this or the previous frame); the device-driven mode
+// skips their pass otherwise.
 bool run_wavefront(const DevScene& S, const FrameParams& P, WavefrontBuffers& W, int own_tiles, bool count,
-                   int tail_paths, int sort_bins, hipStream_t stream, WfFrameStats* fs, const char** err);
+                   int tail_paths, int sort_bins, bool extra_pass, hipStream_t stream, WfTimeline* tl,
+                   WfFrameStats* fs, const char** err);
+bool wavefront_collect(const WavefrontBuffers& W, WfTimeline& T, WfFrameStats* fs, const char** err);
 size_t wavefront_queue_entries(size_t paths, int max_extra);
 
 // Packed-tile layout of the multi-GPU gather: element i of a rank's packed buffer is pixel

@@ -173,6 +173,9 @@ struct WfParams {
     int finish_step;       // tail: wf_finish_step (1) or the per-segment wf_finish (0)
     int shade_min;         // wf_finish_step: shade once this many lanes wait (or none traverses)
     int drain_min;         // wf_finish_step: hand paths back to the next round below this many busy lanes
+    int dev_ctl;           // device-side control (enqueue_wavefront): kernels read their queue sizes from
+                           // the counters and skip once the live count fell below `tail`
+    int finish_q;          // dev_ctl: the finish queue when every enqueued bulk round ran (written by generate)
 };
 
 // counter slots (cslot): [q*8 + shard] ray queues q = 0, 1; [16 + shard] shadow queue; [24] extra allocator
@@ -182,6 +185,17 @@ constexpr int kCntChunkFinish = 25;
 constexpr int kCntSorted = 26;                 // hits the sort kept (misses dropped) = shade's input size
 constexpr uint32_t kNoKey = 0xffffffffu;       // sort key of a miss (dropped by the sort)
 constexpr int kCntDiagSegs = 27, kCntDiagIters = 28, kCntDiagTime = 29;   // wf_finish diagnostics
+// dev_ctl: [30] tail mode (set by the first extend launch that found fewer than `tail` live
+// paths; later bulk launches of the pass return at once), [31] the queue the finish launch reads
+constexpr int kCntTailMode = 30, kCntFinishQ = 31;
+
+// dev_ctl statistics: rounds run, wf_trace launches run, rays they traced
+__device__ __forceinline__ void stat_add(const WfParams& Q, int word, uint32_t v) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&Q.W.counts[kWfStat + word], v);
+}
+__device__ __forceinline__ bool tail_mode(const WfParams& Q) {
+    return Q.dev_ctl && __builtin_amdgcn_readfirstlane(Q.W.counts[cslot(kCntTailMode)]) != 0u;
+}
 constexpr int kCntChunkExtend = 32;   // 8 per-XCD chunk counters each
 constexpr int kCntChunkConnect = 40;
 
@@ -256,6 +270,7 @@ __global__ void __launch_bounds__(kBlock) wf_generate(DevScene S, FrameParams P,
     float4* qout = Q.W.q[0] + 2 * (size_t)shard * Q.seg_cap;
     uint32_t n_paths = 0;
     const uint32_t total = Q.base_paths;
+    if (Q.dev_ctl && blockIdx.x == 0 && threadIdx.x == 0) Q.W.counts[cslot(kCntFinishQ)] = (uint32_t)Q.finish_q;
     for (uint32_t base = blockIdx.x * kBlock; base < total; base += gridDim.x * kBlock) {
         uint32_t pid = base + threadIdx.x;
         bool valid = pid < total;
@@ -305,15 +320,17 @@ __global__ void __launch_bounds__(kBlock) wf_generate(DevScene S, FrameParams P,
 // region and the rays / shadow rays it appends to its queue shard stay grouped by region for
 // the next extend / connect launches (which hand shard k's range to XCD k).
 template <bool FULL, bool SORTED>
-__global__ void __launch_bounds__(kBlock) wf_shade(DevScene S, FrameParams P, WfParams Q, int cur, uint32_t n) {
+__global__ void __launch_bounds__(kBlock) wf_shade(DevScene S, FrameParams P, WfParams Q, int cur) {
     __shared__ HaltonDim lds_halton[kHaltonLds];
     __shared__ MatRec lds_mat[kMatLds];
     __shared__ BlockAlloc ba_ray, ba_sh;
+    if (tail_mode(Q)) return;
     const ShadeTabs halton = load_tabs(S, lds_halton, lds_mat);
     const Uniforms& U = P.U;
     const int next = 1 - cur;
     const int shard = blockIdx.x & (kShards - 1);
     const ShardPrefix cnt = load_prefix(Q.W.counts + cslot(cur * kShards));
+    uint32_t n = cnt.end[kShards - 1];
     const float4* qin = Q.W.q[cur];
     float4* qout = Q.W.q[next] + 2 * (size_t)shard * Q.seg_cap;
     float4* sqout = Q.W.sq + 3 * (size_t)shard * Q.seg_cap;
@@ -418,6 +435,7 @@ __device__ __forceinline__ uint32_t sort_key(const DevScene& S, const WfParams& 
 
 __global__ void __launch_bounds__(kSortThreads) wf_sort_hist(DevScene S, WfParams Q, int cur) {
     __shared__ uint32_t h[kSortMaxBins];
+    if (tail_mode(Q)) return;
     const uint32_t shift = __builtin_ctz(kSortMaxBins) - __builtin_ctz(Q.sort_bins);
     const uint32_t K = Q.sort_bins;
     const ShardPrefix cnt = load_prefix(Q.W.counts + cslot(cur * kShards));
@@ -436,6 +454,7 @@ __global__ void __launch_bounds__(kSortThreads) wf_sort_hist(DevScene S, WfParam
 // one block per bin: exclusive scan of the bin's kSortBlocks block counts (in place) + bin total
 __global__ void __launch_bounds__(kSortBlocks) wf_sort_rowscan(WfParams Q) {
     __shared__ uint32_t w[kSortBlocks / 64];
+    if (tail_mode(Q)) return;
     uint32_t* row = Q.W.sort_table + (size_t)blockIdx.x * kSortBlocks;
     const uint32_t v = row[threadIdx.x];
     const uint32_t incl = wave_incl_scan(v);
@@ -450,6 +469,7 @@ __global__ void __launch_bounds__(kSortBlocks) wf_sort_rowscan(WfParams Q) {
 
 __global__ void __launch_bounds__(kSortThreads) wf_sort_scatter(DevScene S, WfParams Q, int cur) {
     __shared__ uint32_t off[kSortMaxBins];
+    if (tail_mode(Q)) return;
     const uint32_t shift = __builtin_ctz(kSortMaxBins) - __builtin_ctz(Q.sort_bins);
     __shared__ uint32_t w[kSortThreads / 64];
     const uint32_t K = Q.sort_bins, per = K / kSortThreads;   // 1, 2 or 4 bins per thread
@@ -497,19 +517,39 @@ __global__ void __launch_bounds__(kSortThreads) wf_sort_scatter(DevScene S, WfPa
 // triangle.  The wave therefore runs ~(total units of its rays)/64 iterations instead of
 // (slowest ray) x (rays per lane).
 template <bool ANY, bool COUNT>
-__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) wf_trace(DevScene S, FrameParams P, WfParams Q, int cur, uint32_t n_host) {
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) wf_trace(DevScene S, FrameParams P, WfParams Q, int cur) {
     __shared__ int lds_stack[kStackSize * kBlock];
     __shared__ uint4 lds_top[kTopNodes * 5];   // BVH top levels (BFS order: root, its children, ...)
     int* stack = &lds_stack[threadIdx.x];
+    if (Q.dev_ctl) {
+        // device-side round control: extend decides (uniformly, from the counters) whether this
+        // round runs in bulk or the rest of the pass goes to the finish launch
+        const bool tm = tail_mode(Q);
+        if (ANY) {
+            if (tm) return;
+        } else {
+            const ShardPrefix c0 = load_prefix(Q.W.counts + cslot(cur * kShards));
+            if (tm || c0.end[kShards - 1] < Q.tail) {
+                if (!tm && blockIdx.x == 0 && threadIdx.x == 0) {
+                    Q.W.counts[cslot(kCntTailMode)] = 1u;
+                    Q.W.counts[cslot(kCntFinishQ)] = (uint32_t)cur;
+                }
+                return;
+            }
+        }
+    }
     const uint32_t n_top = (uint32_t)min(S.num_nodes8, kTopNodes);
     for (uint32_t i = threadIdx.x; i < n_top * 5; i += kBlock)
         lds_top[i] = reinterpret_cast<const uint4*>(S.nodes8)[i];
     __syncthreads();
     const ShardPrefix cnt = load_prefix(ANY ? Q.W.counts + cslot(kCntShadowQ) : Q.W.counts + cslot(cur * kShards));
-    uint32_t n = n_host;
-    if (ANY) {
-        n = cnt.end[kShards - 1];
-    } else if (blockIdx.x == 0 && threadIdx.x < 2 * kShards) {  // reset the queues shade / connect fill
+    const uint32_t n = cnt.end[kShards - 1];
+    if (Q.dev_ctl) {
+        stat_add(Q, kStatTraceRays, n);
+        stat_add(Q, kStatTraceLaunches, 1u);
+        if (!ANY) stat_add(Q, kStatRounds, 1u);
+    }
+    if (!ANY && blockIdx.x == 0 && threadIdx.x < 2 * kShards) {  // reset the queues shade / connect fill
         const int next = 1 - cur;
         uint32_t k = threadIdx.x & (kShards - 1);
         Q.W.counts[cslot(threadIdx.x < kShards ? next * kShards + k : kCntShadowQ + k)] = 0;
@@ -703,7 +743,8 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 
 
 // ---- finish: run the remaining paths to completion --------------------------------------------------
 template <bool COUNT, bool FULL>
-__global__ void __launch_bounds__(kBlock) wf_finish(DevScene S, FrameParams P, WfParams Q, int cur, uint32_t n) {
+__global__ void __launch_bounds__(kBlock) wf_finish(DevScene S, FrameParams P, WfParams Q, int cur) {
+    if (cur < 0) cur = (int)__builtin_amdgcn_readfirstlane(Q.W.counts[cslot(kCntFinishQ)]);   // dev_ctl
     // Persistent: every lane runs ONE path segment (closest hit, shade, shadow ray) per iteration
     // and picks up the next remaining path as soon as its own ends, so a wave waits for its
     // slowest segment, not for its slowest path.  Paths come in chunks of 64 from one counter.
@@ -713,6 +754,8 @@ __global__ void __launch_bounds__(kBlock) wf_finish(DevScene S, FrameParams P, W
     const ShadeTabs halton = load_tabs(S, lds_halton, lds_mat);
     const Uniforms& U = P.U;
     const ShardPrefix cnt = load_prefix(Q.W.counts + cslot(cur * kShards));
+    const uint32_t n = cnt.end[kShards - 1];
+    if (Q.dev_ctl && n > 0) stat_add(Q, kStatRounds, 1u);
     const float4* qin = Q.W.q[cur];
     int* stack = &lds_stack[threadIdx.x];
     uint32_t* chunk_ctr = Q.W.counts + cslot(kCntChunkFinish);
@@ -821,7 +864,8 @@ __global__ void __launch_bounds__(kBlock) wf_finish(DevScene S, FrameParams P, W
 // left at the tail (up to ~20 segments) no longer wait for their wave's worst ray every segment.
 template <bool COUNT, bool FULL, int WAVES>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES, WAVES)))
-wf_finish_step(DevScene S, FrameParams P, WfParams Q, int cur, uint32_t n) {
+wf_finish_step(DevScene S, FrameParams P, WfParams Q, int cur) {
+    if (cur < 0) cur = (int)__builtin_amdgcn_readfirstlane(Q.W.counts[cslot(kCntFinishQ)]);   // dev_ctl
     __shared__ int lds_stack[kStackSize * kBlock];
     __shared__ uint4 lds_top[kTopNodes * 5];
     __shared__ HaltonDim lds_halton[kHaltonLds];
@@ -832,6 +876,8 @@ wf_finish_step(DevScene S, FrameParams P, WfParams Q, int cur, uint32_t n) {
     const ShadeTabs halton = load_tabs(S, lds_halton, lds_mat);   // ends with a block barrier
     const Uniforms& U = P.U;
     const ShardPrefix cnt = load_prefix(Q.W.counts + cslot(cur * kShards));
+    const uint32_t n = cnt.end[kShards - 1];
+    if (Q.dev_ctl && n > 0) stat_add(Q, kStatRounds, 1u);
     const float4* qin = Q.W.q[cur];
     uint32_t* chunk_ctr = Q.W.counts + cslot(kCntChunkFinish);
     constexpr uint32_t kChunk = 64;
@@ -1184,7 +1230,7 @@ size_t wavefront_queue_entries(size_t paths, int max_extra) {
 }
 
 static unsigned grid_for(uint32_t n, unsigned cap) {
-    unsigned g = (unsigned)((n + kBlock - 1) / kBlock);
+    unsigned g = (unsigned)(((uint64_t)n + kBlock - 1) / kBlock);
     if (g > cap) g = cap;
     g = (g + kShards - 1) / kShards * kShards;  // multiple of 8: segment bound (see header)
     return g == 0 ? kShards : g;
@@ -1229,13 +1275,28 @@ static void launch_finish(const DevScene& S, const FrameParams& P, const WfParam
     static const int waves = env_int("RT_FINISH_WAVES", 4);
     if (STEP && waves == 3) {
         static const unsigned cap = resident_grid(wf_finish_step<COUNT, FULL, 3>, 2);
-        hipLaunchKernelGGL((wf_finish_step<COUNT, FULL, 3>), dim3(grid_for(n, cap)), dim3(kBlock), 0, stream, S, P, Q, cur, n);
+        hipLaunchKernelGGL((wf_finish_step<COUNT, FULL, 3>), dim3(grid_for(n, cap)), dim3(kBlock), 0, stream, S, P, Q, cur);
     } else if (STEP) {
         static const unsigned cap = resident_grid(wf_finish_step<COUNT, FULL, 4>, 2);
-        hipLaunchKernelGGL((wf_finish_step<COUNT, FULL, 4>), dim3(grid_for(n, cap)), dim3(kBlock), 0, stream, S, P, Q, cur, n);
+        hipLaunchKernelGGL((wf_finish_step<COUNT, FULL, 4>), dim3(grid_for(n, cap)), dim3(kBlock), 0, stream, S, P, Q, cur);
     } else {
         static const unsigned cap = resident_grid(wf_finish<COUNT, FULL>, 2);
-        hipLaunchKernelGGL((wf_finish<COUNT, FULL>), dim3(grid_for(n, cap)), dim3(kBlock), 0, stream, S, P, Q, cur, n);
+        hipLaunchKernelGGL((wf_finish<COUNT, FULL>), dim3(grid_for(n, cap)), dim3(kBlock), 0, stream, S, P, Q, cur);
+    }
+}
+
+static void launch_finish_any(const DevScene& S, const FrameParams& P, const WfParams& Q, bool count, bool full, int cur,
+                              uint32_t n, hipStream_t stream) {
+    if (Q.finish_step) {
+        if (count) full ? launch_finish<true, true, true>(S, P, Q, cur, n, stream)
+                        : launch_finish<true, true, false>(S, P, Q, cur, n, stream);
+        else full ? launch_finish<true, false, true>(S, P, Q, cur, n, stream)
+                  : launch_finish<true, false, false>(S, P, Q, cur, n, stream);
+    } else {
+        if (count) full ? launch_finish<false, true, true>(S, P, Q, cur, n, stream)
+                        : launch_finish<false, true, false>(S, P, Q, cur, n, stream);
+        else full ? launch_finish<false, false, true>(S, P, Q, cur, n, stream)
+                  : launch_finish<false, false, false>(S, P, Q, cur, n, stream);
     }
 }
 
@@ -1285,17 +1346,7 @@ static bool iterate(const DevScene& S, const FrameParams& P, WfParams& Q, int& c
                 for (int k = 0; k < kShards; ++k)
                     WF_CHECK(hipMemsetAsync(W.counts + cslot((1 - cur) * kShards + k), 0, sizeof(uint32_t), stream));
                 if (wf_log()) WF_CHECK(hipMemsetAsync(W.counts + kWfDiagHist, 0, 64 * sizeof(uint32_t), stream));
-                if (Q.finish_step) {
-                    if (count) full ? launch_finish<true, true, true>(S, P, Q, cur, n, stream)
-                                    : launch_finish<true, true, false>(S, P, Q, cur, n, stream);
-                    else full ? launch_finish<true, false, true>(S, P, Q, cur, n, stream)
-                              : launch_finish<true, false, false>(S, P, Q, cur, n, stream);
-                } else {
-                    if (count) full ? launch_finish<false, true, true>(S, P, Q, cur, n, stream)
-                                    : launch_finish<false, true, false>(S, P, Q, cur, n, stream);
-                    else full ? launch_finish<false, false, true>(S, P, Q, cur, n, stream)
-                              : launch_finish<false, false, false>(S, P, Q, cur, n, stream);
-                }
+                launch_finish_any(S, P, Q, count, full, cur, n, stream);
                 WF_CHECK(hipGetLastError());
                 WF_CHECK(hipEventRecord(W.ev[1], stream));
                 WF_CHECK(hipMemcpyAsync(W.h_counts, W.counts, kWfCountWords * sizeof(uint32_t), hipMemcpyDeviceToHost,
@@ -1328,8 +1379,8 @@ static bool iterate(const DevScene& S, const FrameParams& P, WfParams& Q, int& c
         WF_CHECK(hipEventRecord(W.ev[0], stream));
         unsigned g = grid_for(n, 8192);
         unsigned gt = grid_for(n, trace_grid_cap());
-        if (count) hipLaunchKernelGGL((wf_trace<false, true>), dim3(gt), dim3(kBlock), 0, stream, S, P, Q, cur, n);
-        else hipLaunchKernelGGL((wf_trace<false, false>), dim3(gt), dim3(kBlock), 0, stream, S, P, Q, cur, n);
+        if (count) hipLaunchKernelGGL((wf_trace<false, true>), dim3(gt), dim3(kBlock), 0, stream, S, P, Q, cur);
+        else hipLaunchKernelGGL((wf_trace<false, false>), dim3(gt), dim3(kBlock), 0, stream, S, P, Q, cur);
         WF_CHECK(hipEventRecord(W.ev[1], stream));
         const bool sort = Q.sort_bins != 0;
         if (sort) {
@@ -1339,15 +1390,15 @@ static bool iterate(const DevScene& S, const FrameParams& P, WfParams& Q, int& c
         }
         WF_CHECK(hipEventRecord(W.ev[4], stream));
         if (full) {
-            if (sort) hipLaunchKernelGGL((wf_shade<true, true>), dim3(g), dim3(kBlock), 0, stream, S, P, Q, cur, n);
-            else hipLaunchKernelGGL((wf_shade<true, false>), dim3(g), dim3(kBlock), 0, stream, S, P, Q, cur, n);
+            if (sort) hipLaunchKernelGGL((wf_shade<true, true>), dim3(g), dim3(kBlock), 0, stream, S, P, Q, cur);
+            else hipLaunchKernelGGL((wf_shade<true, false>), dim3(g), dim3(kBlock), 0, stream, S, P, Q, cur);
         } else {
-            if (sort) hipLaunchKernelGGL((wf_shade<false, true>), dim3(g), dim3(kBlock), 0, stream, S, P, Q, cur, n);
-            else hipLaunchKernelGGL((wf_shade<false, false>), dim3(g), dim3(kBlock), 0, stream, S, P, Q, cur, n);
+            if (sort) hipLaunchKernelGGL((wf_shade<false, true>), dim3(g), dim3(kBlock), 0, stream, S, P, Q, cur);
+            else hipLaunchKernelGGL((wf_shade<false, false>), dim3(g), dim3(kBlock), 0, stream, S, P, Q, cur);
         }
         WF_CHECK(hipEventRecord(W.ev[2], stream));
-        if (count) hipLaunchKernelGGL((wf_trace<true, true>), dim3(gt), dim3(kBlock), 0, stream, S, P, Q, cur, n);
-        else hipLaunchKernelGGL((wf_trace<true, false>), dim3(gt), dim3(kBlock), 0, stream, S, P, Q, cur, n);
+        if (count) hipLaunchKernelGGL((wf_trace<true, true>), dim3(gt), dim3(kBlock), 0, stream, S, P, Q, cur);
+        else hipLaunchKernelGGL((wf_trace<true, false>), dim3(gt), dim3(kBlock), 0, stream, S, P, Q, cur);
         WF_CHECK(hipGetLastError());
         WF_CHECK(hipEventRecord(W.ev[3], stream));
         WF_CHECK(hipMemcpyAsync(W.h_counts, W.counts, kWfCountWords * sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
@@ -1386,8 +1437,140 @@ static bool iterate(const DevScene& S, const FrameParams& P, WfParams& Q, int& c
     return true;
 }
 
+// ---- device-side control: the whole frame enqueued without host round trips ------------------------
+// The host enqueues `rounds_for(paths)` bulk rounds per pass (enough for the live paths to fall
+// below the finish threshold when about half of them end per round), then one finish launch;
+// the extend launch of a round that finds fewer than `tail` live paths flags tail mode and
+// names its queue as the finish input, and every later bulk launch of the pass returns at once.
+// Per-stage times come from events between the launches, ray counts and rounds from device
+// counters; both are collected by wavefront_collect once the frame has finished.
+namespace {
+struct Enqueue {
+    WfTimeline& T;
+    hipStream_t stream;
+    int last = -1;
+    bool mark(const char** err) {
+        if (T.n_ev >= WfTimeline::kMaxEv) {
+            *err = "wavefront timeline: too many events";
+            return false;
+        }
+        const hipError_t e = hipEventRecord(T.ev[T.n_ev], stream);
+        if (e != hipSuccess) {
+            *err = hipGetErrorString(e);
+            return false;
+        }
+        last = T.n_ev++;
+        return true;
+    }
+    // closes the span [previous mark, now) as `stage`
+    bool span(int stage, const char** err) {
+        const int a = last;
+        if (!mark(err)) return false;
+        T.spans[T.n_spans++] = WfTimeline::Span{stage, a, last};
+        return true;
+    }
+};
+}  // namespace
+
+static int rounds_for(uint64_t paths, uint32_t tail) {
+    if (paths < tail) return 0;
+    int k = 2;
+    while (k < 16 && (paths >> (k - 1)) >= tail) ++k;
+    return k;
+}
+
+static bool enqueue_pass(const DevScene& S, const FrameParams& P, const WfParams& Q, int rounds, bool count, bool full,
+                         Enqueue& E, const char** err) {
+    hipStream_t stream = E.stream;
+    const unsigned gt = trace_grid_cap(), g = 8192;
+    for (int k = 0; k < rounds; ++k) {
+        const int cur = k & 1;
+        if (count) hipLaunchKernelGGL((wf_trace<false, true>), dim3(gt), dim3(kBlock), 0, stream, S, P, Q, cur);
+        else hipLaunchKernelGGL((wf_trace<false, false>), dim3(gt), dim3(kBlock), 0, stream, S, P, Q, cur);
+        if (!E.span(1, err)) return false;
+        if (Q.sort_bins) {
+            hipLaunchKernelGGL(wf_sort_hist, dim3(kSortBlocks), dim3(kSortThreads), 0, stream, S, Q, cur);
+            hipLaunchKernelGGL(wf_sort_rowscan, dim3(Q.sort_bins), dim3(kSortBlocks), 0, stream, Q);
+            hipLaunchKernelGGL(wf_sort_scatter, dim3(kSortBlocks), dim3(kSortThreads), 0, stream, S, Q, cur);
+            if (!E.span(6, err)) return false;
+        }
+        if (full) {
+            if (Q.sort_bins) hipLaunchKernelGGL((wf_shade<true, true>), dim3(g), dim3(kBlock), 0, stream, S, P, Q, cur);
+            else hipLaunchKernelGGL((wf_shade<true, false>), dim3(g), dim3(kBlock), 0, stream, S, P, Q, cur);
+        } else {
+            if (Q.sort_bins) hipLaunchKernelGGL((wf_shade<false, true>), dim3(g), dim3(kBlock), 0, stream, S, P, Q, cur);
+            else hipLaunchKernelGGL((wf_shade<false, false>), dim3(g), dim3(kBlock), 0, stream, S, P, Q, cur);
+        }
+        if (!E.span(2, err)) return false;
+        if (count) hipLaunchKernelGGL((wf_trace<true, true>), dim3(gt), dim3(kBlock), 0, stream, S, P, Q, cur);
+        else hipLaunchKernelGGL((wf_trace<true, false>), dim3(gt), dim3(kBlock), 0, stream, S, P, Q, cur);
+        if (!E.span(3, err)) return false;
+    }
+    WF_CHECK(hipMemsetAsync(Q.W.counts + cslot(kCntChunkFinish), 0, sizeof(uint32_t), stream));
+    launch_finish_any(S, P, Q, count, full, -1, 1u << 30, stream);   // resident grid; input queue from the counters
+    WF_CHECK(hipGetLastError());
+    return E.span(5, err);
+}
+
+static bool enqueue_wavefront(const DevScene& S, const FrameParams& P, WfParams& Q, bool count, bool full,
+                              int maxExtra, bool extra_pass, hipStream_t stream, WfTimeline& T, const char** err) {
+    WavefrontBuffers& W = Q.W;
+    T.n_ev = T.n_spans = 0;
+    Enqueue E{T, stream};
+    Q.dev_ctl = 1;
+    Q.drain_min = 0;
+    const size_t npix = (size_t)P.U.width * P.U.height;
+    if (!E.mark(err)) return false;
+    WF_CHECK(hipMemsetAsync(W.counts, 0, kWfCountWords * sizeof(uint32_t), stream));
+    WF_CHECK(hipMemcpyAsync(W.motion_prev, P.motion, npix * sizeof(float2), hipMemcpyDeviceToDevice, stream));
+    const int rounds = rounds_for(Q.base_paths, Q.tail);
+    Q.finish_q = rounds & 1;
+    hipLaunchKernelGGL(wf_generate, dim3(grid_for(Q.base_paths, 16384)), dim3(kBlock), 0, stream, S, P, Q);
+    WF_CHECK(hipGetLastError());
+    if (!E.span(0, err)) return false;
+    if (!enqueue_pass(S, P, Q, rounds, count, full, E, err)) return false;
+    const bool with_extra = maxExtra > 0 && extra_pass;
+    if (with_extra) {
+        // second pass over the motion-adaptive extra samples (:779-789), appended to queue 0
+        const int rounds2 = rounds_for((uint64_t)Q.own_pixels * (uint64_t)maxExtra, Q.tail);
+        WF_CHECK(hipMemsetAsync(W.counts, 0, cslot(kShards) * sizeof(uint32_t), stream));
+        WF_CHECK(hipMemsetAsync(W.counts + cslot(kCntChunkExtend), 0, cslot(2 * kShards) * sizeof(uint32_t), stream));
+        WF_CHECK(hipMemsetD32Async(W.counts + cslot(kCntTailMode), 0u, 1, stream));
+        WF_CHECK(hipMemsetD32Async(W.counts + cslot(kCntFinishQ), (uint32_t)(rounds2 & 1), 1, stream));
+        hipLaunchKernelGGL(wf_extra, dim3(grid_for(Q.own_pixels, 1u << 30)), dim3(kBlock), 0, stream, S, P, Q, 0);
+        WF_CHECK(hipGetLastError());
+        if (!E.span(4, err)) return false;
+        if (!enqueue_pass(S, P, Q, rounds2, count, full, E, err)) return false;
+    }
+    hipLaunchKernelGGL(wf_resolve, dim3(grid_for(Q.own_pixels, 1u << 30)), dim3(kBlock), 0, stream, S, P, Q,
+                       with_extra ? 1 : 0);
+    WF_CHECK(hipGetLastError());
+    if (!E.span(4, err)) return false;
+    WF_CHECK(hipMemcpyAsync(W.h_counts, W.counts, kWfCountWords * sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
+    T.pending = true;
+    return true;
+}
+
+bool wavefront_collect(const WavefrontBuffers& W, WfTimeline& T, WfFrameStats* fs, const char** err) {
+    if (!T.pending) return true;
+    T.pending = false;
+    *fs = WfFrameStats{};
+    for (int i = 0; i < T.n_spans; ++i) {
+        const WfTimeline::Span& sp = T.spans[i];
+        float ms = 0.0f;
+        WF_CHECK(hipEventElapsedTime(&ms, T.ev[sp.a], T.ev[sp.b]));
+        fs->stage_ms[sp.stage] += ms;
+        if (sp.stage == 1 || sp.stage == 3) fs->trace_ms += ms;
+    }
+    fs->iterations = (int)W.h_counts[kWfStat + kStatRounds];
+    fs->trace_launches = (int)W.h_counts[kWfStat + kStatTraceLaunches];
+    fs->trace_rays = W.h_counts[kWfStat + kStatTraceRays];
+    return true;
+}
+
 bool run_wavefront(const DevScene& S, const FrameParams& P, WavefrontBuffers& W, int own_tiles, bool count,
-                   int tail_paths, int sort_bins, hipStream_t stream, WfFrameStats* fs, const char** err) {
+                   int tail_paths, int sort_bins, bool extra_pass, hipStream_t stream, WfTimeline* tl,
+                   WfFrameStats* fs, const char** err) {
     WfParams Q;
     Q.W = W;
     Q.spp = max(P.U.samplesPerPixel, 1);
@@ -1418,6 +1601,13 @@ bool run_wavefront(const DevScene& S, const FrameParams& P, WavefrontBuffers& W,
     const bool full = needs_full(P.U);
     const int maxExtra = (P.U.enableMotionAdaptiveSampling != 0) ? max(P.U.motionSamplingMaxExtraSamples, 0) : 0;
     size_t npix = (size_t)P.U.width * P.U.height;
+    static const bool host_ctl = env_int("RT_WF_HOST", 0) != 0 || getenv("RT_WF_DUMP") != nullptr;
+    // tail <= 1 (bulk rounds only, a test configuration) keeps the host loop: its round count is
+    // only bounded by maxBounces * (maxBounces + 1)
+    if (tl && !host_ctl && !wf_log() && Q.drain_min == 0 && Q.tail > 1)
+        return enqueue_wavefront(S, P, Q, count, full, maxExtra, extra_pass, stream, *tl, err);
+    Q.dev_ctl = 0;
+    Q.finish_q = 0;
 
     WF_CHECK(hipEventRecord(W.ev[0], stream));
     WF_CHECK(hipMemsetAsync(W.counts, 0, kWfCountWords * sizeof(uint32_t), stream));
