@@ -74,7 +74,7 @@ struct rt_ctx {
     // wavefront pipeline state
     WavefrontBuffers wf;
     DevBuf d_wf_color, d_wf_accum, d_wf_meta, d_wf_q0, d_wf_q1, d_wf_hits, d_wf_sq, d_wf_counts, d_wf_mprev, d_wf_extra;
-    DevBuf d_wf_sorted, d_wf_sort_table, d_wf_sort_total;
+    DevBuf d_wf_sorted, d_wf_sort_table, d_wf_sort_total, d_wf_params;
     WfFrameStats wfs{};
     WfTimeline wft;
     bool last_wavefront = false;
@@ -169,7 +169,7 @@ static size_t ctx_bytes(const rt_ctx* c) {
                            &c->d_accum[0], &c->d_accum[1], &c->d_depth, &c->d_motion, &c->d_gbuffer, &c->d_counters,
                            &c->d_wf_color, &c->d_wf_accum, &c->d_wf_meta, &c->d_wf_q0, &c->d_wf_q1, &c->d_wf_hits,
                            &c->d_wf_sq, &c->d_wf_counts, &c->d_wf_mprev, &c->d_wf_extra,
-                           &c->d_wf_sorted, &c->d_wf_sort_table, &c->d_wf_sort_total, &c->d_tri_bin};
+                           &c->d_wf_sorted, &c->d_wf_sort_table, &c->d_wf_sort_total, &c->d_tri_bin, &c->d_wf_params};
     size_t s = 0;
     for (auto* b : all) s += b->bytes;
     return s;
@@ -211,6 +211,10 @@ static rt_status ensure_wavefront(rt_ctx* c, size_t own_px, int spp, int max_ext
         HIPC(c, hipHostMalloc((void**)&W.h_counts, kWfCountWords * 4, 0));
         for (auto& e : W.ev) HIPC(c, hipEventCreate(&e));
         for (auto& e : c->wft.ev) HIPC(c, hipEventCreate(&e));
+        for (auto& e : W.param_ev) HIPC(c, hipEventCreate(&e));
+        if ((st = dev_alloc(c, c->d_wf_params, sizeof(FrameParams)))) return st;
+        HIPC(c, hipHostMalloc((void**)&W.h_params, sizeof(FrameParams) * WavefrontBuffers::kParamSlots, 0));
+        W.d_params = (FrameParams*)c->d_wf_params.p;
     }
     W.p_color = (float4*)c->d_wf_color.p;
     W.p_accum = (float4*)c->d_wf_accum.p;
@@ -294,7 +298,7 @@ rt_status rt_destroy(rt_ctx* c) {
                      &c->d_accum[1], &c->d_depth, &c->d_motion, &c->d_gbuffer, &c->d_counters,
                      &c->d_wf_color, &c->d_wf_accum, &c->d_wf_meta, &c->d_wf_q0, &c->d_wf_q1, &c->d_wf_hits,
                      &c->d_wf_sq, &c->d_wf_counts, &c->d_wf_mprev, &c->d_wf_extra,
-                     &c->d_wf_sorted, &c->d_wf_sort_table, &c->d_wf_sort_total, &c->d_tri_bin};
+                     &c->d_wf_sorted, &c->d_wf_sort_table, &c->d_wf_sort_total, &c->d_tri_bin, &c->d_wf_params};
     for (auto* b : all) dev_free(*b);
     if (c->h_counters) hipHostFree(c->h_counters);
     if (c->wf.h_counts) hipHostFree(c->wf.h_counts);
@@ -302,6 +306,10 @@ rt_status rt_destroy(rt_ctx* c) {
         if (e) hipEventDestroy(e);
     for (auto& e : c->wft.ev)
         if (e) hipEventDestroy(e);
+    if (c->wft.exec) hipGraphExecDestroy(c->wft.exec);
+    for (auto& e : c->wf.param_ev)
+        if (e) hipEventDestroy(e);
+    if (c->wf.h_params) hipHostFree(c->wf.h_params);
     if (c->ev0) hipEventDestroy(c->ev0);
     if (c->ev1) hipEventDestroy(c->ev1);
     if (c->own_stream) hipStreamDestroy(c->own_stream);

@@ -1,6 +1,9 @@
 // rt_kernels.h — kernel parameter blocks and launch entry points (device code lives in *.hip).
 #pragma once
 #include <hip/hip_runtime.h>
+
+#include <vector>
+
 #include "rt_device.h"
 
 namespace rt {
@@ -103,6 +106,13 @@ struct WavefrontBuffers {
     size_t cap_paths = 0;         // base + extra paths
     size_t cap_pixels = 0;
     hipEvent_t ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
+    // FrameParams of the frame in flight: one device copy the kernels read (so a captured frame
+    // graph replays with new uniforms), uploaded from a ring of pinned host slots
+    static constexpr int kParamSlots = 4;
+    FrameParams* d_params = nullptr;
+    FrameParams* h_params = nullptr;
+    hipEvent_t param_ev[kParamSlots] = {nullptr, nullptr, nullptr, nullptr};
+    int param_slot = 0;
 };
 // Hit sort: kSortBlocks blocks of kSortThreads share one partition of the queue in the histogram
 // and scatter kernels; bins are a power of two in [kSortMinBins, kSortMaxBins].
@@ -133,6 +143,12 @@ struct WfTimeline {
     Span spans[kMaxEv];
     int n_ev = 0, n_spans = 0;
     bool pending = false;
+    // the frame as a HIP graph (RT_GRAPH=1, default): replayed while `key` (everything the
+    // launches bake in) is unchanged, re-captured otherwise
+    hipGraphExec_t exec = nullptr;
+    std::vector<uint64_t> key;
+    int captures = 0;
+    bool in_graph = false;   // capturing: no event records
 };
 // Runs (host-driven: queue sizes read back every round; with RT_WF_LOG / RT_WF_DUMP /
 // RT_WF_HOST=1) or enqueues (device-driven, the default: `tl` receives the timeline, stats come

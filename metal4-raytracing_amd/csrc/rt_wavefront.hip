@@ -25,6 +25,7 @@
 #include "rt_shade.h"
 
 #include <cstdio>
+#include <cstring>
 #include <vector>
 
 namespace rt {
@@ -176,6 +177,7 @@ struct WfParams {
     int dev_ctl;           // device-side control (enqueue_wavefront): kernels read their queue sizes from
                            // the counters and skip once the live count fell below `tail`
     int finish_q;          // dev_ctl: the finish queue when every enqueued bulk round ran (written by generate)
+    const FrameParams* Pd; // this frame's FrameParams in device memory (W.d_params)
 };
 
 // counter slots (cslot): [q*8 + shard] ray queues q = 0, 1; [16 + shard] shadow queue; [24] extra allocator
@@ -258,7 +260,8 @@ __device__ __forceinline__ void write_pixel_outputs(const FrameParams& P, uint32
 }  // namespace
 
 // ---- generate -------------------------------------------------------------------------------------
-__global__ void __launch_bounds__(kBlock) wf_generate(DevScene S, FrameParams P, WfParams Q) {
+__global__ void __launch_bounds__(kBlock) wf_generate(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q) {
+    const FrameParams& P = *Pp;   // per-frame parameters in device memory (graph replay)
     __shared__ HaltonDim lds_halton[kHaltonLds];
     __shared__ BlockAlloc ba;
     const ShadeTabs halton = load_tabs(S, lds_halton, nullptr);   // no shading: Halton only
@@ -320,7 +323,8 @@ __global__ void __launch_bounds__(kBlock) wf_generate(DevScene S, FrameParams P,
 // region and the rays / shadow rays it appends to its queue shard stay grouped by region for
 // the next extend / connect launches (which hand shard k's range to XCD k).
 template <bool FULL, bool SORTED>
-__global__ void __launch_bounds__(kBlock) wf_shade(DevScene S, FrameParams P, WfParams Q, int cur) {
+__global__ void __launch_bounds__(kBlock) wf_shade(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int cur) {
+    const FrameParams& P = *Pp;   // per-frame parameters in device memory (graph replay)
     __shared__ HaltonDim lds_halton[kHaltonLds];
     __shared__ MatRec lds_mat[kMatLds];
     __shared__ BlockAlloc ba_ray, ba_sh;
@@ -517,7 +521,8 @@ __global__ void __launch_bounds__(kSortThreads) wf_sort_scatter(DevScene S, WfPa
 // triangle.  The wave therefore runs ~(total units of its rays)/64 iterations instead of
 // (slowest ray) x (rays per lane).
 template <bool ANY, bool COUNT>
-__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) wf_trace(DevScene S, FrameParams P, WfParams Q, int cur) {
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) wf_trace(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int cur) {
+    const FrameParams& P = *Pp;   // per-frame parameters in device memory (graph replay)
     __shared__ int lds_stack[kStackSize * kBlock];
     __shared__ uint4 lds_top[kTopNodes * 5];   // BVH top levels (BFS order: root, its children, ...)
     int* stack = &lds_stack[threadIdx.x];
@@ -743,7 +748,8 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 
 
 // ---- finish: run the remaining paths to completion --------------------------------------------------
 template <bool COUNT, bool FULL>
-__global__ void __launch_bounds__(kBlock) wf_finish(DevScene S, FrameParams P, WfParams Q, int cur) {
+__global__ void __launch_bounds__(kBlock) wf_finish(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int cur) {
+    const FrameParams& P = *Pp;   // per-frame parameters in device memory (graph replay)
     if (cur < 0) cur = (int)__builtin_amdgcn_readfirstlane(Q.W.counts[cslot(kCntFinishQ)]);   // dev_ctl
     // Persistent: every lane runs ONE path segment (closest hit, shade, shadow ray) per iteration
     // and picks up the next remaining path as soon as its own ends, so a wave waits for its
@@ -864,7 +870,8 @@ __global__ void __launch_bounds__(kBlock) wf_finish(DevScene S, FrameParams P, W
 // left at the tail (up to ~20 segments) no longer wait for their wave's worst ray every segment.
 template <bool COUNT, bool FULL, int WAVES>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES, WAVES)))
-wf_finish_step(DevScene S, FrameParams P, WfParams Q, int cur) {
+wf_finish_step(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int cur) {
+    const FrameParams& P = *Pp;   // per-frame parameters in device memory (graph replay)
     if (cur < 0) cur = (int)__builtin_amdgcn_readfirstlane(Q.W.counts[cslot(kCntFinishQ)]);   // dev_ctl
     __shared__ int lds_stack[kStackSize * kBlock];
     __shared__ uint4 lds_top[kTopNodes * 5];
@@ -1141,7 +1148,8 @@ wf_finish_step(DevScene S, FrameParams P, WfParams Q, int cur) {
 }
 
 // ---- motion-adaptive extra samples (:779-789) -----------------------------------------------------------
-__global__ void __launch_bounds__(kBlock) wf_extra(DevScene S, FrameParams P, WfParams Q, int qidx) {
+__global__ void __launch_bounds__(kBlock) wf_extra(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int qidx) {
+    const FrameParams& P = *Pp;   // per-frame parameters in device memory (graph replay)
     __shared__ HaltonDim lds_halton[kHaltonLds];
     const ShadeTabs halton = load_tabs(S, lds_halton, nullptr);   // no shading: Halton only
     const Uniforms& U = P.U;
@@ -1191,7 +1199,8 @@ __global__ void __launch_bounds__(kBlock) wf_extra(DevScene S, FrameParams P, Wf
 }
 
 // ---- resolve (:777, :792-819) -------------------------------------------------------------------------
-__global__ void __launch_bounds__(kBlock) wf_resolve(DevScene S, FrameParams P, WfParams Q, int with_extra) {
+__global__ void __launch_bounds__(kBlock) wf_resolve(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int with_extra) {
+    const FrameParams& P = *Pp;   // per-frame parameters in device memory (graph replay)
     const Uniforms& U = P.U;
     uint32_t i = blockIdx.x * kBlock + threadIdx.x;
     if (i >= Q.own_pixels) return;
@@ -1275,13 +1284,13 @@ static void launch_finish(const DevScene& S, const FrameParams& P, const WfParam
     static const int waves = env_int("RT_FINISH_WAVES", 4);
     if (STEP && waves == 3) {
         static const unsigned cap = resident_grid(wf_finish_step<COUNT, FULL, 3>, 2);
-        hipLaunchKernelGGL((wf_finish_step<COUNT, FULL, 3>), dim3(grid_for(n, cap)), dim3(kBlock), 0, stream, S, P, Q, cur);
+        hipLaunchKernelGGL((wf_finish_step<COUNT, FULL, 3>), dim3(grid_for(n, cap)), dim3(kBlock), 0, stream, S, Q.Pd, Q, cur);
     } else if (STEP) {
         static const unsigned cap = resident_grid(wf_finish_step<COUNT, FULL, 4>, 2);
-        hipLaunchKernelGGL((wf_finish_step<COUNT, FULL, 4>), dim3(grid_for(n, cap)), dim3(kBlock), 0, stream, S, P, Q, cur);
+        hipLaunchKernelGGL((wf_finish_step<COUNT, FULL, 4>), dim3(grid_for(n, cap)), dim3(kBlock), 0, stream, S, Q.Pd, Q, cur);
     } else {
         static const unsigned cap = resident_grid(wf_finish<COUNT, FULL>, 2);
-        hipLaunchKernelGGL((wf_finish<COUNT, FULL>), dim3(grid_for(n, cap)), dim3(kBlock), 0, stream, S, P, Q, cur);
+        hipLaunchKernelGGL((wf_finish<COUNT, FULL>), dim3(grid_for(n, cap)), dim3(kBlock), 0, stream, S, Q.Pd, Q, cur);
     }
 }
 
@@ -1379,8 +1388,8 @@ static bool iterate(const DevScene& S, const FrameParams& P, WfParams& Q, int& c
         WF_CHECK(hipEventRecord(W.ev[0], stream));
         unsigned g = grid_for(n, 8192);
         unsigned gt = grid_for(n, trace_grid_cap());
-        if (count) hipLaunchKernelGGL((wf_trace<false, true>), dim3(gt), dim3(kBlock), 0, stream, S, P, Q, cur);
-        else hipLaunchKernelGGL((wf_trace<false, false>), dim3(gt), dim3(kBlock), 0, stream, S, P, Q, cur);
+        if (count) hipLaunchKernelGGL((wf_trace<false, true>), dim3(gt), dim3(kBlock), 0, stream, S, Q.Pd, Q, cur);
+        else hipLaunchKernelGGL((wf_trace<false, false>), dim3(gt), dim3(kBlock), 0, stream, S, Q.Pd, Q, cur);
         WF_CHECK(hipEventRecord(W.ev[1], stream));
         const bool sort = Q.sort_bins != 0;
         if (sort) {
@@ -1390,15 +1399,15 @@ static bool iterate(const DevScene& S, const FrameParams& P, WfParams& Q, int& c
         }
         WF_CHECK(hipEventRecord(W.ev[4], stream));
         if (full) {
-            if (sort) hipLaunchKernelGGL((wf_shade<true, true>), dim3(g), dim3(kBlock), 0, stream, S, P, Q, cur);
-            else hipLaunchKernelGGL((wf_shade<true, false>), dim3(g), dim3(kBlock), 0, stream, S, P, Q, cur);
+            if (sort) hipLaunchKernelGGL((wf_shade<true, true>), dim3(g), dim3(kBlock), 0, stream, S, Q.Pd, Q, cur);
+            else hipLaunchKernelGGL((wf_shade<true, false>), dim3(g), dim3(kBlock), 0, stream, S, Q.Pd, Q, cur);
         } else {
-            if (sort) hipLaunchKernelGGL((wf_shade<false, true>), dim3(g), dim3(kBlock), 0, stream, S, P, Q, cur);
-            else hipLaunchKernelGGL((wf_shade<false, false>), dim3(g), dim3(kBlock), 0, stream, S, P, Q, cur);
+            if (sort) hipLaunchKernelGGL((wf_shade<false, true>), dim3(g), dim3(kBlock), 0, stream, S, Q.Pd, Q, cur);
+            else hipLaunchKernelGGL((wf_shade<false, false>), dim3(g), dim3(kBlock), 0, stream, S, Q.Pd, Q, cur);
         }
         WF_CHECK(hipEventRecord(W.ev[2], stream));
-        if (count) hipLaunchKernelGGL((wf_trace<true, true>), dim3(gt), dim3(kBlock), 0, stream, S, P, Q, cur);
-        else hipLaunchKernelGGL((wf_trace<true, false>), dim3(gt), dim3(kBlock), 0, stream, S, P, Q, cur);
+        if (count) hipLaunchKernelGGL((wf_trace<true, true>), dim3(gt), dim3(kBlock), 0, stream, S, Q.Pd, Q, cur);
+        else hipLaunchKernelGGL((wf_trace<true, false>), dim3(gt), dim3(kBlock), 0, stream, S, Q.Pd, Q, cur);
         WF_CHECK(hipGetLastError());
         WF_CHECK(hipEventRecord(W.ev[3], stream));
         WF_CHECK(hipMemcpyAsync(W.h_counts, W.counts, kWfCountWords * sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
@@ -1450,6 +1459,7 @@ struct Enqueue {
     hipStream_t stream;
     int last = -1;
     bool mark(const char** err) {
+        if (T.in_graph) return true;   // events recorded by graph nodes carry no timestamps (HIP)
         if (T.n_ev >= WfTimeline::kMaxEv) {
             *err = "wavefront timeline: too many events";
             return false;
@@ -1464,6 +1474,7 @@ struct Enqueue {
     }
     // closes the span [previous mark, now) as `stage`
     bool span(int stage, const char** err) {
+        if (T.in_graph) return true;
         const int a = last;
         if (!mark(err)) return false;
         T.spans[T.n_spans++] = WfTimeline::Span{stage, a, last};
@@ -1485,8 +1496,8 @@ static bool enqueue_pass(const DevScene& S, const FrameParams& P, const WfParams
     const unsigned gt = trace_grid_cap(), g = 8192;
     for (int k = 0; k < rounds; ++k) {
         const int cur = k & 1;
-        if (count) hipLaunchKernelGGL((wf_trace<false, true>), dim3(gt), dim3(kBlock), 0, stream, S, P, Q, cur);
-        else hipLaunchKernelGGL((wf_trace<false, false>), dim3(gt), dim3(kBlock), 0, stream, S, P, Q, cur);
+        if (count) hipLaunchKernelGGL((wf_trace<false, true>), dim3(gt), dim3(kBlock), 0, stream, S, Q.Pd, Q, cur);
+        else hipLaunchKernelGGL((wf_trace<false, false>), dim3(gt), dim3(kBlock), 0, stream, S, Q.Pd, Q, cur);
         if (!E.span(1, err)) return false;
         if (Q.sort_bins) {
             hipLaunchKernelGGL(wf_sort_hist, dim3(kSortBlocks), dim3(kSortThreads), 0, stream, S, Q, cur);
@@ -1495,15 +1506,15 @@ static bool enqueue_pass(const DevScene& S, const FrameParams& P, const WfParams
             if (!E.span(6, err)) return false;
         }
         if (full) {
-            if (Q.sort_bins) hipLaunchKernelGGL((wf_shade<true, true>), dim3(g), dim3(kBlock), 0, stream, S, P, Q, cur);
-            else hipLaunchKernelGGL((wf_shade<true, false>), dim3(g), dim3(kBlock), 0, stream, S, P, Q, cur);
+            if (Q.sort_bins) hipLaunchKernelGGL((wf_shade<true, true>), dim3(g), dim3(kBlock), 0, stream, S, Q.Pd, Q, cur);
+            else hipLaunchKernelGGL((wf_shade<true, false>), dim3(g), dim3(kBlock), 0, stream, S, Q.Pd, Q, cur);
         } else {
-            if (Q.sort_bins) hipLaunchKernelGGL((wf_shade<false, true>), dim3(g), dim3(kBlock), 0, stream, S, P, Q, cur);
-            else hipLaunchKernelGGL((wf_shade<false, false>), dim3(g), dim3(kBlock), 0, stream, S, P, Q, cur);
+            if (Q.sort_bins) hipLaunchKernelGGL((wf_shade<false, true>), dim3(g), dim3(kBlock), 0, stream, S, Q.Pd, Q, cur);
+            else hipLaunchKernelGGL((wf_shade<false, false>), dim3(g), dim3(kBlock), 0, stream, S, Q.Pd, Q, cur);
         }
         if (!E.span(2, err)) return false;
-        if (count) hipLaunchKernelGGL((wf_trace<true, true>), dim3(gt), dim3(kBlock), 0, stream, S, P, Q, cur);
-        else hipLaunchKernelGGL((wf_trace<true, false>), dim3(gt), dim3(kBlock), 0, stream, S, P, Q, cur);
+        if (count) hipLaunchKernelGGL((wf_trace<true, true>), dim3(gt), dim3(kBlock), 0, stream, S, Q.Pd, Q, cur);
+        else hipLaunchKernelGGL((wf_trace<true, false>), dim3(gt), dim3(kBlock), 0, stream, S, Q.Pd, Q, cur);
         if (!E.span(3, err)) return false;
     }
     WF_CHECK(hipMemsetAsync(Q.W.counts + cslot(kCntChunkFinish), 0, sizeof(uint32_t), stream));
@@ -1512,24 +1523,24 @@ static bool enqueue_pass(const DevScene& S, const FrameParams& P, const WfParams
     return E.span(5, err);
 }
 
-static bool enqueue_wavefront(const DevScene& S, const FrameParams& P, WfParams& Q, bool count, bool full,
-                              int maxExtra, bool extra_pass, hipStream_t stream, WfTimeline& T, const char** err) {
+// Issues one frame on `stream` (or into the graph being captured from it).  Everything the
+// launches bake in comes from S, Q and the buffer pointers in P; the per-frame values of P are
+// read by the kernels from Q.Pd.
+static bool record_frame(const DevScene& S, const FrameParams& P, WfParams& Q, bool count, bool full, int maxExtra,
+                         bool with_extra, hipStream_t stream, WfTimeline& T, const char** err) {
     WavefrontBuffers& W = Q.W;
     T.n_ev = T.n_spans = 0;
     Enqueue E{T, stream};
-    Q.dev_ctl = 1;
-    Q.drain_min = 0;
     const size_t npix = (size_t)P.U.width * P.U.height;
     if (!E.mark(err)) return false;
     WF_CHECK(hipMemsetAsync(W.counts, 0, kWfCountWords * sizeof(uint32_t), stream));
     WF_CHECK(hipMemcpyAsync(W.motion_prev, P.motion, npix * sizeof(float2), hipMemcpyDeviceToDevice, stream));
     const int rounds = rounds_for(Q.base_paths, Q.tail);
     Q.finish_q = rounds & 1;
-    hipLaunchKernelGGL(wf_generate, dim3(grid_for(Q.base_paths, 16384)), dim3(kBlock), 0, stream, S, P, Q);
+    hipLaunchKernelGGL(wf_generate, dim3(grid_for(Q.base_paths, 16384)), dim3(kBlock), 0, stream, S, Q.Pd, Q);
     WF_CHECK(hipGetLastError());
     if (!E.span(0, err)) return false;
     if (!enqueue_pass(S, P, Q, rounds, count, full, E, err)) return false;
-    const bool with_extra = maxExtra > 0 && extra_pass;
     if (with_extra) {
         // second pass over the motion-adaptive extra samples (:779-789), appended to queue 0
         const int rounds2 = rounds_for((uint64_t)Q.own_pixels * (uint64_t)maxExtra, Q.tail);
@@ -1537,16 +1548,89 @@ static bool enqueue_wavefront(const DevScene& S, const FrameParams& P, WfParams&
         WF_CHECK(hipMemsetAsync(W.counts + cslot(kCntChunkExtend), 0, cslot(2 * kShards) * sizeof(uint32_t), stream));
         WF_CHECK(hipMemsetD32Async(W.counts + cslot(kCntTailMode), 0u, 1, stream));
         WF_CHECK(hipMemsetD32Async(W.counts + cslot(kCntFinishQ), (uint32_t)(rounds2 & 1), 1, stream));
-        hipLaunchKernelGGL(wf_extra, dim3(grid_for(Q.own_pixels, 1u << 30)), dim3(kBlock), 0, stream, S, P, Q, 0);
+        hipLaunchKernelGGL(wf_extra, dim3(grid_for(Q.own_pixels, 1u << 30)), dim3(kBlock), 0, stream, S, Q.Pd, Q, 0);
         WF_CHECK(hipGetLastError());
         if (!E.span(4, err)) return false;
         if (!enqueue_pass(S, P, Q, rounds2, count, full, E, err)) return false;
     }
-    hipLaunchKernelGGL(wf_resolve, dim3(grid_for(Q.own_pixels, 1u << 30)), dim3(kBlock), 0, stream, S, P, Q,
+    hipLaunchKernelGGL(wf_resolve, dim3(grid_for(Q.own_pixels, 1u << 30)), dim3(kBlock), 0, stream, S, Q.Pd, Q,
                        with_extra ? 1 : 0);
     WF_CHECK(hipGetLastError());
     if (!E.span(4, err)) return false;
     WF_CHECK(hipMemcpyAsync(W.h_counts, W.counts, kWfCountWords * sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
+    return true;
+}
+
+// Everything a captured frame graph bakes in (launch arguments, buffer pointers, round counts).
+static std::vector<uint64_t> graph_key(const DevScene& S, const FrameParams& P, const WfParams& Q, bool count, bool full,
+                                       int maxExtra, bool with_extra) {
+    std::vector<uint64_t> k;
+    auto put = [&k](const auto& v) {
+        uint64_t w = 0;
+        static_assert(sizeof(v) <= 8, "key field");
+        std::memcpy(&w, &v, sizeof(v));
+        k.push_back(w);
+    };
+    put(S.tris); put(S.nodes8); put(S.tri_info); put(S.pos); put(S.prev_pos); put(S.nrm); put(S.inst);
+    put(S.prev_inst); put(S.materials); put(S.lights); put(S.halton); put(S.tri_bin); put(S.max_submeshes);
+    put(S.num_materials); put(S.num_tris); put(S.num_nodes8);
+    const WavefrontBuffers& W = Q.W;
+    put(W.queue_entries); put(W.p_color); put(W.p_accum); put(W.p_meta); put(W.q[0]); put(W.q[1]); put(W.hits);
+    put(W.sq); put(W.counts); put(W.h_counts); put(W.motion_prev); put(W.px_extra); put(W.sorted); put(W.sort_table);
+    put(W.sort_total); put(W.d_params);
+    put(Q.base_paths); put(Q.own_pixels); put(Q.seg_cap); put(Q.spp); put(Q.refill_min); put(Q.tri_vote);
+    put(Q.chunk); put(Q.tail); put(Q.sort_bins); put(Q.sort_xcd); put(Q.steal); put(Q.diag); put(Q.finish_step);
+    put(Q.shade_min); put(Q.drain_min); put(Q.dev_ctl); put(Q.Pd);
+    put(P.motion); put(P.U.width); put(P.U.height);
+    put(count); put(full); put(maxExtra); put(with_extra);
+    return k;
+}
+
+static bool enqueue_wavefront(const DevScene& S, const FrameParams& P, WfParams& Q, bool count, bool full,
+                              int maxExtra, bool extra_pass, hipStream_t stream, WfTimeline& T, const char** err) {
+    Q.dev_ctl = 1;
+    Q.drain_min = 0;
+    Q.finish_q = 0;   // set by record_frame from the round count
+    const bool with_extra = maxExtra > 0 && extra_pass;
+    static const bool use_graph = env_int("RT_GRAPH", 0) != 0;
+    if (!use_graph) {
+        if (!record_frame(S, P, Q, count, full, maxExtra, with_extra, stream, T, err)) return false;
+        T.pending = true;
+        return true;
+    }
+    // HIP graph of the whole frame, captured once per configuration and replayed every frame
+    std::vector<uint64_t> key = graph_key(S, P, Q, count, full, maxExtra, with_extra);
+    if (!T.exec || key != T.key) {
+        if (T.exec) {
+            WF_CHECK(hipGraphExecDestroy(T.exec));
+            T.exec = nullptr;
+        }
+        T.key.clear();
+        WF_CHECK(hipStreamBeginCapture(stream, hipStreamCaptureModeRelaxed));
+        T.in_graph = true;
+        const bool ok = record_frame(S, P, Q, count, full, maxExtra, with_extra, stream, T, err);
+        T.in_graph = false;
+        hipGraph_t graph = nullptr;
+        const hipError_t e = hipStreamEndCapture(stream, &graph);
+        if (!ok || e != hipSuccess) {
+            if (graph) hipGraphDestroy(graph);
+            if (ok) *err = hipGetErrorString(e);
+            return false;
+        }
+        const hipError_t ei = hipGraphInstantiate(&T.exec, graph, nullptr, nullptr, 0);
+        hipGraphDestroy(graph);
+        if (ei != hipSuccess) {
+            T.exec = nullptr;
+            *err = hipGetErrorString(ei);
+            return false;
+        }
+        T.key = std::move(key);
+        ++T.captures;
+    }
+    // graph replay: per-stage times are not available (no timestamps on graph event nodes), only
+    // the whole frame (rt_stats.last_frame_ms, events around the replay)
+    T.n_ev = T.n_spans = 0;
+    WF_CHECK(hipGraphLaunch(T.exec, stream));
     T.pending = true;
     return true;
 }
@@ -1598,6 +1682,15 @@ bool run_wavefront(const DevScene& S, const FrameParams& P, WavefrontBuffers& W,
     }
     *fs = WfFrameStats{};
     float* stage_ms = fs->stage_ms;
+    {   // this frame's parameters -> device (the slot's previous upload has executed once its event has)
+        const int slot = W.param_slot;
+        W.param_slot = (slot + 1) % WavefrontBuffers::kParamSlots;
+        WF_CHECK(hipEventSynchronize(W.param_ev[slot]));
+        W.h_params[slot] = P;
+        WF_CHECK(hipMemcpyAsync(W.d_params, &W.h_params[slot], sizeof(FrameParams), hipMemcpyHostToDevice, stream));
+        WF_CHECK(hipEventRecord(W.param_ev[slot], stream));
+        Q.Pd = W.d_params;
+    }
     const bool full = needs_full(P.U);
     const int maxExtra = (P.U.enableMotionAdaptiveSampling != 0) ? max(P.U.motionSamplingMaxExtraSamples, 0) : 0;
     size_t npix = (size_t)P.U.width * P.U.height;
@@ -1612,7 +1705,7 @@ bool run_wavefront(const DevScene& S, const FrameParams& P, WavefrontBuffers& W,
     WF_CHECK(hipEventRecord(W.ev[0], stream));
     WF_CHECK(hipMemsetAsync(W.counts, 0, kWfCountWords * sizeof(uint32_t), stream));
     WF_CHECK(hipMemcpyAsync(W.motion_prev, P.motion, npix * sizeof(float2), hipMemcpyDeviceToDevice, stream));
-    hipLaunchKernelGGL(wf_generate, dim3(grid_for(Q.base_paths, 16384)), dim3(kBlock), 0, stream, S, P, Q);
+    hipLaunchKernelGGL(wf_generate, dim3(grid_for(Q.base_paths, 16384)), dim3(kBlock), 0, stream, S, Q.Pd, Q);
     WF_CHECK(hipGetLastError());
     WF_CHECK(hipEventRecord(W.ev[1], stream));
     WF_CHECK(hipMemcpyAsync(W.h_counts, W.counts, kWfCountWords * sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
@@ -1627,7 +1720,7 @@ bool run_wavefront(const DevScene& S, const FrameParams& P, WavefrontBuffers& W,
     if (maxExtra > 0) {
         // the extra-sample pass appends primary rays to queue `cur` (reset here)
         WF_CHECK(hipMemsetAsync(W.counts + cslot(cur * kShards), 0, cslot(kShards) * sizeof(uint32_t), stream));
-        hipLaunchKernelGGL(wf_extra, dim3(grid_for(Q.own_pixels, 1u << 30)), dim3(kBlock), 0, stream, S, P, Q, cur);
+        hipLaunchKernelGGL(wf_extra, dim3(grid_for(Q.own_pixels, 1u << 30)), dim3(kBlock), 0, stream, S, Q.Pd, Q, cur);
         WF_CHECK(hipGetLastError());
         WF_CHECK(hipMemcpyAsync(W.h_counts, W.counts, kWfCountWords * sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
         WF_CHECK(hipStreamSynchronize(stream));
@@ -1636,7 +1729,7 @@ bool run_wavefront(const DevScene& S, const FrameParams& P, WavefrontBuffers& W,
             if (!iterate(S, P, Q, cur, n_extra, count, full, stream, fs, err)) return false;
         }
     }
-    hipLaunchKernelGGL(wf_resolve, dim3(grid_for(Q.own_pixels, 1u << 30)), dim3(kBlock), 0, stream, S, P, Q,
+    hipLaunchKernelGGL(wf_resolve, dim3(grid_for(Q.own_pixels, 1u << 30)), dim3(kBlock), 0, stream, S, Q.Pd, Q,
                        maxExtra > 0 ? 1 : 0);
     WF_CHECK(hipGetLastError());
     WF_CHECK(hipEventRecord(W.ev[1], stream));
