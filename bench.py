@@ -37,7 +37,7 @@ B_TRI = 48
 B_HIT = 16 + 48 + 48
 B_PIXEL = 4 + 16 + 16 + 4 + 16
 B_QRAY = 48  # wf_trace queue entry: extend 32 B ray in + 16 B hit out; connect 48 B shadow entry in
-TRAFFIC_JSON_REL = "profiles/r01_traffic_wf_trace.json"
+TRAFFIC_JSON_REL = "profiles/r01_traffic.json"
 TRAFFIC_JSON = os.path.join(os.path.dirname(os.path.abspath(__file__)), TRAFFIC_JSON_REL)
 
 
@@ -112,6 +112,10 @@ def main():
     # the queue traversal kernel alone (wavefront): its own node / triangle visits per traced ray
     q_nodes_per_ray = cst.trace_nodes / max(cst.trace_rays, 1)
     q_tris_per_ray = cst.trace_tris / max(cst.trace_rays, 1)
+    # the persistent finish kernel: the rest of the visits, over the rays it traced
+    f_rays_c = rays_c - cst.trace_rays
+    f_nodes_per_ray = (cst.node_visits - cst.trace_nodes) / max(f_rays_c, 1)
+    f_tris_per_ray = (cst.tri_tests - cst.trace_tris) / max(f_rays_c, 1)
     R.samplesPerPixel = a.spp  # resets frameIndex (didSet)
 
     for _ in range(a.warmup):
@@ -122,7 +126,7 @@ def main():
     kernel_ms = []
     stage_ms = np.zeros(7)
     closest = 0
-    trace_rays, trace_launches, trace_ms = 0, 0, 0.0
+    trace_rays, trace_launches, trace_ms, trace_closest, finish_launches = 0, 0, 0.0, 0, 0
     for _ in range(a.steps):
         st = frame()
         rays += st.closest_rays + st.shadow_rays
@@ -130,6 +134,8 @@ def main():
         trace_rays += st.trace_rays
         trace_launches += st.trace_launches
         trace_ms += st.trace_ms
+        trace_closest += st.trace_closest_rays
+        finish_launches += st.finish_launches
         kernel_ms.append(st.last_frame_ms)
         stage_ms += np.array(list(st.kernel_ms))
         last_st = st
@@ -151,39 +157,56 @@ def main():
 
     value = rays / dt / 1e9
     ms_per_step = dt / a.steps * 1e3
+    kernels = []
     if last_st.pipeline == 1 and trace_launches > 0:
-        # dominant kernel: wf_trace (extend + connect launches), per launch.  Algorithmic bytes per
-        # traced ray: 48 B queue entry in (+ hit record out) + 80 B per 8-wide node fetched + 48 B
-        # per triangle tested (DESIGN.md 'Roofline').
-        kernel = "rt::wf_trace<{false,true}, false> (extend + connect)"
-        rays_per_launch = trace_rays / trace_launches
-        launch_ms = trace_ms / trace_launches
-        bytes_per_launch = rays_per_launch * (B_QRAY + q_nodes_per_ray * B_NODE + q_tris_per_ray * B_TRI)
-        npr, tpr = q_nodes_per_ray, q_tris_per_ray
-    else:
+        # wf_trace (extend + connect launches), per launch.  Algorithmic bytes per traced ray: 48 B
+        # queue entry in (+ hit record out) + 80 B per 8-wide node fetched + 48 B per triangle
+        # tested (DESIGN.md 'Roofline').
+        rpl = trace_rays / trace_launches
+        kernels.append(dict(
+            kernel="rt::wf_trace<{false,true}, false> (extend + connect)", launches=trace_launches / a.steps,
+            launch_ms=trace_ms / trace_launches, rays_per_launch=rpl, nodes_per_ray=q_nodes_per_ray,
+            tris_per_ray=q_tris_per_ray,
+            bytes_per_launch=rpl * (B_QRAY + q_nodes_per_ray * B_NODE + q_tris_per_ray * B_TRI)))
+    if last_st.pipeline == 1 and finish_launches > 0:
+        # wf_finish_step: the tail paths to completion.  Per ray 48 B (ray + hit) + nodes + triangles
+        # as above; per closest hit the shading gathers (B_HIT); the path state in and out (48 B x 2)
+        # once per path is left out (not counted per ray).
+        f_rays = (rays - trace_rays) / finish_launches
+        f_closest = (closest - trace_closest) / finish_launches
+        kernels.append(dict(
+            kernel="rt::wf_finish_step<false, false, 4>", launches=finish_launches / a.steps,
+            launch_ms=float(stage_ms[5]) / finish_launches, rays_per_launch=f_rays, nodes_per_ray=f_nodes_per_ray,
+            tris_per_ray=f_tris_per_ray,
+            bytes_per_launch=f_rays * (B_RAY + f_nodes_per_ray * B_NODE + f_tris_per_ray * B_TRI) + f_closest * B_HIT))
+    if not kernels:
         # megakernel: the whole frame is one launch
-        kernel = "rt::megakernel<false, false>"
-        rays_per_launch = rays / a.steps / n
-        closest_per_launch = closest / a.steps / n
-        pixels_per_launch = a.width * a.height / n
-        launch_ms = kms
-        bytes_per_launch = (rays_per_launch * (B_RAY + nodes_per_ray * B_NODE + tris_per_ray * B_TRI)
-                            + closest_per_launch * B_HIT + pixels_per_launch * B_PIXEL)
-        npr, tpr = nodes_per_ray, tris_per_ray
-    achieved = bytes_per_launch / (launch_ms * 1e-3) / 1e9
+        rpl = rays / a.steps / n
+        kernels.append(dict(
+            kernel="rt::megakernel<false, false>", launches=1, launch_ms=kms, rays_per_launch=rpl,
+            nodes_per_ray=nodes_per_ray, tris_per_ray=tris_per_ray,
+            bytes_per_launch=(rpl * (B_RAY + nodes_per_ray * B_NODE + tris_per_ray * B_TRI)
+                              + closest / a.steps / n * B_HIT + a.width * a.height / n * B_PIXEL)))
+    for k in kernels:
+        k["achieved"] = k["bytes_per_launch"] / (k["launch_ms"] * 1e-3) / 1e9
+        k["ms_per_frame"] = k["launch_ms"] * k["launches"]
+    # the dominant kernel: the most device time per frame
+    dom = max(kernels, key=lambda k: k["ms_per_frame"])
+    kernel, launch_ms, bytes_per_launch = dom["kernel"], dom["launch_ms"], dom["bytes_per_launch"]
+    rays_per_launch, npr, tpr, achieved = dom["rays_per_launch"], dom["nodes_per_ray"], dom["tris_per_ray"], dom["achieved"]
     traffic, traffic_src, l2_hit = None, None, None
     if a.traffic_csv:
-        traffic = read_traffic(a.traffic_csv.split(","), r"wf_trace<(true|false),false>"
-                               if last_st.pipeline == 1 else r"megakernel<false,")
+        traffic = read_traffic(a.traffic_csv.split(","), traffic_key(kernel))
         traffic_src = "live: " + a.traffic_csv
     elif os.path.exists(TRAFFIC_JSON):
         with open(TRAFFIC_JSON) as f:
             tj = json.load(f)
-        if tj.get("kernel") == kernel and tj.get("config") == [a.scene, a.width, a.height, a.spp, a.bounces]:
-            traffic, traffic_src = tj["bytes_per_launch"], TRAFFIC_JSON_REL + " (" + tj.get("source", "") + ")"
-            # TCC hit rates (rocprofv3 TCC_HIT/TCC_MISS pass) of the traversal and shade kernels
+        if tj.get("config") == [a.scene, a.width, a.height, a.spp, a.bounces]:
+            if tj.get("kernel") == kernel:
+                traffic, traffic_src = tj["bytes_per_launch"], TRAFFIC_JSON_REL + " (" + tj.get("source", "") + ")"
+            # TCC hit rates (rocprofv3 TCC_HIT/TCC_MISS pass) of the traversal, shade and finish kernels
             hits = tj.get("l2_hit") or {}
-            l2_hit = {k: v for k, v in hits.items() if re.search(r"wf_(trace|shade|finish)<", k)} or None
+            l2_hit = {k: v for k, v in hits.items() if re.search(r"wf_(trace|shade|finish)", k)} or None
 
     cpu = None
     if not a.no_cpu and n == 1:
@@ -221,12 +244,25 @@ def main():
             "l2_hit": l2_hit,
             "kernel": kernel, "launch_ms": round(launch_ms, 4), "bytes_per_launch": int(bytes_per_launch),
             "rays_per_launch": int(rays_per_launch), "nodes_per_ray": round(npr, 3), "tris_per_ray": round(tpr, 3),
+            # every timed kernel of the frame with its own roofline, for comparison
+            "kernels": [{"kernel": k["kernel"], "ms_per_frame": round(k["ms_per_frame"], 3),
+                         "launch_ms": round(k["launch_ms"], 4), "achieved_GBs": round(k["achieved"], 1),
+                         "frac": round(k["achieved"] / HBM_PEAK_GBS, 4), "nodes_per_ray": round(k["nodes_per_ray"], 3),
+                         "tris_per_ray": round(k["tris_per_ray"], 3)} for k in kernels],
         },
         "cpu_baseline": cpu,
     }
     print(json.dumps(line), flush=True)
     if n > 1:
         dist.destroy_process_group()
+
+
+TRAFFIC_KEYS = {"rt::wf_trace": r"wf_trace<(true|false),false>", "rt::wf_finis": r"wf_finish_step<false,false"}
+
+
+def traffic_key(kernel):
+    """rocprof kernel-name pattern of the bench line's dominant kernel"""
+    return TRAFFIC_KEYS.get(kernel[:12], r"megakernel<false,")
 
 
 def read_traffic(paths, kernel_key):

@@ -134,6 +134,9 @@ typedef struct rt_stats {
     uint64_t trace_tris;    /* triangles it tested (counting frames only) */
     int32_t trace_launches; /* its launches */
     float trace_ms;         /* its summed device time (HIP events on the render stream) */
+    uint64_t trace_closest_rays; /* the closest-hit (extend) share of trace_rays */
+    int32_t finish_launches;     /* wavefront: persistent finish launches (their time: kernel_ms[5]) */
+    int32_t _pad;
 } rt_stats;
 
 rt_status rt_create(const rt_opts* opts, rt_ctx** out);

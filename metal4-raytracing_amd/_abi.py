@@ -143,6 +143,9 @@ class Stats(C.Structure):
         ("trace_tris", C.c_uint64),
         ("trace_launches", C.c_int32),
         ("trace_ms", C.c_float),
+        ("trace_closest_rays", C.c_uint64),
+        ("finish_launches", C.c_int32),
+        ("_pad", C.c_int32),
     ]
 
 

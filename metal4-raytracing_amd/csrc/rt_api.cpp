@@ -701,6 +701,8 @@ rt_status rt_wait(rt_ctx* c) {
         c->stats.trace_rays = c->last_wavefront ? c->wfs.trace_rays : 0;
         c->stats.trace_launches = c->last_wavefront ? c->wfs.trace_launches : 0;
         c->stats.trace_ms = c->last_wavefront ? c->wfs.trace_ms : 0.0f;
+        c->stats.trace_closest_rays = c->last_wavefront ? c->wfs.trace_closest_rays : 0;
+        c->stats.finish_launches = c->last_wavefront ? c->wfs.finish_launches : 0;
         auto total = [c](int slot) {
             unsigned long long t = 0;
             for (int r = 0; r < kCntReplicas; ++r) t += c->h_counters[cnt_word(slot, r)];

@@ -83,8 +83,8 @@ constexpr int kCntStride = 32;
 constexpr int kWfDiagHist = 48 * kCntStride;        // 64 words: wf_finish wave end-time histogram (50 us bins)
 constexpr int kWfDiagSteps = kWfDiagHist + 64;        // 66 words: wf_trace steps-per-ray histograms + max
 constexpr int kWfStat = kWfDiagSteps + 66;              // 3 words: rounds, wf_trace launches, their rays
-constexpr int kStatRounds = 0, kStatTraceLaunches = 1, kStatTraceRays = 2;
-constexpr int kWfCountWords = 48 * kCntStride + 64 + 66 + 3;
+constexpr int kStatRounds = 0, kStatTraceLaunches = 1, kStatTraceRays = 2, kStatExtendRays = 3, kStatFinish = 4;
+constexpr int kWfCountWords = 48 * kCntStride + 64 + 66 + 5;
 __host__ __device__ constexpr uint32_t cslot(int c) { return (uint32_t)c * kCntStride; }
 struct WavefrontBuffers {
     size_t queue_entries = 0;     // kShards segments of queue_entries / kShards
@@ -127,8 +127,10 @@ struct WfFrameStats {
     float stage_ms[7];
     int iterations;
     unsigned long long trace_rays;  // rays traced by wf_trace launches (extend + connect)
+    unsigned long long trace_closest_rays;   // the extend share
     int trace_launches;
     float trace_ms;                 // their summed device time
+    int finish_launches;
 };
 // Runs one frame; returns false on a HIP error (message in *err).
 // tail_paths: finish-kernel threshold (0 = default / RT_TAIL_RAYS).

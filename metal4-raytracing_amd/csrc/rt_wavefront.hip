@@ -552,7 +552,10 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 
     if (Q.dev_ctl) {
         stat_add(Q, kStatTraceRays, n);
         stat_add(Q, kStatTraceLaunches, 1u);
-        if (!ANY) stat_add(Q, kStatRounds, 1u);
+        if (!ANY) {
+            stat_add(Q, kStatRounds, 1u);
+            stat_add(Q, kStatExtendRays, n);
+        }
     }
     if (!ANY && blockIdx.x == 0 && threadIdx.x < 2 * kShards) {  // reset the queues shade / connect fill
         const int next = 1 - cur;
@@ -761,6 +764,7 @@ __global__ void __launch_bounds__(kBlock) wf_finish(DevScene S, const FrameParam
     const Uniforms& U = P.U;
     const ShardPrefix cnt = load_prefix(Q.W.counts + cslot(cur * kShards));
     const uint32_t n = cnt.end[kShards - 1];
+    if (Q.dev_ctl) stat_add(Q, kStatFinish, 1u);
     if (Q.dev_ctl && n > 0) stat_add(Q, kStatRounds, 1u);
     const float4* qin = Q.W.q[cur];
     int* stack = &lds_stack[threadIdx.x];
@@ -884,6 +888,7 @@ wf_finish_step(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int c
     const Uniforms& U = P.U;
     const ShardPrefix cnt = load_prefix(Q.W.counts + cslot(cur * kShards));
     const uint32_t n = cnt.end[kShards - 1];
+    if (Q.dev_ctl) stat_add(Q, kStatFinish, 1u);
     if (Q.dev_ctl && n > 0) stat_add(Q, kStatRounds, 1u);
     const float4* qin = Q.W.q[cur];
     uint32_t* chunk_ctr = Q.W.counts + cslot(kCntChunkFinish);
@@ -1364,6 +1369,7 @@ static bool iterate(const DevScene& S, const FrameParams& P, WfParams& Q, int& c
                 float a = 0;
                 WF_CHECK(hipEventElapsedTime(&a, W.ev[0], W.ev[1]));
                 stage_ms[5] += a;
+                ++fs->finish_launches;
                 ++fs->iterations;
                 const uint32_t n_next = Q.drain_min > 0 ? queue_total(W.h_counts, 1 - cur) : 0u;
                 if (wf_log()) {
@@ -1422,6 +1428,7 @@ static bool iterate(const DevScene& S, const FrameParams& P, WfParams& Q, int& c
         stage_ms[2] += b;
         stage_ms[3] += c;
         fs->trace_rays += (unsigned long long)n + queue_total(W.h_counts, 2);  // extend + connect rays
+        fs->trace_closest_rays += n;
         fs->trace_launches += 2;
         fs->trace_ms += a + c;
         if (wf_log()) {
@@ -1649,6 +1656,8 @@ bool wavefront_collect(const WavefrontBuffers& W, WfTimeline& T, WfFrameStats* f
     fs->iterations = (int)W.h_counts[kWfStat + kStatRounds];
     fs->trace_launches = (int)W.h_counts[kWfStat + kStatTraceLaunches];
     fs->trace_rays = W.h_counts[kWfStat + kStatTraceRays];
+    fs->trace_closest_rays = W.h_counts[kWfStat + kStatExtendRays];
+    fs->finish_launches = (int)W.h_counts[kWfStat + kStatFinish];
     return true;
 }
 

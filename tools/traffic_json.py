@@ -34,13 +34,13 @@ def main():
     csvs, bench_json, out = sys.argv[1], sys.argv[2], sys.argv[3]
     line = json.loads(open(bench_json).read().strip().splitlines()[-1])
     cfg = line["config"]
-    per_launch = bench.read_traffic(csvs.split(","), r"wf_trace<(true|false),false>")
+    per_launch = bench.read_traffic(csvs.split(","), bench.traffic_key(line["roofline"]["kernel"]))
     res = {
         "kernel": line["roofline"]["kernel"],
         "config": [cfg["scene"], cfg["width"], cfg["height"], cfg["spp"], cfg["max_bounces"]],
         "bytes_per_launch": per_launch,
         "algorithmic_bytes_per_launch": line["roofline"]["bytes_per_launch"],
-        "source": "rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE, per wf_trace<*, false> dispatch, "
+        "source": "rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE, per dispatch of the dominant kernel, "
                   + os.path.basename(out).split("_")[0],
     }
     if len(sys.argv) > 4 and os.path.exists(sys.argv[4]):
