@@ -53,6 +53,11 @@ static int env_int(const char* name, int dflt) {  // tuning experiments
     return e ? atoi(e) : dflt;
 }
 
+static bool use_graph() {  // RT_GRAPH=1: the device-driven frame as a captured HIP graph
+    static const bool v = env_int("RT_GRAPH", 0) != 0;
+    return v;
+}
+
 static bool wf_log() {  // RT_WF_LOG=1: per-iteration queue sizes and stage times on stderr
     static const bool v = env_int("RT_WF_LOG", 0) != 0;
     return v;
@@ -1533,13 +1538,17 @@ static bool enqueue_pass(const DevScene& S, const FrameParams& P, const WfParams
 // Issues one frame on `stream` (or into the graph being captured from it).  Everything the
 // launches bake in comes from S, Q and the buffer pointers in P; the per-frame values of P are
 // read by the kernels from Q.Pd.
+// h_stage: graph mode, the pinned copy of this frame's FrameParams the graph uploads first.
 static bool record_frame(const DevScene& S, const FrameParams& P, WfParams& Q, bool count, bool full, int maxExtra,
-                         bool with_extra, hipStream_t stream, WfTimeline& T, const char** err) {
+                         bool with_extra, const FrameParams* h_stage, hipStream_t stream, WfTimeline& T,
+                         const char** err) {
     WavefrontBuffers& W = Q.W;
     T.n_ev = T.n_spans = 0;
     Enqueue E{T, stream};
     const size_t npix = (size_t)P.U.width * P.U.height;
     if (!E.mark(err)) return false;
+    if (h_stage)
+        WF_CHECK(hipMemcpyAsync(W.d_params, h_stage, sizeof(FrameParams), hipMemcpyHostToDevice, stream));
     WF_CHECK(hipMemsetAsync(W.counts, 0, kWfCountWords * sizeof(uint32_t), stream));
     WF_CHECK(hipMemcpyAsync(W.motion_prev, P.motion, npix * sizeof(float2), hipMemcpyDeviceToDevice, stream));
     const int rounds = rounds_for(Q.base_paths, Q.tail);
@@ -1599,13 +1608,17 @@ static bool enqueue_wavefront(const DevScene& S, const FrameParams& P, WfParams&
     Q.drain_min = 0;
     Q.finish_q = 0;   // set by record_frame from the round count
     const bool with_extra = maxExtra > 0 && extra_pass;
-    static const bool use_graph = env_int("RT_GRAPH", 0) != 0;
-    if (!use_graph) {
-        if (!record_frame(S, P, Q, count, full, maxExtra, with_extra, stream, T, err)) return false;
+    if (!use_graph()) {
+        if (!record_frame(S, P, Q, count, full, maxExtra, with_extra, nullptr, stream, T, err)) return false;
         T.pending = true;
         return true;
     }
-    // HIP graph of the whole frame, captured once per configuration and replayed every frame
+    // HIP graph of the whole frame, captured once per configuration and replayed every frame.
+    // Its first node uploads the FrameParams from one pinned staging slot; the slot is rewritten
+    // only after the previous replay finished (one graph frame in flight per context).
+    WavefrontBuffers& W = Q.W;
+    WF_CHECK(hipEventSynchronize(W.param_ev[0]));
+    W.h_params[0] = P;
     std::vector<uint64_t> key = graph_key(S, P, Q, count, full, maxExtra, with_extra);
     if (!T.exec || key != T.key) {
         if (T.exec) {
@@ -1615,7 +1628,7 @@ static bool enqueue_wavefront(const DevScene& S, const FrameParams& P, WfParams&
         T.key.clear();
         WF_CHECK(hipStreamBeginCapture(stream, hipStreamCaptureModeRelaxed));
         T.in_graph = true;
-        const bool ok = record_frame(S, P, Q, count, full, maxExtra, with_extra, stream, T, err);
+        const bool ok = record_frame(S, P, Q, count, full, maxExtra, with_extra, &W.h_params[0], stream, T, err);
         T.in_graph = false;
         hipGraph_t graph = nullptr;
         const hipError_t e = hipStreamEndCapture(stream, &graph);
@@ -1638,6 +1651,7 @@ static bool enqueue_wavefront(const DevScene& S, const FrameParams& P, WfParams&
     // the whole frame (rt_stats.last_frame_ms, events around the replay)
     T.n_ev = T.n_spans = 0;
     WF_CHECK(hipGraphLaunch(T.exec, stream));
+    WF_CHECK(hipEventRecord(W.param_ev[0], stream));
     T.pending = true;
     return true;
 }
@@ -1691,22 +1705,24 @@ bool run_wavefront(const DevScene& S, const FrameParams& P, WavefrontBuffers& W,
     }
     *fs = WfFrameStats{};
     float* stage_ms = fs->stage_ms;
-    {   // this frame's parameters -> device (the slot's previous upload has executed once its event has)
+    static const bool host_ctl = env_int("RT_WF_HOST", 0) != 0 || getenv("RT_WF_DUMP") != nullptr;
+    // tail <= 1 (bulk rounds only, a test configuration) keeps the host loop: its round count is
+    // only bounded by maxBounces * (maxBounces + 1)
+    const bool dev = tl && !host_ctl && !wf_log() && Q.drain_min == 0 && Q.tail > 1;
+    Q.Pd = W.d_params;
+    if (!(dev && use_graph())) {   // this frame's parameters -> device (graph mode: inside the graph)
+        // the slot's previous upload has executed once its event has
         const int slot = W.param_slot;
         W.param_slot = (slot + 1) % WavefrontBuffers::kParamSlots;
         WF_CHECK(hipEventSynchronize(W.param_ev[slot]));
         W.h_params[slot] = P;
         WF_CHECK(hipMemcpyAsync(W.d_params, &W.h_params[slot], sizeof(FrameParams), hipMemcpyHostToDevice, stream));
         WF_CHECK(hipEventRecord(W.param_ev[slot], stream));
-        Q.Pd = W.d_params;
     }
     const bool full = needs_full(P.U);
     const int maxExtra = (P.U.enableMotionAdaptiveSampling != 0) ? max(P.U.motionSamplingMaxExtraSamples, 0) : 0;
     size_t npix = (size_t)P.U.width * P.U.height;
-    static const bool host_ctl = env_int("RT_WF_HOST", 0) != 0 || getenv("RT_WF_DUMP") != nullptr;
-    // tail <= 1 (bulk rounds only, a test configuration) keeps the host loop: its round count is
-    // only bounded by maxBounces * (maxBounces + 1)
-    if (tl && !host_ctl && !wf_log() && Q.drain_min == 0 && Q.tail > 1)
+    if (dev)
         return enqueue_wavefront(S, P, Q, count, full, maxExtra, extra_pass, stream, *tl, err);
     Q.dev_ctl = 0;
     Q.finish_q = 0;
