@@ -54,6 +54,7 @@ def parse():
     p.add_argument("--tile", type=int, default=64)
     p.add_argument("--pipeline", default="wavefront", choices=["wavefront", "megakernel"])
     p.add_argument("--sort-bins", type=int, default=0, help="hit-sort bins (0 = library default, -1 = no sort)")
+    p.add_argument("--bvh", default="sah", choices=["sah", "lbvh"], help="host binned-SAH or on-device LBVH build")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample time")
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--traffic-csv", default=None, help="rocprofv3 --pmc counter_collection.csv for traffic")
@@ -76,7 +77,8 @@ def main():
 
     scene = rt.Scene.preset(a.scene)
     t0 = time.time()
-    R = rt.Renderer(scene, a.width, a.height, device=local, pipeline=a.pipeline, seed=3, sort_bins=a.sort_bins)
+    R = rt.Renderer(scene, a.width, a.height, device=local, pipeline=a.pipeline, seed=3, sort_bins=a.sort_bins,
+                   bvh=a.bvh)
     setup_s = time.time() - t0
     R.samplesPerPixel = a.spp
     R.maxBounces = a.bounces
@@ -235,7 +237,7 @@ def main():
             "rays_per_frame": int(rays / a.steps), "kernel_ms_per_frame": round(kms, 3),
             "setup_s": round(setup_s, 2),
             # [generate, extend, shade, connect, resolve, finish, hit sort]
-            "stage_ms": [round(x / a.steps, 3) for x in stage_ms[:7]], "sort_bins": a.sort_bins,
+            "stage_ms": [round(x / a.steps, 3) for x in stage_ms[:7]], "sort_bins": a.sort_bins, "bvh": a.bvh,
             "pipeline_used": ["megakernel", "wavefront"][last_st.pipeline], "iterations": last_st.iterations,
         },
         "roofline": {

@@ -12,6 +12,8 @@
  *                              SubMesh.swift:38-54, Scene.swift:93)
  *   rt_bvh_build               createMTL4AccelerationStructures BLAS+TLAS build
  *                              (Renderer.swift:464-606, Utilities.swift:101-290)
+ *   rt_bvh_build_device        the same build on the GPU (LBVH + 8-wide collapse); also the
+ *                              legacy full rebuild of a deformed scene (Renderer.swift:1252-1277)
  *   rt_set_instance_transforms updateInstanceDescriptors (Renderer.swift:937-973): current ->
  *                              previous copy, then new transforms
  *   rt_skin                    SkinningPass.dispatchSkinning + prev-position copy
@@ -146,6 +148,12 @@ rt_status rt_set_stream(rt_ctx* ctx, void* hip_stream);  /* NULL restores the ow
 
 rt_status rt_scene_upload(rt_ctx* ctx, const rt_scene_desc* scene);
 rt_status rt_bvh_build(rt_ctx* ctx);
+/* On-device build from the uploaded (and possibly skinned / re-transformed) geometry: Morton
+ * sort + radix tree + top-down collapse into the same 8-wide layout.  Milliseconds instead of the
+ * host SAH build's seconds; traversal visits more nodes per ray (LBVH quality).  Images are
+ * identical to those of a host-built tree (conservative boxes).  Fails with
+ * RT_ERR_UNSUPPORTED when the tree is deeper than the traversal stack. */
+rt_status rt_bvh_build_device(rt_ctx* ctx);
 rt_status rt_bvh_refit(rt_ctx* ctx);
 rt_status rt_set_instance_transforms(rt_ctx* ctx, const rt_packed_float4x3* transforms, uint32_t count);
 /* Linear-blend skinning of one skinned mesh (Skinning.metal:7-49). `joint_matrices` are

@@ -213,7 +213,7 @@ class Renderer:
     """
 
     def __init__(self, scene, width, height, device=0, pipeline="wavefront", seed=1, stream=None, tail_paths=0,
-                 sort_bins=0):
+                 sort_bins=0, bvh="sah"):
         object.__setattr__(self, "_ctx", None)
         self.scene = scene
         self.width, self.height = int(width), int(height)
@@ -230,7 +230,8 @@ class Renderer:
         d = scene.desc()
         self.light_count = int(d.light_count)
         _check(lib().rt_scene_upload(ctx, C.byref(d)), ctx)
-        _check(lib().rt_bvh_build(ctx), ctx)
+        self.bvh_builder = bvh   # "sah": host binned-SAH build; "lbvh": on-device build
+        _check((lib().rt_bvh_build_device if bvh == "lbvh" else lib().rt_bvh_build)(ctx), ctx)
         self.random = random_offsets(seed, self.width, self.height)
         _check(lib().rt_resize(ctx, self.width, self.height, self.random.ctypes.data_as(C.POINTER(C.c_uint32))), ctx)
         self.camera = camera_default(self.width, self.height)
@@ -310,8 +311,11 @@ class Renderer:
     def refit(self):
         _check(lib().rt_bvh_refit(self._ctx), self._ctx)
 
-    def rebuild(self):
-        _check(lib().rt_bvh_build(self._ctx), self._ctx)
+    def rebuild(self, device=None):
+        """Full BVH rebuild from the current geometry (Renderer.swift:1252-1277); on the GPU when
+        device is True (default: the builder this renderer was created with)."""
+        dev = (self.bvh_builder == "lbvh") if device is None else device
+        _check((lib().rt_bvh_build_device if dev else lib().rt_bvh_build)(self._ctx), self._ctx)
 
     def tile_count(self, tile_size, rank, nranks):
         ts = TileSet(tile_size, rank, nranks, 0)

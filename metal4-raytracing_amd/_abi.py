@@ -181,7 +181,7 @@ RT_PIPELINE_WAVEFRONT = 1
 EXPORTED_SYMBOLS = [
     # rt_api.h
     "rt_create", "rt_destroy", "rt_last_error", "rt_set_stream", "rt_scene_upload", "rt_bvh_build",
-    "rt_bvh_refit", "rt_set_instance_transforms", "rt_skin", "rt_resize", "rt_render_frame", "rt_wait",
+    "rt_bvh_build_device", "rt_bvh_refit", "rt_set_instance_transforms", "rt_skin", "rt_resize", "rt_render_frame", "rt_wait",
     "rt_read_radiance", "rt_read_aux", "rt_tile_count", "rt_pack_tiles", "rt_unpack_tiles",
     "rt_pack_tiles_host", "rt_unpack_tiles_host",
     "rt_set_counting", "rt_get_stats", "rt_version", "rt_debug_trace_host",
@@ -205,6 +205,7 @@ def declare(lib):
         "rt_set_stream": (st, [vp, vp]),
         "rt_scene_upload": (st, [vp, P(SceneDesc)]),
         "rt_bvh_build": (st, [vp]),
+        "rt_bvh_build_device": (st, [vp]),
         "rt_bvh_refit": (st, [vp]),
         "rt_set_instance_transforms": (st, [vp, P(PackedFloat4x3), C.c_uint32]),
         "rt_skin": (st, [vp, C.c_uint32, P(C.c_float), C.c_uint32]),

@@ -64,7 +64,9 @@ struct rt_ctx {
     // device buffers
     DevBuf d_pos, d_prev_pos, d_nrm, d_rest_pos, d_rest_nrm, d_jidx, d_jw, d_joints;
     DevBuf d_tri_info, d_inst, d_prev_inst, d_mat, d_lights, d_halton;
-    DevBuf d_tris, d_nodes, d_node_box, d_slot_to_tri, d_levels, d_maxabs, d_tri_bin;
+    DevBuf d_tris, d_nodes, d_node_box, d_slot_to_tri, d_levels, d_maxabs, d_tri_bin, d_lbvh_scratch;
+    uint32_t num_nodes8 = 0;
+    uint32_t* h_lbvh = nullptr;   // pinned word for the device builder's level counts
     DevBuf d_random, d_accum[2], d_depth, d_motion, d_gbuffer, d_counters;
     int width = 0, height = 0;
     int read_idx = 0;   // accum[read_idx] = history (TextureIndexAccumulation)
@@ -169,7 +171,8 @@ static size_t ctx_bytes(const rt_ctx* c) {
                            &c->d_accum[0], &c->d_accum[1], &c->d_depth, &c->d_motion, &c->d_gbuffer, &c->d_counters,
                            &c->d_wf_color, &c->d_wf_accum, &c->d_wf_meta, &c->d_wf_q0, &c->d_wf_q1, &c->d_wf_hits,
                            &c->d_wf_sq, &c->d_wf_counts, &c->d_wf_mprev, &c->d_wf_extra,
-                           &c->d_wf_sorted, &c->d_wf_sort_table, &c->d_wf_sort_total, &c->d_tri_bin, &c->d_wf_params};
+                           &c->d_wf_sorted, &c->d_wf_sort_table, &c->d_wf_sort_total, &c->d_tri_bin, &c->d_wf_params,
+                           &c->d_lbvh_scratch};
     size_t s = 0;
     for (auto* b : all) s += b->bytes;
     return s;
@@ -298,8 +301,10 @@ rt_status rt_destroy(rt_ctx* c) {
                      &c->d_accum[1], &c->d_depth, &c->d_motion, &c->d_gbuffer, &c->d_counters,
                      &c->d_wf_color, &c->d_wf_accum, &c->d_wf_meta, &c->d_wf_q0, &c->d_wf_q1, &c->d_wf_hits,
                      &c->d_wf_sq, &c->d_wf_counts, &c->d_wf_mprev, &c->d_wf_extra,
-                     &c->d_wf_sorted, &c->d_wf_sort_table, &c->d_wf_sort_total, &c->d_tri_bin, &c->d_wf_params};
+                     &c->d_wf_sorted, &c->d_wf_sort_table, &c->d_wf_sort_total, &c->d_tri_bin, &c->d_wf_params,
+                     &c->d_lbvh_scratch};
     for (auto* b : all) dev_free(*b);
+    if (c->h_lbvh) hipHostFree(c->h_lbvh);
     if (c->h_counters) hipHostFree(c->h_counters);
     if (c->wf.h_counts) hipHostFree(c->wf.h_counts);
     for (auto& e : c->wf.ev)
@@ -493,6 +498,48 @@ rt_status rt_bvh_build(rt_ctx* c) {
     for (uint32_t k = 0; k < n; ++k) tri_bin[c->bvh8.tri_order[k]] = (uint16_t)(((uint64_t)k * kSortMaxBins) / n);
     if ((st = dev_upload(c, c->d_tri_bin, tri_bin.data(), (size_t)n * 2))) return st;
     HIPC(c, hipStreamSynchronize(c->stream));
+    c->num_nodes8 = (uint32_t)nn;
+    c->bvh_ready = true;
+    return RT_OK;
+}
+
+rt_status rt_bvh_build_device(rt_ctx* c) {
+    if (!c) FAIL(c, RT_ERR_INVALID_ARG, "null ctx");
+    if (!c->scene_ready) FAIL(c, RT_ERR_STATE, "rt_bvh_build_device before rt_scene_upload");
+    if (c->num_tris < 2) return rt_bvh_build(c);   // nothing to sort: the host path is exact and instant
+    HIPC(c, hipSetDevice(c->device));
+    const uint32_t n = c->num_tris;
+    rt_status st;
+    if ((st = dev_alloc(c, c->d_lbvh_scratch, lbvh_scratch_bytes(n)))) return st;
+    if ((st = dev_alloc(c, c->d_nodes, (size_t)n * sizeof(Bvh8Node)))) return st;
+    if ((st = dev_alloc(c, c->d_node_box, (size_t)n * 6 * sizeof(float)))) return st;
+    if ((st = dev_alloc(c, c->d_slot_to_tri, (size_t)n * 4))) return st;
+    if ((st = dev_alloc(c, c->d_tri_bin, (size_t)n * 2))) return st;
+    if ((st = dev_alloc(c, c->d_levels, (size_t)n * 4))) return st;
+    if ((st = dev_alloc(c, c->d_tris, (size_t)n * 48))) return st;
+    if ((st = dev_alloc(c, c->d_maxabs, 4))) return st;
+    if (!c->h_lbvh) HIPC(c, hipHostMalloc((void**)&c->h_lbvh, 16, 0));
+    LbvhInput in{(const float4*)c->d_pos.p, (const uint4*)c->d_tri_info.p, (const float*)c->d_inst.p, n};
+    LbvhOutput out{(Bvh8Node*)c->d_nodes.p, (float*)c->d_node_box.p, (uint32_t*)c->d_slot_to_tri.p,
+                   (uint16_t*)c->d_tri_bin.p, (uint32_t*)c->d_levels.p, c->h_lbvh};
+    LbvhResult res;
+    const char* err = nullptr;
+    if (!lbvh_build(in, out, c->d_lbvh_scratch.p, c->stream, &res, &err)) {
+        c->bvh_ready = false;
+        FAIL(c, RT_ERR_UNSUPPORTED, std::string("device BVH build: ") + (err ? err : "?"));
+    }
+    // world-space triangles in the new slot order
+    HIPC(c, hipMemsetAsync(c->d_maxabs.p, 0, 4, c->stream));
+    launch_flatten((const uint4*)c->d_tri_info.p, (const uint32_t*)c->d_slot_to_tri.p, (const float4*)c->d_pos.p,
+                   (const float*)c->d_inst.p, (float4*)c->d_tris.p, n, (unsigned*)c->d_maxabs.p, c->stream);
+    HIPC(c, hipGetLastError());
+    HIPC(c, hipStreamSynchronize(c->stream));
+    if (res.num_nodes >= (1u << 23)) FAIL(c, RT_ERR_UNSUPPORTED, "BVH too large (2^23 nodes)");
+    c->level_off = res.level_off;
+    c->bvh8 = Bvh8Result();            // the host copy describes the host builder's trees only
+    c->bvh8.pad = res.pad;
+    c->bvh8.max_depth = res.max_depth;
+    c->num_nodes8 = res.num_nodes;
     c->bvh_ready = true;
     return RT_OK;
 }
@@ -629,7 +676,7 @@ rt_status rt_render_frame(rt_ctx* c, const Uniforms* U, const rt_tile_set* tiles
     S.max_submeshes = c->max_sub;
     S.num_materials = (int)c->h_mat.size();
     S.num_tris = (int)c->num_tris;
-    S.num_nodes8 = (int)c->bvh8.nodes.size();
+    S.num_nodes8 = (int)c->num_nodes8;
     FrameParams P;
     P.U = *U;
     P.random = (const uint32_t*)c->d_random.p;
@@ -819,7 +866,7 @@ rt_status rt_get_stats(rt_ctx* c, rt_stats* out) {
     if (!c || !out) FAIL(c, RT_ERR_INVALID_ARG, "null argument");
     rt_status st = rt_wait(c);
     if (st) return st;
-    c->stats.bvh_nodes = c->bvh8.nodes.size();
+    c->stats.bvh_nodes = c->num_nodes8;
     c->stats.triangles = c->num_tris;
     c->stats.device_bytes = ctx_bytes(c);
     *out = c->stats;

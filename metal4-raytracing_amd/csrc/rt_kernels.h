@@ -175,6 +175,33 @@ __host__ __device__ __forceinline__ void tile_pixel(size_t i, int tile, int rank
     y = (tid / tiles_x) * tile + r / tile;
 }
 
+// On-device BVH build (rt_lbvh.hip): LBVH over Morton codes collapsed into the compressed 8-wide
+// layout of rt_bvh.h.  Inputs are the uploaded scene streams; outputs are caller-allocated device
+// arrays sized for n triangles (nodes8 / node_box / levels: n entries, tri_order n, tri_bin n).
+struct LbvhInput {
+    const float4* pos;
+    const uint4* tri_info;
+    const float* inst;
+    uint32_t n;
+};
+struct LbvhOutput {
+    Bvh8Node* nodes8;
+    float* node_box;        // 6 floats per node (padded lo, hi)
+    uint32_t* tri_order;    // 8-wide triangle slot -> original triangle id
+    uint16_t* tri_bin;      // hit-sort bin per original triangle
+    uint32_t* levels;       // refit level list (the identity: nodes are allocated level by level)
+    uint32_t* h_scratch;    // 1 pinned host word
+};
+struct LbvhResult {
+    std::vector<uint32_t> level_off;   // level k = nodes [level_off[k], level_off[k + 1])
+    uint32_t num_nodes = 0;
+    int max_depth = 0;
+    float pad = 0.0f;
+};
+size_t lbvh_scratch_bytes(uint32_t n);
+bool lbvh_build(const LbvhInput& in, const LbvhOutput& out, void* scratch, hipStream_t s, LbvhResult* res,
+                const char** err);
+
 // Utility kernels (rt_util.hip)
 void launch_pack_tiles(const float4* src, float4* dst, int width, int height, int tile, int rank, int nranks,
                        int tiles_x, int own, hipStream_t s);

@@ -61,10 +61,11 @@ def _check_frame(R, o):
 
 
 @pytest.mark.parametrize("pipeline", PIPELINES)
-@pytest.mark.parametrize("rebuild", [False, True])
+@pytest.mark.parametrize("rebuild", ["refit", "host", "device"])
 def test_skinning_refit_parity(rt, orc, assets, pipeline, rebuild):
-    """C5: skin the robot stand-in at t = 0.35 s, refit (or rebuild) the BVH, render; oracle on the
-    host-skinned mesh with prevPositions = rest pose."""
+    """C5: skin the robot stand-in at t = 0.35 s, refit the BVH or rebuild it (host SAH build, or
+    the on-device LBVH build), render; oracle on the host-skinned mesh with prevPositions = rest
+    pose."""
     W, H = 96, 64
     sc = rt.Scene.preset("c5", assets)
     desc = sc.desc()
@@ -79,7 +80,7 @@ def test_skinning_refit_parity(rt, orc, assets, pipeline, rebuild):
     R.samplesPerPixel = 2
     R.maxBounces = 2
     R.skin(m, J)
-    R.rebuild() if rebuild else R.refit()
+    R.refit() if rebuild == "refit" else R.rebuild(device=rebuild == "device")
     u = R.draw()
     R.wait()
     sp, sn = orc.skin(rest_p, rest_n, ji, jw, J)
