@@ -581,6 +581,12 @@ bool lbvh_build(const LbvhInput& in, const LbvhOutput& out, void* scratch, hipSt
         *err = "lbvh: collapse capacity guard tripped";
         return false;
     }
+    LB_CHECK(hipMemcpyAsync(h_next, misc + 9, 4, hipMemcpyDeviceToHost, s));   // triangle slots filled
+    LB_CHECK(hipStreamSynchronize(s));
+    if (*h_next != n) {
+        *err = "lbvh: leaves do not cover every triangle once";
+        return false;
+    }
     LB_CHECK(hipMemcpyAsync(h_next, misc + 6, 4, hipMemcpyDeviceToHost, s));
     lbvh_tri_bin_k<<<blocks(n), kThreads, 0, s>>>(out.tri_order, n, out.tri_bin);
     lbvh_iota_k<<<blocks(total), kThreads, 0, s>>>(out.levels, total);
