@@ -76,7 +76,7 @@ struct rt_ctx {
     // wavefront pipeline state
     WavefrontBuffers wf;
     DevBuf d_wf_color, d_wf_accum, d_wf_meta, d_wf_q0, d_wf_q1, d_wf_hits, d_wf_sq, d_wf_counts, d_wf_mprev, d_wf_extra;
-    DevBuf d_wf_sorted, d_wf_sort_table, d_wf_sort_total, d_wf_params;
+    DevBuf d_wf_sorted, d_wf_sort_table, d_wf_sort_total, d_wf_params, d_wf_pray, d_wf_psray;
     WfFrameStats wfs{};
     WfTimeline wft;
     bool last_wavefront = false;
@@ -172,7 +172,7 @@ static size_t ctx_bytes(const rt_ctx* c) {
                            &c->d_wf_color, &c->d_wf_accum, &c->d_wf_meta, &c->d_wf_q0, &c->d_wf_q1, &c->d_wf_hits,
                            &c->d_wf_sq, &c->d_wf_counts, &c->d_wf_mprev, &c->d_wf_extra,
                            &c->d_wf_sorted, &c->d_wf_sort_table, &c->d_wf_sort_total, &c->d_tri_bin, &c->d_wf_params,
-                           &c->d_lbvh_scratch};
+                           &c->d_lbvh_scratch, &c->d_wf_pray, &c->d_wf_psray};
     size_t s = 0;
     for (auto* b : all) s += b->bytes;
     return s;
@@ -189,13 +189,14 @@ static rt_status ensure_wavefront(rt_ctx* c, size_t own_px, int spp, int max_ext
         if ((st = dev_alloc(c, c->d_wf_color, paths * 16))) return st;
         if ((st = dev_alloc(c, c->d_wf_accum, paths * 16))) return st;
         if ((st = dev_alloc(c, c->d_wf_meta, paths * 16))) return st;
+        if ((st = dev_alloc(c, c->d_wf_pray, paths * 32))) return st;
+        if ((st = dev_alloc(c, c->d_wf_psray, paths * 48))) return st;
         if ((st = dev_alloc(c, c->d_wf_q0, qe * 32))) return st;
         if ((st = dev_alloc(c, c->d_wf_q1, qe * 32))) return st;
         if ((st = dev_alloc(c, c->d_wf_hits, qe * 16))) return st;
         if ((st = dev_alloc(c, c->d_wf_sq, qe * 48))) return st;
-        if (c->sort_bins) {
-            if ((st = dev_alloc(c, c->d_wf_sorted, qe * 48))) return st;
-        }
+        // hit sort output (3 float4 per hit) / finish input in priority order (2 per ray)
+        if ((st = dev_alloc(c, c->d_wf_sorted, qe * 48))) return st;
         W.cap_paths = paths;
         W.queue_entries = qe;
     }
@@ -222,6 +223,8 @@ static rt_status ensure_wavefront(rt_ctx* c, size_t own_px, int spp, int max_ext
     W.p_color = (float4*)c->d_wf_color.p;
     W.p_accum = (float4*)c->d_wf_accum.p;
     W.p_meta = (uint4*)c->d_wf_meta.p;
+    W.p_ray = (float4*)c->d_wf_pray.p;
+    W.p_sray = (float4*)c->d_wf_psray.p;
     W.q[0] = (float4*)c->d_wf_q0.p;
     W.q[1] = (float4*)c->d_wf_q1.p;
     W.hits = (float4*)c->d_wf_hits.p;
@@ -302,7 +305,7 @@ rt_status rt_destroy(rt_ctx* c) {
                      &c->d_wf_color, &c->d_wf_accum, &c->d_wf_meta, &c->d_wf_q0, &c->d_wf_q1, &c->d_wf_hits,
                      &c->d_wf_sq, &c->d_wf_counts, &c->d_wf_mprev, &c->d_wf_extra,
                      &c->d_wf_sorted, &c->d_wf_sort_table, &c->d_wf_sort_total, &c->d_tri_bin, &c->d_wf_params,
-                     &c->d_lbvh_scratch};
+                     &c->d_lbvh_scratch, &c->d_wf_pray, &c->d_wf_psray};
     for (auto* b : all) dev_free(*b);
     if (c->h_lbvh) hipHostFree(c->h_lbvh);
     if (c->h_counters) hipHostFree(c->h_counters);

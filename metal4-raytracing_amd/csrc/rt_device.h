@@ -114,6 +114,7 @@ __host__ __device__ __forceinline__ NodeWords load_node8(const Bvh8Node* nodes, 
     return w;
 }
 
+template <bool PK = false>
 __host__ __device__ __forceinline__ void test_node8_words(const NodeWords& W, const RaySetup& R, float tmin, float tmax,
                                                           uint32_t& ihits, uint32_t& tmask, uint32_t& child_base,
                                                           uint32_t& tri_base, bool& flip) {
@@ -137,21 +138,47 @@ __host__ __device__ __forceinline__ void test_node8_words(const NodeWords& W, co
     const uint32_t fz0 = R.iz >= 0.0f ? qz.z : qz.x, fz1 = R.iz >= 0.0f ? qz.w : qz.y;
     const float tf_max = tmax * 1.0000004f;
     uint32_t ih = 0, tm = 0;
-    #pragma unroll
-    for (int c = 0; c < 8; ++c) {
-        const int b = c & 3;
-        const uint32_t wnx = c < 4 ? nx0 : nx1, wfx = c < 4 ? fx0 : fx1;
-        const uint32_t wny = c < 4 ? ny0 : ny1, wfy = c < 4 ? fy0 : fy1;
-        const uint32_t wnz = c < 4 ? nz0 : nz1, wfz = c < 4 ? fz0 : fz1;
-        const float tnx = __builtin_fmaf(byte_f(wnx, b), ax, bx), tfx = __builtin_fmaf(byte_f(wfx, b), ax, bx);
-        const float tny = __builtin_fmaf(byte_f(wny, b), ay, by), tfy = __builtin_fmaf(byte_f(wfy, b), ay, by);
-        const float tnz = __builtin_fmaf(byte_f(wnz, b), az, bz), tfz = __builtin_fmaf(byte_f(wfz, b), az, bz);
-        const float tn = fmaxf(fmaxf(tnx, tny), fmaxf(tnz, tmin));
-        const float tf = fminf(fminf(tfx, tfy), fminf(tfz, tf_max));
-        if (tn <= tf) {
-            const uint32_t m = ((c < 4 ? h1.z : h1.w) >> (8 * b)) & 0xffu;
-            if (m & 0x80u) ih |= 1u << (m & 7u);
-            else tm |= ((1u << ((m >> 5) + 1u)) - 1u) << (m & 31u);
+    if (PK) {
+        // children c and c + 4 in one packed FMA per plane (v_pk_fma_f32): the byte words of a
+        // plane hold children 0..3 and 4..7.  Fewer VALU instructions, more register pairs.
+        typedef float f2v __attribute__((ext_vector_type(2)));
+        const f2v ax2 = {ax, ax}, ay2 = {ay, ay}, az2 = {az, az}, bx2 = {bx, bx}, by2 = {by, by}, bz2 = {bz, bz};
+        #pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            const f2v qnx = {byte_f(nx0, b), byte_f(nx1, b)}, qfx = {byte_f(fx0, b), byte_f(fx1, b)};
+            const f2v qny = {byte_f(ny0, b), byte_f(ny1, b)}, qfy = {byte_f(fy0, b), byte_f(fy1, b)};
+            const f2v qnz = {byte_f(nz0, b), byte_f(nz1, b)}, qfz = {byte_f(fz0, b), byte_f(fz1, b)};
+            const f2v tnx = __builtin_elementwise_fma(qnx, ax2, bx2), tfx = __builtin_elementwise_fma(qfx, ax2, bx2);
+            const f2v tny = __builtin_elementwise_fma(qny, ay2, by2), tfy = __builtin_elementwise_fma(qfy, ay2, by2);
+            const f2v tnz = __builtin_elementwise_fma(qnz, az2, bz2), tfz = __builtin_elementwise_fma(qfz, az2, bz2);
+            #pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const float tn = fmaxf(fmaxf(tnx[h], tny[h]), fmaxf(tnz[h], tmin));
+                const float tf = fminf(fminf(tfx[h], tfy[h]), fminf(tfz[h], tf_max));
+                if (tn <= tf) {
+                    const uint32_t m = ((h == 0 ? h1.z : h1.w) >> (8 * b)) & 0xffu;
+                    if (m & 0x80u) ih |= 1u << (m & 7u);
+                    else tm |= ((1u << ((m >> 5) + 1u)) - 1u) << (m & 31u);
+                }
+            }
+        }
+    } else {
+        #pragma unroll
+        for (int c = 0; c < 8; ++c) {
+            const int b = c & 3;
+            const uint32_t wnx = c < 4 ? nx0 : nx1, wfx = c < 4 ? fx0 : fx1;
+            const uint32_t wny = c < 4 ? ny0 : ny1, wfy = c < 4 ? fy0 : fy1;
+            const uint32_t wnz = c < 4 ? nz0 : nz1, wfz = c < 4 ? fz0 : fz1;
+            const float tnx = __builtin_fmaf(byte_f(wnx, b), ax, bx), tfx = __builtin_fmaf(byte_f(wfx, b), ax, bx);
+            const float tny = __builtin_fmaf(byte_f(wny, b), ay, by), tfy = __builtin_fmaf(byte_f(wfy, b), ay, by);
+            const float tnz = __builtin_fmaf(byte_f(wnz, b), az, bz), tfz = __builtin_fmaf(byte_f(wfz, b), az, bz);
+            const float tn = fmaxf(fmaxf(tnx, tny), fmaxf(tnz, tmin));
+            const float tf = fminf(fminf(tfx, tfy), fminf(tfz, tf_max));
+            if (tn <= tf) {
+                const uint32_t m = ((c < 4 ? h1.z : h1.w) >> (8 * b)) & 0xffu;
+                if (m & 0x80u) ih |= 1u << (m & 7u);
+                else tm |= ((1u << ((m >> 5) + 1u)) - 1u) << (m & 31u);
+            }
         }
     }
     ihits = ih;

@@ -80,11 +80,11 @@ constexpr int kShards = 8;        // queue segments (one allocation counter each
 // [32..39] / [40..47] per-XCD chunk counters of the extend / connect launches; each slot on a
 // 128-B line of its own (cslot), so the per-XCD shards never contend for one line's atomics.
 constexpr int kCntStride = 32;
-constexpr int kWfDiagHist = 48 * kCntStride;        // 64 words: wf_finish wave end-time histogram (50 us bins)
+constexpr int kWfDiagHist = 50 * kCntStride;        // 64 words: wf_finish wave end-time histogram (50 us bins)
 constexpr int kWfDiagSteps = kWfDiagHist + 64;        // 66 words: wf_trace steps-per-ray histograms + max
 constexpr int kWfStat = kWfDiagSteps + 66;              // 3 words: rounds, wf_trace launches, their rays
 constexpr int kStatRounds = 0, kStatTraceLaunches = 1, kStatTraceRays = 2, kStatExtendRays = 3, kStatFinish = 4;
-constexpr int kWfCountWords = 48 * kCntStride + 64 + 66 + 5;
+constexpr int kWfCountWords = 50 * kCntStride + 64 + 66 + 5;
 __host__ __device__ constexpr uint32_t cslot(int c) { return (uint32_t)c * kCntStride; }
 struct WavefrontBuffers {
     size_t queue_entries = 0;     // kShards segments of queue_entries / kShards
@@ -98,6 +98,10 @@ struct WavefrontBuffers {
     uint32_t* h_counts = nullptr; // pinned host mirror
     float2* motion_prev = nullptr;
     uint2* px_extra = nullptr;    // per own pixel: (first extra path - base_paths, count)
+    // wf_finish_q: per path, its next closest ray (o, d) and its shadow query (o; d, tmax;
+    // contribution, continues)
+    float4* p_ray = nullptr;
+    float4* p_sray = nullptr;
     // per-bounce hit sort (wf_sort_*): the hits reordered by key as {o, d, hit} float4 triples,
     // per-(bin, block) counts, per-bin totals
     float4* sorted = nullptr;

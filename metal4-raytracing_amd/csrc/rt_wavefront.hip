@@ -24,6 +24,10 @@
 // contribution, then step s+1), and samples are summed per pixel in sample order.
 #include "rt_shade.h"
 
+#ifndef RT_FINISH_PK
+#define RT_FINISH_PK 0   // packed variant measured slower (3.37 -> 3.5 ms finish)
+#endif
+
 #include <cstdio>
 #include <cstring>
 #include <vector>
@@ -33,6 +37,7 @@ namespace rt {
 namespace {
 
 constexpr uint32_t kTailRaysDefault = 4194304;
+constexpr bool kFinishPk = RT_FINISH_PK;   // packed-FMA node test in the finish kernels (build flag)
 static uint32_t tail_rays() {  // RT_TAIL_RAYS overrides (tuning experiments)
     static uint32_t v = [] { const char* e = getenv("RT_TAIL_RAYS"); return e ? (uint32_t)atol(e) : kTailRaysDefault; }();
     return v;
@@ -179,6 +184,8 @@ struct WfParams {
     int finish_step;       // tail: wf_finish_step (1) or the per-segment wf_finish (0)
     int shade_min;         // wf_finish_step: shade once this many lanes wait (or none traverses)
     int drain_min;         // wf_finish_step: hand paths back to the next round below this many busy lanes
+    int prio;              // finish input reordered by wf_prio (likely-long paths first) into W.sorted
+    int fchunk;            // wf_finish_step: paths per chunk grab
     int dev_ctl;           // device-side control (enqueue_wavefront): kernels read their queue sizes from
                            // the counters and skip once the live count fell below `tail`
     int finish_q;          // dev_ctl: the finish queue when every enqueued bulk round ran (written by generate)
@@ -195,6 +202,7 @@ constexpr int kCntDiagSegs = 27, kCntDiagIters = 28, kCntDiagTime = 29;   // wf_
 // dev_ctl: [30] tail mode (set by the first extend launch that found fewer than `tail` live
 // paths; later bulk launches of the pass return at once), [31] the queue the finish launch reads
 constexpr int kCntTailMode = 30, kCntFinishQ = 31;
+constexpr int kCntPrioHi = 48, kCntPrioLo = 49;   // wf_prio allocation counters (reset per launch)
 
 // dev_ctl statistics: rounds run, wf_trace launches run, rays they traced
 __device__ __forceinline__ void stat_add(const WfParams& Q, int word, uint32_t v) {
@@ -897,7 +905,7 @@ wf_finish_step(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int c
     if (Q.dev_ctl && n > 0) stat_add(Q, kStatRounds, 1u);
     const float4* qin = Q.W.q[cur];
     uint32_t* chunk_ctr = Q.W.counts + cslot(kCntChunkFinish);
-    constexpr uint32_t kChunk = 64;
+    const uint32_t kChunk = (uint32_t)Q.fchunk;   // paths per grab
     constexpr int kIdle = 0, kClosest = 1, kShadow = 2, kReady = 3;
     TraceCounters tc{0, 0};
     bool overflow = false;
@@ -966,8 +974,10 @@ wf_finish_step(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int c
             if (mode == kIdle) {
                 const uint32_t g = wnext + mbcnt64(idle);
                 if (g < wend) {
-                    const uint32_t e = entry_of(cnt, g, Q.seg_cap);
-                    const float4 o = qin[2 * (size_t)e], d = qin[2 * (size_t)e + 1];
+                    // Q.prio: the input was reordered (wf_prio: likely-long paths first) into a
+                    // flat array of {o, d} pairs
+                    const float4* src = Q.prio ? Q.W.sorted + 2 * (size_t)g : qin + 2 * (size_t)entry_of(cnt, g, Q.seg_cap);
+                    const float4 o = src[0], d = src[1];
                     pid = __float_as_uint(o.w);
                     meta = Q.W.p_meta[pid];
                     const float4 c = Q.W.p_color[pid], a = Q.W.p_accum[pid];
@@ -1090,7 +1100,7 @@ wf_finish_step(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int c
                 } else {
                     w = load_node8(S.nodes8, ni);
                 }
-                test_node8_words(w, R, 0.0f, best, g_hits, t_mask, g_base, t_base, g_flip);
+                test_node8_words<kFinishPk>(w, R, 0.0f, best, g_hits, t_mask, g_base, t_base, g_flip);
             }
             if (!tdone && !t_mask && !g_hits && sp == 0) tdone = true;
             if (tdone) {
@@ -1152,6 +1162,348 @@ wf_finish_step(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int c
             atomicMax(&Q.W.counts[cslot(kCntDiagIters)], iters);
             atomicMax(&Q.W.counts[cslot(kCntDiagTime)], dt);
             atomicAdd(&Q.W.counts[kWfDiagHist + min(dt / 5000u, 63u)], 1u);
+        }
+    }
+    flush_counters(P, n_closest, n_shadow, 0, tc, COUNT, overflow);
+}
+
+// ---- finish input order: likely-long paths first ---------------------------------------------------
+// The finish launch lasts as long as its longest remaining paths: ~20 segments of glass paths
+// whose queries run inside the dragon.  Handing those out first lets their serial chains run
+// while the rest of the work fills the machine around them.  A path that is inside (or passing
+// through) glass has transparencyPasses > 0 (:561-572).  Two-way partition of the queue into a
+// flat array: such paths from the front, the others from the back.
+__global__ void __launch_bounds__(kBlock) wf_prio(WfParams Q, int cur) {
+    __shared__ BlockAlloc ba_hi, ba_lo;
+    if (cur < 0) cur = (int)__builtin_amdgcn_readfirstlane(Q.W.counts[cslot(kCntFinishQ)]);
+    const ShardPrefix cnt = load_prefix(Q.W.counts + cslot(cur * kShards));
+    const uint32_t n = cnt.end[kShards - 1];
+    const float4* qin = Q.W.q[cur];
+    for (uint32_t base = blockIdx.x * kBlock; base < n; base += gridDim.x * kBlock) {
+        const uint32_t g = base + threadIdx.x;
+        float4 o = make_float4(0, 0, 0, 0), d = o;
+        bool hi = false, lo = false;
+        if (g < n) {
+            const uint32_t e = entry_of(cnt, g, Q.seg_cap);
+            o = qin[2 * (size_t)e];
+            d = qin[2 * (size_t)e + 1];
+            const uint32_t pid = __float_as_uint(o.w);
+            hi = ((Q.W.p_meta[pid].z >> 8) & 0xffu) != 0u;
+            lo = !hi;
+        }
+        const uint32_t a = block_alloc(hi, &Q.W.counts[cslot(kCntPrioHi)], ba_hi);
+        const uint32_t b = block_alloc(lo, &Q.W.counts[cslot(kCntPrioLo)], ba_lo);
+        if (hi || lo) {
+            const uint32_t slot = hi ? a : n - 1 - b;
+            Q.W.sorted[2 * (size_t)slot] = o;
+            Q.W.sorted[2 * (size_t)slot + 1] = d;
+        }
+    }
+}
+
+// ---- finish with wave-local queues -------------------------------------------------------------------
+// The step-interleaved finish kernel shades ready lanes at partial masks while the others idle or
+// traverse; its VALU lane utilisation is ~19 %.  Here a lane never waits to be shaded: a lane
+// whose closest-hit query found a hit pushes (path id, hit) onto its wave's hit queue in LDS and
+// takes new work at once.  Once 64 hits are queued (or nothing else is left to do) all 64 lanes
+// shade one queued hit each at full width, whatever their own traversal state, and push the
+// path's shadow ray or continuation onto the wave's ray queue (path id only; the ray itself goes
+// to per-path global slots).  Idle lanes refill from the ray queue first, then from the global
+// path queue.  Per-path order is the reference's: emission (shade), shadow contribution (its
+// query), then the next segment, so the image is bit-identical.
+struct TravState {
+    RaySetup R;
+    float best, bu, bv;
+    uint32_t best_id, g_base, g_hits, t_base, t_mask;
+    bool g_flip, hit_any;
+    int sp;
+};
+
+__device__ __forceinline__ void trav_start(TravState& T, f3 o, f3 d, float tmax) {
+    T.R = ray_setup(o, d);
+    T.best = tmax;
+    T.best_id = 0xffffffffu;
+    T.bu = T.bv = 0.0f;
+    T.g_base = 0;
+    T.g_hits = 1;   // virtual group holding the root
+    T.g_flip = false;
+    T.t_mask = 0;
+    T.sp = 0;
+    T.hit_any = false;
+}
+
+// one traversal step (one 8-wide node or up to two triangles); true once the query is finished
+template <bool COUNT>
+__device__ __forceinline__ bool trav_step(const DevScene& S, TravState& T, bool any, int* stack, const uint4* lds_top,
+                                          uint32_t n_top, TraceCounters& tc, bool& overflow) {
+    bool tdone = false;
+    if (T.t_mask) {
+        const int k0 = lowest_bit(T.t_mask);
+        T.t_mask &= T.t_mask - 1u;
+        const bool two = T.t_mask != 0u;
+        const int k1 = two ? lowest_bit(T.t_mask) : k0;
+        if (two) T.t_mask &= T.t_mask - 1u;
+        const float4* tp0 = S.tris + 3 * (size_t)(T.t_base + (uint32_t)k0);
+        const float4* tp1 = S.tris + 3 * (size_t)(T.t_base + (uint32_t)k1);
+        const float4 a0 = tp0[0], a1 = tp0[1], a2 = tp0[2];
+        const float4 b0 = tp1[0], b1 = tp1[1], b2 = tp1[2];
+        if (COUNT) tc.tris += two ? 2u : 1u;
+        float t, u, v;
+        if (intersect_triangle(T.R.pre, T.R.o, ld3(a0), ld3(a1), ld3(a2), 0.0f, T.best, &t, &u, &v)) {
+            const uint32_t id = __float_as_uint(a0.w);
+            if (any) {
+                T.hit_any = true;
+                tdone = true;
+            } else if (t < T.best || id < T.best_id) {
+                T.best = t;
+                T.best_id = id;
+                T.bu = u;
+                T.bv = v;
+            }
+        }
+        if (two && !tdone && intersect_triangle(T.R.pre, T.R.o, ld3(b0), ld3(b1), ld3(b2), 0.0f, T.best, &t, &u, &v)) {
+            const uint32_t id = __float_as_uint(b0.w);
+            if (any) {
+                T.hit_any = true;
+                tdone = true;
+            } else if (t < T.best || id < T.best_id) {
+                T.best = t;
+                T.best_id = id;
+                T.bu = u;
+                T.bv = v;
+            }
+        }
+    } else {
+        if (!T.g_hits) {   // sp > 0 here (checked at the end of the previous step)
+            --T.sp;
+            const uint32_t ent = (uint32_t)stack[T.sp * kBlock];
+            T.g_base = ent >> 9;
+            T.g_flip = (ent >> 8) & 1u;
+            T.g_hits = ent & 0xffu;
+        }
+        const int r = T.g_flip ? highest_bit(T.g_hits) : lowest_bit(T.g_hits);
+        T.g_hits &= ~(1u << r);
+        if (T.g_hits) {
+            if (T.sp < kStackSize) {
+                stack[T.sp * kBlock] = (int)pack_group(T.g_base, T.g_flip, T.g_hits);
+                ++T.sp;
+            } else {
+                overflow = true;
+            }
+        }
+        if (COUNT) tc.nodes++;
+        const uint32_t ni = T.g_base + (uint32_t)r;
+        NodeWords w;
+        if (ni < n_top) {
+            const uint4* l = lds_top + 5 * ni;
+            w.h0 = __builtin_bit_cast(float4, l[0]);
+            w.h1 = l[1];
+            w.qx = l[2];
+            w.qy = l[3];
+            w.qz = l[4];
+        } else {
+            w = load_node8(S.nodes8, ni);
+        }
+        test_node8_words<kFinishPk>(w, T.R, 0.0f, T.best, T.g_hits, T.t_mask, T.g_base, T.t_base, T.g_flip);
+    }
+    return tdone || (!T.t_mask && !T.g_hits && T.sp == 0);
+}
+
+constexpr int kWaveQ = 128;   // hit / ray queue entries per wave (LDS)
+
+template <bool COUNT, bool FULL>
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 4)))
+wf_finish_q(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int cur) {
+    const FrameParams& P = *Pp;   // per-frame parameters in device memory (graph replay)
+    if (cur < 0) cur = (int)__builtin_amdgcn_readfirstlane(Q.W.counts[cslot(kCntFinishQ)]);   // dev_ctl
+    __shared__ int lds_stack[kStackSize * kBlock];
+    __shared__ uint4 lds_top[kTopNodes * 5];
+    __shared__ HaltonDim lds_halton[kHaltonLds];
+    __shared__ MatRec lds_mat[kMatLds];
+    __shared__ float4 lds_hq_hit[kBlock / 64][kWaveQ];   // (t, triangle id bits, u, v)
+    __shared__ uint32_t lds_hq_pid[kBlock / 64][kWaveQ];
+    __shared__ uint32_t lds_rq[kBlock / 64][kWaveQ];     // path id | 0x80000000 for a shadow query
+    int* stack = &lds_stack[threadIdx.x];
+    const int wave = threadIdx.x >> 6;
+    const uint32_t lane = lane_id();
+    const uint32_t n_top = (uint32_t)min(S.num_nodes8, kTopNodes);
+    for (uint32_t i = threadIdx.x; i < n_top * 5; i += kBlock) lds_top[i] = reinterpret_cast<const uint4*>(S.nodes8)[i];
+    const ShadeTabs halton = load_tabs(S, lds_halton, lds_mat);   // ends with a block barrier
+    const Uniforms& U = P.U;
+    const ShardPrefix cnt = load_prefix(Q.W.counts + cslot(cur * kShards));
+    const uint32_t n = cnt.end[kShards - 1];
+    if (Q.dev_ctl) stat_add(Q, kStatFinish, 1u);
+    if (Q.dev_ctl && n > 0) stat_add(Q, kStatRounds, 1u);
+    const float4* qin = Q.W.q[cur];
+    float4* const p_ray = Q.W.p_ray;     // 2 per path: next closest ray (o, d)
+    float4* const p_sray = Q.W.p_sray;   // 3 per path: shadow ray (o; d, tmax; contribution, next)
+    uint32_t* chunk_ctr = Q.W.counts + cslot(kCntChunkFinish);
+    constexpr uint32_t kChunk = 64;
+    constexpr int kIdle = 0, kClosest = 1, kShadow = 2, kHit = 3;   // kHit: a hit waiting for queue space
+    TraceCounters tc{0, 0};
+    bool overflow = false;
+    uint32_t n_closest = 0, n_shadow = 0;
+    f2 zero2;
+    zero2.x = 0.0f;
+    zero2.y = 0.0f;
+    uint32_t wnext = 0, wend = 0, hq_n = 0, rq_n = 0;   // wave-uniform
+    bool exhausted = false;
+    int mode = kIdle;
+    uint32_t pid = 0;
+    TravState T;
+    trav_start(T, mk3(0, 0, 0), mk3(1, 0, 0), 0.0f);
+
+    while (true) {
+        // ---- refill idle lanes: queued shadow / continuation rays first, then new paths
+        unsigned long long idle = __ballot(mode == kIdle);
+        if (idle != 0ull && (__popcll(idle) >= Q.refill_min || idle == ~0ull || rq_n > 0)) {
+            const uint32_t take = min((uint32_t)__popcll(idle), rq_n);
+            if (take > 0) {
+                if (mode == kIdle) {
+                    const uint32_t k = mbcnt64(idle);
+                    if (k < take) {
+                        const uint32_t e = lds_rq[wave][rq_n - 1 - k];
+                        pid = e & 0x7fffffffu;
+                        if (e >> 31) {
+                            const float4 so = p_sray[3 * (size_t)pid], sd = p_sray[3 * (size_t)pid + 1];
+                            trav_start(T, ld3(so), ld3(sd), sd.w);
+                            mode = kShadow;
+                            n_shadow++;
+                        } else {
+                            const float4 o = p_ray[2 * (size_t)pid], d = p_ray[2 * (size_t)pid + 1];
+                            trav_start(T, ld3(o), ld3(d), INFINITY);
+                            mode = kClosest;
+                            n_closest++;
+                        }
+                    }
+                }
+                rq_n -= take;
+                idle = __ballot(mode == kIdle);
+            }
+            const bool refill = idle != 0ull && (__popcll(idle) >= Q.refill_min || idle == ~0ull);
+            if (wnext >= wend && !exhausted && refill) {
+                uint32_t base = 0;
+                if (lane == 0) base = atomicAdd(chunk_ctr, kChunk);
+                base = __builtin_amdgcn_readfirstlane(base);
+                if (base >= n) {
+                    exhausted = true;
+                } else {
+                    wnext = base;
+                    wend = min(base + kChunk, n);
+                }
+            }
+            if (refill && wnext < wend) {
+                if (mode == kIdle) {
+                    const uint32_t g = wnext + mbcnt64(idle);
+                    if (g < wend) {
+                        const uint32_t e = entry_of(cnt, g, Q.seg_cap);
+                        const float4 o = qin[2 * (size_t)e], d = qin[2 * (size_t)e + 1];
+                        pid = __float_as_uint(o.w);
+                        p_ray[2 * (size_t)pid] = o;   // the shading reads the segment's ray from here
+                        p_ray[2 * (size_t)pid + 1] = d;
+                        trav_start(T, ld3(o), ld3(d), INFINITY);
+                        mode = kClosest;
+                        n_closest++;
+                    }
+                }
+                wnext += (uint32_t)__popcll(idle);
+            }
+        }
+        const unsigned long long busy = __ballot(mode == kClosest || mode == kShadow);
+        if (busy == 0ull && hq_n == 0 && rq_n == 0 && __ballot(mode == kHit) == 0ull && exhausted && wnext >= wend)
+            break;
+
+        // ---- one traversal step
+        if (mode == kClosest || mode == kShadow) {
+            const bool any = mode == kShadow;
+            if (trav_step<COUNT>(S, T, any, stack, lds_top, n_top, tc, overflow)) {
+                if (any) {   // shadow query done: unoccluded -> add its contribution (:741-743)
+                    const float4 c = p_sray[3 * (size_t)pid + 2];
+                    if (!T.hit_any) {
+                        const float4 a = Q.W.p_accum[pid];
+                        Q.W.p_accum[pid] = make_float4(a.x + c.x, a.y + c.y, a.z + c.z, 0.0f);
+                    }
+                    if (c.w != 0.0f) {   // the path continues: its next ray was stored by the shading
+                        const float4 o = p_ray[2 * (size_t)pid], d = p_ray[2 * (size_t)pid + 1];
+                        trav_start(T, ld3(o), ld3(d), INFINITY);
+                        mode = kClosest;
+                        n_closest++;
+                    } else {
+                        mode = kIdle;
+                    }
+                } else {
+                    mode = T.best_id == 0xffffffffu ? kIdle : kHit;   // miss -> path ends (:321-322)
+                }
+            }
+        }
+
+        // ---- queue the hits (lanes that find no space keep theirs and retry)
+        {
+            const unsigned long long hm = __ballot(mode == kHit);
+            if (hm != 0ull) {
+                const uint32_t pos = hq_n + mbcnt64(hm);
+                if (mode == kHit && pos < (uint32_t)kWaveQ) {
+                    lds_hq_hit[wave][pos] = make_float4(T.best, __uint_as_float(T.best_id), T.bu, T.bv);
+                    lds_hq_pid[wave][pos] = pid;
+                    mode = kIdle;
+                }
+                hq_n = min(hq_n + (uint32_t)__popcll(hm), (uint32_t)kWaveQ);
+            }
+        }
+
+        // ---- shade 64 queued hits at full width (fewer once nothing else is left)
+        const bool starving = exhausted && wnext >= wend && rq_n == 0;
+        const uint32_t m = min(hq_n, 64u);
+        if (m > 0 && rq_n + m <= (uint32_t)kWaveQ &&
+            (m == 64u || __ballot(mode == kClosest || mode == kShadow) == 0ull ||
+             (starving && __popcll(__ballot(mode == kIdle)) >= Q.shade_min))) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");   // ray / path stores of this wave
+            uint32_t push = 0;   // this lane's ray-queue entry + 1 (0: none)
+            if (lane < m) {
+                const uint32_t slot = hq_n - m + lane;
+                const uint32_t spid = lds_hq_pid[wave][slot];
+                const float4 hv = lds_hq_hit[wave][slot];
+                Hit h;
+                h.t = hv.x;
+                h.id = __float_as_uint(hv.y);
+                h.u = hv.z;
+                h.v = hv.w;
+                const uint4 meta = Q.W.p_meta[spid];
+                const float4 pc = Q.W.p_color[spid], pa = Q.W.p_accum[spid];
+                const float4 o = p_ray[2 * (size_t)spid], d = p_ray[2 * (size_t)spid + 1];
+                PathRegs pr;
+                pr.color = mk3(pc.x, pc.y, pc.z);
+                pr.accum = mk3(pa.x, pa.y, pa.z);
+                pr.bounce = (int)(meta.z & 0xffu);
+                pr.tpass = (int)((meta.z >> 8) & 0xffu);
+                pr.step = (int)(meta.z >> 16);
+                f3 rayO = ld3(o), rayD = ld3(d);
+                const int sample = (int)meta.y;
+                StepResult r;
+                shade_step<FULL>(S, U, halton, (int)meta.w, sample, rayO, rayD, h, pr, sample == 0 && pr.step == 0,
+                                 zero2, false, zero2, r);
+                write_pixel_outputs(P, meta.x, r, FULL);
+                Q.W.p_accum[spid] = make_float4(pr.accum.x, pr.accum.y, pr.accum.z, 0.0f);
+                if (r.next) {
+                    Q.W.p_color[spid] = make_float4(pr.color.x, pr.color.y, pr.color.z, 0.0f);
+                    Q.W.p_meta[spid] = make_uint4(meta.x, meta.y, pack_state(pr.bounce, pr.tpass, pr.step), meta.w);
+                    p_ray[2 * (size_t)spid] = make_float4(rayO.x, rayO.y, rayO.z, 0.0f);
+                    p_ray[2 * (size_t)spid + 1] = make_float4(rayD.x, rayD.y, rayD.z, 0.0f);
+                }
+                if (r.shadow) {
+                    p_sray[3 * (size_t)spid] = make_float4(r.so.x, r.so.y, r.so.z, 0.0f);
+                    p_sray[3 * (size_t)spid + 1] = make_float4(r.sd.x, r.sd.y, r.sd.z, r.stmax);
+                    p_sray[3 * (size_t)spid + 2] = make_float4(r.contrib.x, r.contrib.y, r.contrib.z, r.next ? 1.0f : 0.0f);
+                    push = (spid | 0x80000000u) + 1u;
+                } else if (r.next) {
+                    push = spid + 1u;
+                }
+            }
+            hq_n -= m;
+            const unsigned long long pm = __ballot(push != 0u);
+            if (push != 0u) lds_rq[wave][rq_n + mbcnt64(pm)] = push - 1u;
+            rq_n += (uint32_t)__popcll(pm);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");   // before another lane loads them
         }
     }
     flush_counters(P, n_closest, n_shadow, 0, tc, COUNT, overflow);
@@ -1304,9 +1656,22 @@ static void launch_finish(const DevScene& S, const FrameParams& P, const WfParam
     }
 }
 
+template <bool COUNT, bool FULL>
+static void launch_finish_q(const WfParams& Q, const DevScene& S, int cur, uint32_t n, hipStream_t stream) {
+    static const unsigned cap = resident_grid(wf_finish_q<COUNT, FULL>, 2);
+    hipLaunchKernelGGL((wf_finish_q<COUNT, FULL>), dim3(grid_for(n, cap)), dim3(kBlock), 0, stream, S, Q.Pd, Q, cur);
+}
+
 static void launch_finish_any(const DevScene& S, const FrameParams& P, const WfParams& Q, bool count, bool full, int cur,
                               uint32_t n, hipStream_t stream) {
-    if (Q.finish_step) {
+    if (Q.prio) {
+        (void)hipMemsetAsync(Q.W.counts + cslot(kCntPrioHi), 0, cslot(2) * sizeof(uint32_t), stream);
+        hipLaunchKernelGGL(wf_prio, dim3(grid_for(n, 4096)), dim3(kBlock), 0, stream, Q, cur);
+    }
+    if (Q.finish_step == 2) {
+        if (count) full ? launch_finish_q<true, true>(Q, S, cur, n, stream) : launch_finish_q<true, false>(Q, S, cur, n, stream);
+        else full ? launch_finish_q<false, true>(Q, S, cur, n, stream) : launch_finish_q<false, false>(Q, S, cur, n, stream);
+    } else if (Q.finish_step) {
         if (count) full ? launch_finish<true, true, true>(S, P, Q, cur, n, stream)
                         : launch_finish<true, true, false>(S, P, Q, cur, n, stream);
         else full ? launch_finish<true, false, true>(S, P, Q, cur, n, stream)
@@ -1693,11 +2058,19 @@ bool run_wavefront(const DevScene& S, const FrameParams& P, WavefrontBuffers& W,
     Q.sort_xcd = sort_xcd;
     Q.steal = steal;
     Q.diag = wf_log() ? 1 : 0;
+    // tail kernel: 0 per-segment wf_finish, 1 step-interleaved wf_finish_step, 2 wave-queue wf_finish_q
     static const int finish_step = env_int("RT_FINISH_STEP", 1), shade_min = env_int("RT_SHADE_MIN", 16);
     Q.finish_step = finish_step;
     Q.shade_min = shade_min;
     static const int drain_min = env_int("RT_DRAIN", 0);   // measured slower on C3g: off
-    Q.drain_min = Q.finish_step ? drain_min : 0;
+    Q.drain_min = Q.finish_step == 1 ? drain_min : 0;
+    static const int prio = env_int("RT_PRIO", 0), fchunk = env_int("RT_FCHUNK", 64);
+    Q.fchunk = max(1, fchunk);
+    Q.prio = (prio && Q.finish_step == 1 && W.sorted) ? 1 : 0;
+    if (Q.finish_step == 2 && (!W.p_ray || !W.p_sray)) {
+        *err = "wave-queue finish kernel without its path ray slots";
+        return false;
+    }
     if (sort_bins && (sort_bins < kSortMinBins || sort_bins > kSortMaxBins || (sort_bins & (sort_bins - 1)) ||
                       !S.tri_bin || !W.sorted)) {
         *err = "bad hit-sort configuration";
