@@ -55,6 +55,8 @@ def parse():
     p.add_argument("--pipeline", default="wavefront", choices=["wavefront", "megakernel"])
     p.add_argument("--sort-bins", type=int, default=0, help="hit-sort bins (0 = library default, -1 = no sort)")
     p.add_argument("--bvh", default="sah", choices=["sah", "lbvh"], help="host binned-SAH or on-device LBVH build")
+    p.add_argument("--frames-in-flight", type=int, default=0,
+                   help="frames the renderer overlaps (0 = library default 2, 1 = one at a time)")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample time")
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--traffic-csv", default=None, help="rocprofv3 --pmc counter_collection.csv for traffic")
@@ -78,7 +80,7 @@ def main():
     scene = rt.Scene.preset(a.scene)
     t0 = time.time()
     R = rt.Renderer(scene, a.width, a.height, device=local, pipeline=a.pipeline, seed=3, sort_bins=a.sort_bins,
-                   bvh=a.bvh)
+                   bvh=a.bvh, frames_in_flight=a.frames_in_flight)
     setup_s = time.time() - t0
     R.samplesPerPixel = a.spp
     R.maxBounces = a.bounces
@@ -97,6 +99,14 @@ def main():
         if gather is not None:
             gather.gather()   # packed tiles -> rank 0 over RCCL, unpacked into its radiance target
         return st
+
+    def submit():
+        # one step: single GPU, the frame is only submitted (the renderer keeps two frames in
+        # flight and waits for a slot's previous frame itself); multi-GPU, rendered and gathered
+        if gather is None:
+            R.draw(tiles=tiles)
+        else:
+            frame()
 
     def barrier():
         if n > 1:
@@ -121,29 +131,29 @@ def main():
     R.samplesPerPixel = a.spp  # resets frameIndex (didSet)
 
     for _ in range(a.warmup):
-        frame()
+        submit()
+    R.wait()
+    s0 = R.stats()
     barrier()
     t0 = time.perf_counter()
-    rays = 0
-    kernel_ms = []
-    stage_ms = np.zeros(7)
-    closest = 0
-    trace_rays, trace_launches, trace_ms, trace_closest, finish_launches = 0, 0, 0.0, 0, 0
     for _ in range(a.steps):
-        st = frame()
-        rays += st.closest_rays + st.shadow_rays
-        closest += st.closest_rays
-        trace_rays += st.trace_rays
-        trace_launches += st.trace_launches
-        trace_ms += st.trace_ms
-        trace_closest += st.trace_closest_rays
-        finish_launches += st.finish_launches
-        kernel_ms.append(st.last_frame_ms)
-        stage_ms += np.array(list(st.kernel_ms))
-        last_st = st
+        submit()
+    R.wait()
     barrier()
     dt = time.perf_counter() - t0
+    # the running totals of every frame of the timed region (HIP events per stage on the
+    # renderer's streams, ray counters read back per frame)
+    last_st = s1 = R.stats()
+    assert s1.frames_total - s0.frames_total == a.steps
+    d = lambda f: getattr(s1, f) - getattr(s0, f)
+    closest = d("total_closest_rays")
+    rays = closest + d("total_shadow_rays")
+    trace_rays, trace_launches, trace_ms = d("total_trace_rays"), d("total_trace_launches"), d("total_trace_ms")
+    trace_closest, finish_launches = d("total_trace_closest_rays"), d("total_finish_launches")
+    stage_ms = np.array(list(s1.total_kernel_ms)) - np.array(list(s0.total_kernel_ms))
+    kernel_ms = [d("total_frame_ms") / a.steps]
 
+    rays_local, closest_local = rays, closest   # this rank's, for the per-kernel roofline
     tot = torch.tensor([dt, float(rays), float(closest), float(np.mean(kernel_ms))], dtype=torch.float64, device=dev)
     if n > 1:
         mx = tot.clone()
@@ -174,8 +184,8 @@ def main():
         # wf_finish_step: the tail paths to completion.  Per ray 48 B (ray + hit) + nodes + triangles
         # as above; per closest hit the shading gathers (B_HIT); the path state in and out (48 B x 2)
         # once per path is left out (not counted per ray).
-        f_rays = (rays - trace_rays) / finish_launches
-        f_closest = (closest - trace_closest) / finish_launches
+        f_rays = (rays_local - trace_rays) / finish_launches
+        f_closest = (closest_local - trace_closest) / finish_launches
         kernels.append(dict(
             kernel="rt::wf_finish_step<false, false, 4>", launches=finish_launches / a.steps,
             launch_ms=float(stage_ms[5]) / finish_launches, rays_per_launch=f_rays, nodes_per_ray=f_nodes_per_ray,
@@ -183,17 +193,22 @@ def main():
             bytes_per_launch=f_rays * (B_RAY + f_nodes_per_ray * B_NODE + f_tris_per_ray * B_TRI) + f_closest * B_HIT))
     if not kernels:
         # megakernel: the whole frame is one launch
-        rpl = rays / a.steps / n
+        rpl = rays_local / a.steps
         kernels.append(dict(
             kernel="rt::megakernel<false, false>", launches=1, launch_ms=kms, rays_per_launch=rpl,
             nodes_per_ray=nodes_per_ray, tris_per_ray=tris_per_ray,
             bytes_per_launch=(rpl * (B_RAY + nodes_per_ray * B_NODE + tris_per_ray * B_TRI)
-                              + closest / a.steps / n * B_HIT + a.width * a.height / n * B_PIXEL)))
+                              + closest_local / a.steps * B_HIT + a.width * a.height / n * B_PIXEL)))
     for k in kernels:
         k["achieved"] = k["bytes_per_launch"] / (k["launch_ms"] * 1e-3) / 1e9
         k["ms_per_frame"] = k["launch_ms"] * k["launches"]
     # the dominant kernel: the most device time per frame
     dom = max(kernels, key=lambda k: k["ms_per_frame"])
+    # the whole frame: every timed kernel's algorithmic bytes over the wall time per frame (with
+    # frames in flight the kernels of two frames share the GPU, so per-launch durations stretch
+    # while the aggregate rate rises)
+    job_bytes = sum(k["bytes_per_launch"] * k["launches"] for k in kernels)
+    job_achieved = job_bytes / (dt / a.steps) / 1e9   # per GPU (rank 0's kernels)
     kernel, launch_ms, bytes_per_launch = dom["kernel"], dom["launch_ms"], dom["bytes_per_launch"]
     rays_per_launch, npr, tpr, achieved = dom["rays_per_launch"], dom["nodes_per_ray"], dom["tris_per_ray"], dom["achieved"]
     traffic, traffic_src, l2_hit = None, None, None
@@ -231,7 +246,8 @@ def main():
                 "reference OBJ assets, seeded random offsets",
         "config": {
             "workload": f"{a.scene}: glass dragon scene (configs[2]) {a.width}x{a.height}x{a.spp}spp, {a.bounces} bounces, "
-                        f"one frame per step, {'tile-split ' + str(T) + 'px + RCCL gather' if n > 1 else 'single GPU'}",
+                        f"one frame per step, {'tile-split ' + str(T) + 'px + RCCL gather' if n > 1 else 'single GPU'}"
+                        f"{', frames submitted back to back (overlapping frames in flight)' if n == 1 else ''}",
             "scene": a.scene, "triangles": scene.triangle_count, "width": a.width, "height": a.height,
             "spp": a.spp, "max_bounces": a.bounces, "pipeline": a.pipeline, "parallelism": f"tiles{n}",
             "rays_per_frame": int(rays / a.steps), "kernel_ms_per_frame": round(kms, 3),
@@ -239,11 +255,14 @@ def main():
             # [generate, extend, shade, connect, resolve, finish, hit sort]
             "stage_ms": [round(x / a.steps, 3) for x in stage_ms[:7]], "sort_bins": a.sort_bins, "bvh": a.bvh,
             "pipeline_used": ["megakernel", "wavefront"][last_st.pipeline], "iterations": last_st.iterations,
+            "frames_in_flight": last_st.frames_in_flight,
         },
         "roofline": {
             "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": traffic_src,
             "l2_hit": l2_hit,
+            "job_achieved": round(job_achieved, 1), "job_frac": round(job_achieved / HBM_PEAK_GBS, 4),
+            "job_bytes_per_frame": int(job_bytes),
             "kernel": kernel, "launch_ms": round(launch_ms, 4), "bytes_per_launch": int(bytes_per_launch),
             "rays_per_launch": int(rays_per_launch), "nodes_per_ray": round(npr, 3), "tris_per_ray": round(tpr, 3),
             # every timed kernel of the frame with its own roofline, for comparison

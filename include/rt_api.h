@@ -102,7 +102,12 @@ typedef struct rt_opts {
     int32_t sort_bins;  /* wavefront: hits are sorted into this many bins of BVH leaf order between
                            extend and shade (a power of two in [1024, 4096]); 0 = default (no
                            sort), < 0 = no sort.  Never changes the image, only memory locality. */
-    int32_t reserved[4];
+    int32_t frames_in_flight; /* wavefront on the context's own stream: frames rendered concurrently,
+                                 each overlapping the previous one until it needs that frame's
+                                 accumulation / motion output; 0 = default (2), 1 = one at a time,
+                                 at most 3.
+                                 Images are identical either way. */
+    int32_t reserved[3];
 } rt_opts;
 
 /* Image-space tile partition for multi-GPU rendering: the image is cut into
@@ -138,7 +143,20 @@ typedef struct rt_stats {
     float trace_ms;         /* its summed device time (HIP events on the render stream) */
     uint64_t trace_closest_rays; /* the closest-hit (extend) share of trace_rays */
     int32_t finish_launches;     /* wavefront: persistent finish launches (their time: kernel_ms[5]) */
-    int32_t _pad;
+    int32_t frames_in_flight;    /* frames the last rt_render_frame could overlap (1..3) */
+    /* running totals over every finished frame since rt_create (frames submitted back to back
+       without rt_wait are each counted) */
+    uint64_t frames_total;
+    uint64_t total_closest_rays;
+    uint64_t total_shadow_rays;
+    uint64_t total_paths;
+    double total_frame_ms;         /* sum of last_frame_ms */
+    double total_kernel_ms[7];     /* sums of kernel_ms */
+    uint64_t total_trace_rays;     /* sums of trace_rays, trace_closest_rays, trace_ms, trace_launches, */
+    uint64_t total_trace_closest_rays;   /* finish_launches */
+    double total_trace_ms;
+    uint64_t total_trace_launches;
+    uint64_t total_finish_launches;
 } rt_stats;
 
 rt_status rt_create(const rt_opts* opts, rt_ctx** out);

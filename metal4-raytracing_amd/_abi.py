@@ -117,7 +117,7 @@ class SceneDesc(C.Structure):
 
 class Opts(C.Structure):
     _fields_ = [("device", C.c_int32), ("pipeline", C.c_int32), ("tail_paths", C.c_int32), ("sort_bins", C.c_int32),
-                ("reserved", C.c_int32 * 4)]
+                ("frames_in_flight", C.c_int32), ("reserved", C.c_int32 * 3)]
 
 
 class TileSet(C.Structure):
@@ -145,7 +145,18 @@ class Stats(C.Structure):
         ("trace_ms", C.c_float),
         ("trace_closest_rays", C.c_uint64),
         ("finish_launches", C.c_int32),
-        ("_pad", C.c_int32),
+        ("frames_in_flight", C.c_int32),
+        ("frames_total", C.c_uint64),
+        ("total_closest_rays", C.c_uint64),
+        ("total_shadow_rays", C.c_uint64),
+        ("total_paths", C.c_uint64),
+        ("total_frame_ms", C.c_double),
+        ("total_kernel_ms", C.c_double * 7),
+        ("total_trace_rays", C.c_uint64),
+        ("total_trace_closest_rays", C.c_uint64),
+        ("total_trace_ms", C.c_double),
+        ("total_trace_launches", C.c_uint64),
+        ("total_finish_launches", C.c_uint64),
     ]
 
 

@@ -29,6 +29,27 @@ struct MeshInfo {
     uint32_t vbase = 0, vcount = 0, joint_count = 0;
     bool skinned = false;
 };
+
+// One frame in flight (Renderer.swift:207, 1406-1409 keeps up to 3): its wavefront memory, its
+// per-frame targets and statistics, and the stream it renders on.  Consecutive frames rotate over
+// the slots and overlap except where frame f needs frame f-1's results (the history target and
+// the previous motion vectors: the extra-sample pass and the resolve).
+struct FrameSlot {
+    DevBuf color, accum, meta, q0, q1, hits, sq, counts, extra, sorted, sort_table, sort_total, params, pray, psray;
+    DevBuf depth, gbuffer, counters;
+    WavefrontBuffers wf;
+    WfTimeline wft;
+    WfFrameStats wfs{};
+    unsigned long long* h_counters = nullptr;   // pinned copy of `counters` after the frame
+    hipStream_t own_stream = nullptr;           // slots 1..; slot 0 renders on rt_ctx::stream
+    hipEvent_t ev0 = nullptr, ev1 = nullptr, done = nullptr;
+    bool pending = false, wavefront = false, used = false;
+    uint64_t seq = 0;                           // frame number (harvest order)
+    DevBuf* bufs[18] = {&color, &accum, &meta, &q0, &q1, &hits, &sq, &counts, &extra, &sorted,
+                        &sort_table, &sort_total, &params, &pray, &psray, &depth, &gbuffer, &counters};
+};
+constexpr int kMaxSlots = 3;
+constexpr int kMotionTargets = kMaxSlots + 1;
 }  // namespace
 
 struct rt_ctx {
@@ -37,10 +58,8 @@ struct rt_ctx {
     int tail_paths = 0;
     int sort_bins = kSortBinsDefault;   // 0 = no hit sort
     hipStream_t own_stream = nullptr, stream = nullptr;
-    hipEvent_t ev0 = nullptr, ev1 = nullptr;
     std::string err;
     bool counting = false;
-    bool frame_pending = false;
 
     // host scene copies
     std::vector<float4> h_pos, h_nrm;
@@ -67,19 +86,24 @@ struct rt_ctx {
     DevBuf d_tris, d_nodes, d_node_box, d_slot_to_tri, d_levels, d_maxabs, d_tri_bin, d_lbvh_scratch;
     uint32_t num_nodes8 = 0;
     uint32_t* h_lbvh = nullptr;   // pinned word for the device builder's level counts
-    DevBuf d_random, d_accum[2], d_depth, d_motion, d_gbuffer, d_counters;
+    DevBuf d_random, d_accum[2];
+    // Motion vectors rotate over kMaxSlots + 1 targets: a wavefront frame writes d_motion[m + 1]
+    // and reads the previous frame's d_motion[m], so it never overwrites a target an older frame
+    // still in flight reads (the megakernel reads and rewrites d_motion[m] in place).
+    DevBuf d_motion[kMotionTargets];
+    int motion_cur = 0;
     int width = 0, height = 0;
     int read_idx = 0;   // accum[read_idx] = history (TextureIndexAccumulation)
-    unsigned long long* h_counters = nullptr;  // pinned
     rt_stats stats{};
 
-    // wavefront pipeline state
-    WavefrontBuffers wf;
-    DevBuf d_wf_color, d_wf_accum, d_wf_meta, d_wf_q0, d_wf_q1, d_wf_hits, d_wf_sq, d_wf_counts, d_wf_mprev, d_wf_extra;
-    DevBuf d_wf_sorted, d_wf_sort_table, d_wf_sort_total, d_wf_params, d_wf_pray, d_wf_psray;
-    WfFrameStats wfs{};
-    WfTimeline wft;
-    bool last_wavefront = false;
+    // frames in flight
+    FrameSlot slot[kMaxSlots];
+    int max_in_flight = 2;           // rt_opts.frames_in_flight
+    int nslots = 1;                  // slots in use (1: megakernel, external stream)
+    uint64_t frame_no = 0;           // frames submitted since rt_resize
+    int last_slot = 0;               // slot of the newest frame
+    hipEvent_t scene_ev = nullptr;   // ctx->stream work a slot-1 frame must follow
+    rt_stats totals{};   // the running-total fields of rt_stats
 
     // motion bookkeeping for the extra-sample pass: motion vectors are exactly zero unless the
     // camera, an instance transform or skinned positions differ from their previous copies
@@ -168,73 +192,81 @@ static size_t ctx_bytes(const rt_ctx* c) {
     const DevBuf* all[] = {&c->d_pos, &c->d_prev_pos, &c->d_nrm, &c->d_rest_pos, &c->d_rest_nrm, &c->d_jidx, &c->d_jw,
                            &c->d_joints, &c->d_tri_info, &c->d_inst, &c->d_prev_inst, &c->d_mat, &c->d_lights,
                            &c->d_halton, &c->d_tris, &c->d_nodes, &c->d_node_box, &c->d_slot_to_tri, &c->d_levels, &c->d_maxabs, &c->d_random,
-                           &c->d_accum[0], &c->d_accum[1], &c->d_depth, &c->d_motion, &c->d_gbuffer, &c->d_counters,
-                           &c->d_wf_color, &c->d_wf_accum, &c->d_wf_meta, &c->d_wf_q0, &c->d_wf_q1, &c->d_wf_hits,
-                           &c->d_wf_sq, &c->d_wf_counts, &c->d_wf_mprev, &c->d_wf_extra,
-                           &c->d_wf_sorted, &c->d_wf_sort_table, &c->d_wf_sort_total, &c->d_tri_bin, &c->d_wf_params,
-                           &c->d_lbvh_scratch, &c->d_wf_pray, &c->d_wf_psray};
+                           &c->d_accum[0], &c->d_accum[1], &c->d_tri_bin, &c->d_lbvh_scratch,
+                           };
     size_t s = 0;
     for (auto* b : all) s += b->bytes;
+    for (const DevBuf& b : c->d_motion) s += b.bytes;
+    for (const FrameSlot& f : c->slot)
+        for (const DevBuf* b : f.bufs) s += b->bytes;
     return s;
 }
 
-static rt_status ensure_wavefront(rt_ctx* c, size_t own_px, int spp, int max_extra) {
-    WavefrontBuffers& W = c->wf;
+static rt_status ensure_wavefront(rt_ctx* c, FrameSlot& fs, size_t own_px, int spp, int max_extra) {
+    WavefrontBuffers& W = fs.wf;
     size_t paths = own_px * (size_t)(spp + max_extra);
     size_t npix = (size_t)c->width * c->height;
     if (paths >= (1ull << 32)) FAIL(c, RT_ERR_UNSUPPORTED, "too many paths for one frame");
     rt_status st;
     if (W.cap_paths < paths || W.queue_entries < wavefront_queue_entries(paths, max_extra)) {
         size_t qe = wavefront_queue_entries(paths, max_extra);
-        if ((st = dev_alloc(c, c->d_wf_color, paths * 16))) return st;
-        if ((st = dev_alloc(c, c->d_wf_accum, paths * 16))) return st;
-        if ((st = dev_alloc(c, c->d_wf_meta, paths * 16))) return st;
-        if ((st = dev_alloc(c, c->d_wf_pray, paths * 32))) return st;
-        if ((st = dev_alloc(c, c->d_wf_psray, paths * 48))) return st;
-        if ((st = dev_alloc(c, c->d_wf_q0, qe * 32))) return st;
-        if ((st = dev_alloc(c, c->d_wf_q1, qe * 32))) return st;
-        if ((st = dev_alloc(c, c->d_wf_hits, qe * 16))) return st;
-        if ((st = dev_alloc(c, c->d_wf_sq, qe * 48))) return st;
+        if ((st = dev_alloc(c, fs.color, paths * 16))) return st;
+        if ((st = dev_alloc(c, fs.accum, paths * 16))) return st;
+        if ((st = dev_alloc(c, fs.meta, paths * 16))) return st;
+        if ((st = dev_alloc(c, fs.pray, paths * 32))) return st;
+        if ((st = dev_alloc(c, fs.psray, paths * 48))) return st;
+        if ((st = dev_alloc(c, fs.q0, qe * 32))) return st;
+        if ((st = dev_alloc(c, fs.q1, qe * 32))) return st;
+        if ((st = dev_alloc(c, fs.hits, qe * 16))) return st;
+        if ((st = dev_alloc(c, fs.sq, qe * 48))) return st;
         // hit sort output (3 float4 per hit) / finish input in priority order (2 per ray)
-        if ((st = dev_alloc(c, c->d_wf_sorted, qe * 48))) return st;
+        if ((st = dev_alloc(c, fs.sorted, qe * 48))) return st;
         W.cap_paths = paths;
         W.queue_entries = qe;
     }
     if (W.cap_pixels < npix || W.cap_pixels < own_px) {
         size_t px = std::max(npix, own_px);
-        if ((st = dev_alloc(c, c->d_wf_mprev, px * 8))) return st;
-        if ((st = dev_alloc(c, c->d_wf_extra, px * 8))) return st;
+        if ((st = dev_alloc(c, fs.extra, px * 8))) return st;
         W.cap_pixels = px;
     }
-    if (c->sort_bins && !c->d_wf_sort_table.p) {
-        if ((st = dev_alloc(c, c->d_wf_sort_table, (size_t)kSortMaxBins * kSortBlocks * 4))) return st;
-        if ((st = dev_alloc(c, c->d_wf_sort_total, (size_t)kSortMaxBins * 4))) return st;
+    if (c->sort_bins && !fs.sort_table.p) {
+        if ((st = dev_alloc(c, fs.sort_table, (size_t)kSortMaxBins * kSortBlocks * 4))) return st;
+        if ((st = dev_alloc(c, fs.sort_total, (size_t)kSortMaxBins * 4))) return st;
     }
-    if (!c->d_wf_counts.p) {
-        if ((st = dev_alloc(c, c->d_wf_counts, kWfCountWords * 4))) return st;
+    if (!fs.counts.p) {
+        if ((st = dev_alloc(c, fs.counts, kWfCountWords * 4))) return st;
         HIPC(c, hipHostMalloc((void**)&W.h_counts, kWfCountWords * 4, 0));
         for (auto& e : W.ev) HIPC(c, hipEventCreate(&e));
-        for (auto& e : c->wft.ev) HIPC(c, hipEventCreate(&e));
+        for (auto& e : fs.wft.ev) HIPC(c, hipEventCreate(&e));
         for (auto& e : W.param_ev) HIPC(c, hipEventCreate(&e));
-        if ((st = dev_alloc(c, c->d_wf_params, sizeof(FrameParams)))) return st;
+        if ((st = dev_alloc(c, fs.params, sizeof(FrameParams)))) return st;
         HIPC(c, hipHostMalloc((void**)&W.h_params, sizeof(FrameParams) * WavefrontBuffers::kParamSlots, 0));
-        W.d_params = (FrameParams*)c->d_wf_params.p;
+        W.d_params = (FrameParams*)fs.params.p;
     }
-    W.p_color = (float4*)c->d_wf_color.p;
-    W.p_accum = (float4*)c->d_wf_accum.p;
-    W.p_meta = (uint4*)c->d_wf_meta.p;
-    W.p_ray = (float4*)c->d_wf_pray.p;
-    W.p_sray = (float4*)c->d_wf_psray.p;
-    W.q[0] = (float4*)c->d_wf_q0.p;
-    W.q[1] = (float4*)c->d_wf_q1.p;
-    W.hits = (float4*)c->d_wf_hits.p;
-    W.sq = (float4*)c->d_wf_sq.p;
-    W.counts = (uint32_t*)c->d_wf_counts.p;
-    W.motion_prev = (float2*)c->d_wf_mprev.p;
-    W.px_extra = (uint2*)c->d_wf_extra.p;
-    W.sorted = (float4*)c->d_wf_sorted.p;
-    W.sort_table = (uint32_t*)c->d_wf_sort_table.p;
-    W.sort_total = (uint32_t*)c->d_wf_sort_total.p;
+    W.p_color = (float4*)fs.color.p;
+    W.p_accum = (float4*)fs.accum.p;
+    W.p_meta = (uint4*)fs.meta.p;
+    W.p_ray = (float4*)fs.pray.p;
+    W.p_sray = (float4*)fs.psray.p;
+    W.q[0] = (float4*)fs.q0.p;
+    W.q[1] = (float4*)fs.q1.p;
+    W.hits = (float4*)fs.hits.p;
+    W.sq = (float4*)fs.sq.p;
+    W.counts = (uint32_t*)fs.counts.p;
+    W.px_extra = (uint2*)fs.extra.p;
+    W.sorted = (float4*)fs.sorted.p;
+    W.sort_table = (uint32_t*)fs.sort_table.p;
+    W.sort_total = (uint32_t*)fs.sort_total.p;
+    return RT_OK;
+}
+
+static hipStream_t slot_stream(rt_ctx* c, int k) { return k == 0 ? c->stream : c->slot[k].own_stream; }
+
+// Waits for every frame in flight.  Everything that changes what frames read (scene, BVH,
+// targets, transforms) runs after it, so a frame never sees a half-updated scene.
+static rt_status drain_frames(rt_ctx* c) {
+    for (int k = 0; k < kMaxSlots; ++k)
+        if (c->slot[k].used) HIPC(c, hipStreamSynchronize(slot_stream(c, k)));
     return RT_OK;
 }
 
@@ -270,11 +302,19 @@ rt_status rt_create(const rt_opts* opts, rt_ctx** out) {
         delete c;
         FAIL((rt_ctx*)nullptr, RT_ERR_INVALID_ARG, "sort_bins must be a power of two in [1024, 4096]");
     }
+    if (opts && opts->frames_in_flight > 0) c->max_in_flight = std::min(opts->frames_in_flight, kMaxSlots);
+    if (const char* e = getenv("RT_FRAMES_IN_FLIGHT")) c->max_in_flight = std::max(1, std::min(atoi(e), kMaxSlots));
     hipError_t e = hipSetDevice(c->device);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking);
-    if (e == hipSuccess) e = hipEventCreate(&c->ev0);
-    if (e == hipSuccess) e = hipEventCreate(&c->ev1);
-    if (e == hipSuccess) e = hipHostMalloc((void**)&c->h_counters, sizeof(unsigned long long) * kCounterWords, 0);
+    for (FrameSlot& f : c->slot) {
+        if (e == hipSuccess) e = hipEventCreate(&f.ev0);
+        if (e == hipSuccess) e = hipEventCreate(&f.ev1);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&f.done, hipEventDisableTiming);
+        if (e == hipSuccess) e = hipHostMalloc((void**)&f.h_counters, sizeof(unsigned long long) * kCounterWords, 0);
+    }
+    for (int k = 1; k < kMaxSlots; ++k)
+        if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->slot[k].own_stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->scene_ev, hipEventDisableTiming);
     if (e != hipSuccess) {
         g_err = std::string("HIP init: ") + hipGetErrorString(e);
         delete c;
@@ -283,7 +323,9 @@ rt_status rt_create(const rt_opts* opts, rt_ctx** out) {
     c->stream = c->own_stream;
     auto tab = halton_table();
     rt_status st = dev_upload(c, c->d_halton, tab.data(), tab.size() * sizeof(HaltonDim));
-    if (!st) st = dev_alloc(c, c->d_counters, sizeof(unsigned long long) * kCounterWords);
+    for (FrameSlot& f : c->slot)
+        if (!st) st = dev_alloc(c, f.counters, sizeof(unsigned long long) * kCounterWords);
+
     if (!st && hipStreamSynchronize(c->stream) != hipSuccess) st = RT_ERR_HIP;
     if (st) {
         g_err = c->err;
@@ -298,28 +340,32 @@ rt_status rt_destroy(rt_ctx* c) {
     if (!c) return RT_OK;
     hipSetDevice(c->device);
     if (c->stream) hipStreamSynchronize(c->stream);
+    for (FrameSlot& f : c->slot)
+        if (f.own_stream) hipStreamSynchronize(f.own_stream);
     DevBuf* all[] = {&c->d_pos, &c->d_prev_pos, &c->d_nrm, &c->d_rest_pos, &c->d_rest_nrm, &c->d_jidx, &c->d_jw,
                      &c->d_joints, &c->d_tri_info, &c->d_inst, &c->d_prev_inst, &c->d_mat, &c->d_lights, &c->d_halton,
                      &c->d_tris, &c->d_nodes, &c->d_node_box, &c->d_slot_to_tri, &c->d_levels, &c->d_maxabs, &c->d_random, &c->d_accum[0],
-                     &c->d_accum[1], &c->d_depth, &c->d_motion, &c->d_gbuffer, &c->d_counters,
-                     &c->d_wf_color, &c->d_wf_accum, &c->d_wf_meta, &c->d_wf_q0, &c->d_wf_q1, &c->d_wf_hits,
-                     &c->d_wf_sq, &c->d_wf_counts, &c->d_wf_mprev, &c->d_wf_extra,
-                     &c->d_wf_sorted, &c->d_wf_sort_table, &c->d_wf_sort_total, &c->d_tri_bin, &c->d_wf_params,
-                     &c->d_lbvh_scratch, &c->d_wf_pray, &c->d_wf_psray};
+                     &c->d_accum[1], &c->d_tri_bin, &c->d_lbvh_scratch};
     for (auto* b : all) dev_free(*b);
+    for (DevBuf& b : c->d_motion) dev_free(b);
     if (c->h_lbvh) hipHostFree(c->h_lbvh);
-    if (c->h_counters) hipHostFree(c->h_counters);
-    if (c->wf.h_counts) hipHostFree(c->wf.h_counts);
-    for (auto& e : c->wf.ev)
-        if (e) hipEventDestroy(e);
-    for (auto& e : c->wft.ev)
-        if (e) hipEventDestroy(e);
-    if (c->wft.exec) hipGraphExecDestroy(c->wft.exec);
-    for (auto& e : c->wf.param_ev)
-        if (e) hipEventDestroy(e);
-    if (c->wf.h_params) hipHostFree(c->wf.h_params);
-    if (c->ev0) hipEventDestroy(c->ev0);
-    if (c->ev1) hipEventDestroy(c->ev1);
+    if (c->scene_ev) hipEventDestroy(c->scene_ev);
+    for (FrameSlot& f : c->slot) {
+        for (DevBuf* b : f.bufs) dev_free(*b);
+        if (f.h_counters) hipHostFree(f.h_counters);
+        if (f.wf.h_counts) hipHostFree(f.wf.h_counts);
+        for (auto& e : f.wf.ev)
+            if (e) hipEventDestroy(e);
+        for (auto& e : f.wft.ev)
+            if (e) hipEventDestroy(e);
+        if (f.wft.exec) hipGraphExecDestroy(f.wft.exec);
+        for (auto& e : f.wf.param_ev)
+            if (e) hipEventDestroy(e);
+        if (f.wf.h_params) hipHostFree(f.wf.h_params);
+        for (hipEvent_t ev : {f.ev0, f.ev1, f.done})
+            if (ev) hipEventDestroy(ev);
+        if (f.own_stream) hipStreamDestroy(f.own_stream);
+    }
     if (c->own_stream) hipStreamDestroy(c->own_stream);
     delete c;
     return RT_OK;
@@ -327,12 +373,15 @@ rt_status rt_destroy(rt_ctx* c) {
 
 rt_status rt_set_stream(rt_ctx* c, void* s) {
     if (!c) FAIL(c, RT_ERR_INVALID_ARG, "null ctx");
+    rt_status st = drain_frames(c);
+    if (st) return st;
     c->stream = s ? (hipStream_t)s : c->own_stream;
     return RT_OK;
 }
 
 rt_status rt_scene_upload(rt_ctx* c, const rt_scene_desc* sd) {
     if (!c || !sd) FAIL(c, RT_ERR_INVALID_ARG, "null argument");
+    if (rt_status dst = drain_frames(c)) return dst;
     HIPC(c, hipSetDevice(c->device));
     if (sd->mesh_count == 0) FAIL(c, RT_ERR_INVALID_ARG, "scene has no meshes");
     if (sd->light_count == 0 || !sd->lights) FAIL(c, RT_ERR_INVALID_ARG, "scene has no lights");
@@ -447,6 +496,7 @@ rt_status rt_scene_upload(rt_ctx* c, const rt_scene_desc* sd) {
 
 rt_status rt_bvh_build(rt_ctx* c) {
     if (!c) FAIL(c, RT_ERR_INVALID_ARG, "null ctx");
+    if (rt_status dst = drain_frames(c)) return dst;
     if (!c->scene_ready) FAIL(c, RT_ERR_STATE, "rt_bvh_build before rt_scene_upload");
     HIPC(c, hipSetDevice(c->device));
     HIPC(c, hipStreamSynchronize(c->stream));
@@ -508,6 +558,7 @@ rt_status rt_bvh_build(rt_ctx* c) {
 
 rt_status rt_bvh_build_device(rt_ctx* c) {
     if (!c) FAIL(c, RT_ERR_INVALID_ARG, "null ctx");
+    if (rt_status dst = drain_frames(c)) return dst;
     if (!c->scene_ready) FAIL(c, RT_ERR_STATE, "rt_bvh_build_device before rt_scene_upload");
     if (c->num_tris < 2) return rt_bvh_build(c);   // nothing to sort: the host path is exact and instant
     HIPC(c, hipSetDevice(c->device));
@@ -549,6 +600,7 @@ rt_status rt_bvh_build_device(rt_ctx* c) {
 
 rt_status rt_bvh_refit(rt_ctx* c) {
     if (!c) FAIL(c, RT_ERR_INVALID_ARG, "null ctx");
+    if (rt_status dst = drain_frames(c)) return dst;
     if (!c->bvh_ready) FAIL(c, RT_ERR_STATE, "rt_bvh_refit before rt_bvh_build");
     HIPC(c, hipSetDevice(c->device));
     rt_status st = dev_alloc(c, c->d_maxabs, 4);
@@ -568,6 +620,7 @@ rt_status rt_bvh_refit(rt_ctx* c) {
 
 rt_status rt_set_instance_transforms(rt_ctx* c, const rt_packed_float4x3* t, uint32_t count) {
     if (!c || !t) FAIL(c, RT_ERR_INVALID_ARG, "null argument");
+    if (rt_status dst = drain_frames(c)) return dst;
     if (!c->scene_ready || count != c->num_inst) FAIL(c, RT_ERR_INVALID_ARG, "transform count != mesh count");
     HIPC(c, hipSetDevice(c->device));
     // prev <- cur (Renderer.swift:939-944), then the new transforms
@@ -582,6 +635,7 @@ rt_status rt_set_instance_transforms(rt_ctx* c, const rt_packed_float4x3* t, uin
 
 rt_status rt_skin(rt_ctx* c, uint32_t mesh_index, const float* joints, uint32_t joint_count) {
     if (!c || !joints) FAIL(c, RT_ERR_INVALID_ARG, "null argument");
+    if (rt_status dst = drain_frames(c)) return dst;
     if (!c->scene_ready || mesh_index >= c->meshes.size()) FAIL(c, RT_ERR_INVALID_ARG, "bad mesh index");
     const MeshInfo& mi = c->meshes[mesh_index];
     if (!mi.skinned) FAIL(c, RT_ERR_INVALID_ARG, "mesh is not skinned");
@@ -603,6 +657,7 @@ rt_status rt_skin(rt_ctx* c, uint32_t mesh_index, const float* joints, uint32_t 
 
 rt_status rt_resize(rt_ctx* c, int32_t w, int32_t h, const uint32_t* offsets) {
     if (!c || !offsets) FAIL(c, RT_ERR_INVALID_ARG, "null argument");
+    if (rt_status dst = drain_frames(c)) return dst;
     if (w <= 0 || h <= 0 || (int64_t)w * h > (1ll << 30)) FAIL(c, RT_ERR_INVALID_ARG, "bad size");
     HIPC(c, hipSetDevice(c->device));
     size_t n = (size_t)w * h;
@@ -612,11 +667,20 @@ rt_status rt_resize(rt_ctx* c, int32_t w, int32_t h, const uint32_t* offsets) {
         if ((st = dev_alloc(c, c->d_accum[i], n * 16))) return st;
         HIPC(c, hipMemsetAsync(c->d_accum[i].p, 0, n * 16, c->stream));
     }
-    if ((st = dev_alloc(c, c->d_depth, n * 4))) return st;
-    if ((st = dev_alloc(c, c->d_motion, n * 8))) return st;
-    HIPC(c, hipMemsetAsync(c->d_depth.p, 0, n * 4, c->stream));
-    HIPC(c, hipMemsetAsync(c->d_motion.p, 0, n * 8, c->stream));
-    dev_free(c->d_gbuffer);
+    for (DevBuf& m : c->d_motion) {
+        if ((st = dev_alloc(c, m, n * 8))) return st;
+        HIPC(c, hipMemsetAsync(m.p, 0, n * 8, c->stream));
+    }
+    c->motion_cur = 0;
+    for (FrameSlot& f : c->slot) {
+        if ((st = dev_alloc(c, f.depth, n * 4))) return st;
+        HIPC(c, hipMemsetAsync(f.depth.p, 0, n * 4, c->stream));
+        dev_free(f.gbuffer);
+        f.used = false;
+        f.pending = false;
+    }
+    c->frame_no = 0;
+    c->last_slot = 0;
     HIPC(c, hipStreamSynchronize(c->stream));
     c->width = w;
     c->height = h;
@@ -646,6 +710,61 @@ static rt_status resolve_tiles(rt_ctx* c, const rt_tile_set* t, int& ts, int& ra
     return RT_OK;
 }
 
+// Folds a finished frame of slot k into rt_stats (its per-frame fields) and the running totals.
+// Waits for that frame: called before the slot is reused and from rt_wait, oldest frame first.
+static rt_status harvest(rt_ctx* c, int k) {
+    FrameSlot& f = c->slot[k];
+    if (!f.pending) return RT_OK;
+    f.pending = false;
+    HIPC(c, hipEventSynchronize(f.done));
+    float ms = 0.0f;
+    HIPC(c, hipEventElapsedTime(&ms, f.ev0, f.ev1));
+    rt_stats& S = c->stats;
+    S.last_frame_ms = ms;
+    for (float& km : S.kernel_ms) km = 0.0f;
+    if (f.wavefront) {
+        const char* err = nullptr;
+        if (!wavefront_collect(f.wf, f.wft, &f.wfs, &err))
+            FAIL(c, RT_ERR_HIP, std::string("wavefront stats: ") + (err ? err : "?"));
+        std::memcpy(S.kernel_ms, f.wfs.stage_ms, sizeof S.kernel_ms);
+    } else {
+        S.kernel_ms[0] = ms;
+    }
+    S.pipeline = f.wavefront ? RT_PIPELINE_WAVEFRONT : RT_PIPELINE_MEGAKERNEL;
+    S.iterations = f.wavefront ? f.wfs.iterations : 0;
+    S.trace_rays = f.wavefront ? f.wfs.trace_rays : 0;
+    S.trace_launches = f.wavefront ? f.wfs.trace_launches : 0;
+    S.trace_ms = f.wavefront ? f.wfs.trace_ms : 0.0f;
+    S.trace_closest_rays = f.wavefront ? f.wfs.trace_closest_rays : 0;
+    S.finish_launches = f.wavefront ? f.wfs.finish_launches : 0;
+    auto total = [&f](int w) {
+        unsigned long long t = 0;
+        for (int r = 0; r < kCntReplicas; ++r) t += f.h_counters[cnt_word(w, r)];
+        return t;
+    };
+    S.closest_rays = total(kCntClosest);
+    S.shadow_rays = total(kCntShadow);
+    S.node_visits = total(kCntNodes);
+    S.tri_tests = total(kCntTris);
+    S.paths = total(kCntPaths);
+    S.trace_nodes = f.wavefront ? total(kCntTraceNodes) : 0;
+    S.trace_tris = f.wavefront ? total(kCntTraceTris) : 0;
+    rt_stats& T = c->totals;
+    T.frames_total += 1;
+    T.total_closest_rays += S.closest_rays;
+    T.total_shadow_rays += S.shadow_rays;
+    T.total_paths += S.paths;
+    T.total_frame_ms += S.last_frame_ms;
+    for (int i = 0; i < 7; ++i) T.total_kernel_ms[i] += S.kernel_ms[i];
+    T.total_trace_rays += S.trace_rays;
+    T.total_trace_closest_rays += S.trace_closest_rays;
+    T.total_trace_ms += S.trace_ms;
+    T.total_trace_launches += (uint64_t)S.trace_launches;
+    T.total_finish_launches += (uint64_t)S.finish_launches;
+    if (total(kCntOverflow)) FAIL(c, RT_ERR_STATE, "traversal stack overflow");
+    return RT_OK;
+}
+
 rt_status rt_render_frame(rt_ctx* c, const Uniforms* U, const rt_tile_set* tiles) {
     if (!c || !U) FAIL(c, RT_ERR_INVALID_ARG, "null argument");
     if (!c->bvh_ready) FAIL(c, RT_ERR_STATE, "rt_render_frame before rt_bvh_build");
@@ -659,9 +778,27 @@ rt_status rt_render_frame(rt_ctx* c, const Uniforms* U, const rt_tile_set* tiles
     rt_status st = resolve_tiles(c, tiles, ts, rank, nranks, tiles_x, own);
     if (st) return st;
     size_t n = (size_t)c->width * c->height;
-    if (U->enableDenoiseGBuffer && !c->d_gbuffer.p) {
-        if ((st = dev_alloc(c, c->d_gbuffer, 4 * n * 16))) return st;
-        HIPC(c, hipMemsetAsync(c->d_gbuffer.p, 0, 4 * n * 16, c->stream));
+    // DebugTextureModeMotion reads sample 0's motion from later samples of the same pixel
+    // (Raytracing.metal:483): only the per-pixel kernel orders samples that way.
+    bool wavefront = c->pipeline == RT_PIPELINE_WAVEFRONT && U->debugTextureMode != DebugTextureModeMotion;
+    // Frames in flight (Renderer.swift:1406-1409): wavefront frames on the context's own stream
+    // rotate over max_in_flight slots; a caller's stream, the megakernel and graph mode keep one.
+    const int nfl = (wavefront && c->stream == c->own_stream && !wavefront_graph_mode()) ? c->max_in_flight : 1;
+    const int k = c->frame_no > 0 ? (c->last_slot + 1) % nfl : 0;
+    FrameSlot& F = c->slot[k];
+    const hipStream_t stream = slot_stream(c, k);
+    if ((st = harvest(c, k))) return st;   // the slot's previous frame (nfl back) has finished
+    // the previous frame, when it runs on the other stream: this frame's history inputs (the
+    // accumulation target and motion vectors it wrote) are read after it has finished
+    const FrameSlot& prev = c->slot[c->last_slot];
+    const bool cross = c->frame_no > 0 && c->last_slot != k && prev.used;
+    if (k != 0) {   // scene / target updates enqueued on ctx->stream come first
+        HIPC(c, hipEventRecord(c->scene_ev, c->stream));
+        HIPC(c, hipStreamWaitEvent(stream, c->scene_ev, 0));
+    }
+    if (U->enableDenoiseGBuffer && !F.gbuffer.p) {
+        if ((st = dev_alloc(c, F.gbuffer, 4 * n * 16))) return st;
+        HIPC(c, hipMemsetAsync(F.gbuffer.p, 0, 4 * n * 16, stream));
     }
     DevScene S;
     S.tris = (const float4*)c->d_tris.p;
@@ -680,53 +817,60 @@ rt_status rt_render_frame(rt_ctx* c, const Uniforms* U, const rt_tile_set* tiles
     S.num_materials = (int)c->h_mat.size();
     S.num_tris = (int)c->num_tris;
     S.num_nodes8 = (int)c->num_nodes8;
+    const int m_prev = c->motion_cur, m_out = wavefront ? (c->motion_cur + 1) % kMotionTargets : c->motion_cur;
     FrameParams P;
     P.U = *U;
     P.random = (const uint32_t*)c->d_random.p;
     P.accum_in = (const float4*)c->d_accum[c->read_idx].p;
     P.accum_out = (float4*)c->d_accum[1 - c->read_idx].p;
-    P.depth = (float*)c->d_depth.p;
-    P.motion = (float2*)c->d_motion.p;
-    P.gbuffer = U->enableDenoiseGBuffer ? (float4*)c->d_gbuffer.p : nullptr;
-    P.counters = (unsigned long long*)c->d_counters.p;
+    P.depth = (float*)F.depth.p;
+    P.motion = (float2*)c->d_motion[m_out].p;
+    P.gbuffer = U->enableDenoiseGBuffer ? (float4*)F.gbuffer.p : nullptr;
+    P.counters = (unsigned long long*)F.counters.p;
     P.tile_size = ts;
     P.rank = rank;
     P.nranks = nranks;
     P.tiles_x = tiles_x;
-    HIPC(c, hipMemsetAsync(c->d_counters.p, 0, sizeof(unsigned long long) * kCounterWords, c->stream));
-    // DebugTextureModeMotion reads sample 0's motion from later samples of the same pixel
-    // (Raytracing.metal:483): only the per-pixel kernel orders samples that way.
-    bool wavefront = c->pipeline == RT_PIPELINE_WAVEFRONT && U->debugTextureMode != DebugTextureModeMotion;
     if (wavefront) {
         int spp = std::max(U->samplesPerPixel, 1);
         int max_extra = U->enableMotionAdaptiveSampling ? std::max(U->motionSamplingMaxExtraSamples, 0) : 0;
-        if ((st = ensure_wavefront(c, (size_t)own * ts * ts, spp, max_extra))) return st;
+        if ((st = ensure_wavefront(c, F, (size_t)own * ts * ts, spp, max_extra))) return st;
+        F.wf.motion_prev = (float2*)c->d_motion[m_prev].p;
     }
+    HIPC(c, hipMemsetAsync(F.counters.p, 0, sizeof(unsigned long long) * kCounterWords, stream));
     // extra samples can only be non-zero when something moved in this frame or the previous one
     const bool moving = c->inst_moved || c->skin_moved ||
                         std::memcmp(&U->camera, &U->previousCamera, sizeof(Camera)) != 0;
     const bool extra_pass = moving || c->last_moving;
     c->last_moving = moving;
-    HIPC(c, hipEventRecord(c->ev0, c->stream));
-    for (float& k : c->stats.kernel_ms) k = 0.0f;
-    c->wft.pending = false;
+    HIPC(c, hipEventRecord(F.ev0, stream));
+    F.wft.pending = false;
     if (wavefront) {
         const char* err = nullptr;
-        c->wfs = WfFrameStats{};
-        if (own > 0 && !run_wavefront(S, P, c->wf, own, c->counting, c->tail_paths, c->sort_bins, extra_pass, c->stream,
-                                      &c->wft, &c->wfs, &err))
+        F.wfs = WfFrameStats{};
+        if (own > 0 && !run_wavefront(S, P, F.wf, own, c->counting, c->tail_paths, c->sort_bins, extra_pass, stream,
+                                      cross ? prev.done : nullptr, &F.wft, &F.wfs, &err))
             FAIL(c, RT_ERR_HIP, std::string("wavefront: ") + (err ? err : "?"));
+        if (own == 0 && cross) HIPC(c, hipStreamWaitEvent(stream, prev.done, 0));
     } else {
+        if (cross) HIPC(c, hipStreamWaitEvent(stream, prev.done, 0));
         int nblocks = own * (ts / 16) * (ts / 16);
-        if (nblocks > 0) launch_megakernel(S, P, nblocks, c->counting, c->stream);
+        if (nblocks > 0) launch_megakernel(S, P, nblocks, c->counting, stream);
     }
     HIPC(c, hipGetLastError());
-    HIPC(c, hipEventRecord(c->ev1, c->stream));
-    c->last_wavefront = wavefront;
-    HIPC(c, hipMemcpyAsync(c->h_counters, c->d_counters.p, sizeof(unsigned long long) * kCounterWords,
-                           hipMemcpyDeviceToHost, c->stream));
+    HIPC(c, hipEventRecord(F.ev1, stream));
+    HIPC(c, hipMemcpyAsync(F.h_counters, F.counters.p, sizeof(unsigned long long) * kCounterWords,
+                           hipMemcpyDeviceToHost, stream));
+    HIPC(c, hipEventRecord(F.done, stream));
+    F.wavefront = wavefront;
+    F.pending = true;
+    F.used = true;
+    F.seq = c->frame_no;
+    c->last_slot = k;
+    c->frame_no += 1;
+    c->motion_cur = m_out;
+    c->stats.frames_in_flight = nfl;
     c->read_idx = 1 - c->read_idx;  // swap accumulationTargets (Renderer.swift:1492-1494)
-    c->frame_pending = true;
     return RT_OK;
 }
 
@@ -734,40 +878,12 @@ rt_status rt_wait(rt_ctx* c) {
     if (!c) FAIL(c, RT_ERR_INVALID_ARG, "null ctx");
     HIPC(c, hipSetDevice(c->device));
     HIPC(c, hipStreamSynchronize(c->stream));
-    if (c->frame_pending) {
-        float ms = 0.0f;
-        HIPC(c, hipEventElapsedTime(&ms, c->ev0, c->ev1));
-        c->stats.last_frame_ms = ms;
-        if (c->last_wavefront) {
-            const char* err = nullptr;
-            if (!wavefront_collect(c->wf, c->wft, &c->wfs, &err))
-                FAIL(c, RT_ERR_HIP, std::string("wavefront stats: ") + (err ? err : "?"));
-            std::memcpy(c->stats.kernel_ms, c->wfs.stage_ms, sizeof c->stats.kernel_ms);
-        } else {
-            c->stats.kernel_ms[0] = ms;
-        }
-        c->stats.pipeline = c->last_wavefront ? RT_PIPELINE_WAVEFRONT : RT_PIPELINE_MEGAKERNEL;
-        c->stats.iterations = c->last_wavefront ? c->wfs.iterations : 0;
-        c->stats.trace_rays = c->last_wavefront ? c->wfs.trace_rays : 0;
-        c->stats.trace_launches = c->last_wavefront ? c->wfs.trace_launches : 0;
-        c->stats.trace_ms = c->last_wavefront ? c->wfs.trace_ms : 0.0f;
-        c->stats.trace_closest_rays = c->last_wavefront ? c->wfs.trace_closest_rays : 0;
-        c->stats.finish_launches = c->last_wavefront ? c->wfs.finish_launches : 0;
-        auto total = [c](int slot) {
-            unsigned long long t = 0;
-            for (int r = 0; r < kCntReplicas; ++r) t += c->h_counters[cnt_word(slot, r)];
-            return t;
-        };
-        c->stats.closest_rays = total(kCntClosest);
-        c->stats.shadow_rays = total(kCntShadow);
-        c->stats.node_visits = total(kCntNodes);
-        c->stats.tri_tests = total(kCntTris);
-        c->stats.paths = total(kCntPaths);
-        c->stats.trace_nodes = c->last_wavefront ? total(kCntTraceNodes) : 0;
-        c->stats.trace_tris = c->last_wavefront ? total(kCntTraceTris) : 0;
-        c->frame_pending = false;
-        if (total(kCntOverflow)) FAIL(c, RT_ERR_STATE, "traversal stack overflow");
-    }
+    // oldest frame first, so rt_stats ends on the newest one
+    int order[kMaxSlots];
+    for (int k = 0; k < kMaxSlots; ++k) order[k] = k;
+    std::sort(order, order + kMaxSlots, [c](int a, int b) { return c->slot[a].seq < c->slot[b].seq; });
+    for (int k : order)
+        if (rt_status st = harvest(c, k)) return st;
     return RT_OK;
 }
 
@@ -786,17 +902,19 @@ rt_status rt_read_aux(rt_ctx* c, float* depth, float* motion, float* gbuffer) {
     rt_status st = rt_wait(c);
     if (st) return st;
     size_t n = (size_t)c->width * c->height;
-    if (depth) HIPC(c, hipMemcpy(depth, c->d_depth.p, n * 4, hipMemcpyDeviceToHost));
-    if (motion) HIPC(c, hipMemcpy(motion, c->d_motion.p, n * 8, hipMemcpyDeviceToHost));
+    const FrameSlot& f = c->slot[c->last_slot];   // the newest frame's targets
+    if (depth) HIPC(c, hipMemcpy(depth, f.depth.p, n * 4, hipMemcpyDeviceToHost));
+    if (motion) HIPC(c, hipMemcpy(motion, c->d_motion[c->motion_cur].p, n * 8, hipMemcpyDeviceToHost));
     if (gbuffer) {
-        if (!c->d_gbuffer.p) FAIL(c, RT_ERR_STATE, "G-buffer was never enabled");
-        HIPC(c, hipMemcpy(gbuffer, c->d_gbuffer.p, 4 * n * 16, hipMemcpyDeviceToHost));
+        if (!f.gbuffer.p) FAIL(c, RT_ERR_STATE, "G-buffer was never enabled");
+        HIPC(c, hipMemcpy(gbuffer, f.gbuffer.p, 4 * n * 16, hipMemcpyDeviceToHost));
     }
     return RT_OK;
 }
 
 rt_status rt_pack_tiles(rt_ctx* c, const rt_tile_set* t, void* dst) {
     if (!c || !dst) FAIL(c, RT_ERR_INVALID_ARG, "null argument");
+    if (rt_status dst = drain_frames(c)) return dst;
     if (!c->width) FAIL(c, RT_ERR_STATE, "no targets");
     int ts, rank, nranks, tiles_x, own;
     rt_status st = resolve_tiles(c, t, ts, rank, nranks, tiles_x, own);
@@ -810,6 +928,7 @@ rt_status rt_pack_tiles(rt_ctx* c, const rt_tile_set* t, void* dst) {
 
 rt_status rt_unpack_tiles(rt_ctx* c, const rt_tile_set* t, const void* src) {
     if (!c || !src) FAIL(c, RT_ERR_INVALID_ARG, "null argument");
+    if (rt_status dst = drain_frames(c)) return dst;
     if (!c->width) FAIL(c, RT_ERR_STATE, "no targets");
     int ts, rank, nranks, tiles_x, own;
     rt_status st = resolve_tiles(c, t, ts, rank, nranks, tiles_x, own);
@@ -873,6 +992,18 @@ rt_status rt_get_stats(rt_ctx* c, rt_stats* out) {
     c->stats.triangles = c->num_tris;
     c->stats.device_bytes = ctx_bytes(c);
     *out = c->stats;
+    const rt_stats& T = c->totals;
+    out->frames_total = T.frames_total;
+    out->total_closest_rays = T.total_closest_rays;
+    out->total_shadow_rays = T.total_shadow_rays;
+    out->total_paths = T.total_paths;
+    out->total_frame_ms = T.total_frame_ms;
+    std::memcpy(out->total_kernel_ms, T.total_kernel_ms, sizeof T.total_kernel_ms);
+    out->total_trace_rays = T.total_trace_rays;
+    out->total_trace_closest_rays = T.total_trace_closest_rays;
+    out->total_trace_ms = T.total_trace_ms;
+    out->total_trace_launches = T.total_trace_launches;
+    out->total_finish_launches = T.total_finish_launches;
     return RT_OK;
 }
 

@@ -96,7 +96,7 @@ struct WavefrontBuffers {
     float4* sq = nullptr;
     uint32_t* counts = nullptr;   // device counter slots (see cslot)
     uint32_t* h_counts = nullptr; // pinned host mirror
-    float2* motion_prev = nullptr;
+    float2* motion_prev = nullptr;   // the previous frame's motion target (set per frame)
     uint2* px_extra = nullptr;    // per own pixel: (first extra path - base_paths, count)
     // wf_finish_q: per path, its next closest ray (o, d) and its shadow query (o; d, tmax;
     // contribution, continues)
@@ -161,10 +161,13 @@ struct WfTimeline {
 // from wavefront_collect after the stream finished) one frame; false on a HIP error (*err).
 // sort_bins: hit-sort bins (0 = no sort).  extra_pass: the motion-adaptive extra samples can be
 // non-zero this frame (something moved in this or the previous frame); the device-driven mode
-// skips their pass otherwise.
+// skips their pass otherwise.  prev_done (may be null): the previous frame, in flight on another
+// stream; the extra-sample pass and the resolve (which read its accumulation and motion outputs)
+// are ordered after it, everything before them overlaps it.
 bool run_wavefront(const DevScene& S, const FrameParams& P, WavefrontBuffers& W, int own_tiles, bool count,
-                   int tail_paths, int sort_bins, bool extra_pass, hipStream_t stream, WfTimeline* tl,
-                   WfFrameStats* fs, const char** err);
+                   int tail_paths, int sort_bins, bool extra_pass, hipStream_t stream, hipEvent_t prev_done,
+                   WfTimeline* tl, WfFrameStats* fs, const char** err);
+bool wavefront_graph_mode();   // RT_GRAPH=1 (one frame in flight)
 bool wavefront_collect(const WavefrontBuffers& W, WfTimeline& T, WfFrameStats* fs, const char** err);
 size_t wavefront_queue_entries(size_t paths, int max_extra);
 

@@ -1905,23 +1905,22 @@ static bool enqueue_pass(const DevScene& S, const FrameParams& P, const WfParams
 // read by the kernels from Q.Pd.
 // h_stage: graph mode, the pinned copy of this frame's FrameParams the graph uploads first.
 static bool record_frame(const DevScene& S, const FrameParams& P, WfParams& Q, bool count, bool full, int maxExtra,
-                         bool with_extra, const FrameParams* h_stage, hipStream_t stream, WfTimeline& T,
-                         const char** err) {
+                         bool with_extra, const FrameParams* h_stage, hipStream_t stream, hipEvent_t prev_done,
+                         WfTimeline& T, const char** err) {
     WavefrontBuffers& W = Q.W;
     T.n_ev = T.n_spans = 0;
     Enqueue E{T, stream};
-    const size_t npix = (size_t)P.U.width * P.U.height;
     if (!E.mark(err)) return false;
     if (h_stage)
         WF_CHECK(hipMemcpyAsync(W.d_params, h_stage, sizeof(FrameParams), hipMemcpyHostToDevice, stream));
     WF_CHECK(hipMemsetAsync(W.counts, 0, kWfCountWords * sizeof(uint32_t), stream));
-    WF_CHECK(hipMemcpyAsync(W.motion_prev, P.motion, npix * sizeof(float2), hipMemcpyDeviceToDevice, stream));
     const int rounds = rounds_for(Q.base_paths, Q.tail);
     Q.finish_q = rounds & 1;
     hipLaunchKernelGGL(wf_generate, dim3(grid_for(Q.base_paths, 16384)), dim3(kBlock), 0, stream, S, Q.Pd, Q);
     WF_CHECK(hipGetLastError());
     if (!E.span(0, err)) return false;
     if (!enqueue_pass(S, P, Q, rounds, count, full, E, err)) return false;
+    if (prev_done) WF_CHECK(hipStreamWaitEvent(stream, prev_done, 0));
     if (with_extra) {
         // second pass over the motion-adaptive extra samples (:779-789), appended to queue 0
         const int rounds2 = rounds_for((uint64_t)Q.own_pixels * (uint64_t)maxExtra, Q.tail);
@@ -1968,13 +1967,14 @@ static std::vector<uint64_t> graph_key(const DevScene& S, const FrameParams& P, 
 }
 
 static bool enqueue_wavefront(const DevScene& S, const FrameParams& P, WfParams& Q, bool count, bool full,
-                              int maxExtra, bool extra_pass, hipStream_t stream, WfTimeline& T, const char** err) {
+                              int maxExtra, bool extra_pass, hipStream_t stream, hipEvent_t prev_done, WfTimeline& T,
+                              const char** err) {
     Q.dev_ctl = 1;
     Q.drain_min = 0;
     Q.finish_q = 0;   // set by record_frame from the round count
     const bool with_extra = maxExtra > 0 && extra_pass;
     if (!use_graph()) {
-        if (!record_frame(S, P, Q, count, full, maxExtra, with_extra, nullptr, stream, T, err)) return false;
+        if (!record_frame(S, P, Q, count, full, maxExtra, with_extra, nullptr, stream, prev_done, T, err)) return false;
         T.pending = true;
         return true;
     }
@@ -1993,7 +1993,7 @@ static bool enqueue_wavefront(const DevScene& S, const FrameParams& P, WfParams&
         T.key.clear();
         WF_CHECK(hipStreamBeginCapture(stream, hipStreamCaptureModeRelaxed));
         T.in_graph = true;
-        const bool ok = record_frame(S, P, Q, count, full, maxExtra, with_extra, &W.h_params[0], stream, T, err);
+        const bool ok = record_frame(S, P, Q, count, full, maxExtra, with_extra, &W.h_params[0], stream, nullptr, T, err);
         T.in_graph = false;
         hipGraph_t graph = nullptr;
         const hipError_t e = hipStreamEndCapture(stream, &graph);
@@ -2021,6 +2021,8 @@ static bool enqueue_wavefront(const DevScene& S, const FrameParams& P, WfParams&
     return true;
 }
 
+bool wavefront_graph_mode() { return use_graph(); }
+
 bool wavefront_collect(const WavefrontBuffers& W, WfTimeline& T, WfFrameStats* fs, const char** err) {
     if (!T.pending) return true;
     T.pending = false;
@@ -2041,8 +2043,8 @@ bool wavefront_collect(const WavefrontBuffers& W, WfTimeline& T, WfFrameStats* f
 }
 
 bool run_wavefront(const DevScene& S, const FrameParams& P, WavefrontBuffers& W, int own_tiles, bool count,
-                   int tail_paths, int sort_bins, bool extra_pass, hipStream_t stream, WfTimeline* tl,
-                   WfFrameStats* fs, const char** err) {
+                   int tail_paths, int sort_bins, bool extra_pass, hipStream_t stream, hipEvent_t prev_done,
+                   WfTimeline* tl, WfFrameStats* fs, const char** err) {
     WfParams Q;
     Q.W = W;
     Q.spp = max(P.U.samplesPerPixel, 1);
@@ -2094,15 +2096,13 @@ bool run_wavefront(const DevScene& S, const FrameParams& P, WavefrontBuffers& W,
     }
     const bool full = needs_full(P.U);
     const int maxExtra = (P.U.enableMotionAdaptiveSampling != 0) ? max(P.U.motionSamplingMaxExtraSamples, 0) : 0;
-    size_t npix = (size_t)P.U.width * P.U.height;
     if (dev)
-        return enqueue_wavefront(S, P, Q, count, full, maxExtra, extra_pass, stream, *tl, err);
+        return enqueue_wavefront(S, P, Q, count, full, maxExtra, extra_pass, stream, prev_done, *tl, err);
     Q.dev_ctl = 0;
     Q.finish_q = 0;
 
     WF_CHECK(hipEventRecord(W.ev[0], stream));
     WF_CHECK(hipMemsetAsync(W.counts, 0, kWfCountWords * sizeof(uint32_t), stream));
-    WF_CHECK(hipMemcpyAsync(W.motion_prev, P.motion, npix * sizeof(float2), hipMemcpyDeviceToDevice, stream));
     hipLaunchKernelGGL(wf_generate, dim3(grid_for(Q.base_paths, 16384)), dim3(kBlock), 0, stream, S, Q.Pd, Q);
     WF_CHECK(hipGetLastError());
     WF_CHECK(hipEventRecord(W.ev[1], stream));
@@ -2114,6 +2114,7 @@ bool run_wavefront(const DevScene& S, const FrameParams& P, WavefrontBuffers& W,
     int cur = 0;
     if (!iterate(S, P, Q, cur, queue_total(W.h_counts, 0), count, full, stream, fs, err)) return false;
 
+    if (prev_done) WF_CHECK(hipStreamWaitEvent(stream, prev_done, 0));
     WF_CHECK(hipEventRecord(W.ev[0], stream));
     if (maxExtra > 0) {
         // the extra-sample pass appends primary rays to queue `cur` (reset here)
