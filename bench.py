@@ -101,12 +101,12 @@ def main():
         return st
 
     def submit():
-        # one step: single GPU, the frame is only submitted (the renderer keeps two frames in
-        # flight and waits for a slot's previous frame itself); multi-GPU, rendered and gathered
-        if gather is None:
-            R.draw(tiles=tiles)
-        else:
-            frame()
+        # one step: the frame is submitted and, multi-GPU, its tiles packed, gathered to rank 0
+        # over RCCL and unpacked there, all enqueued without a host wait (the renderer keeps two
+        # frames in flight and waits for a slot's previous frame itself)
+        R.draw(tiles=tiles)
+        if gather is not None:
+            gather.gather()
 
     def barrier():
         if n > 1:

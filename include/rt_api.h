@@ -195,10 +195,15 @@ rt_status rt_read_aux(rt_ctx* ctx, float* depth, float* motion, float* gbuffer);
 
 /* Multi-GPU: pack this rank's tiles of the latest radiance into a device buffer of
  * rt_tile_count(...) * tile_size^2 * 4 floats, and the inverse on the gathering rank
- * (writing into the latest radiance target). Device pointers; ordered on the ctx stream. */
+ * (writing into the latest radiance target). Device pointers; enqueued after the newest frame
+ * on the ctx stream (the _on forms: on `hip_stream`, e.g. the stream the collective runs on),
+ * without a host wait.  The next frames overlap them (see frames_in_flight); rt_wait waits for
+ * them too. */
 int32_t rt_tile_count(int32_t width, int32_t height, const rt_tile_set* tiles);
 rt_status rt_pack_tiles(rt_ctx* ctx, const rt_tile_set* tiles, void* device_dst);
 rt_status rt_unpack_tiles(rt_ctx* ctx, const rt_tile_set* tiles, const void* device_src);
+rt_status rt_pack_tiles_on(rt_ctx* ctx, const rt_tile_set* tiles, void* device_dst, void* hip_stream);
+rt_status rt_unpack_tiles_on(rt_ctx* ctx, const rt_tile_set* tiles, const void* device_src, void* hip_stream);
 /* Host-memory forms of the same layout (RGBA fp32 images of width x height), for gathers that
  * land in host memory and for tests of the tile protocol without a device. */
 rt_status rt_pack_tiles_host(int32_t width, int32_t height, const rt_tile_set* tiles, const float* src_rgba,

@@ -322,13 +322,23 @@ class Renderer:
         ts = TileSet(tile_size, rank, nranks, 0)
         return int(lib().rt_tile_count(self.width, self.height, C.byref(ts)))
 
-    def pack_tiles(self, tile_size, rank, nranks, device_ptr):
+    def pack_tiles(self, tile_size, rank, nranks, device_ptr, stream=None):
+        """Packs this rank's tiles of the newest frame (after it, on `stream`: a HIP stream handle,
+        None = the renderer's stream); no host wait."""
         ts = TileSet(tile_size, rank, nranks, 0)
-        _check(lib().rt_pack_tiles(self._ctx, C.byref(ts), C.c_void_p(device_ptr)), self._ctx)
+        if stream is None:
+            _check(lib().rt_pack_tiles(self._ctx, C.byref(ts), C.c_void_p(device_ptr)), self._ctx)
+        else:
+            _check(lib().rt_pack_tiles_on(self._ctx, C.byref(ts), C.c_void_p(device_ptr), C.c_void_p(stream)),
+                   self._ctx)
 
-    def unpack_tiles(self, tile_size, rank, nranks, device_ptr):
+    def unpack_tiles(self, tile_size, rank, nranks, device_ptr, stream=None):
         ts = TileSet(tile_size, rank, nranks, 0)
-        _check(lib().rt_unpack_tiles(self._ctx, C.byref(ts), C.c_void_p(device_ptr)), self._ctx)
+        if stream is None:
+            _check(lib().rt_unpack_tiles(self._ctx, C.byref(ts), C.c_void_p(device_ptr)), self._ctx)
+        else:
+            _check(lib().rt_unpack_tiles_on(self._ctx, C.byref(ts), C.c_void_p(device_ptr), C.c_void_p(stream)),
+                   self._ctx)
 
     def set_stream(self, stream_handle):
         _check(lib().rt_set_stream(self._ctx, C.c_void_p(stream_handle) if stream_handle else None), self._ctx)

@@ -194,6 +194,7 @@ EXPORTED_SYMBOLS = [
     "rt_create", "rt_destroy", "rt_last_error", "rt_set_stream", "rt_scene_upload", "rt_bvh_build",
     "rt_bvh_build_device", "rt_bvh_refit", "rt_set_instance_transforms", "rt_skin", "rt_resize", "rt_render_frame", "rt_wait",
     "rt_read_radiance", "rt_read_aux", "rt_tile_count", "rt_pack_tiles", "rt_unpack_tiles",
+    "rt_pack_tiles_on", "rt_unpack_tiles_on",
     "rt_pack_tiles_host", "rt_unpack_tiles_host",
     "rt_set_counting", "rt_get_stats", "rt_version", "rt_debug_trace_host",
     # rt_scene.h
@@ -228,6 +229,8 @@ def declare(lib):
         "rt_tile_count": (C.c_int32, [C.c_int32, C.c_int32, P(TileSet)]),
         "rt_pack_tiles": (st, [vp, P(TileSet), vp]),
         "rt_unpack_tiles": (st, [vp, P(TileSet), vp]),
+        "rt_pack_tiles_on": (st, [vp, P(TileSet), vp, vp]),
+        "rt_unpack_tiles_on": (st, [vp, P(TileSet), vp, vp]),
         "rt_pack_tiles_host": (st, [C.c_int32, C.c_int32, P(TileSet), P(C.c_float), P(C.c_float)]),
         "rt_unpack_tiles_host": (st, [C.c_int32, C.c_int32, P(TileSet), P(C.c_float), P(C.c_float)]),
         "rt_set_counting": (st, [vp, C.c_int32]),

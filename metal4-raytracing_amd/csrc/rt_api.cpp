@@ -103,6 +103,8 @@ struct rt_ctx {
     uint64_t frame_no = 0;           // frames submitted since rt_resize
     int last_slot = 0;               // slot of the newest frame
     hipEvent_t scene_ev = nullptr;   // ctx->stream work a slot-1 frame must follow
+    bool tiles_pending = false;      // a pack / unpack extended the newest frame's `done`
+    int last_tiles[3] = {0, 0, 0};   // tile_size, rank, nranks of the newest frame
     rt_stats totals{};   // the running-total fields of rt_stats
 
     // motion bookkeeping for the extra-sample pass: motion vectors are exactly zero unless the
@@ -266,7 +268,10 @@ static hipStream_t slot_stream(rt_ctx* c, int k) { return k == 0 ? c->stream : c
 // targets, transforms) runs after it, so a frame never sees a half-updated scene.
 static rt_status drain_frames(rt_ctx* c) {
     for (int k = 0; k < kMaxSlots; ++k)
-        if (c->slot[k].used) HIPC(c, hipStreamSynchronize(slot_stream(c, k)));
+        if (c->slot[k].used) {
+            HIPC(c, hipStreamSynchronize(slot_stream(c, k)));
+            HIPC(c, hipEventSynchronize(c->slot[k].done));
+        }
     return RT_OK;
 }
 
@@ -791,7 +796,11 @@ rt_status rt_render_frame(rt_ctx* c, const Uniforms* U, const rt_tile_set* tiles
     // the previous frame, when it runs on the other stream: this frame's history inputs (the
     // accumulation target and motion vectors it wrote) are read after it has finished
     const FrameSlot& prev = c->slot[c->last_slot];
-    const bool cross = c->frame_no > 0 && c->last_slot != k && prev.used;
+    const bool cross = c->frame_no > 0 && prev.used && (c->last_slot != k || c->tiles_pending);
+    // a pack / unpack of the previous frame on another stream: the tiles this frame owns are
+    // disjoint from the ones it wrote unless the tile set changed
+    const bool retile = ts != c->last_tiles[0] || rank != c->last_tiles[1] || nranks != c->last_tiles[2];
+    if (c->tiles_pending && retile && prev.used) HIPC(c, hipStreamWaitEvent(stream, prev.done, 0));
     if (k != 0) {   // scene / target updates enqueued on ctx->stream come first
         HIPC(c, hipEventRecord(c->scene_ev, c->stream));
         HIPC(c, hipStreamWaitEvent(stream, c->scene_ev, 0));
@@ -868,6 +877,10 @@ rt_status rt_render_frame(rt_ctx* c, const Uniforms* U, const rt_tile_set* tiles
     F.seq = c->frame_no;
     c->last_slot = k;
     c->frame_no += 1;
+    c->tiles_pending = false;
+    c->last_tiles[0] = ts;
+    c->last_tiles[1] = rank;
+    c->last_tiles[2] = nranks;
     c->motion_cur = m_out;
     c->stats.frames_in_flight = nfl;
     c->read_idx = 1 - c->read_idx;  // swap accumulationTargets (Renderer.swift:1492-1494)
@@ -884,6 +897,8 @@ rt_status rt_wait(rt_ctx* c) {
     std::sort(order, order + kMaxSlots, [c](int a, int b) { return c->slot[a].seq < c->slot[b].seq; });
     for (int k : order)
         if (rt_status st = harvest(c, k)) return st;
+    const FrameSlot& f = c->slot[c->last_slot];
+    if (f.used) HIPC(c, hipEventSynchronize(f.done));   // and a pack / unpack after it
     return RT_OK;
 }
 
@@ -912,32 +927,45 @@ rt_status rt_read_aux(rt_ctx* c, float* depth, float* motion, float* gbuffer) {
     return RT_OK;
 }
 
-rt_status rt_pack_tiles(rt_ctx* c, const rt_tile_set* t, void* dst) {
-    if (!c || !dst) FAIL(c, RT_ERR_INVALID_ARG, "null argument");
-    if (rt_status dst = drain_frames(c)) return dst;
+// Pack / unpack run on `stream` after the newest frame, without a host wait, and extend that
+// frame's `done` event over themselves: the frame that next writes the same accumulation target
+// (two frames later) waits for it before its resolve, so the gather of frame f overlaps the
+// rendering of frame f+1.
+static rt_status tiles_op(rt_ctx* c, const rt_tile_set* t, const void* src, void* dst, hipStream_t stream, bool pack) {
+    if (!c || (pack ? !dst : !src)) FAIL(c, RT_ERR_INVALID_ARG, "null argument");
     if (!c->width) FAIL(c, RT_ERR_STATE, "no targets");
     int ts, rank, nranks, tiles_x, own;
     rt_status st = resolve_tiles(c, t, ts, rank, nranks, tiles_x, own);
     if (st) return st;
     HIPC(c, hipSetDevice(c->device));
-    launch_pack_tiles((const float4*)c->d_accum[c->read_idx].p, (float4*)dst, c->width, c->height, ts, rank, nranks,
-                      tiles_x, own, c->stream);
+    if (!stream) stream = c->stream;
+    FrameSlot& f = c->slot[c->last_slot];
+    if (f.used) HIPC(c, hipStreamWaitEvent(stream, f.done, 0));
+    float4* accum = (float4*)c->d_accum[c->read_idx].p;
+    if (pack)
+        launch_pack_tiles(accum, (float4*)dst, c->width, c->height, ts, rank, nranks, tiles_x, own, stream);
+    else
+        launch_unpack_tiles((const float4*)src, accum, c->width, c->height, ts, rank, nranks, tiles_x, own, stream);
     HIPC(c, hipGetLastError());
+    if (f.used) {
+        HIPC(c, hipEventRecord(f.done, stream));
+        c->tiles_pending = true;
+    }
     return RT_OK;
 }
 
+rt_status rt_pack_tiles(rt_ctx* c, const rt_tile_set* t, void* dst) { return tiles_op(c, t, nullptr, dst, nullptr, true); }
+
 rt_status rt_unpack_tiles(rt_ctx* c, const rt_tile_set* t, const void* src) {
-    if (!c || !src) FAIL(c, RT_ERR_INVALID_ARG, "null argument");
-    if (rt_status dst = drain_frames(c)) return dst;
-    if (!c->width) FAIL(c, RT_ERR_STATE, "no targets");
-    int ts, rank, nranks, tiles_x, own;
-    rt_status st = resolve_tiles(c, t, ts, rank, nranks, tiles_x, own);
-    if (st) return st;
-    HIPC(c, hipSetDevice(c->device));
-    launch_unpack_tiles((const float4*)src, (float4*)c->d_accum[c->read_idx].p, c->width, c->height, ts, rank, nranks,
-                        tiles_x, own, c->stream);
-    HIPC(c, hipGetLastError());
-    return RT_OK;
+    return tiles_op(c, t, src, nullptr, nullptr, false);
+}
+
+rt_status rt_pack_tiles_on(rt_ctx* c, const rt_tile_set* t, void* dst, void* stream) {
+    return tiles_op(c, t, nullptr, dst, (hipStream_t)stream, true);
+}
+
+rt_status rt_unpack_tiles_on(rt_ctx* c, const rt_tile_set* t, const void* src, void* stream) {
+    return tiles_op(c, t, src, nullptr, (hipStream_t)stream, false);
 }
 
 static rt_status host_tiles(int32_t w, int32_t h, const rt_tile_set* t, int& ts, int& rank, int& nranks, int& tiles_x,

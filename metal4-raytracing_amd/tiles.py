@@ -72,25 +72,26 @@ class TileGather:
         self.recv = ([torch.empty_like(self.packed) for _ in range(nranks)] if rank == dst else None)
 
     def gather(self, image=None):
-        """Gathers this frame's tiles on the dst rank. Device path: the dst renderer's target then
-        holds the full frame (returns None). Host path: returns the full (H, W, 4) image on dst,
+        """Gathers this frame's tiles on the dst rank. Device path: enqueued without a host wait;
+        after the dst renderer's wait() its target holds the full frame (returns None). Host path: returns the full (H, W, 4) image on dst,
         None elsewhere."""
         import torch
         import torch.distributed as dist
         if self.R is not None:
-            self.R.pack_tiles(self.T, self.rank, self.n, self.packed.data_ptr())
-            self.R.wait()
+            # after the newest frame, on the stream the collective is ordered on; the renderer's
+            # next frame overlaps the pack and the gather
+            self.R.pack_tiles(self.T, self.rank, self.n, self.packed.data_ptr(),
+                              stream=torch.cuda.current_stream().cuda_stream)
         else:
             self.packed.copy_(torch.from_numpy(pack_host(image, self.T, self.rank, self.n, self.max_own)))
         dist.gather(self.packed, self.recv, dst=self.dst)
         if self.rank != self.dst:
             return None
         if self.R is not None:
-            torch.cuda.current_stream().synchronize()
+            s = torch.cuda.current_stream().cuda_stream
             for r in range(self.n):
                 if r != self.rank:
-                    self.R.unpack_tiles(self.T, r, self.n, self.recv[r].data_ptr())
-            self.R.wait()
+                    self.R.unpack_tiles(self.T, r, self.n, self.recv[r].data_ptr(), stream=s)
             return None
         out = np.zeros((self.h, self.w, 4), np.float32)
         for r in range(self.n):

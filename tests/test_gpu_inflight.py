@@ -92,3 +92,36 @@ def test_in_flight_then_megakernel_frame(rt, assets):
     for img, mot in out[1:]:
         assert np.array_equal(out[0][0], img)
         assert np.array_equal(out[0][1], mot)
+
+
+def test_in_flight_tile_gather(rt, assets):
+    """Two ranks' renderers (tile split, frames in flight) with the per-frame gather enqueued on
+    a separate stream without host waits (rank 1 packs, rank 0 unpacks, the pattern of
+    TileGather.gather over RCCL): rank 0's image after the last frame equals the one-GPU image,
+    through camera motion (each pixel's history stays its own rank's)."""
+    import torch
+    sc = rt.Scene.preset("c1", assets)
+    W, H, T, K = 200, 136, 64, 5
+    full = make_renderer(rt, sc, W, H, "wavefront", seed=5, frames_in_flight=1)
+    ranks = [make_renderer(rt, sc, W, H, "wavefront", seed=5, frames_in_flight=2) for _ in range(2)]
+    for R in [full] + ranks:
+        R.maxBounces = 3
+    cam0 = full.camera
+    cnt = ranks[1].tile_count(T, 1, 2)
+    s = torch.cuda.Stream()
+    keep = []
+    for i in range(K):
+        for R in [full] + ranks:
+            R.camera = _moved(rt, cam0, 0.05 * i * i, 0.02 * i)
+        full.draw()
+        for r, R in enumerate(ranks):
+            R.draw(tiles=(T, r, 2))
+        with torch.cuda.stream(s):
+            buf = torch.empty((cnt, T, T, 4), dtype=torch.float32, device="cuda")
+            ranks[1].pack_tiles(T, 1, 2, buf.data_ptr(), stream=s.cuda_stream)
+            ranks[0].unpack_tiles(T, 1, 2, buf.data_ptr(), stream=s.cuda_stream)
+        keep.append(buf)
+    ref = full.radiance()
+    img = ranks[0].radiance()
+    assert ranks[0].stats().frames_in_flight == 2
+    assert np.array_equal(img, ref)
