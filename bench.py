@@ -219,8 +219,11 @@ def main():
         with open(TRAFFIC_JSON) as f:
             tj = json.load(f)
         if tj.get("config") == [a.scene, a.width, a.height, a.spp, a.bounces]:
+            by_kernel = tj.get("bytes_per_launch_by_kernel") or {}
             if tj.get("kernel") == kernel:
-                traffic, traffic_src = tj["bytes_per_launch"], TRAFFIC_JSON_REL + " (" + tj.get("source", "") + ")"
+                by_kernel.setdefault(kernel, tj["bytes_per_launch"])
+            if by_kernel.get(kernel) is not None:
+                traffic, traffic_src = by_kernel[kernel], TRAFFIC_JSON_REL + " (" + tj.get("source", "") + ")"
             # TCC hit rates (rocprofv3 TCC_HIT/TCC_MISS pass) of the traversal, shade and finish kernels
             hits = tj.get("l2_hit") or {}
             l2_hit = {k: v for k, v in hits.items() if re.search(r"wf_(trace|shade|finish)", k)} or None

@@ -35,10 +35,14 @@ def main():
     line = json.loads(open(bench_json).read().strip().splitlines()[-1])
     cfg = line["config"]
     per_launch = bench.read_traffic(csvs.split(","), bench.traffic_key(line["roofline"]["kernel"]))
+    # every timed kernel of the line (the dominant one can change between runs)
+    by_kernel = {k["kernel"]: bench.read_traffic(csvs.split(","), bench.traffic_key(k["kernel"]))
+                 for k in line["roofline"].get("kernels", [])}
     res = {
         "kernel": line["roofline"]["kernel"],
         "config": [cfg["scene"], cfg["width"], cfg["height"], cfg["spp"], cfg["max_bounces"]],
         "bytes_per_launch": per_launch,
+        "bytes_per_launch_by_kernel": by_kernel,
         "algorithmic_bytes_per_launch": line["roofline"]["bytes_per_launch"],
         "source": "rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE, per dispatch of the dominant kernel, "
                   + os.path.basename(out).split("_")[0],
