@@ -54,13 +54,30 @@ typedef struct rt_ctx rt_ctx;
 
 /* ---- scene description (caller-owned, copied by rt_scene_upload) ------------------------- */
 
+/* A decoded texture (the MTLTexture of SubMesh.swift:69-241): width x height RGBA8 texels,
+ * row-major, row 0 = the image's top row (texcoord v = 0 after the shader's flip,
+ * Raytracing.metal:416).  Base color and emission slots decode sRGB, the others are linear
+ * (the loader options of SubMesh.swift:80-97). */
+typedef struct rt_texture_desc {
+    const uint8_t* rgba8;
+    uint32_t width;
+    uint32_t height;
+} rt_texture_desc;
+
+/* Texture slot k of a submesh <-> MATERIAL_TEXTURE_* bit k of its material's textureFlags:
+ * 0 base color, 1 tangent-space normal, 2 roughness, 3 metallic, 4 AO, 5 emission, 6 opacity. */
+#define RT_TEXTURE_SLOTS 7
+
 /* One Submesh: a material group of one mesh (SubMesh.swift:18-54). Indices are u32
- * (u16 assets are widened, SubMesh.swift:243-265), three per triangle. */
+ * (u16 assets are widened, SubMesh.swift:243-265), three per triangle.  textures[k]: index into
+ * rt_scene_desc.textures for every slot whose bit is set in material.textureFlags (other
+ * entries are ignored); the AO slot is not sampled (ENABLE_AO = 0, ShaderTypes.h:155-156). */
 typedef struct rt_submesh_desc {
     const uint32_t* indices;
     uint32_t index_count;
     uint32_t _pad;
     Material material;
+    int32_t textures[8];
 } rt_submesh_desc;
 
 /* One Mesh = one instance of the two-level acceleration structure (Mesh.swift:17-68). Vertex
@@ -87,6 +104,9 @@ typedef struct rt_scene_desc {
     uint32_t light_count;
     const rt_mesh_desc* meshes;
     const Light* lights;
+    uint32_t texture_count;
+    uint32_t _pad;
+    const rt_texture_desc* textures;
 } rt_scene_desc;
 
 /* ---- context ------------------------------------------------------------------------------- */

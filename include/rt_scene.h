@@ -67,6 +67,24 @@ rt_status rt_scene_preset(const char* name, const char* asset_dir, rt_scene** ou
 
 /* Flattened description. Pointers stay valid until the scene is modified or freed. */
 rt_status rt_scene_get_desc(rt_scene* scene, rt_scene_desc* out);
+
+/* Textures (SubMesh.swift:69-241).  add_texture copies width x height RGBA8 texels (row 0 = top);
+ * load_texture decodes a PNG file (the MTKTextureLoader stand-in).  bind_texture attaches texture
+ * `texture_id` to slot `slot` (RT_TEXTURE_SLOTS order) of submesh `submesh_index` of the scene's
+ * mesh `mesh_index` (the flattened mesh order of rt_scene_get_desc), sets the slot's
+ * textureFlags bit and, for the base color slot, baseColor = 1 (SubMesh.swift:120-124).
+ * OBJ materials bind their MTL maps when the files decode: map_Kd (base color), norm / bump /
+ * map_Bump (normal), map_Pr (roughness), map_Pm (metallic), map_Ke (emission), map_d
+ * (opacity); a map that fails to load leaves its slot unbound, as the reference's loader does. */
+rt_status rt_scene_add_texture(rt_scene* scene, const uint8_t* rgba8, uint32_t width, uint32_t height, uint32_t* id);
+rt_status rt_scene_load_texture(rt_scene* scene, const char* png_path, uint32_t* id);
+rt_status rt_scene_bind_texture(rt_scene* scene, uint32_t mesh_index, uint32_t submesh_index, uint32_t slot,
+                                uint32_t texture_id);
+
+/* PNG decode into RGBA8 (row 0 = top): call with rgba8 = NULL for the size, then with a buffer
+ * of width * height * 4 bytes.  err_buf (optional) receives the reason of a failure. */
+rt_status rt_decode_png(const uint8_t* data, size_t size, uint8_t* rgba8, uint32_t* width, uint32_t* height,
+                        char* err_buf, size_t err_len);
 /* Totals for reports. */
 uint64_t rt_scene_triangle_count(const rt_scene* scene);
 

@@ -17,7 +17,8 @@ import os
 import numpy as np
 
 from . import _abi
-from ._abi import (Camera, Float3, Light, MaterialOverride, PackedFloat4x3, SceneDesc, Stats, TileSet, Uniforms,
+from ._abi import (TEXTURE_SLOTS, Camera, Float3, Light, MaterialOverride, PackedFloat4x3, SceneDesc, Stats, TextureDesc,
+                   TileSet, Uniforms,
                    f3)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -66,6 +67,21 @@ def uniforms_default(width, height, light_count=2):
     u = Uniforms()
     lib().rt_uniforms_default(width, height, light_count, C.byref(u))
     return u
+
+
+def decode_png(data):
+    """PNG bytes -> (H, W, 4) uint8 RGBA (row 0 = top), the library's texture decoder."""
+    buf = (C.c_uint8 * len(data)).from_buffer_copy(data)
+    w, h = C.c_uint32(0), C.c_uint32(0)
+    err = C.create_string_buffer(256)
+    st = lib().rt_decode_png(buf, len(data), None, C.byref(w), C.byref(h), err, 256)
+    if st != 0:
+        raise RTError(st, err.value.decode())
+    out = np.empty((h.value, w.value, 4), dtype=np.uint8)
+    st = lib().rt_decode_png(buf, len(data), out.ctypes.data, C.byref(w), C.byref(h), err, 256)
+    if st != 0:
+        raise RTError(st, err.value.decode())
+    return out
 
 
 def camera_default(width, height):
@@ -145,6 +161,26 @@ class Scene:
         _check(lib().rt_scene_add_procedural(self._h, kind.encode(), mtl_path.encode() if mtl_path else None, p, r,
                                              scale, C.byref(material_override) if material_override else None),
                scene=self._h)
+
+    def add_texture(self, rgba8):
+        """Adds an (H, W, 4) uint8 texture (row 0 = top); returns its id."""
+        a = np.ascontiguousarray(rgba8, dtype=np.uint8)
+        assert a.ndim == 3 and a.shape[2] == 4, a.shape
+        tid = C.c_uint32(0)
+        _check(lib().rt_scene_add_texture(self._h, a.ctypes.data, a.shape[1], a.shape[0], C.byref(tid)), scene=self._h)
+        return tid.value
+
+    def load_texture(self, png_path):
+        """Decodes a PNG file into the scene's textures (MTKTextureLoader stand-in); returns its id."""
+        tid = C.c_uint32(0)
+        _check(lib().rt_scene_load_texture(self._h, png_path.encode(), C.byref(tid)), scene=self._h)
+        return tid.value
+
+    def bind_texture(self, mesh_index, submesh_index, slot, texture_id):
+        """slot: 'baseColor' | 'normal' | 'roughness' | 'metallic' | 'ao' | 'emission' | 'opacity'
+        (or its index).  Sets the material's textureFlags bit (and baseColor = 1 for baseColor)."""
+        k = TEXTURE_SLOTS[slot] if isinstance(slot, str) else int(slot)
+        _check(lib().rt_scene_bind_texture(self._h, mesh_index, submesh_index, k, texture_id), scene=self._h)
 
     def set_lights(self, lights):
         arr = (Light * len(lights))(*lights)
@@ -317,6 +353,11 @@ class Renderer:
         device is True (default: the builder this renderer was created with)."""
         dev = (self.bvh_builder == "lbvh") if device is None else device
         _check((lib().rt_bvh_build_device if dev else lib().rt_bvh_build)(self._ctx), self._ctx)
+
+    def upload(self, desc):
+        """Re-uploads a scene description (rt_scene_upload) and rebuilds the BVH."""
+        _check(lib().rt_scene_upload(self._ctx, C.byref(desc)), self._ctx)
+        self.rebuild()
 
     def tile_count(self, tile_size, rank, nranks):
         ts = TileSet(tile_size, rank, nranks, 0)

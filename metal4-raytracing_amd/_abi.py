@@ -81,12 +81,20 @@ class PackedFloat4x3(C.Structure):
     _fields_ = [("columns", (C.c_float * 3) * 4)]
 
 
+class TextureDesc(C.Structure):  # rt_texture_desc
+    _fields_ = [("rgba8", C.c_void_p), ("width", C.c_uint32), ("height", C.c_uint32)]
+
+
+TEXTURE_SLOTS = {"baseColor": 0, "normal": 1, "roughness": 2, "metallic": 3, "ao": 4, "emission": 5, "opacity": 6}
+
+
 class SubmeshDesc(C.Structure):
     _fields_ = [
         ("indices", C.POINTER(C.c_uint32)),
         ("index_count", C.c_uint32),
         ("_pad", C.c_uint32),
         ("material", Material),
+        ("textures", C.c_int32 * 8),
     ]
 
 
@@ -112,6 +120,9 @@ class SceneDesc(C.Structure):
         ("light_count", C.c_uint32),
         ("meshes", C.POINTER(MeshDesc)),
         ("lights", C.POINTER(Light)),
+        ("texture_count", C.c_uint32),
+        ("_pad", C.c_uint32),
+        ("textures", C.POINTER(TextureDesc)),
     ]
 
 
@@ -201,6 +212,7 @@ EXPORTED_SYMBOLS = [
     "rt_material_override_glass", "rt_scene_new", "rt_scene_free", "rt_scene_last_error",
     "rt_scene_add_obj", "rt_scene_add_procedural", "rt_scene_set_lights", "rt_scene_set_light_intensity",
     "rt_scene_preset", "rt_scene_get_desc", "rt_scene_triangle_count", "rt_scene_joint_matrices",
+    "rt_scene_add_texture", "rt_scene_load_texture", "rt_scene_bind_texture", "rt_decode_png",
     "rt_camera_default", "rt_camera_orbit", "rt_uniforms_default", "rt_random_offsets",
 ]
 
@@ -249,6 +261,10 @@ def declare(lib):
         "rt_scene_set_light_intensity": (st, [vp, C.c_float]),
         "rt_scene_preset": (st, [C.c_char_p, C.c_char_p, P(vp), P(C.c_int32)]),
         "rt_scene_get_desc": (st, [vp, P(SceneDesc)]),
+        "rt_scene_add_texture": (st, [vp, vp, C.c_uint32, C.c_uint32, P(C.c_uint32)]),
+        "rt_scene_load_texture": (st, [vp, C.c_char_p, P(C.c_uint32)]),
+        "rt_scene_bind_texture": (st, [vp, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32]),
+        "rt_decode_png": (st, [vp, C.c_size_t, vp, P(C.c_uint32), P(C.c_uint32), C.c_char_p, C.c_size_t]),
         "rt_scene_triangle_count": (C.c_uint64, [vp]),
         "rt_scene_joint_matrices": (st, [vp, C.c_uint32, C.c_double, P(C.c_float), C.c_uint32, P(C.c_uint32)]),
         "rt_camera_default": (None, [C.c_int32, C.c_int32, P(Camera)]),

@@ -83,6 +83,8 @@ struct rt_ctx {
     // device buffers
     DevBuf d_pos, d_prev_pos, d_nrm, d_rest_pos, d_rest_nrm, d_jidx, d_jw, d_joints;
     DevBuf d_tri_info, d_inst, d_prev_inst, d_mat, d_lights, d_halton;
+    DevBuf d_tex_texels, d_tex_info, d_mat_tex, d_uv, d_tex_lut;   // texture path (textured scenes)
+    bool textured = false;
     DevBuf d_tris, d_nodes, d_node_box, d_slot_to_tri, d_levels, d_maxabs, d_tri_bin, d_lbvh_scratch;
     uint32_t num_nodes8 = 0;
     uint32_t* h_lbvh = nullptr;   // pinned word for the device builder's level counts
@@ -195,7 +197,7 @@ static size_t ctx_bytes(const rt_ctx* c) {
                            &c->d_joints, &c->d_tri_info, &c->d_inst, &c->d_prev_inst, &c->d_mat, &c->d_lights,
                            &c->d_halton, &c->d_tris, &c->d_nodes, &c->d_node_box, &c->d_slot_to_tri, &c->d_levels, &c->d_maxabs, &c->d_random,
                            &c->d_accum[0], &c->d_accum[1], &c->d_tri_bin, &c->d_lbvh_scratch,
-                           };
+                           &c->d_tex_texels, &c->d_tex_info, &c->d_mat_tex, &c->d_uv, &c->d_tex_lut};
     size_t s = 0;
     for (auto* b : all) s += b->bytes;
     for (const DevBuf& b : c->d_motion) s += b.bytes;
@@ -350,7 +352,8 @@ rt_status rt_destroy(rt_ctx* c) {
     DevBuf* all[] = {&c->d_pos, &c->d_prev_pos, &c->d_nrm, &c->d_rest_pos, &c->d_rest_nrm, &c->d_jidx, &c->d_jw,
                      &c->d_joints, &c->d_tri_info, &c->d_inst, &c->d_prev_inst, &c->d_mat, &c->d_lights, &c->d_halton,
                      &c->d_tris, &c->d_nodes, &c->d_node_box, &c->d_slot_to_tri, &c->d_levels, &c->d_maxabs, &c->d_random, &c->d_accum[0],
-                     &c->d_accum[1], &c->d_tri_bin, &c->d_lbvh_scratch};
+                     &c->d_accum[1], &c->d_tri_bin, &c->d_lbvh_scratch, &c->d_tex_texels, &c->d_tex_info,
+                     &c->d_mat_tex, &c->d_uv, &c->d_tex_lut};
     for (auto* b : all) dev_free(*b);
     for (DevBuf& b : c->d_motion) dev_free(b);
     if (c->h_lbvh) hipHostFree(c->h_lbvh);
@@ -384,6 +387,62 @@ rt_status rt_set_stream(rt_ctx* c, void* s) {
     return RT_OK;
 }
 
+// Texture path: the texel pool, its table, every material slot's texture
+// ids and the per-vertex UVs (Model.vertexDescriptor's zero default when a mesh has none,
+// Model.swift:329-333).  Nothing is uploaded for an untextured scene.
+static rt_status upload_textures(rt_ctx* c, const rt_scene_desc* sd) {
+    const uint32_t slots = (uint32_t)c->max_sub * sd->mesh_count;
+    std::vector<int4> mt(2 * (size_t)slots, make_int4(0, -1, -1, -1));
+    bool textured = false;
+    for (uint32_t m = 0; m < sd->mesh_count; ++m)
+        for (uint32_t s = 0; s < sd->meshes[m].submesh_count; ++s) {
+            const rt_submesh_desc& sm = sd->meshes[m].submeshes[s];
+            uint32_t flags = sm.material.textureFlags & ~(1u << 4);   // ENABLE_AO = 0
+            if (!flags) continue;
+            textured = true;
+            int t[8];
+            for (int k = 0; k < 8; ++k) t[k] = (k < RT_TEXTURE_SLOTS && (flags >> k & 1u)) ? sm.textures[k] : -1;
+            const size_t slot = (size_t)m * c->max_sub + s;
+            mt[2 * slot] = make_int4((int)flags, t[0], t[1], t[2]);
+            mt[2 * slot + 1] = make_int4(t[3], t[4], t[5], t[6]);
+        }
+    c->textured = textured;
+    if (!textured) return RT_OK;
+    std::vector<uint4> info(sd->texture_count);
+    std::vector<uint8_t> texels;
+    uint64_t off = 0;
+    for (uint32_t t = 0; t < sd->texture_count; ++t) {
+        const rt_texture_desc& td = sd->textures[t];
+        info[t] = make_uint4((uint32_t)off, td.width, td.height, 0u);
+        off += (uint64_t)td.width * td.height;
+    }
+    texels.resize(off * 4);
+    for (uint32_t t = 0; t < sd->texture_count; ++t)
+        std::memcpy(&texels[4 * (size_t)info[t].x], sd->textures[t].rgba8, 4 * (size_t)info[t].y * info[t].z);
+    std::vector<float2> uv(c->num_verts, make_float2(0.0f, 0.0f));
+    uint32_t vbase = 0;
+    for (uint32_t m = 0; m < sd->mesh_count; ++m) {
+        const rt_mesh_desc& md = sd->meshes[m];
+        if (md.uvs)
+            for (uint32_t v = 0; v < md.vertex_count; ++v) uv[vbase + v] = make_float2(md.uvs[v].x, md.uvs[v].y);
+        vbase += md.vertex_count;
+    }
+    // texel byte -> float: [0, 256) linear b / 255, [256, 512) sRGB EOTF (MTKTextureLoader .SRGB)
+    float lut[512];
+    for (int b = 0; b < 256; ++b) {
+        const double v = b / 255.0;
+        lut[b] = (float)v;
+        lut[256 + b] = (float)(v <= 0.04045 ? v / 12.92 : std::pow((v + 0.055) / 1.055, 2.4));
+    }
+    rt_status st;
+    if ((st = dev_upload(c, c->d_tex_texels, texels.data(), texels.size()))) return st;
+    if ((st = dev_upload(c, c->d_tex_info, info.data(), info.size() * sizeof(uint4)))) return st;
+    if ((st = dev_upload(c, c->d_mat_tex, mt.data(), mt.size() * sizeof(int4)))) return st;
+    if ((st = dev_upload(c, c->d_uv, uv.data(), uv.size() * sizeof(float2)))) return st;
+    if ((st = dev_upload(c, c->d_tex_lut, lut, sizeof lut))) return st;
+    return RT_OK;
+}
+
 rt_status rt_scene_upload(rt_ctx* c, const rt_scene_desc* sd) {
     if (!c || !sd) FAIL(c, RT_ERR_INVALID_ARG, "null argument");
     if (rt_status dst = drain_frames(c)) return dst;
@@ -405,14 +464,23 @@ rt_status rt_scene_upload(rt_ctx* c, const rt_scene_desc* sd) {
             const rt_submesh_desc& sm = md.submeshes[s];
             if (sm.index_count % 3) FAIL(c, RT_ERR_INVALID_ARG, "index count not a multiple of 3");
             if (sm.index_count && !sm.indices) FAIL(c, RT_ERR_INVALID_ARG, "null indices");
-            if (sm.material.textureFlags != 0)
-                FAIL(c, RT_ERR_UNSUPPORTED, "textured materials are not supported yet (SURVEY §8f rank 2)");
+            for (int k = 0; k < RT_TEXTURE_SLOTS; ++k)
+                if (k != 4 && (sm.material.textureFlags >> k & 1u) &&   // the AO slot is never sampled
+                    (sm.textures[k] < 0 || (uint32_t)sm.textures[k] >= sd->texture_count || !sd->textures))
+                    FAIL(c, RT_ERR_INVALID_ARG, "textured material without a valid texture for a flagged slot");
             for (uint32_t i = 0; i < sm.index_count; ++i)
                 if (sm.indices[i] >= md.vertex_count) FAIL(c, RT_ERR_INVALID_ARG, "index out of range");
             nt += sm.index_count / 3;
         }
     }
     if (nt >= (1ull << 31) || nv >= (1ull << 32)) FAIL(c, RT_ERR_UNSUPPORTED, "scene too large");
+    uint64_t ntexels = 0;
+    for (uint32_t t = 0; t < sd->texture_count; ++t) {
+        const rt_texture_desc& td = sd->textures[t];
+        if (!td.rgba8 || td.width == 0 || td.height == 0) FAIL(c, RT_ERR_INVALID_ARG, "bad texture");
+        ntexels += (uint64_t)td.width * td.height;
+    }
+    if (ntexels >= (1ull << 32)) FAIL(c, RT_ERR_UNSUPPORTED, "texture pool above 2^32 texels");
     c->max_sub = max_sub;
     c->num_inst = sd->mesh_count;
     c->num_tris = (uint32_t)nt;
@@ -466,6 +534,7 @@ rt_status rt_scene_upload(rt_ctx* c, const rt_scene_desc* sd) {
     }
     c->h_lights.assign(sd->lights, sd->lights + sd->light_count);
     rt_status st;
+    if ((st = upload_textures(c, sd))) return st;
     if ((st = dev_upload(c, c->d_pos, c->h_pos.data(), nv * 16))) return st;
     if ((st = dev_upload(c, c->d_prev_pos, c->h_pos.data(), nv * 16))) return st;  // previousPositions = positions (SubMesh.swift:60)
     if ((st = dev_upload(c, c->d_nrm, c->h_nrm.data(), nv * 16))) return st;
@@ -826,6 +895,14 @@ rt_status rt_render_frame(rt_ctx* c, const Uniforms* U, const rt_tile_set* tiles
     S.num_materials = (int)c->h_mat.size();
     S.num_tris = (int)c->num_tris;
     S.num_nodes8 = (int)c->num_nodes8;
+    S.textured = c->textured ? 1 : 0;
+    if (c->textured) {
+        S.tex_texels = (const uchar4*)c->d_tex_texels.p;
+        S.tex_info = (const uint4*)c->d_tex_info.p;
+        S.mat_tex = (const int4*)c->d_mat_tex.p;
+        S.uv = (const float2*)c->d_uv.p;
+        S.tex_lut = (const float*)c->d_tex_lut.p;
+    }
     const int m_prev = c->motion_cur, m_out = wavefront ? (c->motion_cur + 1) % kMotionTargets : c->motion_cur;
     FrameParams P;
     P.U = *U;

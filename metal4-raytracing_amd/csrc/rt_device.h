@@ -38,6 +38,13 @@ struct DevScene {
     int num_materials;         // instances * max_submeshes
     int num_tris;
     int num_nodes8;
+    // texture path, set for textured scenes only (textured != 0)
+    const uchar4* tex_texels = nullptr;   // RGBA8 pool, each texture row-major from its top row
+    const uint4* tex_info = nullptr;      // per texture: (first texel, width, height, 0)
+    const int4* mat_tex = nullptr;        // per material slot: (flags, t0, t1, t2), (t3, t4, t5, t6)
+    const float2* uv = nullptr;           // per vertex
+    const float* tex_lut = nullptr;       // byte -> float: [0, 256) linear, [256, 512) sRGB
+    int textured = 0;
 };
 
 struct Hit {

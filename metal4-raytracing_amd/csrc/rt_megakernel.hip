@@ -115,7 +115,7 @@ megakernel(DevScene S, FrameParams P) {
 }
 
 void launch_megakernel(const DevScene& S, const FrameParams& P, int nblocks, bool count, hipStream_t stream) {
-    const bool full = needs_full(P.U);
+    const bool full = needs_full(P.U, S);
     if (count) {
         if (full) hipLaunchKernelGGL((megakernel<true, true>), dim3(nblocks), dim3(kBlock), 0, stream, S, P);
         else hipLaunchKernelGGL((megakernel<true, false>), dim3(nblocks), dim3(kBlock), 0, stream, S, P);

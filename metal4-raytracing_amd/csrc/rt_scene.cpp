@@ -76,6 +76,22 @@ struct Submesh {
     std::string material_name;
     std::vector<uint32_t> indices;
     Material material;
+    int32_t tex[8] = {-1, -1, -1, -1, -1, -1, -1, -1};   // scene texture per slot (RT_TEXTURE_SLOTS)
+    std::string tex_path[RT_TEXTURE_SLOTS];                // MTL maps, bound by rt_scene_add_obj
+};
+
+// MTL map statements -> texture slot (ModelIO's material semantics, SubMesh.swift:117-166)
+static int map_slot(const char* key) {
+    static const struct { const char* k; int slot; } kMaps[] = {
+        {"map_Kd", 0}, {"norm", 1}, {"bump", 1}, {"map_Bump", 1}, {"map_bump", 1}, {"map_Pr", 2},
+        {"map_Pm", 3}, {"map_Ke", 5}, {"map_d", 6}};
+    for (const auto& m : kMaps)
+        if (!std::strcmp(key, m.k)) return m.slot;
+    return -1;
+}
+struct MtlEntry {
+    Material material;
+    std::string maps[RT_TEXTURE_SLOTS];
 };
 
 struct Skin {
@@ -122,12 +138,17 @@ static void apply_override(Material& m, const rt_material_override* ov) {
     if (ov->has_opacity) m.opacity = std::min(std::max(ov->opacity, 0.0f), 1.0f);
 }
 
+static std::string dir_of(const std::string& p) {
+    size_t s = p.find_last_of('/');
+    return s == std::string::npos ? std::string(".") : p.substr(0, s);
+}
+
 // ---- MTL -------------------------------------------------------------------------------------
-static bool parse_mtl(const std::string& path, std::map<std::string, Material>& out) {
+static bool parse_mtl(const std::string& path, std::map<std::string, MtlEntry>& out) {
     FILE* f = std::fopen(path.c_str(), "r");
     if (!f) return false;
     char line[4096];
-    Material* cur = nullptr;
+    MtlEntry* ent = nullptr;
     while (std::fgets(line, sizeof line, f)) {
         char* p = line;
         while (*p == ' ' || *p == '\t') ++p;
@@ -138,9 +159,20 @@ static bool parse_mtl(const std::string& path, std::map<std::string, Material>& 
         if (!std::strcmp(key, "newmtl")) {
             char name[1024] = {0};
             std::sscanf(rest, " %1023[^\r\n]", name);
-            out[name] = default_material();
-            cur = &out[name];
-        } else if (cur) {
+            out[name].material = default_material();
+            ent = &out[name];
+        } else if (ent) {
+            Material* cur = &ent->material;
+            const int slot = map_slot(key);
+            if (slot >= 0) {   // the file name is the statement's last token (options come first)
+                std::string r(rest);
+                while (!r.empty() && (r.back() == '\n' || r.back() == '\r' || r.back() == ' ' || r.back() == '\t'))
+                    r.pop_back();
+                size_t sp = r.find_last_of(" \t");
+                std::string file = sp == std::string::npos ? r : r.substr(sp + 1);
+                if (!file.empty()) ent->maps[slot] = file[0] == '/' ? file : dir_of(path) + "/" + file;
+                continue;
+            }
             float a = 0, b = 0, c = 0;
             int k = std::sscanf(rest, "%f %f %f", &a, &b, &c);
             if (!std::strcmp(key, "Kd") && k >= 3) cur->baseColor = f3(a, b, c);
@@ -149,16 +181,10 @@ static bool parse_mtl(const std::string& path, std::map<std::string, Material>& 
             else if (!std::strcmp(key, "Ni") && k >= 1) cur->refractionIndex = a;
             else if (!std::strcmp(key, "d") && k >= 1) cur->opacity = std::min(std::max(a, 0.0f), 1.0f);
             else if (!std::strcmp(key, "Tr") && k >= 1) cur->opacity = std::min(std::max(1.0f - a, 0.0f), 1.0f);
-            // map_* texture statements: texture path is §8f "next"; textureFlags stay 0.
         }
     }
     std::fclose(f);
     return true;
-}
-
-static std::string dir_of(const std::string& p) {
-    size_t s = p.find_last_of('/');
-    return s == std::string::npos ? std::string(".") : p.substr(0, s);
 }
 
 // ---- OBJ -------------------------------------------------------------------------------------
@@ -176,7 +202,7 @@ static bool load_obj(const std::string& path, std::vector<Mesh>& meshes, std::st
     FILE* f = std::fopen(path.c_str(), "r");
     if (!f) { err = "cannot open " + path; return false; }
     std::vector<float> V, VT, VN;
-    std::map<std::string, Material> mtl;
+    std::map<std::string, MtlEntry> mtl;
     Mesh* mesh = nullptr;
     std::unordered_map<ObjKey, uint32_t, ObjKeyHash> dedup;
     std::map<std::string, size_t> sub_of;
@@ -198,7 +224,9 @@ static bool load_obj(const std::string& path, std::vector<Mesh>& meshes, std::st
             Submesh s;
             s.material_name = cur_mtl;
             auto mi = mtl.find(cur_mtl);
-            s.material = (mi != mtl.end()) ? mi->second : default_material();
+            s.material = (mi != mtl.end()) ? mi->second.material : default_material();
+            if (mi != mtl.end())
+                for (int k = 0; k < RT_TEXTURE_SLOTS; ++k) s.tex_path[k] = mi->second.maps[k];
             mesh->submeshes.push_back(s);
             cur_sub = mesh->submeshes.size() - 1;
             sub_of[cur_mtl] = cur_sub;
@@ -583,10 +611,58 @@ struct rt_scene {
     std::vector<Model> models;
     std::vector<Light> lights;
     std::string err;
+    struct Texture {
+        std::vector<uint8_t> texels;   // RGBA8, row 0 = top
+        uint32_t w = 0, h = 0;
+        std::string path;              // file it was decoded from (dedup of MTL maps)
+    };
+    std::vector<Texture> textures;
     // flattened description caches
     std::vector<rt_mesh_desc> mesh_descs;
     std::vector<std::vector<rt_submesh_desc>> sub_descs;
+    std::vector<rt_texture_desc> tex_descs;
 };
+
+// Texture binding of one submesh slot (SubMesh.swift:117-166): flag bit + texture, and the base
+// color map replaces baseColor by white (:120-124).
+static void bind_slot(Submesh& sm, int slot, uint32_t id) {
+    sm.tex[slot] = (int32_t)id;
+    sm.material.textureFlags |= 1u << slot;
+    if (slot == 0) sm.material.baseColor = f3(1.0f, 1.0f, 1.0f);
+}
+
+static rt_status load_png_file(rt_scene* s, const std::string& path, uint32_t* id) {
+    for (size_t i = 0; i < s->textures.size(); ++i)
+        if (!s->textures[i].path.empty() && s->textures[i].path == path) {
+            *id = (uint32_t)i;
+            return RT_OK;
+        }
+    FILE* f = std::fopen(path.c_str(), "rb");
+    if (!f) {
+        s->err = "cannot open " + path;
+        return RT_ERR_IO;
+    }
+    std::vector<uint8_t> data;
+    uint8_t buf[1 << 16];
+    size_t n;
+    while ((n = std::fread(buf, 1, sizeof buf, f)) > 0) data.insert(data.end(), buf, buf + n);
+    std::fclose(f);
+    rt_scene::Texture t;
+    char eb[256] = {0};
+    rt_status st = rt_decode_png(data.data(), data.size(), nullptr, &t.w, &t.h, eb, sizeof eb);
+    if (!st) {
+        t.texels.resize((size_t)t.w * t.h * 4);
+        st = rt_decode_png(data.data(), data.size(), t.texels.data(), &t.w, &t.h, eb, sizeof eb);
+    }
+    if (st) {
+        s->err = path + ": " + eb;
+        return st;
+    }
+    t.path = path;
+    s->textures.push_back(std::move(t));
+    *id = (uint32_t)(s->textures.size() - 1);
+    return RT_OK;
+}
 
 static Light area_light_default() {  // Scene.setupLight (Scene.swift:161-169)
     Light l;
@@ -652,6 +728,13 @@ rt_status rt_scene_add_obj(rt_scene* s, const char* obj_path, const float positi
     model.scale = scale;
     std::string err;
     if (!load_obj(obj_path, model.meshes, err)) { s->err = err; return RT_ERR_IO; }
+    for (auto& m : model.meshes)   // MTL maps; one that fails to load stays unbound (SubMesh.swift:100-107)
+        for (auto& sm : m.submeshes)
+            for (int k = 0; k < RT_TEXTURE_SLOTS; ++k) {
+                uint32_t id;
+                if (!sm.tex_path[k].empty() && load_png_file(s, sm.tex_path[k], &id) == RT_OK) bind_slot(sm, k, id);
+            }
+    s->err.clear();
     finish_model(s, std::move(model), ov);
     return RT_OK;
 }
@@ -685,9 +768,9 @@ rt_status rt_scene_add_procedural(rt_scene* s, const char* kind, const char* mtl
         return RT_ERR_INVALID_ARG;
     }
     if (mtl_path) {
-        std::map<std::string, Material> mtl;
+        std::map<std::string, MtlEntry> mtl;
         if (!parse_mtl(mtl_path, mtl) || mtl.empty()) { s->err = std::string("cannot read ") + mtl_path; return RT_ERR_IO; }
-        model.meshes[0].submeshes[0].material = mtl.begin()->second;
+        model.meshes[0].submeshes[0].material = mtl.begin()->second.material;
     }
     finish_model(s, std::move(model), ov);
     return RT_OK;
@@ -799,6 +882,7 @@ rt_status rt_scene_get_desc(rt_scene* s, rt_scene_desc* out) {
                 d.indices = sm.indices.data();
                 d.index_count = (uint32_t)sm.indices.size();
                 d.material = sm.material;
+                for (int k = 0; k < 8; ++k) d.textures[k] = sm.tex[k];
                 subs.push_back(d);
             }
             s->sub_descs.push_back(std::move(subs));
@@ -825,7 +909,60 @@ rt_status rt_scene_get_desc(rt_scene* s, rt_scene_desc* out) {
     out->meshes = s->mesh_descs.data();
     out->light_count = (uint32_t)s->lights.size();
     out->lights = s->lights.data();
+    s->tex_descs.clear();
+    for (auto& t : s->textures) {
+        rt_texture_desc d;
+        d.rgba8 = t.texels.data();
+        d.width = t.w;
+        d.height = t.h;
+        s->tex_descs.push_back(d);
+    }
+    out->texture_count = (uint32_t)s->tex_descs.size();
+    out->_pad = 0;
+    out->textures = s->tex_descs.data();
     return RT_OK;
+}
+
+rt_status rt_scene_add_texture(rt_scene* s, const uint8_t* rgba8, uint32_t width, uint32_t height, uint32_t* id) {
+    if (!s || !rgba8 || !id) return RT_ERR_INVALID_ARG;
+    if (width == 0 || height == 0 || (uint64_t)width * height > (1ull << 28)) {
+        s->err = "bad texture size";
+        return RT_ERR_INVALID_ARG;
+    }
+    rt_scene::Texture t;
+    t.w = width;
+    t.h = height;
+    t.texels.assign(rgba8, rgba8 + (size_t)width * height * 4);
+    s->textures.push_back(std::move(t));
+    *id = (uint32_t)(s->textures.size() - 1);
+    return RT_OK;
+}
+
+rt_status rt_scene_load_texture(rt_scene* s, const char* png_path, uint32_t* id) {
+    if (!s || !png_path || !id) return RT_ERR_INVALID_ARG;
+    return load_png_file(s, png_path, id);
+}
+
+rt_status rt_scene_bind_texture(rt_scene* s, uint32_t mesh_index, uint32_t submesh_index, uint32_t slot,
+                                uint32_t texture_id) {
+    if (!s) return RT_ERR_INVALID_ARG;
+    if (slot >= RT_TEXTURE_SLOTS || texture_id >= s->textures.size()) {
+        s->err = "bad texture slot / id";
+        return RT_ERR_INVALID_ARG;
+    }
+    uint32_t k = 0;
+    for (auto& model : s->models)
+        for (auto& m : model.meshes) {
+            if (k++ != mesh_index) continue;
+            if (submesh_index >= m.submeshes.size()) {
+                s->err = "bad submesh index";
+                return RT_ERR_INVALID_ARG;
+            }
+            bind_slot(m.submeshes[submesh_index], (int)slot, texture_id);
+            return RT_OK;
+        }
+    s->err = "bad mesh index";
+    return RT_ERR_INVALID_ARG;
 }
 
 uint64_t rt_scene_triangle_count(const rt_scene* s) {

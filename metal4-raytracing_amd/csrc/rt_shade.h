@@ -74,13 +74,60 @@ struct StepResult {
 
 __device__ __forceinline__ f3 ldf3(const rt_float3& v) { return mk3(v.x, v.y, v.z); }
 
-__host__ __device__ __forceinline__ bool needs_full(const Uniforms& U) {
-    return U.debugTextureMode != DebugTextureModeNone || U.enableDenoiseGBuffer != 0;
+// ---- texture path --------------------------------------------------------
+// The reference samples with sampler(linear, linear, mip linear, address::repeat) in a compute
+// kernel, i.e. bilinear from LOD 0 (Raytracing.metal:420).  Here: texel centres at integer + 0.5,
+// wrap-around neighbours, each corner decoded through the byte table (sRGB for base color and
+// emission maps, linear otherwise; alpha always linear), weights applied in a fixed order.
+__device__ __forceinline__ float4 tex_sample(const DevScene& S, int t, f2 uv, bool srgb) {
+    const uint4 ti = S.tex_info[t];
+    const int w = (int)ti.y, h = (int)ti.z;
+    float x = uv.x * (float)w - 0.5f, y = uv.y * (float)h - 0.5f;
+    if (!(fabsf(x) < 1.0e9f)) x = 0.0f;   // NaN / huge coordinates
+    if (!(fabsf(y) < 1.0e9f)) y = 0.0f;
+    const float fx = floorf(x), fy = floorf(y);
+    const float ax = x - fx, ay = y - fy, bx = 1.0f - ax, by = 1.0f - ay;
+    int x0 = (int)((long long)fx % w), y0 = (int)((long long)fy % h);
+    if (x0 < 0) x0 += w;
+    if (y0 < 0) y0 += h;
+    const int x1 = x0 + 1 == w ? 0 : x0 + 1, y1 = y0 + 1 == h ? 0 : y0 + 1;
+    const uchar4* T = S.tex_texels + ti.x;
+    const uchar4 c00 = T[(size_t)y0 * w + x0], c10 = T[(size_t)y0 * w + x1];
+    const uchar4 c01 = T[(size_t)y1 * w + x0], c11 = T[(size_t)y1 * w + x1];
+    const float* L = S.tex_lut;
+    const float* Lc = L + (srgb ? 256 : 0);
+    auto bil = [&](const float* lut, unsigned a, unsigned b, unsigned c, unsigned d) {
+        return (lut[a] * bx + lut[b] * ax) * by + (lut[c] * bx + lut[d] * ax) * ay;
+    };
+    return make_float4(bil(Lc, c00.x, c10.x, c01.x, c11.x), bil(Lc, c00.y, c10.y, c01.y, c11.y),
+                       bil(Lc, c00.z, c10.z, c01.z, c11.z), bil(L, c00.w, c10.w, c01.w, c11.w));
+}
+
+__device__ __forceinline__ f2 ld2(const float2& v) { return f2{v.x, v.y}; }
+
+// computeTangentBasis (Raytracing.metal:185-218): object-space dP/du, dP/dv of the hit triangle
+// from its vertices in the order (indices[3t+1], indices[3t+2], indices[3t]).
+__device__ __forceinline__ bool tangent_basis(const DevScene& S, const uint4& ti, f3& tangent, f3& bitangent) {
+    const f3 p0 = ld3(S.pos[ti.y]), p1 = ld3(S.pos[ti.z]), p2 = ld3(S.pos[ti.x]);
+    const f2 uv0 = ld2(S.uv[ti.y]), uv1 = ld2(S.uv[ti.z]), uv2 = ld2(S.uv[ti.x]);
+    const f3 e1 = p1 - p0, e2 = p2 - p0;
+    const float d1x = uv1.x - uv0.x, d1y = uv1.y - uv0.y, d2x = uv2.x - uv0.x, d2y = uv2.y - uv0.y;
+    const float denom = d1x * d2y - d1y * d2x;
+    if (fabsf(denom) < 1e-8f) return false;
+    const float r = 1.0f / denom;
+    tangent = (e1 * d2y - e2 * d1y) * r;
+    bitangent = (e2 * d1x - e1 * d2x) * r;
+    return length(tangent) > 1e-8f && length(bitangent) > 1e-8f;
+}
+
+__host__ __device__ __forceinline__ bool needs_full(const Uniforms& U, const DevScene& S) {
+    return U.debugTextureMode != DebugTextureModeNone || U.enableDenoiseGBuffer != 0 || S.textured != 0;
 }
 
 // prevMotion / hadPrimaryHit / motionVector: only read by DebugTextureModeMotion.
-// FULL = false compiles out the debug-visualisation and G-buffer branches (the caller selects
-// FULL = true whenever uniforms.debugTextureMode != 0 or enableDenoiseGBuffer != 0).
+// FULL = false compiles out the texture maps, the debug-visualisation and the G-buffer branches
+// (the caller selects FULL = true whenever the scene is textured, uniforms.debugTextureMode != 0
+// or enableDenoiseGBuffer != 0).
 template <bool FULL>
 __device__ __forceinline__ void shade_step(const DevScene& S, const Uniforms& U, const ShadeTabs& halton, int hidx,
                                            int sampleIndex, f3& rayO, f3& rayD, const Hit& h, PathRegs& p,
@@ -133,16 +180,52 @@ __device__ __forceinline__ void shade_step(const DevScene& S, const Uniforms& U,
     if (length(objN) < 1e-10f) Ng = -rayD;                                            // :395-397
 
     f3 albedo = ld3(mat.base);                                                        // :399
-    // textureFlags == 0 for every uploaded material (rt_scene_upload rejects others)
-    const float roughness = 1.0f, metallic = 0.0f, ao = 1.0f;                         // :431-446
+    float roughness = 1.0f, metallic = 0.0f;                                          // :431-441
+    const float ao = 1.0f;                                                            // :443-446 (ENABLE_AO 0)
     float opacity = clampf(mat.base.w, 0.0f, 1.0f);                                   // :448
     f3 emission = ld3(mat.emis);                                                      // :453
+    // texture maps (:400-456): FULL kernels only (the caller selects FULL for textured scenes)
+    unsigned tflags = 0;
+    int tnormal = -1;
+    f2 tc = f2{0.0f, 0.0f};
+    float4 bsample = make_float4(1.0f, 1.0f, 1.0f, 1.0f);
+    if (FULL && S.textured) {
+        const int slot = instanceIndex * S.max_submeshes + geometryIndex;
+        const int4 t0 = S.mat_tex[2 * slot], t1 = S.mat_tex[2 * slot + 1];
+        tflags = (unsigned)t0.x;
+        tnormal = t0.z;
+        if (tflags) {                                                                 // :412-417
+            const f2 a = ld2(S.uv[ti.y]), b = ld2(S.uv[ti.z]), c = ld2(S.uv[ti.x]);
+            tc.x = (bu * a.x + bv * b.x) + bw * c.x;
+            tc.y = (bu * a.y + bv * b.y) + bw * c.y;
+            tc.y = 1.0f - tc.y;
+        }
+        if (tflags & MATERIAL_TEXTURE_BASECOLOR) {                                    // :423-428
+            bsample = tex_sample(S, t0.y, tc, true);
+            albedo = albedo * mk3(bsample.x, bsample.y, bsample.z);
+        }
+        if (tflags & MATERIAL_TEXTURE_ROUGHNESS) roughness = tex_sample(S, t0.w, tc, false).x;   // :431-434
+        if (tflags & MATERIAL_TEXTURE_METALLIC) metallic = tex_sample(S, t1.x, tc, false).x;     // :436-439
+        if (tflags & MATERIAL_TEXTURE_OPACITY) opacity = opacity * tex_sample(S, t1.w, tc, false).x;  // :448-451
+        if (tflags & MATERIAL_TEXTURE_EMISSION) {                                     // :453-456
+            const float4 e = tex_sample(S, t1.z, tc, true);
+            emission = mk3(e.x, e.y, e.z);
+        }
+    }
 
     if (FULL && U.debugTextureMode != DebugTextureModeNone) {                         // :459-490
         f3 dc = mk3(0.0f, 0.0f, 0.0f);
         int m = U.debugTextureMode;
-        if (m == DebugTextureModeBaseColor) dc = mk3(1.0f, 0.0f, 1.0f);
-        else if (m == DebugTextureModeNormal) dc = Ng * 0.5f + mk3(0.5f, 0.5f, 0.5f);
+        if (m == DebugTextureModeBaseColor)
+            dc = (tflags & MATERIAL_TEXTURE_BASECOLOR) ? mk3(bsample.x, bsample.y, bsample.z) : mk3(1.0f, 0.0f, 1.0f);
+        else if (m == DebugTextureModeNormal) {
+            if (tflags & MATERIAL_TEXTURE_NORMAL) {
+                const float4 nm = tex_sample(S, tnormal, tc, false);
+                dc = mk3(nm.x, nm.y, nm.z);
+            } else {
+                dc = Ng * 0.5f + mk3(0.5f, 0.5f, 0.5f);
+            }
+        }
         else if (m == DebugTextureModeRoughness) dc = mk3(roughness, roughness, roughness);
         else if (m == DebugTextureModeMetallic) dc = mk3(metallic, metallic, metallic);
         else if (m == DebugTextureModeAO) dc = mk3(1.0f, 0.0f, 1.0f);
@@ -157,7 +240,18 @@ __device__ __forceinline__ void shade_step(const DevScene& S, const Uniforms& U,
         return;  // break
     }
 
-    f3 shadingNormal = Ng;                                                            // :492 (no normal map)
+    f3 shadingNormal = Ng;                                                            // :492
+    if (FULL && (tflags & MATERIAL_TEXTURE_NORMAL)) {                                 // :493-504
+        f3 tangent, bitangent;
+        if (tangent_basis(S, ti, tangent, bitangent)) {
+            f3 worldT = xform(M, tangent, 0.0f);
+            worldT = normalize(worldT - Ng * dot(worldT, Ng));
+            const f3 worldB = normalize(cross(Ng, worldT));
+            const float4 nm = tex_sample(S, tnormal, tc, false);
+            const f3 n = mk3(nm.x * 2.0f - 1.0f, nm.y * 2.0f - 1.0f, nm.z * 2.0f - 1.0f);
+            shadingNormal = normalize((n.x * worldT + n.y * worldB) + n.z * Ng);
+        }
+    }
 
     if (FULL && gbuf_pending && U.enableDenoiseGBuffer != 0 && sampleIndex == 0) {   // :506-515
         float rr = clampf(roughness, 0.0f, 1.0f);

@@ -2094,7 +2094,7 @@ bool run_wavefront(const DevScene& S, const FrameParams& P, WavefrontBuffers& W,
         WF_CHECK(hipMemcpyAsync(W.d_params, &W.h_params[slot], sizeof(FrameParams), hipMemcpyHostToDevice, stream));
         WF_CHECK(hipEventRecord(W.param_ev[slot], stream));
     }
-    const bool full = needs_full(P.U);
+    const bool full = needs_full(P.U, S);
     const int maxExtra = (P.U.enableMotionAdaptiveSampling != 0) ? max(P.U.motionSamplingMaxExtraSamples, 0) : 0;
     if (dev)
         return enqueue_wavefront(S, P, Q, count, full, maxExtra, extra_pass, stream, prev_done, *tl, err);

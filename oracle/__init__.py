@@ -73,6 +73,8 @@ def lib():
         L.rt_oracle_skin.restype = None
         L.rt_oracle_scene_set_previous.argtypes = [vp, C.c_uint32, vp, vp]
         L.rt_oracle_scene_set_previous.restype = C.c_int
+        L.rt_oracle_tex_sample.argtypes = [vp, C.c_int32, C.c_float, C.c_float, C.c_int32, FP]
+        L.rt_oracle_tex_sample.restype = C.c_int
         _lib = L
     return _lib
 
@@ -102,6 +104,12 @@ class OracleScene:
     @property
     def triangles(self):
         return int(lib().rt_oracle_scene_triangles(self._h))
+
+    def tex_sample(self, tex, u, v, srgb=False):
+        out = (C.c_float * 4)()
+        if lib().rt_oracle_tex_sample(self._h, tex, u, v, 1 if srgb else 0, out) != 0:
+            raise ValueError("bad texture")
+        return np.array(list(out), dtype=np.float32)
 
     def intersect(self, o, d, tmin=0.0, tmax=float("inf"), any_hit=False, brute=False):
         fo = (C.c_float * 3)(*o)

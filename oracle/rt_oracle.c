@@ -114,6 +114,12 @@ struct rt_oracle_scene {
     const rt_float3** prev_pos;
     Material** mats;       /* [mesh][sub] */
     Light* lights;
+    /* texture path (SubMesh.swift:69-241, Raytracing.metal:399-504) */
+    const rt_float2** uv;  /* per mesh, NULL = zero UVs (Model.swift:329-333) */
+    int32_t (**mtex)[8];   /* [mesh][sub] texture per slot */
+    const rt_texture_desc* tex;
+    uint32_t ntex;
+    float lut[512];        /* byte -> float: linear, then sRGB */
 };
 
 /* object->world: ((c0*x + c1*y) + c2*z) + c3*w with the MTLPackedFloat4x3 columns
@@ -203,6 +209,15 @@ int rt_oracle_scene_create(const rt_scene_desc* d, rt_oracle_scene** out) {
     s->xf = calloc(s->nmesh, sizeof(float[12]));
     s->prev_xf = calloc(s->nmesh, sizeof(float[12]));
     s->mats = (Material**)calloc(s->nmesh, sizeof(Material*));
+    s->uv = (const rt_float2**)calloc(s->nmesh, sizeof(void*));
+    s->mtex = calloc(s->nmesh, sizeof(*s->mtex));
+    s->tex = d->textures;
+    s->ntex = d->texture_count;
+    for (int b = 0; b < 256; ++b) {   /* MTKTextureLoader .SRGB true / false (SubMesh.swift:80-97) */
+        double v = b / 255.0;
+        s->lut[b] = (float)v;
+        s->lut[256 + b] = (float)(v <= 0.04045 ? v / 12.92 : pow((v + 0.055) / 1.055, 2.4));
+    }
     uint32_t n = 0;
     for (uint32_t m = 0; m < s->nmesh; ++m)
         for (uint32_t k = 0; k < d->meshes[m].submesh_count; ++k) n += d->meshes[m].submeshes[k].index_count / 3;
@@ -218,9 +233,12 @@ int rt_oracle_scene_create(const rt_scene_desc* d, rt_oracle_scene** out) {
         memcpy(s->xf[m], &md->transform, 48);
         memcpy(s->prev_xf[m], &md->transform, 48);
         s->mats[m] = (Material*)malloc(sizeof(Material) * md->submesh_count);
+        s->uv[m] = md->uvs;
+        s->mtex[m] = malloc(sizeof(int32_t[8]) * md->submesh_count);
         for (uint32_t k = 0; k < md->submesh_count; ++k) {
             const rt_submesh_desc* sm = &md->submeshes[k];
             s->mats[m][k] = sm->material;
+            memcpy(s->mtex[m][k], sm->textures, sizeof(int32_t[8]));
             for (uint32_t q = 0; q < sm->index_count / 3; ++q) {
                 OTri* ot = &s->tri[t];
                 ot->mesh = m; ot->sub = k;
@@ -254,8 +272,8 @@ int rt_oracle_scene_set_previous(rt_oracle_scene* s, uint32_t m, const rt_float3
 
 void rt_oracle_scene_destroy(rt_oracle_scene* s) {
     if (!s) return;
-    for (uint32_t m = 0; m < s->nmesh; ++m) free(s->mats[m]);
-    free(s->mats); free(s->pos); free(s->nrm); free(s->prev_pos); free(s->xf); free(s->prev_xf);
+    for (uint32_t m = 0; m < s->nmesh; ++m) { free(s->mats[m]); free(s->mtex[m]); }
+    free(s->mats); free(s->mtex); free(s->uv); free(s->pos); free(s->nrm); free(s->prev_pos); free(s->xf); free(s->prev_xf);
     free(s->lights); free(s->world); free(s->tri); free(s->order); free(s->nodes);
     free(s);
 }
@@ -404,6 +422,67 @@ static V3 interp(const rt_float3* A, const OTri* t, float u, float v, float w) {
     return vadd(vadd(vscl(f3v(A[t->i1]), u), vscl(f3v(A[t->i2]), v)), vscl(f3v(A[t->i0]), w));
 }
 
+/* ---------------------------------------------------------------- textures */
+typedef struct { float x, y, z, w; } V4;
+
+/* sample(sampler(linear, linear, mip linear, repeat), uv) in a compute kernel = bilinear from
+ * LOD 0 (Raytracing.metal:420): texel centres at i + 0.5, wrapped neighbours, corners decoded
+ * through the byte table (sRGB for base color / emission, alpha linear), weights in this order. */
+static V4 osample(const rt_oracle_scene* s, int t, float u, float v, int srgb) {
+    const rt_texture_desc* T = &s->tex[t];
+    int w = (int)T->width, h = (int)T->height;
+    float x = u * (float)w - 0.5f, y = v * (float)h - 0.5f;
+    if (!(fabsf(x) < 1.0e9f)) x = 0.0f;
+    if (!(fabsf(y) < 1.0e9f)) y = 0.0f;
+    float fx = floorf(x), fy = floorf(y);
+    float ax = x - fx, ay = y - fy, bx = 1.0f - ax, by = 1.0f - ay;
+    long long ix = (long long)fx % w, iy = (long long)fy % h;
+    if (ix < 0) ix += w;
+    if (iy < 0) iy += h;
+    int x0 = (int)ix, y0 = (int)iy, x1 = x0 + 1 == w ? 0 : x0 + 1, y1 = y0 + 1 == h ? 0 : y0 + 1;
+    const uint8_t* c00 = T->rgba8 + 4 * ((size_t)y0 * w + x0);
+    const uint8_t* c10 = T->rgba8 + 4 * ((size_t)y0 * w + x1);
+    const uint8_t* c01 = T->rgba8 + 4 * ((size_t)y1 * w + x0);
+    const uint8_t* c11 = T->rgba8 + 4 * ((size_t)y1 * w + x1);
+    float r[4];
+    for (int c = 0; c < 4; ++c) {
+        const float* L = s->lut + ((srgb && c < 3) ? 256 : 0);
+        r[c] = (L[c00[c]] * bx + L[c10[c]] * ax) * by + (L[c01[c]] * bx + L[c11[c]] * ax) * ay;
+    }
+    V4 o = {r[0], r[1], r[2], r[3]};
+    return o;
+}
+
+int rt_oracle_tex_sample(const rt_oracle_scene* s, int32_t t, float u, float v, int32_t srgb, float out[4]) {
+    if (!s || t < 0 || (uint32_t)t >= s->ntex || !out) return 1;
+    V4 r = osample(s, t, u, v, srgb);
+    out[0] = r.x; out[1] = r.y; out[2] = r.z; out[3] = r.w;
+    return 0;
+}
+
+static void ouv(const rt_oracle_scene* s, int m, uint32_t i, float* u, float* v) {
+    if (s->uv[m]) { *u = s->uv[m][i].x; *v = s->uv[m][i].y; }
+    else { *u = 0.0f; *v = 0.0f; }
+}
+
+/* computeTangentBasis (Raytracing.metal:185-218) */
+static int tangent_basis(const rt_oracle_scene* s, const OTri* t, V3* tangent, V3* bitangent) {
+    const rt_float3* P = s->pos[t->mesh];
+    V3 p0 = f3v(P[t->i1]), p1 = f3v(P[t->i2]), p2 = f3v(P[t->i0]);
+    float u0, v0, u1, v1, u2, v2;
+    ouv(s, (int)t->mesh, t->i1, &u0, &v0);
+    ouv(s, (int)t->mesh, t->i2, &u1, &v1);
+    ouv(s, (int)t->mesh, t->i0, &u2, &v2);
+    V3 e1 = vsub(p1, p0), e2 = vsub(p2, p0);
+    float d1x = u1 - u0, d1y = v1 - v0, d2x = u2 - u0, d2y = v2 - v0;
+    float denom = d1x * d2y - d1y * d2x;
+    if (fabsf(denom) < 1e-8f) return 0;
+    float r = 1.0f / denom;
+    *tangent = vscl(vsub(vscl(e1, d2y), vscl(e2, d1y)), r);
+    *bitangent = vscl(vsub(vscl(e2, d1x), vscl(e1, d2x)), r);
+    return vlen(*tangent) > 1e-8f && vlen(*bitangent) > 1e-8f;
+}
+
 /* ---------------------------------------------------------------- the kernel */
 typedef struct {
     const rt_oracle_scene* s;
@@ -482,15 +561,47 @@ static void render_pixel(const rt_oracle_scene* s, rt_oracle_frame* f, int px, i
             V3 Ng = vnorm(oxform(M, objN, 0.0f));                               /* :392-393 */
             if (vlen(objN) < 1e-10f) Ng = vneg(rd);                             /* :395-397 */
             V3 albedo = f3v(mat->baseColor);                                    /* :399 */
-            float roughness = 1.0f, metallic = 0.0f, ao = 1.0f;                 /* :431-446 (no maps) */
+            float roughness = 1.0f, metallic = 0.0f, ao = 1.0f;                 /* :431-446 (ENABLE_AO 0) */
             float opacity = clampf_(mat->opacity, 0.0f, 1.0f);                  /* :448 */
             V3 emission = f3v(mat->emission);                                   /* :453 */
+            const int32_t* tx = s->mtex[inst][tr->sub];
+            unsigned tfl = mat->textureFlags & ~(unsigned)MATERIAL_TEXTURE_AO;
+            float tcu = 0.0f, tcv = 0.0f;
+            V4 bsm = {1.0f, 1.0f, 1.0f, 1.0f};
+            if (tfl) {                                                          /* :412-417 */
+                float ua, va, ub, vb, uc, vc;
+                ouv(s, inst, tr->i1, &ua, &va);
+                ouv(s, inst, tr->i2, &ub, &vb);
+                ouv(s, inst, tr->i0, &uc, &vc);
+                tcu = (bu * ua + bv * ub) + bw * uc;
+                tcv = (bu * va + bv * vb) + bw * vc;
+                tcv = 1.0f - tcv;
+            }
+            if (tfl & MATERIAL_TEXTURE_BASECOLOR) {                             /* :423-428 */
+                bsm = osample(s, tx[0], tcu, tcv, 1);
+                albedo = vmul(albedo, v3(bsm.x, bsm.y, bsm.z));
+            }
+            if (tfl & MATERIAL_TEXTURE_ROUGHNESS) roughness = osample(s, tx[2], tcu, tcv, 0).x;  /* :431-434 */
+            if (tfl & MATERIAL_TEXTURE_METALLIC) metallic = osample(s, tx[3], tcu, tcv, 0).x;    /* :436-439 */
+            if (tfl & MATERIAL_TEXTURE_OPACITY) opacity = opacity * osample(s, tx[6], tcu, tcv, 0).x;  /* :448-451 */
+            if (tfl & MATERIAL_TEXTURE_EMISSION) {                              /* :453-456 */
+                V4 e = osample(s, tx[5], tcu, tcv, 1);
+                emission = v3(e.x, e.y, e.z);
+            }
 
             if (U->debugTextureMode != DebugTextureModeNone) {                  /* :459-490 */
                 V3 dc = v3(0, 0, 0);
                 int m = U->debugTextureMode;
-                if (m == DebugTextureModeBaseColor) dc = v3(1.0f, 0.0f, 1.0f);
-                else if (m == DebugTextureModeNormal) dc = vadd(vscl(Ng, 0.5f), v3(0.5f, 0.5f, 0.5f));
+                if (m == DebugTextureModeBaseColor)
+                    dc = (tfl & MATERIAL_TEXTURE_BASECOLOR) ? v3(bsm.x, bsm.y, bsm.z) : v3(1.0f, 0.0f, 1.0f);
+                else if (m == DebugTextureModeNormal) {
+                    if (tfl & MATERIAL_TEXTURE_NORMAL) {
+                        V4 nm = osample(s, tx[1], tcu, tcv, 0);
+                        dc = v3(nm.x, nm.y, nm.z);
+                    } else {
+                        dc = vadd(vscl(Ng, 0.5f), v3(0.5f, 0.5f, 0.5f));
+                    }
+                }
                 else if (m == DebugTextureModeRoughness) dc = v3(roughness, roughness, roughness);
                 else if (m == DebugTextureModeMetallic) dc = v3(metallic, metallic, metallic);
                 else if (m == DebugTextureModeAO) dc = v3(1.0f, 0.0f, 1.0f);
@@ -505,6 +616,17 @@ static void render_pixel(const rt_oracle_scene* s, rt_oracle_frame* f, int px, i
                 break;
             }
             V3 sn = Ng;                                                         /* :492 */
+            if (tfl & MATERIAL_TEXTURE_NORMAL) {                                /* :493-504 */
+                V3 T, B;
+                if (tangent_basis(s, tr, &T, &B)) {
+                    V3 wT = oxform(M, T, 0.0f);
+                    wT = vnorm(vsub(wT, vscl(Ng, vdot(wT, Ng))));
+                    V3 wB = vnorm(vcross(Ng, wT));
+                    V4 nm = osample(s, tx[1], tcu, tcv, 0);
+                    V3 n = v3(nm.x * 2.0f - 1.0f, nm.y * 2.0f - 1.0f, nm.z * 2.0f - 1.0f);
+                    sn = vnorm(vadd(vadd(vscl(wT, n.x), vscl(wB, n.y)), vscl(Ng, n.z)));
+                }
+            }
             if (U->enableDenoiseGBuffer != 0 && !wroteG && sampleIndex == 0) {  /* :506-515 */
                 V3 da = vscl(albedo, 1.0f - metallic);
                 V3 sa = vmix(v3(0.04f, 0.04f, 0.04f), albedo, metallic);

@@ -60,6 +60,9 @@ int rt_oracle_render(const rt_oracle_scene* s, rt_oracle_frame* f);
 float rt_oracle_halton(int32_t i, int32_t d);
 void rt_oracle_sincos(float x, float* s, float* c);
 float rt_oracle_pow5(float x);
+/* bilinear LOD-0 repeat sample of scene texture t at (u, v) (v already flipped); srgb: decode
+ * RGB through the sRGB table (base color / emission slots).  0 on success. */
+int rt_oracle_tex_sample(const rt_oracle_scene* s, int32_t t, float u, float v, int32_t srgb, float out[4]);
 /* world-space closest (any=0) / any (any=1) hit; returns 1 on hit */
 int rt_oracle_intersect(const rt_oracle_scene* s, const float o[3], const float d[3], float tmin, float tmax, int any,
                         float* t, uint32_t* id, float* u, float* v);
