@@ -49,6 +49,7 @@ struct FrameSlot {
                         &sort_table, &sort_total, &params, &pray, &psray, &depth, &gbuffer, &counters};
 };
 constexpr int kMaxSlots = 3;
+constexpr int kTailInFlight = 2097152;   // default finish threshold with frames in flight
 constexpr int kMotionTargets = kMaxSlots + 1;
 }  // namespace
 
@@ -934,7 +935,12 @@ rt_status rt_render_frame(rt_ctx* c, const Uniforms* U, const rt_tile_set* tiles
     if (wavefront) {
         const char* err = nullptr;
         F.wfs = WfFrameStats{};
-        if (own > 0 && !run_wavefront(S, P, F.wf, own, c->counting, c->tail_paths, c->sort_bins, extra_pass, stream,
+        // finish threshold: with frames in flight the next frame's bulk rounds overlap this
+        // frame's tail, so more bulk rounds and a shorter tail pay (C3g: 2M paths 5.92 ms per frame
+        // against 6.02 ms at the one-frame-at-a-time optimum of 4M)
+        static const bool tail_env = getenv("RT_TAIL_RAYS") != nullptr;
+        const int tail = c->tail_paths ? c->tail_paths : (nfl > 1 && !tail_env ? kTailInFlight : 0);
+        if (own > 0 && !run_wavefront(S, P, F.wf, own, c->counting, tail, c->sort_bins, extra_pass, stream,
                                       cross ? prev.done : nullptr, &F.wft, &F.wfs, &err))
             FAIL(c, RT_ERR_HIP, std::string("wavefront: ") + (err ? err : "?"));
         if (own == 0 && cross) HIPC(c, hipStreamWaitEvent(stream, prev.done, 0));
