@@ -214,6 +214,27 @@ rt_status rt_wait(rt_ctx* ctx);
 rt_status rt_read_radiance(rt_ctx* ctx, float* rgba);
 rt_status rt_read_aux(rt_ctx* ctx, float* depth, float* motion, float* gbuffer);
 
+/* Display output (FramePresenter.swift:103-238, Shaders.metal:39-52): the newest radiance,
+ * resampled to out_width x out_height by `scaler`, tone-mapped color / (1 + color) and encoded
+ * to 8-bit RGBA rows top-down (alpha 255), written to host memory.  RT_SCALER_NONE samples the
+ * nearest render pixel (the presenter's own path); SPATIAL resamples bilinearly; TEMPORAL blends
+ * with the previous output reprojected through the motion vectors, clamped to the current
+ * neighbourhood, rejected on depth jumps (MetalFX's scalers are unpublished: these are stand-ins
+ * consuming the same inputs).  encode: RT_ENCODE_SRGB8 (default) or RT_ENCODE_LINEAR8. */
+#define RT_SCALER_NONE 0
+#define RT_SCALER_SPATIAL 1
+#define RT_SCALER_TEMPORAL 2
+#define RT_ENCODE_SRGB8 0
+#define RT_ENCODE_LINEAR8 1
+typedef struct rt_present_opts {
+    int32_t out_width;   /* 0 = render width */
+    int32_t out_height;  /* 0 = render height */
+    int32_t scaler;
+    int32_t encode;
+    int32_t reserved[4];
+} rt_present_opts;
+rt_status rt_present(rt_ctx* ctx, const rt_present_opts* opts, uint8_t* host_rgba8);
+
 /* Multi-GPU: pack this rank's tiles of the latest radiance into a device buffer of
  * rt_tile_count(...) * tile_size^2 * 4 floats, and the inverse on the gathering rank
  * (writing into the latest radiance target). Device pointers; enqueued after the newest frame

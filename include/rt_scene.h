@@ -85,6 +85,8 @@ rt_status rt_scene_bind_texture(rt_scene* scene, uint32_t mesh_index, uint32_t s
  * of width * height * 4 bytes.  err_buf (optional) receives the reason of a failure. */
 rt_status rt_decode_png(const uint8_t* data, size_t size, uint8_t* rgba8, uint32_t* width, uint32_t* height,
                         char* err_buf, size_t err_len);
+/* Writes width x height RGBA8 rows (row 0 = top) as an 8-bit RGBA PNG (e.g. rt_present output). */
+rt_status rt_write_png(const char* path, const uint8_t* rgba8, uint32_t width, uint32_t height);
 /* Totals for reports. */
 uint64_t rt_scene_triangle_count(const rt_scene* scene);
 

@@ -84,6 +84,13 @@ def decode_png(data):
     return out
 
 
+def write_png(path, rgba8):
+    """(H, W, 4) uint8 rows top-down -> an RGBA PNG file (e.g. Renderer.present())."""
+    a = np.ascontiguousarray(rgba8, dtype=np.uint8)
+    assert a.ndim == 3 and a.shape[2] == 4, a.shape
+    _check(lib().rt_write_png(str(path).encode(), a.ctypes.data, a.shape[1], a.shape[0]))
+
+
 def camera_default(width, height):
     c = Camera()
     lib().rt_camera_default(width, height, C.byref(c))
@@ -353,6 +360,20 @@ class Renderer:
         device is True (default: the builder this renderer was created with)."""
         dev = (self.bvh_builder == "lbvh") if device is None else device
         _check((lib().rt_bvh_build_device if dev else lib().rt_bvh_build)(self._ctx), self._ctx)
+
+    def present(self, width=None, height=None, scaler="none", srgb=True):
+        """Display image of the newest frame (FramePresenter + Shaders.metal): resampled to
+        width x height ('none' = nearest, 'spatial' = bilinear, 'temporal' = reprojected history
+        through the motion vectors), tone-mapped c / (1 + c), 8-bit sRGB (or linear) RGBA rows
+        top-down."""
+        o = _abi.PresentOpts()
+        o.out_width = int(width or 0)
+        o.out_height = int(height or 0)
+        o.scaler = _abi.SCALERS[scaler]
+        o.encode = 0 if srgb else 1
+        out = np.empty((height or self.height, width or self.width, 4), dtype=np.uint8)
+        _check(lib().rt_present(self._ctx, C.byref(o), out.ctypes.data), self._ctx)
+        return out
 
     def upload(self, desc):
         """Re-uploads a scene description (rt_scene_upload) and rebuilds the BVH."""

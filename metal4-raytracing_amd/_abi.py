@@ -131,6 +131,14 @@ class Opts(C.Structure):
                 ("frames_in_flight", C.c_int32), ("reserved", C.c_int32 * 3)]
 
 
+class PresentOpts(C.Structure):  # rt_present_opts
+    _fields_ = [("out_width", C.c_int32), ("out_height", C.c_int32), ("scaler", C.c_int32), ("encode", C.c_int32),
+                ("reserved", C.c_int32 * 4)]
+
+
+SCALERS = {"none": 0, "spatial": 1, "temporal": 2}
+
+
 class TileSet(C.Structure):
     _fields_ = [("tile_size", C.c_int32), ("rank", C.c_int32), ("nranks", C.c_int32), ("_pad", C.c_int32)]
 
@@ -205,7 +213,7 @@ EXPORTED_SYMBOLS = [
     "rt_create", "rt_destroy", "rt_last_error", "rt_set_stream", "rt_scene_upload", "rt_bvh_build",
     "rt_bvh_build_device", "rt_bvh_refit", "rt_set_instance_transforms", "rt_skin", "rt_resize", "rt_render_frame", "rt_wait",
     "rt_read_radiance", "rt_read_aux", "rt_tile_count", "rt_pack_tiles", "rt_unpack_tiles",
-    "rt_pack_tiles_on", "rt_unpack_tiles_on",
+    "rt_pack_tiles_on", "rt_unpack_tiles_on", "rt_present", "rt_write_png",
     "rt_pack_tiles_host", "rt_unpack_tiles_host",
     "rt_set_counting", "rt_get_stats", "rt_version", "rt_debug_trace_host",
     # rt_scene.h
@@ -242,6 +250,8 @@ def declare(lib):
         "rt_pack_tiles": (st, [vp, P(TileSet), vp]),
         "rt_unpack_tiles": (st, [vp, P(TileSet), vp]),
         "rt_pack_tiles_on": (st, [vp, P(TileSet), vp, vp]),
+        "rt_present": (st, [vp, P(PresentOpts), vp]),
+        "rt_write_png": (st, [C.c_char_p, vp, C.c_uint32, C.c_uint32]),
         "rt_unpack_tiles_on": (st, [vp, P(TileSet), vp, vp]),
         "rt_pack_tiles_host": (st, [C.c_int32, C.c_int32, P(TileSet), P(C.c_float), P(C.c_float)]),
         "rt_unpack_tiles_host": (st, [C.c_int32, C.c_int32, P(TileSet), P(C.c_float), P(C.c_float)]),

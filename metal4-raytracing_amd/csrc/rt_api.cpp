@@ -97,6 +97,11 @@ struct rt_ctx {
     int motion_cur = 0;
     int width = 0, height = 0;
     int read_idx = 0;   // accum[read_idx] = history (TextureIndexAccumulation)
+    uint32_t last_frame_index = 0;   // Uniforms.frameIndex of the newest frame
+    // display output (rt_present): temporal-scaler history at the output size, sRGB thresholds
+    DevBuf d_hist[2], d_hdepth[2], d_present_out, d_present_thr;
+    int hist_w = 0, hist_h = 0, hist_idx = 0;
+    bool hist_valid = false;
     rt_stats stats{};
 
     // frames in flight
@@ -198,7 +203,9 @@ static size_t ctx_bytes(const rt_ctx* c) {
                            &c->d_joints, &c->d_tri_info, &c->d_inst, &c->d_prev_inst, &c->d_mat, &c->d_lights,
                            &c->d_halton, &c->d_tris, &c->d_nodes, &c->d_node_box, &c->d_slot_to_tri, &c->d_levels, &c->d_maxabs, &c->d_random,
                            &c->d_accum[0], &c->d_accum[1], &c->d_tri_bin, &c->d_lbvh_scratch,
-                           &c->d_tex_texels, &c->d_tex_info, &c->d_mat_tex, &c->d_uv, &c->d_tex_lut};
+                           &c->d_tex_texels, &c->d_tex_info, &c->d_mat_tex, &c->d_uv, &c->d_tex_lut,
+                           &c->d_hist[0], &c->d_hist[1], &c->d_hdepth[0], &c->d_hdepth[1], &c->d_present_out,
+                           &c->d_present_thr};
     size_t s = 0;
     for (auto* b : all) s += b->bytes;
     for (const DevBuf& b : c->d_motion) s += b.bytes;
@@ -354,7 +361,8 @@ rt_status rt_destroy(rt_ctx* c) {
                      &c->d_joints, &c->d_tri_info, &c->d_inst, &c->d_prev_inst, &c->d_mat, &c->d_lights, &c->d_halton,
                      &c->d_tris, &c->d_nodes, &c->d_node_box, &c->d_slot_to_tri, &c->d_levels, &c->d_maxabs, &c->d_random, &c->d_accum[0],
                      &c->d_accum[1], &c->d_tri_bin, &c->d_lbvh_scratch, &c->d_tex_texels, &c->d_tex_info,
-                     &c->d_mat_tex, &c->d_uv, &c->d_tex_lut};
+                     &c->d_mat_tex, &c->d_uv, &c->d_tex_lut, &c->d_hist[0], &c->d_hist[1], &c->d_hdepth[0],
+                     &c->d_hdepth[1], &c->d_present_out, &c->d_present_thr};
     for (auto* b : all) dev_free(*b);
     for (DevBuf& b : c->d_motion) dev_free(b);
     if (c->h_lbvh) hipHostFree(c->h_lbvh);
@@ -756,6 +764,7 @@ rt_status rt_resize(rt_ctx* c, int32_t w, int32_t h, const uint32_t* offsets) {
     }
     c->frame_no = 0;
     c->last_slot = 0;
+    c->hist_valid = false;
     HIPC(c, hipStreamSynchronize(c->stream));
     c->width = w;
     c->height = h;
@@ -966,6 +975,7 @@ rt_status rt_render_frame(rt_ctx* c, const Uniforms* U, const rt_tile_set* tiles
     c->last_tiles[2] = nranks;
     c->motion_cur = m_out;
     c->stats.frames_in_flight = nfl;
+    c->last_frame_index = U->frameIndex;
     c->read_idx = 1 - c->read_idx;  // swap accumulationTargets (Renderer.swift:1492-1494)
     return RT_OK;
 }
@@ -1034,6 +1044,61 @@ static rt_status tiles_op(rt_ctx* c, const rt_tile_set* t, const void* src, void
         HIPC(c, hipEventRecord(f.done, stream));
         c->tiles_pending = true;
     }
+    return RT_OK;
+}
+
+rt_status rt_present(rt_ctx* c, const rt_present_opts* o, uint8_t* host_rgba8) {
+    if (!c || !host_rgba8) FAIL(c, RT_ERR_INVALID_ARG, "null argument");
+    if (!c->width) FAIL(c, RT_ERR_STATE, "no targets");
+    const int ow = (o && o->out_width > 0) ? o->out_width : c->width;
+    const int oh = (o && o->out_height > 0) ? o->out_height : c->height;
+    const int scaler = o ? o->scaler : RT_SCALER_NONE;
+    const int encode = o ? o->encode : RT_ENCODE_SRGB8;
+    if (scaler < RT_SCALER_NONE || scaler > RT_SCALER_TEMPORAL || (encode != RT_ENCODE_SRGB8 && encode != RT_ENCODE_LINEAR8))
+        FAIL(c, RT_ERR_INVALID_ARG, "bad scaler / encode");
+    if ((int64_t)ow * oh > (1ll << 28)) FAIL(c, RT_ERR_INVALID_ARG, "output too large");
+    HIPC(c, hipSetDevice(c->device));
+    rt_status st;
+    const size_t n = (size_t)ow * oh;
+    if (!c->d_present_thr.p) {   // linear value at which the sRGB code reaches k + 1 (k + 0.5 of 255)
+        float thr[256];
+        for (int k = 0; k < 255; ++k) {
+            const double s = (k + 0.5) / 255.0;
+            thr[k] = (float)(s <= 0.04045 ? s / 12.92 : std::pow((s + 0.055) / 1.055, 2.4));
+        }
+        thr[255] = INFINITY;
+        if ((st = dev_upload(c, c->d_present_thr, thr, sizeof thr))) return st;
+    }
+    if ((st = dev_alloc(c, c->d_present_out, n * 4))) return st;
+    if (scaler == RT_SCALER_TEMPORAL && (c->hist_w != ow || c->hist_h != oh || !c->d_hist[0].p)) {
+        for (int i = 0; i < 2; ++i) {
+            if ((st = dev_alloc(c, c->d_hist[i], n * 16))) return st;
+            if ((st = dev_alloc(c, c->d_hdepth[i], n * 4))) return st;
+        }
+        c->hist_w = ow;
+        c->hist_h = oh;
+        c->hist_valid = false;
+    }
+    // after the newest frame (and any pack / unpack of it)
+    FrameSlot& f = c->slot[c->last_slot];
+    if (!f.used) FAIL(c, RT_ERR_STATE, "rt_present before the first frame");
+    HIPC(c, hipStreamWaitEvent(c->stream, f.done, 0));
+    const bool temporal = scaler == RT_SCALER_TEMPORAL;
+    const int hi = c->hist_idx;
+    launch_present((const float4*)c->d_accum[c->read_idx].p, (const float*)f.depth.p,
+                   (const float2*)c->d_motion[c->motion_cur].p, temporal ? (const float4*)c->d_hist[hi].p : nullptr,
+                   temporal ? (const float*)c->d_hdepth[hi].p : nullptr,
+                   temporal ? (float4*)c->d_hist[1 - hi].p : nullptr, temporal ? (float*)c->d_hdepth[1 - hi].p : nullptr,
+                   (uchar4*)c->d_present_out.p, (const float*)c->d_present_thr.p, c->width, c->height, ow, oh, scaler,
+                   encode == RT_ENCODE_SRGB8 ? 1 : 0, (temporal && c->hist_valid && c->last_frame_index > 0) ? 1 : 0,
+                   c->stream);
+    HIPC(c, hipGetLastError());
+    if (temporal) {
+        c->hist_idx = 1 - hi;
+        c->hist_valid = true;
+    }
+    HIPC(c, hipMemcpyAsync(host_rgba8, c->d_present_out.p, n * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPC(c, hipStreamSynchronize(c->stream));
     return RT_OK;
 }
 

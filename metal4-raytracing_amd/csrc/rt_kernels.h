@@ -210,6 +210,9 @@ bool lbvh_build(const LbvhInput& in, const LbvhOutput& out, void* scratch, hipSt
                 const char** err);
 
 // Utility kernels (rt_util.hip)
+void launch_present(const float4* accum, const float* depth, const float2* motion, const float4* hist_in,
+                    const float* hdepth_in, float4* hist_out, float* hdepth_out, uchar4* out, const float* thr, int w,
+                    int h, int ow, int oh, int scaler, int srgb, int use_hist, hipStream_t stream);
 void launch_pack_tiles(const float4* src, float4* dst, int width, int height, int tile, int rank, int nranks,
                        int tiles_x, int own, hipStream_t s);
 void launch_unpack_tiles(const float4* src, float4* dst, int width, int height, int tile, int rank, int nranks,

@@ -10,6 +10,7 @@
 // greyscale + alpha, RGBA, tRNS transparency.  16-bit samples are rounded to 8 bits.
 #include <algorithm>
 #include <cstdint>
+#include <cstdio>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -261,6 +262,46 @@ rt_status rt_decode_png(const uint8_t* data, size_t size, uint8_t* rgba8, uint32
         off += (size_t)ph[k] * (rb + 1);
     }
     return RT_OK;
+}
+
+rt_status rt_write_png(const char* path, const uint8_t* rgba8, uint32_t width, uint32_t height) {
+    if (!path || !rgba8 || width == 0 || height == 0) return RT_ERR_INVALID_ARG;
+    const size_t row = (size_t)width * 4;
+    std::vector<uint8_t> raw((row + 1) * height);
+    for (uint32_t y = 0; y < height; ++y) {
+        raw[y * (row + 1)] = 0;   // filter: none
+        std::memcpy(&raw[y * (row + 1) + 1], rgba8 + y * row, row);
+    }
+    uLongf zlen = compressBound((uLong)raw.size());
+    std::vector<uint8_t> z(zlen);
+    if (compress2(z.data(), &zlen, raw.data(), (uLong)raw.size(), 6) != Z_OK) return RT_ERR_IO;
+    FILE* f = std::fopen(path, "wb");
+    if (!f) return RT_ERR_IO;
+    auto put32 = [](uint8_t* p, uint32_t v) { p[0] = v >> 24, p[1] = v >> 16, p[2] = v >> 8, p[3] = v; };
+    auto chunk = [&](const char* type, const uint8_t* body, uint32_t len) {
+        uint8_t hdr[8];
+        put32(hdr, len);
+        std::memcpy(hdr + 4, type, 4);
+        uLong crc = crc32(0L, Z_NULL, 0);
+        crc = crc32(crc, hdr + 4, 4);
+        if (len) crc = crc32(crc, body, len);
+        uint8_t tail[4];
+        put32(tail, (uint32_t)crc);
+        std::fwrite(hdr, 1, 8, f);
+        if (len) std::fwrite(body, 1, len, f);
+        std::fwrite(tail, 1, 4, f);
+    };
+    static const uint8_t sig[8] = {0x89, 'P', 'N', 'G', '\r', '\n', 0x1a, '\n'};
+    std::fwrite(sig, 1, 8, f);
+    uint8_t ihdr[13];
+    put32(ihdr, width);
+    put32(ihdr + 4, height);
+    ihdr[8] = 8, ihdr[9] = 6, ihdr[10] = 0, ihdr[11] = 0, ihdr[12] = 0;
+    chunk("IHDR", ihdr, 13);
+    chunk("IDAT", z.data(), (uint32_t)zlen);
+    chunk("IEND", nullptr, 0);
+    const bool ok = std::ferror(f) == 0;
+    return std::fclose(f) == 0 && ok ? RT_OK : RT_ERR_IO;
 }
 
 }  // extern "C"

@@ -272,3 +272,10 @@ def test_oracle_sampler_spec(rt, orc, assets):
     im = imgs[0]
     got = o.tex_sample(ids[0], (2 + 0.5) / 7, (3 + 0.5) / 5, False)
     assert np.array_equal(got, (im[3, 2] / np.float32(255)).astype(np.float32))
+
+
+def test_write_png_roundtrip(rt, tmp_path):
+    img = _checker(9, 17, 21)
+    p = tmp_path / "o.png"
+    rt.write_png(p, img)
+    assert np.array_equal(rt.decode_png(p.read_bytes()), img)
