@@ -949,7 +949,7 @@ rt_status rt_render_frame(rt_ctx* c, const Uniforms* U, const rt_tile_set* tiles
         // against 6.02 ms at the one-frame-at-a-time optimum of 4M)
         static const bool tail_env = getenv("RT_TAIL_RAYS") != nullptr;
         const int tail = c->tail_paths ? c->tail_paths : (nfl > 1 && !tail_env ? kTailInFlight : 0);
-        if (own > 0 && !run_wavefront(S, P, F.wf, own, c->counting, tail, c->sort_bins, extra_pass, stream,
+        if (own > 0 && !run_wavefront(S, P, F.wf, own, c->counting, tail, c->sort_bins, extra_pass, nfl > 1, stream,
                                       cross ? prev.done : nullptr, &F.wft, &F.wfs, &err))
             FAIL(c, RT_ERR_HIP, std::string("wavefront: ") + (err ? err : "?"));
         if (own == 0 && cross) HIPC(c, hipStreamWaitEvent(stream, prev.done, 0));

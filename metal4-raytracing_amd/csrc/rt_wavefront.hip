@@ -186,6 +186,7 @@ struct WfParams {
     int drain_min;         // wf_finish_step: hand paths back to the next round below this many busy lanes
     int prio;              // finish input reordered by wf_prio (likely-long paths first) into W.sorted
     int fchunk;            // wf_finish_step: paths per chunk grab
+    int finish_frac;       // percent of the resident grid the finish launch takes
     int dev_ctl;           // device-side control (enqueue_wavefront): kernels read their queue sizes from
                            // the counters and skip once the live count fell below `tail`
     int finish_q;          // dev_ctl: the finish queue when every enqueued bulk round ran (written by generate)
@@ -1644,7 +1645,13 @@ template <bool STEP, bool COUNT, bool FULL>
 static void launch_finish(const DevScene& S, const FrameParams& P, const WfParams& Q, int cur, uint32_t n,
                           hipStream_t stream) {
     static const int waves = env_int("RT_FINISH_WAVES", 4);
-    if (STEP && waves == 3) {
+    // Q.finish_frac < 100: the finish kernel takes that share of the resident grid, the rest of
+    // the machine stays free for the next frame's kernels (frames in flight)
+    if (STEP && Q.finish_frac < 100) {
+        static const unsigned full_cap = resident_grid(wf_finish_step<COUNT, FULL, 4>, 2);
+        const unsigned cap = std::max(1u, full_cap * (unsigned)Q.finish_frac / 100u);
+        hipLaunchKernelGGL((wf_finish_step<COUNT, FULL, 4>), dim3(grid_for(n, cap)), dim3(kBlock), 0, stream, S, Q.Pd, Q, cur);
+    } else if (STEP && waves == 3) {
         static const unsigned cap = resident_grid(wf_finish_step<COUNT, FULL, 3>, 2);
         hipLaunchKernelGGL((wf_finish_step<COUNT, FULL, 3>), dim3(grid_for(n, cap)), dim3(kBlock), 0, stream, S, Q.Pd, Q, cur);
     } else if (STEP) {
@@ -1960,7 +1967,7 @@ static std::vector<uint64_t> graph_key(const DevScene& S, const FrameParams& P, 
     put(W.sort_total); put(W.d_params);
     put(Q.base_paths); put(Q.own_pixels); put(Q.seg_cap); put(Q.spp); put(Q.refill_min); put(Q.tri_vote);
     put(Q.chunk); put(Q.tail); put(Q.sort_bins); put(Q.sort_xcd); put(Q.steal); put(Q.diag); put(Q.finish_step);
-    put(Q.shade_min); put(Q.drain_min); put(Q.dev_ctl); put(Q.Pd);
+    put(Q.shade_min); put(Q.drain_min); put(Q.dev_ctl); put(Q.Pd); put(Q.finish_frac); put(Q.fchunk); put(Q.prio);
     put(P.motion); put(P.U.width); put(P.U.height);
     put(count); put(full); put(maxExtra); put(with_extra);
     return k;
@@ -2043,8 +2050,8 @@ bool wavefront_collect(const WavefrontBuffers& W, WfTimeline& T, WfFrameStats* f
 }
 
 bool run_wavefront(const DevScene& S, const FrameParams& P, WavefrontBuffers& W, int own_tiles, bool count,
-                   int tail_paths, int sort_bins, bool extra_pass, hipStream_t stream, hipEvent_t prev_done,
-                   WfTimeline* tl, WfFrameStats* fs, const char** err) {
+                   int tail_paths, int sort_bins, bool extra_pass, bool overlapped, hipStream_t stream,
+                   hipEvent_t prev_done, WfTimeline* tl, WfFrameStats* fs, const char** err) {
     WfParams Q;
     Q.W = W;
     Q.spp = max(P.U.samplesPerPixel, 1);
@@ -2068,6 +2075,10 @@ bool run_wavefront(const DevScene& S, const FrameParams& P, WavefrontBuffers& W,
     Q.drain_min = Q.finish_step == 1 ? drain_min : 0;
     static const int prio = env_int("RT_PRIO", 0), fchunk = env_int("RT_FCHUNK", 64);
     Q.fchunk = max(1, fchunk);
+    // frames in flight: half the machine for the tail, the other half for the next frame's bulk
+    // rounds (C3g: 5.94 -> 5.72 ms per frame); one frame at a time: all of it
+    static const int finish_frac = env_int("RT_FINISH_FRAC", 0);
+    Q.finish_frac = finish_frac > 0 ? min(finish_frac, 100) : (overlapped ? 50 : 100);
     Q.prio = (prio && Q.finish_step == 1 && W.sorted) ? 1 : 0;
     if (Q.finish_step == 2 && (!W.p_ray || !W.p_sray)) {
         *err = "wave-queue finish kernel without its path ray slots";
