@@ -186,7 +186,8 @@ static std::vector<HaltonDim> halton_table() {
 // builder falls back to median splits past its depth limit, so tighter limits bound the depth.
 static bool build_bvh8_fit(const float* world, uint32_t n, BvhResult& b2, Bvh8Result& b8) {
     for (int limit : {64, 48, 40, 32, 28, 24, 21}) {
-        b2 = build_bvh2(world, n, 4, limit);
+        static const int leaf = getenv("RT_BVH_LEAF") ? std::max(1, std::min(4, atoi(getenv("RT_BVH_LEAF")))) : 4;
+        b2 = build_bvh2(world, n, leaf, limit);
         b8 = collapse_bvh8(b2);
         if (b8.max_depth <= kStackSize) return true;
     }

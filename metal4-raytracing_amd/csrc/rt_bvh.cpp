@@ -2,6 +2,7 @@
 #include "rt_bvh.h"
 
 #include <algorithm>
+#include <cstdlib>
 #include <cmath>
 #include <cstring>
 
@@ -103,7 +104,8 @@ struct Builder {
             }
             float pa = b.area();
             float leaf_cost = (float)n;                             // C_isect = 1
-            float split_cost = 1.0f + (pa > 0 ? best_cost / pa : INFINITY);  // C_trav = 1
+            static const float c_trav = getenv("RT_BVH_CTRAV") ? (float)atof(getenv("RT_BVH_CTRAV")) : 1.0f;
+            float split_cost = c_trav + (pa > 0 ? best_cost / pa : INFINITY);  // C_trav (default 1)
             if (best_axis >= 0 && (split_cost < leaf_cost || n > (uint32_t)max_leaf)) {
                 float scale = kBins / ext[best_axis];
                 auto it = std::partition(idx.begin() + s, idx.begin() + e, [&](uint32_t t) {
