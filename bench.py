@@ -57,6 +57,8 @@ def parse():
     p.add_argument("--bvh", default="sah", choices=["sah", "lbvh"], help="host binned-SAH or on-device LBVH build")
     p.add_argument("--frames-in-flight", type=int, default=0,
                    help="frames the renderer overlaps (0 = library default 2, 1 = one at a time)")
+    p.add_argument("--emulate-ranks", type=int, default=0,
+                   help="tuning aid: one process renders rank 0's tiles of an N-way split (no gather)")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample time")
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--traffic-csv", default=None, help="rocprofv3 --pmc counter_collection.csv for traffic")
@@ -85,6 +87,8 @@ def main():
     R.samplesPerPixel = a.spp
     R.maxBounces = a.bounces
     tiles = (a.tile, rank, n) if n > 1 else None
+    if a.emulate_ranks > 1 and n == 1:
+        tiles = (a.tile, 0, a.emulate_ranks)
     T = a.tile
     dev = torch.device("cuda", local)
     gather = None
