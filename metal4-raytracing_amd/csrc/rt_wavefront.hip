@@ -535,7 +535,10 @@ __global__ void __launch_bounds__(kSortThreads) wf_sort_scatter(DevScene S, WfPa
 // triangle.  The wave therefore runs ~(total units of its rays)/64 iterations instead of
 // (slowest ray) x (rays per lane).
 template <bool ANY, bool COUNT>
-__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) wf_trace(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int cur) {
+#ifndef RT_EXTEND_WAVES
+#define RT_EXTEND_WAVES 7   // 70 VGPRs without scratch (8 waves: 64 VGPRs + 24 B/lane of spills)
+#endif
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ANY ? 8 : RT_EXTEND_WAVES, ANY ? 8 : RT_EXTEND_WAVES))) wf_trace(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int cur) {
     const FrameParams& P = *Pp;   // per-frame parameters in device memory (graph replay)
     __shared__ int lds_stack[kStackSize * kBlock];
     __shared__ uint4 lds_top[kTopNodes * 5];   // BVH top levels (BFS order: root, its children, ...)
@@ -1647,7 +1650,11 @@ static void launch_finish(const DevScene& S, const FrameParams& P, const WfParam
     static const int waves = env_int("RT_FINISH_WAVES", 4);
     // Q.finish_frac < 100: the finish kernel takes that share of the resident grid, the rest of
     // the machine stays free for the next frame's kernels (frames in flight)
-    if (STEP && Q.finish_frac < 100) {
+    if (STEP && Q.finish_frac < 100 && waves == 3) {
+        static const unsigned full_cap = resident_grid(wf_finish_step<COUNT, FULL, 3>, 2);
+        const unsigned cap = std::max(1u, full_cap * (unsigned)Q.finish_frac / 100u);
+        hipLaunchKernelGGL((wf_finish_step<COUNT, FULL, 3>), dim3(grid_for(n, cap)), dim3(kBlock), 0, stream, S, Q.Pd, Q, cur);
+    } else if (STEP && Q.finish_frac < 100) {
         static const unsigned full_cap = resident_grid(wf_finish_step<COUNT, FULL, 4>, 2);
         const unsigned cap = std::max(1u, full_cap * (unsigned)Q.finish_frac / 100u);
         hipLaunchKernelGGL((wf_finish_step<COUNT, FULL, 4>), dim3(grid_for(n, cap)), dim3(kBlock), 0, stream, S, Q.Pd, Q, cur);
