@@ -548,7 +548,8 @@ template <bool ANY, bool COUNT>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ANY ? 8 : RT_EXTEND_WAVES, ANY ? 8 : RT_EXTEND_WAVES))) wf_trace(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int cur) {
     const FrameParams& P = *Pp;   // per-frame parameters in device memory (graph replay)
     __shared__ int lds_stack[kStackSize * kBlock];
-    __shared__ uint4 lds_top[kTopNodes * 5];   // BVH top levels (BFS order: root, its children, ...)
+    constexpr int kTop = ANY ? RT_TOP_CONNECT : RT_TOP_EXTEND;
+    __shared__ uint4 lds_top[kTop * 5];   // BVH top levels (BFS order: root, its children, ...)
     int* stack = &lds_stack[threadIdx.x];
     if (Q.dev_ctl) {
         // device-side round control: extend decides (uniformly, from the counters) whether this
@@ -567,7 +568,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ANY
             }
         }
     }
-    const uint32_t n_top = (uint32_t)min(S.num_nodes8, kTopNodes);
+    const uint32_t n_top = (uint32_t)min(S.num_nodes8, kTop);
     for (uint32_t i = threadIdx.x; i < n_top * 5; i += kBlock)
         lds_top[i] = reinterpret_cast<const uint4*>(S.nodes8)[i];
     __syncthreads();
@@ -902,11 +903,11 @@ wf_finish_step(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int c
     const FrameParams& P = *Pp;   // per-frame parameters in device memory (graph replay)
     if (cur < 0) cur = (int)__builtin_amdgcn_readfirstlane(Q.W.counts[cslot(kCntFinishQ)]);   // dev_ctl
     __shared__ int lds_stack[kStackSize * kBlock];
-    __shared__ uint4 lds_top[kTopNodes * 5];
+    __shared__ uint4 lds_top[RT_TOP_FINISH * 5];
     __shared__ HaltonDim lds_halton[kHaltonLds];
     __shared__ MatRec lds_mat[kMatLds];
     int* stack = &lds_stack[threadIdx.x];
-    const uint32_t n_top = (uint32_t)min(S.num_nodes8, kTopNodes);
+    const uint32_t n_top = (uint32_t)min(S.num_nodes8, RT_TOP_FINISH);
     for (uint32_t i = threadIdx.x; i < n_top * 5; i += kBlock) lds_top[i] = reinterpret_cast<const uint4*>(S.nodes8)[i];
     const ShadeTabs halton = load_tabs(S, lds_halton, lds_mat);   // ends with a block barrier
     const Uniforms& U = P.U;
