@@ -375,6 +375,17 @@ class Renderer:
         _check(lib().rt_present(self._ctx, C.byref(o), out.ctypes.data), self._ctx)
         return out
 
+    def resize(self, width, height, seed=1):
+        """mtkView(_:drawableSizeWillChange:) (Renderer.swift:1505-1511): new targets and random
+        offsets, frameIndex = 0.  Frames in flight finish first."""
+        self.width, self.height = int(width), int(height)
+        self.random = random_offsets(seed, self.width, self.height)
+        _check(lib().rt_resize(self._ctx, self.width, self.height, self.random.ctypes.data_as(C.POINTER(C.c_uint32))),
+               self._ctx)
+        self.camera = camera_default(self.width, self.height)
+        self.previousCamera = None
+        self.frameIndex = 0
+
     def upload(self, desc):
         """Re-uploads a scene description (rt_scene_upload) and rebuilds the BVH."""
         _check(lib().rt_scene_upload(self._ctx, C.byref(desc)), self._ctx)

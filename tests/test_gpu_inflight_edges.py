@@ -1,0 +1,90 @@
+"""Edge cases of frames in flight (rt_api.cpp FrameSlot rotation): a resize between frames in
+flight, switching to a caller's stream mid-sequence (one slot from then on), a rank that owns no
+tiles, re-uploading the scene, and the on-device BVH rebuild between in-flight frames.  Each
+sequence must give the same bytes as one-frame-at-a-time rendering."""
+import numpy as np
+import pytest
+
+from helpers import make_renderer
+
+pytestmark = pytest.mark.gpu
+
+
+def _seq(rt, assets, fif, steps):
+    sc = rt.Scene.preset("c1", assets)
+    R = make_renderer(rt, sc, 72, 48, "wavefront", seed=6, frames_in_flight=fif)
+    R.samplesPerPixel, R.maxBounces = 2, 3
+    out = []
+    for st in steps:
+        st(rt, R, sc)
+        R.draw()
+    out.append(R.radiance())
+    out.append(R.aux()[0])
+    return out, R
+
+
+def _draws(n):
+    return [lambda rt, R, sc: None] * n
+
+
+def _check_same(a, b):
+    for x, y in zip(a, b):
+        assert np.array_equal(x, y)
+
+
+def test_resize_between_frames(rt, assets):
+    def resize(rt, R, sc):
+        R.resize(88, 56, seed=9)
+    steps = _draws(3) + [resize] + _draws(3)
+    a, _ = _seq(rt, assets, 1, steps)
+    b, Rb = _seq(rt, assets, 2, steps)
+    assert a[0].shape == (56, 88, 4)
+    _check_same(a, b)
+    assert Rb.stats().frames_in_flight == 2
+
+
+def test_switch_to_caller_stream(rt, assets):
+    import torch
+    s = torch.cuda.Stream()
+
+    def to_stream(rt, R, sc):
+        R.set_stream(s.cuda_stream)
+
+    def back(rt, R, sc):
+        R.set_stream(None)
+    steps = _draws(3) + [to_stream] + _draws(2) + [back] + _draws(2)
+    a, _ = _seq(rt, assets, 1, steps)
+    b, Rb = _seq(rt, assets, 2, steps)
+    _check_same(a, b)
+
+
+def test_caller_stream_uses_one_slot(rt, assets):
+    import torch
+    s = torch.cuda.Stream()
+    sc = rt.Scene.preset("c1", assets)
+    R = make_renderer(rt, sc, 64, 48, "wavefront", seed=6, frames_in_flight=2, stream=s.cuda_stream)
+    R.draw()
+    R.draw()
+    assert R.stats().frames_in_flight == 1
+
+
+def test_rank_without_tiles(rt, assets):
+    sc = rt.Scene.preset("c1", assets)
+    R = make_renderer(rt, sc, 64, 64, "wavefront", seed=6, frames_in_flight=2)
+    assert R.tile_count(64, 3, 4) == 0   # one 64x64 tile, four ranks
+    for _ in range(3):
+        R.draw(tiles=(64, 3, 4))
+    st = R.stats()
+    assert st.frames_total == 3 and st.total_closest_rays == 0 and st.paths == 0
+
+
+def test_reupload_and_device_rebuild_between_frames(rt, assets):
+    def reupload(rt, R, sc):
+        R.upload(sc.desc())
+
+    def rebuild(rt, R, sc):
+        R.rebuild(device=True)
+    steps = _draws(2) + [reupload] + _draws(2) + [rebuild] + _draws(2)
+    a, _ = _seq(rt, assets, 1, steps)
+    b, _ = _seq(rt, assets, 2, steps)
+    _check_same(a, b)
