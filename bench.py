@@ -57,6 +57,8 @@ def parse():
     p.add_argument("--bvh", default="sah", choices=["sah", "lbvh"], help="host binned-SAH or on-device LBVH build")
     p.add_argument("--frames-in-flight", type=int, default=0,
                    help="frames the renderer overlaps (0 = library default 2, 1 = one at a time)")
+    p.add_argument("--animate", action="store_true",
+                   help="configs[4] shape: skin every skinned mesh at t = frame/60 s and refit the BVH before each frame")
     p.add_argument("--emulate-ranks", type=int, default=0,
                    help="tuning aid: one process renders rank 0's tiles of an N-way split (no gather)")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample time")
@@ -104,10 +106,27 @@ def main():
             gather.gather()   # packed tiles -> rank 0 over RCCL, unpacked into its radiance target
         return st
 
+    skinned = []
+    if a.animate:
+        d = scene.desc()
+        skinned = [m for m in range(d.mesh_count) if d.meshes[m].joint_count > 0]
+    tick = [0]
+
+    def animate():
+        # SkinningPass tick (Renderer.swift:1280-1326): joint matrices at t, skin, refit
+        if not skinned:
+            return
+        t = tick[0] / 60.0
+        tick[0] += 1
+        for m in skinned:
+            R.skin(m, scene.joint_matrices(m, t))
+        R.refit()
+
     def submit():
         # one step: the frame is submitted and, multi-GPU, its tiles packed, gathered to rank 0
         # over RCCL and unpacked there, all enqueued without a host wait (the renderer keeps two
         # frames in flight and waits for a slot's previous frame itself)
+        animate()
         R.draw(tiles=tiles)
         if gather is not None:
             gather.gather()
@@ -262,7 +281,7 @@ def main():
             # [generate, extend, shade, connect, resolve, finish, hit sort]
             "stage_ms": [round(x / a.steps, 3) for x in stage_ms[:7]], "sort_bins": a.sort_bins, "bvh": a.bvh,
             "pipeline_used": ["megakernel", "wavefront"][last_st.pipeline], "iterations": last_st.iterations,
-            "frames_in_flight": last_st.frames_in_flight,
+            "frames_in_flight": last_st.frames_in_flight, "animate": bool(skinned),
         },
         "roofline": {
             "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
