@@ -45,8 +45,18 @@ struct FrameSlot {
     hipEvent_t ev0 = nullptr, ev1 = nullptr, done = nullptr;
     bool pending = false, wavefront = false, used = false;
     uint64_t seq = 0;                           // frame number (harvest order)
+    int gen = 0;                                // geometry generation the frame reads
     DevBuf* bufs[18] = {&color, &accum, &meta, &q0, &q1, &hits, &sq, &counts, &extra, &sorted,
                         &sort_table, &sort_total, &params, &pray, &psray, &depth, &gbuffer, &counters};
+};
+// Per-frame geometry (what skinning, instance transforms and refit rewrite between frames), in two
+// generations: frames read generation `gcur`; the first update after a frame copies it into the
+// other generation (once the frames still reading that one have finished) and every update until
+// the next frame writes there, so frames in flight keep their geometry while the next frame's is
+// built (Renderer.swift keeps per-frame position buffers for the same reason, :1290-1303).
+struct Geo {
+    DevBuf pos, prev_pos, nrm, inst, prev_inst, tris, nodes, node_box;
+    DevBuf* all[8] = {&pos, &prev_pos, &nrm, &inst, &prev_inst, &tris, &nodes, &node_box};
 };
 constexpr int kMaxSlots = 3;
 constexpr int kTailInFlight = 2097152;   // default finish threshold with frames in flight
@@ -82,11 +92,18 @@ struct rt_ctx {
     std::vector<uint32_t> level_off;
 
     // device buffers
-    DevBuf d_pos, d_prev_pos, d_nrm, d_rest_pos, d_rest_nrm, d_jidx, d_jw, d_joints;
-    DevBuf d_tri_info, d_inst, d_prev_inst, d_mat, d_lights, d_halton;
+    Geo geo[2];
+    int gcur = 0;            // generation new frames read
+    bool gdirty = false;     // updates since the last frame went into generation 1 - gcur
+    hipStream_t ustream = nullptr;   // geometry updates (skin, transforms, refit)
+    hipEvent_t uev = nullptr;        // end of the latest update batch; frames wait on it
+    bool uev_valid = false;
+    Geo& G() { return geo[gdirty ? 1 - gcur : gcur]; }   // the generation updates and builds write
+    DevBuf d_rest_pos, d_rest_nrm, d_jidx, d_jw, d_joints;
+    DevBuf d_tri_info, d_mat, d_lights, d_halton;
     DevBuf d_tex_texels, d_tex_info, d_mat_tex, d_uv, d_tex_lut;   // texture path (textured scenes)
     bool textured = false;
-    DevBuf d_tris, d_nodes, d_node_box, d_slot_to_tri, d_levels, d_maxabs, d_tri_bin, d_lbvh_scratch;
+    DevBuf d_slot_to_tri, d_levels, d_maxabs, d_tri_bin, d_lbvh_scratch;
     uint32_t num_nodes8 = 0;
     uint32_t* h_lbvh = nullptr;   // pinned word for the device builder's level counts
     DevBuf d_random, d_accum[2];
@@ -200,9 +217,9 @@ static void xform_host(const float* m, const float4& p, float* out) {
 }
 
 static size_t ctx_bytes(const rt_ctx* c) {
-    const DevBuf* all[] = {&c->d_pos, &c->d_prev_pos, &c->d_nrm, &c->d_rest_pos, &c->d_rest_nrm, &c->d_jidx, &c->d_jw,
-                           &c->d_joints, &c->d_tri_info, &c->d_inst, &c->d_prev_inst, &c->d_mat, &c->d_lights,
-                           &c->d_halton, &c->d_tris, &c->d_nodes, &c->d_node_box, &c->d_slot_to_tri, &c->d_levels, &c->d_maxabs, &c->d_random,
+    const DevBuf* all[] = {&c->d_rest_pos, &c->d_rest_nrm, &c->d_jidx, &c->d_jw,
+                           &c->d_joints, &c->d_tri_info, &c->d_mat, &c->d_lights,
+                           &c->d_halton, &c->d_slot_to_tri, &c->d_levels, &c->d_maxabs, &c->d_random,
                            &c->d_accum[0], &c->d_accum[1], &c->d_tri_bin, &c->d_lbvh_scratch,
                            &c->d_tex_texels, &c->d_tex_info, &c->d_mat_tex, &c->d_uv, &c->d_tex_lut,
                            &c->d_hist[0], &c->d_hist[1], &c->d_hdepth[0], &c->d_hdepth[1], &c->d_present_out,
@@ -210,6 +227,8 @@ static size_t ctx_bytes(const rt_ctx* c) {
     size_t s = 0;
     for (auto* b : all) s += b->bytes;
     for (const DevBuf& b : c->d_motion) s += b.bytes;
+    for (const Geo& g : c->geo)
+        for (const DevBuf* b : g.all) s += b->bytes;
     for (const FrameSlot& f : c->slot)
         for (const DevBuf* b : f.bufs) s += b->bytes;
     return s;
@@ -278,11 +297,31 @@ static hipStream_t slot_stream(rt_ctx* c, int k) { return k == 0 ? c->stream : c
 // Waits for every frame in flight.  Everything that changes what frames read (scene, BVH,
 // targets, transforms) runs after it, so a frame never sees a half-updated scene.
 static rt_status drain_frames(rt_ctx* c) {
+    if (c->ustream) HIPC(c, hipStreamSynchronize(c->ustream));
     for (int k = 0; k < kMaxSlots; ++k)
         if (c->slot[k].used) {
             HIPC(c, hipStreamSynchronize(slot_stream(c, k)));
             HIPC(c, hipEventSynchronize(c->slot[k].done));
         }
+    return RT_OK;
+}
+
+// Before a geometry update: the first one after a frame switches to the other generation, once the
+// frames still reading it have finished, seeded with a copy of the current one (on the update
+// stream; frames keep reading the current generation meanwhile).
+static rt_status begin_update(rt_ctx* c) {
+    if (c->gdirty) return RT_OK;
+    const int w = 1 - c->gcur;
+    for (const FrameSlot& f : c->slot)
+        if (f.used && f.gen == w) HIPC(c, hipEventSynchronize(f.done));
+    Geo& src = c->geo[c->gcur];
+    Geo& dst = c->geo[w];
+    for (int i = 0; i < 8; ++i) {
+        if (rt_status st = dev_alloc(c, *dst.all[i], src.all[i]->bytes)) return st;
+        if (src.all[i]->bytes)
+            HIPC(c, hipMemcpyAsync(dst.all[i]->p, src.all[i]->p, src.all[i]->bytes, hipMemcpyDeviceToDevice, c->ustream));
+    }
+    c->gdirty = true;
     return RT_OK;
 }
 
@@ -331,6 +370,8 @@ rt_status rt_create(const rt_opts* opts, rt_ctx** out) {
     for (int k = 1; k < kMaxSlots; ++k)
         if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->slot[k].own_stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&c->scene_ev, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->ustream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->uev, hipEventDisableTiming);
     if (e != hipSuccess) {
         g_err = std::string("HIP init: ") + hipGetErrorString(e);
         delete c;
@@ -358,14 +399,19 @@ rt_status rt_destroy(rt_ctx* c) {
     if (c->stream) hipStreamSynchronize(c->stream);
     for (FrameSlot& f : c->slot)
         if (f.own_stream) hipStreamSynchronize(f.own_stream);
-    DevBuf* all[] = {&c->d_pos, &c->d_prev_pos, &c->d_nrm, &c->d_rest_pos, &c->d_rest_nrm, &c->d_jidx, &c->d_jw,
-                     &c->d_joints, &c->d_tri_info, &c->d_inst, &c->d_prev_inst, &c->d_mat, &c->d_lights, &c->d_halton,
-                     &c->d_tris, &c->d_nodes, &c->d_node_box, &c->d_slot_to_tri, &c->d_levels, &c->d_maxabs, &c->d_random, &c->d_accum[0],
+    DevBuf* all[] = {&c->d_rest_pos, &c->d_rest_nrm, &c->d_jidx, &c->d_jw,
+                     &c->d_joints, &c->d_tri_info, &c->d_mat, &c->d_lights, &c->d_halton,
+                     &c->d_slot_to_tri, &c->d_levels, &c->d_maxabs, &c->d_random, &c->d_accum[0],
                      &c->d_accum[1], &c->d_tri_bin, &c->d_lbvh_scratch, &c->d_tex_texels, &c->d_tex_info,
                      &c->d_mat_tex, &c->d_uv, &c->d_tex_lut, &c->d_hist[0], &c->d_hist[1], &c->d_hdepth[0],
                      &c->d_hdepth[1], &c->d_present_out, &c->d_present_thr};
     for (auto* b : all) dev_free(*b);
     for (DevBuf& b : c->d_motion) dev_free(b);
+    for (Geo& g : c->geo)
+        for (DevBuf* b : g.all) dev_free(*b);
+    if (c->ustream) hipStreamSynchronize(c->ustream);
+    if (c->uev) hipEventDestroy(c->uev);
+    if (c->ustream) hipStreamDestroy(c->ustream);
     if (c->h_lbvh) hipHostFree(c->h_lbvh);
     if (c->scene_ev) hipEventDestroy(c->scene_ev);
     for (FrameSlot& f : c->slot) {
@@ -545,12 +591,12 @@ rt_status rt_scene_upload(rt_ctx* c, const rt_scene_desc* sd) {
     c->h_lights.assign(sd->lights, sd->lights + sd->light_count);
     rt_status st;
     if ((st = upload_textures(c, sd))) return st;
-    if ((st = dev_upload(c, c->d_pos, c->h_pos.data(), nv * 16))) return st;
-    if ((st = dev_upload(c, c->d_prev_pos, c->h_pos.data(), nv * 16))) return st;  // previousPositions = positions (SubMesh.swift:60)
-    if ((st = dev_upload(c, c->d_nrm, c->h_nrm.data(), nv * 16))) return st;
+    if ((st = dev_upload(c, c->G().pos, c->h_pos.data(), nv * 16))) return st;
+    if ((st = dev_upload(c, c->G().prev_pos, c->h_pos.data(), nv * 16))) return st;  // previousPositions = positions (SubMesh.swift:60)
+    if ((st = dev_upload(c, c->G().nrm, c->h_nrm.data(), nv * 16))) return st;
     if ((st = dev_upload(c, c->d_tri_info, c->h_tri_info.data(), nt * 16))) return st;
-    if ((st = dev_upload(c, c->d_inst, c->h_inst.data(), c->h_inst.size() * 4))) return st;
-    if ((st = dev_upload(c, c->d_prev_inst, c->h_inst.data(), c->h_inst.size() * 4))) return st;
+    if ((st = dev_upload(c, c->G().inst, c->h_inst.data(), c->h_inst.size() * 4))) return st;
+    if ((st = dev_upload(c, c->G().prev_inst, c->h_inst.data(), c->h_inst.size() * 4))) return st;
     if ((st = dev_upload(c, c->d_mat, c->h_mat.data(), c->h_mat.size() * sizeof(Material)))) return st;
     if ((st = dev_upload(c, c->d_lights, c->h_lights.data(), c->h_lights.size() * sizeof(Light)))) return st;
     if (any_skin) {
@@ -586,7 +632,7 @@ rt_status rt_bvh_build(rt_ctx* c) {
     HIPC(c, hipStreamSynchronize(c->stream));
     // current world-space triangles (may have been skinned / re-transformed on the device)
     if (c->world_dirty) {
-        HIPC(c, hipMemcpy(c->h_pos.data(), c->d_pos.p, (size_t)c->num_verts * 16, hipMemcpyDeviceToHost));
+        HIPC(c, hipMemcpy(c->h_pos.data(), c->G().pos.p, (size_t)c->num_verts * 16, hipMemcpyDeviceToHost));
         for (uint32_t t = 0; t < c->num_tris; ++t) {
             const uint4& ti = c->h_tri_info[t];
             const float* M = &c->h_inst[12 * (ti.w >> 8)];
@@ -625,9 +671,10 @@ rt_status rt_bvh_build(rt_ctx* c) {
     std::vector<uint32_t> fill(c->level_off.begin(), c->level_off.end() - 1);
     for (size_t k = 0; k < nn; ++k) c->level_nodes[fill[depth[k]]++] = (uint32_t)k;
     rt_status st;
-    if ((st = dev_upload(c, c->d_tris, tris.data(), tris.size() * 16))) return st;
-    if ((st = dev_upload(c, c->d_nodes, c->bvh8.nodes.data(), nn * sizeof(Bvh8Node)))) return st;
-    if ((st = dev_upload(c, c->d_node_box, c->bvh8.node_box.data(), c->bvh8.node_box.size() * 4))) return st;
+    Geo& g = c->G();
+    if ((st = dev_upload(c, g.tris, tris.data(), tris.size() * 16))) return st;
+    if ((st = dev_upload(c, g.nodes, c->bvh8.nodes.data(), nn * sizeof(Bvh8Node)))) return st;
+    if ((st = dev_upload(c, g.node_box, c->bvh8.node_box.data(), c->bvh8.node_box.size() * 4))) return st;
     if ((st = dev_upload(c, c->d_slot_to_tri, c->bvh8.tri_order.data(), (size_t)n * 4))) return st;
     if ((st = dev_upload(c, c->d_levels, c->level_nodes.data(), c->level_nodes.size() * 4))) return st;
     // hit-sort keys: the leaf-order bin of every triangle (DevScene::tri_bin)
@@ -649,16 +696,17 @@ rt_status rt_bvh_build_device(rt_ctx* c) {
     const uint32_t n = c->num_tris;
     rt_status st;
     if ((st = dev_alloc(c, c->d_lbvh_scratch, lbvh_scratch_bytes(n)))) return st;
-    if ((st = dev_alloc(c, c->d_nodes, (size_t)n * sizeof(Bvh8Node)))) return st;
-    if ((st = dev_alloc(c, c->d_node_box, (size_t)n * 6 * sizeof(float)))) return st;
+    Geo& g = c->G();
+    if ((st = dev_alloc(c, g.nodes, (size_t)n * sizeof(Bvh8Node)))) return st;
+    if ((st = dev_alloc(c, g.node_box, (size_t)n * 6 * sizeof(float)))) return st;
     if ((st = dev_alloc(c, c->d_slot_to_tri, (size_t)n * 4))) return st;
     if ((st = dev_alloc(c, c->d_tri_bin, (size_t)n * 2))) return st;
     if ((st = dev_alloc(c, c->d_levels, (size_t)n * 4))) return st;
-    if ((st = dev_alloc(c, c->d_tris, (size_t)n * 48))) return st;
+    if ((st = dev_alloc(c, g.tris, (size_t)n * 48))) return st;
     if ((st = dev_alloc(c, c->d_maxabs, 4))) return st;
     if (!c->h_lbvh) HIPC(c, hipHostMalloc((void**)&c->h_lbvh, 16, 0));
-    LbvhInput in{(const float4*)c->d_pos.p, (const uint4*)c->d_tri_info.p, (const float*)c->d_inst.p, n};
-    LbvhOutput out{(Bvh8Node*)c->d_nodes.p, (float*)c->d_node_box.p, (uint32_t*)c->d_slot_to_tri.p,
+    LbvhInput in{(const float4*)g.pos.p, (const uint4*)c->d_tri_info.p, (const float*)g.inst.p, n};
+    LbvhOutput out{(Bvh8Node*)g.nodes.p, (float*)g.node_box.p, (uint32_t*)c->d_slot_to_tri.p,
                    (uint16_t*)c->d_tri_bin.p, (uint32_t*)c->d_levels.p, c->h_lbvh};
     LbvhResult res;
     const char* err = nullptr;
@@ -668,8 +716,8 @@ rt_status rt_bvh_build_device(rt_ctx* c) {
     }
     // world-space triangles in the new slot order
     HIPC(c, hipMemsetAsync(c->d_maxabs.p, 0, 4, c->stream));
-    launch_flatten((const uint4*)c->d_tri_info.p, (const uint32_t*)c->d_slot_to_tri.p, (const float4*)c->d_pos.p,
-                   (const float*)c->d_inst.p, (float4*)c->d_tris.p, n, (unsigned*)c->d_maxabs.p, c->stream);
+    launch_flatten((const uint4*)c->d_tri_info.p, (const uint32_t*)c->d_slot_to_tri.p, (const float4*)g.pos.p,
+                   (const float*)g.inst.p, (float4*)g.tris.p, n, (unsigned*)c->d_maxabs.p, c->stream);
     HIPC(c, hipGetLastError());
     HIPC(c, hipStreamSynchronize(c->stream));
     if (res.num_nodes >= (1u << 23)) FAIL(c, RT_ERR_UNSUPPORTED, "BVH too large (2^23 nodes)");
@@ -684,19 +732,20 @@ rt_status rt_bvh_build_device(rt_ctx* c) {
 
 rt_status rt_bvh_refit(rt_ctx* c) {
     if (!c) FAIL(c, RT_ERR_INVALID_ARG, "null ctx");
-    if (rt_status dst = drain_frames(c)) return dst;
     if (!c->bvh_ready) FAIL(c, RT_ERR_STATE, "rt_bvh_refit before rt_bvh_build");
     HIPC(c, hipSetDevice(c->device));
-    rt_status st = dev_alloc(c, c->d_maxabs, 4);
+    rt_status st = begin_update(c);   // frames in flight keep their generation
+    if (!st) st = dev_alloc(c, c->d_maxabs, 4);
     if (st) return st;
-    HIPC(c, hipMemsetAsync(c->d_maxabs.p, 0, 4, c->stream));
-    launch_flatten((const uint4*)c->d_tri_info.p, (const uint32_t*)c->d_slot_to_tri.p, (const float4*)c->d_pos.p,
-                   (const float*)c->d_inst.p, (float4*)c->d_tris.p, c->num_tris, (unsigned*)c->d_maxabs.p, c->stream);
+    Geo& g = c->G();
+    HIPC(c, hipMemsetAsync(c->d_maxabs.p, 0, 4, c->ustream));
+    launch_flatten((const uint4*)c->d_tri_info.p, (const uint32_t*)c->d_slot_to_tri.p, (const float4*)g.pos.p,
+                   (const float*)g.inst.p, (float4*)g.tris.p, c->num_tris, (unsigned*)c->d_maxabs.p, c->ustream);
     for (int d = (int)c->level_off.size() - 2; d >= 0; --d) {
         uint32_t off = c->level_off[d], cnt = c->level_off[d + 1] - off;
-        launch_refit8_level((Bvh8Node*)c->d_nodes.p, (float*)c->d_node_box.p, (const float4*)c->d_tris.p,
+        launch_refit8_level((Bvh8Node*)g.nodes.p, (float*)g.node_box.p, (const float4*)g.tris.p,
                             (const uint32_t*)c->d_levels.p + off, cnt, c->bvh8.pad, (const unsigned*)c->d_maxabs.p,
-                            c->stream);
+                            c->ustream);
     }
     HIPC(c, hipGetLastError());
     return RT_OK;
@@ -704,36 +753,38 @@ rt_status rt_bvh_refit(rt_ctx* c) {
 
 rt_status rt_set_instance_transforms(rt_ctx* c, const rt_packed_float4x3* t, uint32_t count) {
     if (!c || !t) FAIL(c, RT_ERR_INVALID_ARG, "null argument");
-    if (rt_status dst = drain_frames(c)) return dst;
     if (!c->scene_ready || count != c->num_inst) FAIL(c, RT_ERR_INVALID_ARG, "transform count != mesh count");
     HIPC(c, hipSetDevice(c->device));
+    if (rt_status st = begin_update(c)) return st;   // frames in flight keep their generation
+    Geo& g = c->G();
     // prev <- cur (Renderer.swift:939-944), then the new transforms
-    HIPC(c, hipMemcpyAsync(c->d_prev_inst.p, c->d_inst.p, c->h_inst.size() * 4, hipMemcpyDeviceToDevice, c->stream));
+    HIPC(c, hipMemcpyAsync(g.prev_inst.p, g.inst.p, c->h_inst.size() * 4, hipMemcpyDeviceToDevice, c->ustream));
     c->inst_moved = std::memcmp(c->h_inst.data(), t, (size_t)count * 48) != 0;
     std::memcpy(c->h_inst.data(), t, (size_t)count * 48);
-    HIPC(c, hipMemcpyAsync(c->d_inst.p, c->h_inst.data(), c->h_inst.size() * 4, hipMemcpyHostToDevice, c->stream));
-    HIPC(c, hipStreamSynchronize(c->stream));
+    HIPC(c, hipMemcpyAsync(g.inst.p, c->h_inst.data(), c->h_inst.size() * 4, hipMemcpyHostToDevice, c->ustream));
+    HIPC(c, hipStreamSynchronize(c->ustream));   // h_inst is the copy's source
     c->world_dirty = true;
     return RT_OK;
 }
 
 rt_status rt_skin(rt_ctx* c, uint32_t mesh_index, const float* joints, uint32_t joint_count) {
     if (!c || !joints) FAIL(c, RT_ERR_INVALID_ARG, "null argument");
-    if (rt_status dst = drain_frames(c)) return dst;
     if (!c->scene_ready || mesh_index >= c->meshes.size()) FAIL(c, RT_ERR_INVALID_ARG, "bad mesh index");
     const MeshInfo& mi = c->meshes[mesh_index];
     if (!mi.skinned) FAIL(c, RT_ERR_INVALID_ARG, "mesh is not skinned");
     if (joint_count != mi.joint_count) FAIL(c, RT_ERR_INVALID_ARG, "joint count mismatch");
     HIPC(c, hipSetDevice(c->device));
-    HIPC(c, hipMemcpyAsync(c->d_joints.p, joints, (size_t)joint_count * 64, hipMemcpyHostToDevice, c->stream));
+    if (rt_status st = begin_update(c)) return st;   // frames in flight keep their generation
+    Geo& g = c->G();
+    HIPC(c, hipMemcpyAsync(c->d_joints.p, joints, (size_t)joint_count * 64, hipMemcpyHostToDevice, c->ustream));
     // previousPositions <- positions (Renderer.swift:1290-1303)
-    HIPC(c, hipMemcpyAsync((float4*)c->d_prev_pos.p + mi.vbase, (float4*)c->d_pos.p + mi.vbase, (size_t)mi.vcount * 16,
-                           hipMemcpyDeviceToDevice, c->stream));
+    HIPC(c, hipMemcpyAsync((float4*)g.prev_pos.p + mi.vbase, (float4*)g.pos.p + mi.vbase, (size_t)mi.vcount * 16,
+                           hipMemcpyDeviceToDevice, c->ustream));
     launch_skin((const float4*)c->d_rest_pos.p + mi.vbase, (const float4*)c->d_rest_nrm.p + mi.vbase,
                 (const ushort4*)c->d_jidx.p + mi.vbase, (const float4*)c->d_jw.p + mi.vbase, (const float*)c->d_joints.p,
-                (float4*)c->d_pos.p + mi.vbase, (float4*)c->d_nrm.p + mi.vbase, mi.vcount, c->stream);
+                (float4*)g.pos.p + mi.vbase, (float4*)g.nrm.p + mi.vbase, mi.vcount, c->ustream);
     HIPC(c, hipGetLastError());
-    HIPC(c, hipStreamSynchronize(c->stream));  // joint upload buffer is reused next call
+    HIPC(c, hipStreamSynchronize(c->ustream));  // joint upload buffer is reused next call
     c->world_dirty = true;
     c->skin_moved = true;   // conservative: positions may now differ from previousPositions
     return RT_OK;
@@ -885,19 +936,27 @@ rt_status rt_render_frame(rt_ctx* c, const Uniforms* U, const rt_tile_set* tiles
         HIPC(c, hipEventRecord(c->scene_ev, c->stream));
         HIPC(c, hipStreamWaitEvent(stream, c->scene_ev, 0));
     }
+    if (c->gdirty) {   // this frame reads the updated generation
+        HIPC(c, hipEventRecord(c->uev, c->ustream));
+        c->uev_valid = true;
+        c->gcur = 1 - c->gcur;
+        c->gdirty = false;
+    }
+    if (c->uev_valid) HIPC(c, hipStreamWaitEvent(stream, c->uev, 0));
+    const Geo& geo = c->geo[c->gcur];
     if (U->enableDenoiseGBuffer && !F.gbuffer.p) {
         if ((st = dev_alloc(c, F.gbuffer, 4 * n * 16))) return st;
         HIPC(c, hipMemsetAsync(F.gbuffer.p, 0, 4 * n * 16, stream));
     }
     DevScene S;
-    S.tris = (const float4*)c->d_tris.p;
-    S.nodes8 = (const Bvh8Node*)c->d_nodes.p;
+    S.tris = (const float4*)geo.tris.p;
+    S.nodes8 = (const Bvh8Node*)geo.nodes.p;
     S.tri_info = (const uint4*)c->d_tri_info.p;
-    S.pos = (const float4*)c->d_pos.p;
-    S.prev_pos = (const float4*)c->d_prev_pos.p;
-    S.nrm = (const float4*)c->d_nrm.p;
-    S.inst = (const float*)c->d_inst.p;
-    S.prev_inst = (const float*)c->d_prev_inst.p;
+    S.pos = (const float4*)geo.pos.p;
+    S.prev_pos = (const float4*)geo.prev_pos.p;
+    S.nrm = (const float4*)geo.nrm.p;
+    S.inst = (const float*)geo.inst.p;
+    S.prev_inst = (const float*)geo.prev_inst.p;
     S.materials = (const Material*)c->d_mat.p;
     S.lights = (const Light*)c->d_lights.p;
     S.halton = (const HaltonDim*)c->d_halton.p;
@@ -968,6 +1027,7 @@ rt_status rt_render_frame(rt_ctx* c, const Uniforms* U, const rt_tile_set* tiles
     F.pending = true;
     F.used = true;
     F.seq = c->frame_no;
+    F.gen = c->gcur;
     c->last_slot = k;
     c->frame_no += 1;
     c->tiles_pending = false;
