@@ -286,6 +286,8 @@ def main():
         "roofline": {
             "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": traffic_src,
+            # measured HBM bytes of one launch (PMC) over the launch time: what actually crossed HBM
+            "hbm_GBs": round(traffic / (launch_ms * 1e-3) / 1e9, 1) if traffic else None,
             "l2_hit": l2_hit,
             "job_achieved": round(job_achieved, 1), "job_frac": round(job_achieved / HBM_PEAK_GBS, 4),
             "job_bytes_per_frame": int(job_bytes),
