@@ -59,6 +59,7 @@ def parse():
                    help="frames the renderer overlaps (0 = library default 2, 1 = one at a time)")
     p.add_argument("--animate", action="store_true",
                    help="configs[4] shape: skin every skinned mesh at t = frame/60 s and refit the BVH before each frame")
+    p.add_argument("--rebuild", action="store_true", help="with --animate: rebuild the BVH on the device instead of refitting")
     p.add_argument("--emulate-ranks", type=int, default=0,
                    help="tuning aid: one process renders rank 0's tiles of an N-way split (no gather)")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample time")
@@ -120,7 +121,7 @@ def main():
         tick[0] += 1
         for m in skinned:
             R.skin(m, scene.joint_matrices(m, t))
-        R.refit()
+        R.rebuild(device=True) if a.rebuild else R.refit()
 
     def submit():
         # one step: the frame is submitted and, multi-GPU, its tiles packed, gathered to rank 0

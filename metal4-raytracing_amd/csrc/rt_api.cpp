@@ -55,8 +55,9 @@ struct FrameSlot {
 // the next frame writes there, so frames in flight keep their geometry while the next frame's is
 // built (Renderer.swift keeps per-frame position buffers for the same reason, :1290-1303).
 struct Geo {
-    DevBuf pos, prev_pos, nrm, inst, prev_inst, tris, nodes, node_box;
-    DevBuf* all[8] = {&pos, &prev_pos, &nrm, &inst, &prev_inst, &tris, &nodes, &node_box};
+    DevBuf pos, prev_pos, nrm, inst, prev_inst, tris, nodes, node_box, tri_bin;
+    DevBuf* all[9] = {&pos, &prev_pos, &nrm, &inst, &prev_inst, &tris, &nodes, &node_box, &tri_bin};
+    uint32_t num_nodes8 = 0;
 };
 constexpr int kMaxSlots = 3;
 constexpr int kTailInFlight = 2097152;   // default finish threshold with frames in flight
@@ -103,7 +104,7 @@ struct rt_ctx {
     DevBuf d_tri_info, d_mat, d_lights, d_halton;
     DevBuf d_tex_texels, d_tex_info, d_mat_tex, d_uv, d_tex_lut;   // texture path (textured scenes)
     bool textured = false;
-    DevBuf d_slot_to_tri, d_levels, d_maxabs, d_tri_bin, d_lbvh_scratch;
+    DevBuf d_slot_to_tri, d_levels, d_maxabs, d_lbvh_scratch;
     uint32_t num_nodes8 = 0;
     uint32_t* h_lbvh = nullptr;   // pinned word for the device builder's level counts
     DevBuf d_random, d_accum[2];
@@ -163,10 +164,10 @@ static rt_status dev_alloc(rt_ctx* c, DevBuf& b, size_t bytes) {
     b.bytes = bytes;
     return RT_OK;
 }
-static rt_status dev_upload(rt_ctx* c, DevBuf& b, const void* src, size_t bytes) {
+static rt_status dev_upload(rt_ctx* c, DevBuf& b, const void* src, size_t bytes, hipStream_t s = nullptr) {
     rt_status st = dev_alloc(c, b, bytes);
     if (st) return st;
-    if (bytes) HIPC(c, hipMemcpyAsync(b.p, src, bytes, hipMemcpyHostToDevice, c->stream));
+    if (bytes) HIPC(c, hipMemcpyAsync(b.p, src, bytes, hipMemcpyHostToDevice, s ? s : c->stream));
     return RT_OK;
 }
 static void dev_free(DevBuf& b) {
@@ -220,7 +221,7 @@ static size_t ctx_bytes(const rt_ctx* c) {
     const DevBuf* all[] = {&c->d_rest_pos, &c->d_rest_nrm, &c->d_jidx, &c->d_jw,
                            &c->d_joints, &c->d_tri_info, &c->d_mat, &c->d_lights,
                            &c->d_halton, &c->d_slot_to_tri, &c->d_levels, &c->d_maxabs, &c->d_random,
-                           &c->d_accum[0], &c->d_accum[1], &c->d_tri_bin, &c->d_lbvh_scratch,
+                           &c->d_accum[0], &c->d_accum[1], &c->d_lbvh_scratch,
                            &c->d_tex_texels, &c->d_tex_info, &c->d_mat_tex, &c->d_uv, &c->d_tex_lut,
                            &c->d_hist[0], &c->d_hist[1], &c->d_hdepth[0], &c->d_hdepth[1], &c->d_present_out,
                            &c->d_present_thr};
@@ -316,11 +317,12 @@ static rt_status begin_update(rt_ctx* c) {
         if (f.used && f.gen == w) HIPC(c, hipEventSynchronize(f.done));
     Geo& src = c->geo[c->gcur];
     Geo& dst = c->geo[w];
-    for (int i = 0; i < 8; ++i) {
+    for (int i = 0; i < 9; ++i) {
         if (rt_status st = dev_alloc(c, *dst.all[i], src.all[i]->bytes)) return st;
         if (src.all[i]->bytes)
             HIPC(c, hipMemcpyAsync(dst.all[i]->p, src.all[i]->p, src.all[i]->bytes, hipMemcpyDeviceToDevice, c->ustream));
     }
+    dst.num_nodes8 = src.num_nodes8;
     c->gdirty = true;
     return RT_OK;
 }
@@ -402,7 +404,7 @@ rt_status rt_destroy(rt_ctx* c) {
     DevBuf* all[] = {&c->d_rest_pos, &c->d_rest_nrm, &c->d_jidx, &c->d_jw,
                      &c->d_joints, &c->d_tri_info, &c->d_mat, &c->d_lights, &c->d_halton,
                      &c->d_slot_to_tri, &c->d_levels, &c->d_maxabs, &c->d_random, &c->d_accum[0],
-                     &c->d_accum[1], &c->d_tri_bin, &c->d_lbvh_scratch, &c->d_tex_texels, &c->d_tex_info,
+                     &c->d_accum[1], &c->d_lbvh_scratch, &c->d_tex_texels, &c->d_tex_info,
                      &c->d_mat_tex, &c->d_uv, &c->d_tex_lut, &c->d_hist[0], &c->d_hist[1], &c->d_hdepth[0],
                      &c->d_hdepth[1], &c->d_present_out, &c->d_present_thr};
     for (auto* b : all) dev_free(*b);
@@ -626,10 +628,11 @@ rt_status rt_scene_upload(rt_ctx* c, const rt_scene_desc* sd) {
 
 rt_status rt_bvh_build(rt_ctx* c) {
     if (!c) FAIL(c, RT_ERR_INVALID_ARG, "null ctx");
-    if (rt_status dst = drain_frames(c)) return dst;
     if (!c->scene_ready) FAIL(c, RT_ERR_STATE, "rt_bvh_build before rt_scene_upload");
     HIPC(c, hipSetDevice(c->device));
-    HIPC(c, hipStreamSynchronize(c->stream));
+    // into the update generation: frames in flight keep theirs (and their tree)
+    if (rt_status ust = begin_update(c)) return ust;
+    HIPC(c, hipStreamSynchronize(c->ustream));
     // current world-space triangles (may have been skinned / re-transformed on the device)
     if (c->world_dirty) {
         HIPC(c, hipMemcpy(c->h_pos.data(), c->G().pos.p, (size_t)c->num_verts * 16, hipMemcpyDeviceToHost));
@@ -672,16 +675,18 @@ rt_status rt_bvh_build(rt_ctx* c) {
     for (size_t k = 0; k < nn; ++k) c->level_nodes[fill[depth[k]]++] = (uint32_t)k;
     rt_status st;
     Geo& g = c->G();
-    if ((st = dev_upload(c, g.tris, tris.data(), tris.size() * 16))) return st;
-    if ((st = dev_upload(c, g.nodes, c->bvh8.nodes.data(), nn * sizeof(Bvh8Node)))) return st;
-    if ((st = dev_upload(c, g.node_box, c->bvh8.node_box.data(), c->bvh8.node_box.size() * 4))) return st;
-    if ((st = dev_upload(c, c->d_slot_to_tri, c->bvh8.tri_order.data(), (size_t)n * 4))) return st;
-    if ((st = dev_upload(c, c->d_levels, c->level_nodes.data(), c->level_nodes.size() * 4))) return st;
+    hipStream_t us = c->ustream;
+    if ((st = dev_upload(c, g.tris, tris.data(), tris.size() * 16, us))) return st;
+    if ((st = dev_upload(c, g.nodes, c->bvh8.nodes.data(), nn * sizeof(Bvh8Node), us))) return st;
+    if ((st = dev_upload(c, g.node_box, c->bvh8.node_box.data(), c->bvh8.node_box.size() * 4, us))) return st;
+    if ((st = dev_upload(c, c->d_slot_to_tri, c->bvh8.tri_order.data(), (size_t)n * 4, us))) return st;
+    if ((st = dev_upload(c, c->d_levels, c->level_nodes.data(), c->level_nodes.size() * 4, us))) return st;
     // hit-sort keys: the leaf-order bin of every triangle (DevScene::tri_bin)
     std::vector<uint16_t> tri_bin(n);
     for (uint32_t k = 0; k < n; ++k) tri_bin[c->bvh8.tri_order[k]] = (uint16_t)(((uint64_t)k * kSortMaxBins) / n);
-    if ((st = dev_upload(c, c->d_tri_bin, tri_bin.data(), (size_t)n * 2))) return st;
-    HIPC(c, hipStreamSynchronize(c->stream));
+    if ((st = dev_upload(c, g.tri_bin, tri_bin.data(), (size_t)n * 2, us))) return st;
+    HIPC(c, hipStreamSynchronize(us));   // the host arrays are the copies' sources
+    g.num_nodes8 = (uint32_t)nn;
     c->num_nodes8 = (uint32_t)nn;
     c->bvh_ready = true;
     return RT_OK;
@@ -689,43 +694,46 @@ rt_status rt_bvh_build(rt_ctx* c) {
 
 rt_status rt_bvh_build_device(rt_ctx* c) {
     if (!c) FAIL(c, RT_ERR_INVALID_ARG, "null ctx");
-    if (rt_status dst = drain_frames(c)) return dst;
     if (!c->scene_ready) FAIL(c, RT_ERR_STATE, "rt_bvh_build_device before rt_scene_upload");
     if (c->num_tris < 2) return rt_bvh_build(c);   // nothing to sort: the host path is exact and instant
     HIPC(c, hipSetDevice(c->device));
+    // into the update generation on the update stream: frames in flight keep their tree
+    rt_status st = begin_update(c);
+    if (st) return st;
     const uint32_t n = c->num_tris;
-    rt_status st;
+    hipStream_t us = c->ustream;
     if ((st = dev_alloc(c, c->d_lbvh_scratch, lbvh_scratch_bytes(n)))) return st;
     Geo& g = c->G();
     if ((st = dev_alloc(c, g.nodes, (size_t)n * sizeof(Bvh8Node)))) return st;
     if ((st = dev_alloc(c, g.node_box, (size_t)n * 6 * sizeof(float)))) return st;
     if ((st = dev_alloc(c, c->d_slot_to_tri, (size_t)n * 4))) return st;
-    if ((st = dev_alloc(c, c->d_tri_bin, (size_t)n * 2))) return st;
+    if ((st = dev_alloc(c, g.tri_bin, (size_t)n * 2))) return st;
     if ((st = dev_alloc(c, c->d_levels, (size_t)n * 4))) return st;
     if ((st = dev_alloc(c, g.tris, (size_t)n * 48))) return st;
     if ((st = dev_alloc(c, c->d_maxabs, 4))) return st;
     if (!c->h_lbvh) HIPC(c, hipHostMalloc((void**)&c->h_lbvh, 16, 0));
     LbvhInput in{(const float4*)g.pos.p, (const uint4*)c->d_tri_info.p, (const float*)g.inst.p, n};
     LbvhOutput out{(Bvh8Node*)g.nodes.p, (float*)g.node_box.p, (uint32_t*)c->d_slot_to_tri.p,
-                   (uint16_t*)c->d_tri_bin.p, (uint32_t*)c->d_levels.p, c->h_lbvh};
+                   (uint16_t*)g.tri_bin.p, (uint32_t*)c->d_levels.p, c->h_lbvh};
     LbvhResult res;
     const char* err = nullptr;
-    if (!lbvh_build(in, out, c->d_lbvh_scratch.p, c->stream, &res, &err)) {
+    if (!lbvh_build(in, out, c->d_lbvh_scratch.p, us, &res, &err)) {
         c->bvh_ready = false;
         FAIL(c, RT_ERR_UNSUPPORTED, std::string("device BVH build: ") + (err ? err : "?"));
     }
     // world-space triangles in the new slot order
-    HIPC(c, hipMemsetAsync(c->d_maxabs.p, 0, 4, c->stream));
+    HIPC(c, hipMemsetAsync(c->d_maxabs.p, 0, 4, us));
     launch_flatten((const uint4*)c->d_tri_info.p, (const uint32_t*)c->d_slot_to_tri.p, (const float4*)g.pos.p,
-                   (const float*)g.inst.p, (float4*)g.tris.p, n, (unsigned*)c->d_maxabs.p, c->stream);
+                   (const float*)g.inst.p, (float4*)g.tris.p, n, (unsigned*)c->d_maxabs.p, us);
     HIPC(c, hipGetLastError());
-    HIPC(c, hipStreamSynchronize(c->stream));
+    HIPC(c, hipStreamSynchronize(us));
     if (res.num_nodes >= (1u << 23)) FAIL(c, RT_ERR_UNSUPPORTED, "BVH too large (2^23 nodes)");
     c->level_off = res.level_off;
     c->bvh8 = Bvh8Result();            // the host copy describes the host builder's trees only
     c->bvh8.pad = res.pad;
     c->bvh8.max_depth = res.max_depth;
     c->num_nodes8 = res.num_nodes;
+    g.num_nodes8 = res.num_nodes;
     c->bvh_ready = true;
     return RT_OK;
 }
@@ -960,11 +968,11 @@ rt_status rt_render_frame(rt_ctx* c, const Uniforms* U, const rt_tile_set* tiles
     S.materials = (const Material*)c->d_mat.p;
     S.lights = (const Light*)c->d_lights.p;
     S.halton = (const HaltonDim*)c->d_halton.p;
-    S.tri_bin = (const uint16_t*)c->d_tri_bin.p;
+    S.tri_bin = (const uint16_t*)geo.tri_bin.p;
     S.max_submeshes = c->max_sub;
     S.num_materials = (int)c->h_mat.size();
     S.num_tris = (int)c->num_tris;
-    S.num_nodes8 = (int)c->num_nodes8;
+    S.num_nodes8 = (int)geo.num_nodes8;
     S.textured = c->textured ? 1 : 0;
     if (c->textured) {
         S.tex_texels = (const uchar4*)c->d_tex_texels.p;

@@ -90,7 +90,7 @@ def test_reupload_and_device_rebuild_between_frames(rt, assets):
     _check_same(a, b)
 
 
-def _animated(rt, assets, fif, frames=6, rebuild_at=None, move=False):
+def _animated(rt, assets, fif, frames=6, rebuild_at=None, move=False, rebuild_every=None):
     sc = rt.Scene.preset("c5", assets)
     d = sc.desc()
     skinned = [m for m in range(d.mesh_count) if d.meshes[m].joint_count > 0]
@@ -104,7 +104,9 @@ def _animated(rt, assets, fif, frames=6, rebuild_at=None, move=False):
         if move:
             mats[skinned[0], 3, 0] += 0.01
             R.set_instance_transforms(mats)
-        if rebuild_at is not None and i == rebuild_at:
+        if rebuild_every is not None:
+            R.rebuild(device=rebuild_every == "device")
+        elif rebuild_at is not None and i == rebuild_at:
             R.rebuild(device=True)
         else:
             R.refit()
@@ -114,7 +116,8 @@ def _animated(rt, assets, fif, frames=6, rebuild_at=None, move=False):
     return img, depth, motion, R.stats()
 
 
-@pytest.mark.parametrize("kw", [dict(), dict(move=True), dict(rebuild_at=3)])
+@pytest.mark.parametrize("kw", [dict(), dict(move=True), dict(rebuild_at=3), dict(rebuild_every="device"),
+                                dict(rebuild_every="host", move=True)])
 def test_animated_frames_in_flight(rt, assets, kw):
     """Per-frame skinning + refit (configs[4] shape) with frames in flight: the updates go to the
     other geometry generation while the previous frame still renders; bytes equal the serial run."""
