@@ -4,7 +4,8 @@
 // Renderer.swift:464-606) and the legacy full-rebuild path (Renderer.swift:1252-1277) with a
 // build that never leaves the GPU:
 //   1. world-space triangle boxes, centroid bounds, max |coordinate| (box padding)
-//   2. 62-bit keys: 30-bit Morton code of the centroid << 32 | triangle id (unique keys)
+//   2. 64-bit keys: Morton code of the centroid (as many bits per axis as fit, up to 21) << id bits
+//      | triangle id (unique keys)
 //   3. stable LSD radix sort of the keys (8-bit digits: per-tile histograms, one scan, a
 //      scatter whose in-tile ranks come from wave ballots, so equal digits keep their order)
 //   4. binary radix tree over the sorted keys (Karras, HPG 2012), one thread per inner node
@@ -17,6 +18,8 @@
 // Boxes are padded exactly as the host builder pads them, so traversal stays conservative and
 // returns the same closest hits as with the host SAH tree: the image does not
 // depend on which builder made the tree.
+#include <algorithm>
+
 #include "rt_kernels.h"
 
 #include <cstring>
@@ -40,12 +43,14 @@ __device__ __forceinline__ float o2f(uint32_t o) {
     return __uint_as_float((o & 0x80000000u) ? (o & 0x7fffffffu) : ~o);
 }
 
-__device__ __forceinline__ uint32_t expand_bits(uint32_t v) {  // 10 bits -> every third bit
-    v = (v * 0x00010001u) & 0xFF0000FFu;
-    v = (v * 0x00000101u) & 0x0F00F00Fu;
-    v = (v * 0x00000011u) & 0xC30C30C3u;
-    v = (v * 0x00000005u) & 0x49249249u;
-    return v;
+__device__ __forceinline__ unsigned long long expand_bits21(uint32_t v) {  // 21 bits -> every third bit
+    unsigned long long x = v & 0x1fffffu;
+    x = (x | x << 32) & 0x1f00000000ffffull;
+    x = (x | x << 16) & 0x1f0000ff0000ffull;
+    x = (x | x << 8) & 0x100f00f00f00f00full;
+    x = (x | x << 4) & 0x10c30c30c30c30c3ull;
+    x = (x | x << 2) & 0x1249249249249249ull;
+    return x;
 }
 
 // 1. triangle boxes (lo.xyz, hi.xyz) in original order, centroid bounds, max |coordinate|
@@ -80,22 +85,33 @@ __global__ void __launch_bounds__(kThreads) lbvh_boxes_k(LbvhInput in, float* tr
     else if (threadIdx.x == 6) atomicMax(maxabs_bits, sb[6]);
 }
 
-// 2. keys = Morton(centroid) << 32 | id
+// 2. keys = Morton(centroid) << id_bits | id: `mb` bits per axis, as many as fit beside the id
+// bits in 64 (14 per axis for 881k triangles; finer cells split dense regions by position
+// instead of by triangle id)
 __global__ void __launch_bounds__(kThreads) lbvh_keys_k(uint32_t n, const float* tri_box, const uint32_t* bounds,
-                                                        unsigned long long* keys) {
+                                                        unsigned long long* keys, int mb, int id_bits) {
     const uint32_t t = blockIdx.x * kThreads + threadIdx.x;
     if (t >= n) return;
-    uint32_t code = 0;
+    unsigned long long code = 0;
+    const float cells = (float)(1u << mb);
     for (int k = 0; k < 3; ++k) {
         const float lo = o2f(bounds[k]), hi = o2f(bounds[3 + k]);
         const float cen = 0.5f * (tri_box[6 * (size_t)t + k] + tri_box[6 * (size_t)t + 3 + k]);
         const float ext = hi - lo;
         float u = ext > 0.0f ? (cen - lo) / ext : 0.0f;
         u = fminf(fmaxf(u, 0.0f), 1.0f);
-        const uint32_t q = min((uint32_t)(u * 1024.0f), 1023u);
-        code |= expand_bits(q) << (2 - k);
+        const uint32_t q = min((uint32_t)(u * cells), (1u << mb) - 1u);
+        code |= expand_bits21(q) << (2 - k);
     }
-    keys[t] = ((unsigned long long)code << 32) | t;
+    keys[t] = (code << id_bits) | t;
+}
+
+// after the radix tree: keep only the triangle id in every key (the later stages read it from
+// the low 32 bits)
+__global__ void __launch_bounds__(kThreads) lbvh_key_ids_k(unsigned long long* keys, uint32_t n,
+                                                           unsigned long long id_mask) {
+    const uint32_t t = blockIdx.x * kThreads + threadIdx.x;
+    if (t < n) keys[t] &= id_mask;
 }
 
 // 3. radix sort pass: per-tile digit histograms -> table[digit * tiles + tile]
@@ -513,20 +529,21 @@ bool lbvh_build(const LbvhInput& in, const LbvhOutput& out, void* scratch, hipSt
     LB_CHECK(hipMemsetAsync(parent, 0xff, 4 * (size_t)n, s));        // -1: unset
     LB_CHECK(hipMemsetAsync(leaf_parent, 0xff, 4 * (size_t)n, s));
     lbvh_boxes_k<<<blocks(n), kThreads, 0, s>>>(in, tri_box, misc, misc + 6);
-    lbvh_keys_k<<<blocks(n), kThreads, 0, s>>>(n, tri_box, misc, keys);
-    // digits over the id bits in use and the 30 Morton bits
     int id_bits = 1;
     while (id_bits < 32 && (1ull << id_bits) < n) ++id_bits;
+    const int mb = std::min(21, (64 - id_bits) / 3);
+    lbvh_keys_k<<<blocks(n), kThreads, 0, s>>>(n, tri_box, misc, keys, mb, id_bits);
+    // 8-bit digits over the key bits in use (ids + 3 * mb Morton bits)
     unsigned long long* src = keys;
     unsigned long long* dst = keys2;
-    for (int shift = 0; shift < 62; shift += 8) {
-        if (shift < 32 && shift >= id_bits) continue;
+    for (int shift = 0; shift < id_bits + 3 * mb; shift += 8) {
         lbvh_hist_k<<<tiles, kThreads, 0, s>>>(src, n, shift, tiles, table);
         lbvh_scan_k<<<1, 1024, 0, s>>>(table, 256 * tiles);
         lbvh_scatter_k<<<tiles, kThreads, 0, s>>>(src, dst, n, shift, tiles, table);
         std::swap(src, dst);
     }
     lbvh_tree_k<<<blocks(n - 1), kThreads, 0, s>>>(src, n, child, parent, leaf_parent, first, count);
+    lbvh_key_ids_k<<<blocks(n), kThreads, 0, s>>>(src, n, (1ull << id_bits) - 1ull);
     lbvh_boxes_up_k<<<blocks(n), kThreads, 0, s>>>(src, n, child, parent, leaf_parent, tri_box, node_box, flag);
     LB_CHECK(hipGetLastError());
     // collapse, one level per launch; the next level's job count comes back to the host
