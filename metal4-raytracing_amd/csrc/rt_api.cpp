@@ -399,6 +399,7 @@ rt_status rt_destroy(rt_ctx* c) {
     if (!c) return RT_OK;
     hipSetDevice(c->device);
     if (c->stream) hipStreamSynchronize(c->stream);
+    if (c->ustream) hipStreamSynchronize(c->ustream);
     for (FrameSlot& f : c->slot)
         if (f.own_stream) hipStreamSynchronize(f.own_stream);
     DevBuf* all[] = {&c->d_rest_pos, &c->d_rest_nrm, &c->d_jidx, &c->d_jw,
@@ -411,7 +412,6 @@ rt_status rt_destroy(rt_ctx* c) {
     for (DevBuf& b : c->d_motion) dev_free(b);
     for (Geo& g : c->geo)
         for (DevBuf* b : g.all) dev_free(*b);
-    if (c->ustream) hipStreamSynchronize(c->ustream);
     if (c->uev) hipEventDestroy(c->uev);
     if (c->ustream) hipStreamDestroy(c->ustream);
     if (c->h_lbvh) hipHostFree(c->h_lbvh);
