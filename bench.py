@@ -160,8 +160,11 @@ def main():
     s0 = R.stats()
     barrier()
     t0 = time.perf_counter()
+    t_host = 0.0
     for _ in range(a.steps):
+        th = time.perf_counter()
         submit()
+        t_host += time.perf_counter() - th
     R.wait()
     barrier()
     dt = time.perf_counter() - t0
@@ -283,6 +286,8 @@ def main():
             "stage_ms": [round(x / a.steps, 3) for x in stage_ms[:7]], "sort_bins": a.sort_bins, "bvh": a.bvh,
             "pipeline_used": ["megakernel", "wavefront"][last_st.pipeline], "iterations": last_st.iterations,
             "frames_in_flight": last_st.frames_in_flight, "animate": bool(skinned),
+            # host time inside the submit calls per step (includes waiting for a free frame slot)
+            "host_submit_ms": round(t_host / a.steps * 1e3, 3),
         },
         "roofline": {
             "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
