@@ -60,7 +60,8 @@ struct Geo {
     uint32_t num_nodes8 = 0;
 };
 constexpr int kMaxSlots = 3;
-constexpr int kTailInFlight = 2097152;   // default finish threshold with frames in flight
+// default finish threshold with 2 / 3 frames in flight (C3g sweeps: 2M and 1M paths)
+constexpr int kTailInFlight[4] = {0, 0, 2097152, 1048576};
 constexpr int kMotionTargets = kMaxSlots + 1;
 }  // namespace
 
@@ -124,7 +125,7 @@ struct rt_ctx {
 
     // frames in flight
     FrameSlot slot[kMaxSlots];
-    int max_in_flight = 2;           // rt_opts.frames_in_flight
+    int max_in_flight = 3;           // rt_opts.frames_in_flight
     int nslots = 1;                  // slots in use (1: megakernel, external stream)
     uint64_t frame_no = 0;           // frames submitted since rt_resize
     int last_slot = 0;               // slot of the newest frame
@@ -1012,12 +1013,13 @@ rt_status rt_render_frame(rt_ctx* c, const Uniforms* U, const rt_tile_set* tiles
     if (wavefront) {
         const char* err = nullptr;
         F.wfs = WfFrameStats{};
-        // finish threshold: with frames in flight the next frame's bulk rounds overlap this
-        // frame's tail, so more bulk rounds and a shorter tail pay (C3g: 2M paths 5.92 ms per frame
-        // against 6.02 ms at the one-frame-at-a-time optimum of 4M)
+        // finish threshold: with frames in flight the next frames' bulk rounds overlap this
+        // frame's tail, so more bulk rounds and a shorter tail pay (C3g, 2 in flight: 2M paths
+        // 5.92 ms per frame against 6.02 ms at the one-frame-at-a-time optimum of 4M; 3 in
+        // flight: 1M)
         static const bool tail_env = getenv("RT_TAIL_RAYS") != nullptr;
-        const int tail = c->tail_paths ? c->tail_paths : (nfl > 1 && !tail_env ? kTailInFlight : 0);
-        if (own > 0 && !run_wavefront(S, P, F.wf, own, c->counting, tail, c->sort_bins, extra_pass, nfl > 1, stream,
+        const int tail = c->tail_paths ? c->tail_paths : (nfl > 1 && !tail_env ? kTailInFlight[nfl] : 0);
+        if (own > 0 && !run_wavefront(S, P, F.wf, own, c->counting, tail, c->sort_bins, extra_pass, nfl, stream,
                                       cross ? prev.done : nullptr, &F.wft, &F.wfs, &err))
             FAIL(c, RT_ERR_HIP, std::string("wavefront: ") + (err ? err : "?"));
         if (own == 0 && cross) HIPC(c, hipStreamWaitEvent(stream, prev.done, 0));

@@ -161,12 +161,12 @@ struct WfTimeline {
 // from wavefront_collect after the stream finished) one frame; false on a HIP error (*err).
 // sort_bins: hit-sort bins (0 = no sort).  extra_pass: the motion-adaptive extra samples can be
 // non-zero this frame (something moved in this or the previous frame); the device-driven mode
-// skips their pass otherwise.  overlapped: frames are in flight (the finish kernel leaves part of
-// the machine to the next frame).  prev_done (may be null): the previous frame, in flight on another
+// skips their pass otherwise.  in_flight: frames that can overlap this one (> 1: the finish
+// kernel takes 1 / in_flight of the resident grid and leaves the rest to the other frames).  prev_done (may be null): the previous frame, in flight on another
 // stream; the extra-sample pass and the resolve (which read its accumulation and motion outputs)
 // are ordered after it, everything before them overlaps it.
 bool run_wavefront(const DevScene& S, const FrameParams& P, WavefrontBuffers& W, int own_tiles, bool count,
-                   int tail_paths, int sort_bins, bool extra_pass, bool overlapped, hipStream_t stream,
+                   int tail_paths, int sort_bins, bool extra_pass, int in_flight, hipStream_t stream,
                    hipEvent_t prev_done, WfTimeline* tl, WfFrameStats* fs, const char** err);
 bool wavefront_graph_mode();   // RT_GRAPH=1 (one frame in flight)
 bool wavefront_collect(const WavefrontBuffers& W, WfTimeline& T, WfFrameStats* fs, const char** err);

@@ -2065,7 +2065,7 @@ bool wavefront_collect(const WavefrontBuffers& W, WfTimeline& T, WfFrameStats* f
 }
 
 bool run_wavefront(const DevScene& S, const FrameParams& P, WavefrontBuffers& W, int own_tiles, bool count,
-                   int tail_paths, int sort_bins, bool extra_pass, bool overlapped, hipStream_t stream,
+                   int tail_paths, int sort_bins, bool extra_pass, int in_flight, hipStream_t stream,
                    hipEvent_t prev_done, WfTimeline* tl, WfFrameStats* fs, const char** err) {
     WfParams Q;
     Q.W = W;
@@ -2090,10 +2090,11 @@ bool run_wavefront(const DevScene& S, const FrameParams& P, WavefrontBuffers& W,
     Q.drain_min = Q.finish_step == 1 ? drain_min : 0;
     static const int prio = env_int("RT_PRIO", 0), fchunk = env_int("RT_FCHUNK", 64);
     Q.fchunk = max(1, fchunk);
-    // frames in flight: half the machine for the tail, the other half for the next frame's bulk
-    // rounds (C3g: 5.94 -> 5.72 ms per frame); one frame at a time: all of it
+    // frames in flight: 1 / in_flight of the machine for the tail, the rest for the other frames'
+    // bulk rounds (C3g, 2 in flight: 5.94 -> 5.72 ms per frame at 50 %; 3 in flight: 33 %); one
+    // frame at a time: all of it
     static const int finish_frac = env_int("RT_FINISH_FRAC", 0);
-    Q.finish_frac = finish_frac > 0 ? min(finish_frac, 100) : (overlapped ? 50 : 100);
+    Q.finish_frac = finish_frac > 0 ? min(finish_frac, 100) : (in_flight > 1 ? 100 / in_flight : 100);
     Q.prio = (prio && Q.finish_step == 1 && W.sorted) ? 1 : 0;
     if (Q.finish_step == 2 && (!W.p_ray || !W.p_sray)) {
         *err = "wave-queue finish kernel without its path ray slots";
