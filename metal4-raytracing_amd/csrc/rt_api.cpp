@@ -125,7 +125,7 @@ struct rt_ctx {
 
     // frames in flight
     FrameSlot slot[kMaxSlots];
-    int max_in_flight = 3;           // rt_opts.frames_in_flight
+    int max_in_flight = 2;           // rt_opts.frames_in_flight
     int nslots = 1;                  // slots in use (1: megakernel, external stream)
     uint64_t frame_no = 0;           // frames submitted since rt_resize
     int last_slot = 0;               // slot of the newest frame
