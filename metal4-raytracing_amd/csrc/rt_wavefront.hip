@@ -1916,7 +1916,8 @@ static bool enqueue_pass(const DevScene& S, const FrameParams& P, const WfParams
         else hipLaunchKernelGGL((wf_trace<true, false>), dim3(gt), dim3(kBlock), 0, stream, S, Q.Pd, Q, cur);
         if (!E.span(3, err)) return false;
     }
-    WF_CHECK(hipMemsetAsync(Q.W.counts + cslot(kCntChunkFinish), 0, sizeof(uint32_t), stream));
+    // the finish chunk counter is zero here: the frame start clears every counter and the
+    // extra-sample pass clears it again before its own finish launch
     launch_finish_any(S, P, Q, count, full, -1, 1u << 30, stream);   // resident grid; input queue from the counters
     WF_CHECK(hipGetLastError());
     return E.span(5, err);
@@ -1950,6 +1951,7 @@ static bool record_frame(const DevScene& S, const FrameParams& P, WfParams& Q, b
         WF_CHECK(hipMemsetAsync(W.counts + cslot(kCntChunkExtend), 0, cslot(2 * kShards) * sizeof(uint32_t), stream));
         WF_CHECK(hipMemsetD32Async(W.counts + cslot(kCntTailMode), 0u, 1, stream));
         WF_CHECK(hipMemsetD32Async(W.counts + cslot(kCntFinishQ), (uint32_t)(rounds2 & 1), 1, stream));
+        WF_CHECK(hipMemsetD32Async(W.counts + cslot(kCntChunkFinish), 0u, 1, stream));
         hipLaunchKernelGGL(wf_extra, dim3(grid_for(Q.own_pixels, 1u << 30)), dim3(kBlock), 0, stream, S, Q.Pd, Q, 0);
         WF_CHECK(hipGetLastError());
         if (!E.span(4, err)) return false;
