@@ -23,12 +23,22 @@ CASES = {
     "c1_ema_f3": ("c1", 48, 48, dict(samplesPerPixel=1, maxBounces=2), 3),
     "c3g_small_b8": ("c3g", 64, 36, dict(samplesPerPixel=1, maxBounces=8), 1),
     "c2_small_b4": ("c2", 64, 36, dict(samplesPerPixel=1, maxBounces=4), 1),
+    # c1 + the train with every texture map kind bound (tests/helpers.py textured_scene)
+    "tex_b3": ("tex", 64, 48, dict(samplesPerPixel=1, maxBounces=3), 1),
 }
 SEED = 11
 
 
+def make_scene(rt, preset, assets):
+    if preset == "tex":
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        from helpers import textured_scene
+        return textured_scene(rt, assets)
+    return rt.Scene.preset(preset, assets)
+
+
 def render_case(rt, oracle, preset, W, H, knobs, frames, assets):
-    scene = rt.Scene.preset(preset, assets)
+    scene = make_scene(rt, preset, assets)
     osc = oracle.OracleScene(scene.desc())
     rnd = rt.random_offsets(SEED, W, H)
     prev, motion = None, None

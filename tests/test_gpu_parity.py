@@ -176,7 +176,8 @@ def test_pipelines_agree_full_frame(rt, assets, W, H, spp, bounces):
 
 
 @pytest.mark.parametrize("pipeline", PIPELINES)
-@pytest.mark.parametrize("name", ["c1_pbr_b1", "c1_pbr_b4", "c1_legacy_b3", "c1_ema_f3", "c3g_small_b8", "c2_small_b4"])
+@pytest.mark.parametrize("name", ["c1_pbr_b1", "c1_pbr_b4", "c1_legacy_b3", "c1_ema_f3", "c3g_small_b8", "c2_small_b4",
+                                  "tex_b3"])
 def test_gpu_matches_golden_fixtures(rt, assets, name, pipeline):
     """The HIP path against the committed fixtures (tests/golden, oracle-generated, seed 11)."""
     import json
@@ -185,7 +186,10 @@ def test_gpu_matches_golden_fixtures(rt, assets, name, pipeline):
     gdir = os.path.join(ROOT, "tests", "golden")
     meta = json.load(open(os.path.join(gdir, "cases.json")))[name]
     g = np.load(os.path.join(gdir, name + ".npz"))
-    scene = rt.Scene.preset(meta["preset"], assets)
+    import sys
+    sys.path.insert(0, gdir)
+    import make_golden
+    scene = make_golden.make_scene(rt, meta["preset"], assets)
     R = make_renderer(rt, scene, meta["width"], meta["height"], pipeline, seed=meta["seed"])
     for k, v in meta["knobs"].items():
         setattr(R, k, v)

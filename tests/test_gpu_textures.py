@@ -10,57 +10,9 @@ import os
 import numpy as np
 import pytest
 
-from helpers import PIPELINES, make_renderer, parity_report
+from helpers import PIPELINES, make_renderer, parity_report, procedural_textures as _textures, textured_scene
 
 pytestmark = pytest.mark.gpu
-
-
-def _textures(seed=1):
-    rng = np.random.default_rng(seed)
-    yy, xx = np.mgrid[0:64, 0:64]
-    base = np.zeros((64, 64, 4), np.uint8)
-    chk = ((xx // 8 + yy // 8) % 2).astype(np.uint8)
-    base[..., 0] = 40 + 200 * chk
-    base[..., 1] = rng.integers(30, 220, size=(64, 64))
-    base[..., 2] = 255 - 180 * chk
-    base[..., 3] = 255
-    # bumps: tangent-space normals from a height field
-    hx = np.cos(xx / 64.0 * 2 * np.pi * 3) * 0.6
-    hy = np.sin(yy / 64.0 * 2 * np.pi * 2) * 0.6
-    n = np.stack([hx, hy, np.ones_like(hx)], axis=-1)
-    n /= np.linalg.norm(n, axis=-1, keepdims=True)
-    normal = np.concatenate([((n * 0.5 + 0.5) * 255).round().astype(np.uint8), np.full((64, 64, 1), 255, np.uint8)],
-                            axis=-1)
-    rough = np.repeat(((xx * 4) % 256).astype(np.uint8)[..., None], 4, axis=-1)
-    metal = np.repeat((255 * ((yy // 4) % 2)).astype(np.uint8)[..., None], 4, axis=-1)
-    emis = np.zeros((32, 32, 4), np.uint8)
-    emis[::5, ::7, :3] = rng.integers(100, 256, size=emis[::5, ::7, :3].shape)
-    emis[..., 3] = 255
-    opac = np.full((16, 16, 4), 255, np.uint8)
-    opac[4:12, 4:12, 0] = 40
-    return dict(base=base, normal=normal, rough=rough, metal=metal, emis=emis, opac=opac)
-
-
-def textured_scene(rt, assets):
-    """c1 (floor with UVs, two spheres without, back wall) + the train (UVs, 6 submeshes)."""
-    sc = rt.Scene.preset("c1", assets)
-    sc.add_model(os.path.join(assets, "train.obj"), (-0.3, 0.0, 0.4), scale=0.5)
-    T = {k: sc.add_texture(v) for k, v in _textures().items()}
-    sc.bind_texture(0, 0, "baseColor", T["base"])        # floor
-    sc.bind_texture(0, 0, "roughness", T["rough"])
-    sc.bind_texture(0, 0, "normal", T["normal"])
-    sc.bind_texture(1, 0, "baseColor", T["base"])        # sphere without UVs: samples (0, 1)
-    sc.bind_texture(1, 0, "metallic", T["metal"])
-    sc.bind_texture(4, 0, "normal", T["normal"])         # train submeshes
-    sc.bind_texture(4, 0, "metallic", T["metal"])
-    sc.bind_texture(4, 1, "emission", T["emis"])
-    sc.bind_texture(4, 2, "opacity", T["opac"])
-    sc.bind_texture(4, 3, "roughness", T["rough"])
-    sc.bind_texture(4, 4, "baseColor", T["base"])
-    sc.bind_texture(4, 5, "baseColor", T["base"])
-    sc.bind_texture(4, 5, "normal", T["normal"])
-    sc.bind_texture(4, 5, "ao", T["rough"])              # AO: bound, never sampled (ENABLE_AO 0)
-    return sc
 
 
 def _pair(rt, orc, assets, pipeline, W=96, H=64, frames=1, **knobs):
