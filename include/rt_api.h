@@ -125,8 +125,9 @@ typedef struct rt_opts {
                            sort), < 0 = no sort.  Never changes the image, only memory locality. */
     int32_t frames_in_flight; /* wavefront on the context's own stream: frames rendered concurrently,
                                  each overlapping the previous one until it needs that frame's
-                                 accumulation / motion output; 0 = default (2), 1 = one at a time,
-                                 at most 3.
+                                 accumulation / motion output; 0 = default (2, or 3 for frames of
+                                 fewer than 6M paths, e.g. a multi-GPU rank's share), 1 = one at
+                                 a time, at most 3.
                                  Images are identical either way. */
     int32_t reserved[3];
 } rt_opts;

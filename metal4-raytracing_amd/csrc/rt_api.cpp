@@ -62,6 +62,7 @@ struct Geo {
 constexpr int kMaxSlots = 3;
 // default finish threshold with 2 / 3 frames in flight (C3g sweeps: 2M and 1M paths)
 constexpr int kTailInFlight[4] = {0, 0, 2097152, 1048576};
+constexpr uint64_t kSmallFrame = 6u << 20;   // paths: below, three frames in flight by default
 constexpr int kMotionTargets = kMaxSlots + 1;
 }  // namespace
 
@@ -125,7 +126,7 @@ struct rt_ctx {
 
     // frames in flight
     FrameSlot slot[kMaxSlots];
-    int max_in_flight = 2;           // rt_opts.frames_in_flight
+    int max_in_flight = 0;           // rt_opts.frames_in_flight; 0 = by frame size (auto_in_flight)
     int nslots = 1;                  // slots in use (1: megakernel, external stream)
     uint64_t frame_no = 0;           // frames submitted since rt_resize
     int last_slot = 0;               // slot of the newest frame
@@ -927,8 +928,16 @@ rt_status rt_render_frame(rt_ctx* c, const Uniforms* U, const rt_tile_set* tiles
     // (Raytracing.metal:483): only the per-pixel kernel orders samples that way.
     bool wavefront = c->pipeline == RT_PIPELINE_WAVEFRONT && U->debugTextureMode != DebugTextureModeMotion;
     // Frames in flight (Renderer.swift:1406-1409): wavefront frames on the context's own stream
-    // rotate over max_in_flight slots; a caller's stream, the megakernel and graph mode keep one.
-    const int nfl = (wavefront && c->stream == c->own_stream && !wavefront_graph_mode()) ? c->max_in_flight : 1;
+    // rotate over the frames-in-flight slots; a caller's stream, the megakernel and graph mode keep
+    // one.  By default two, three for frames of fewer than kSmallFrame paths (a multi-GPU rank's
+    // share of the 1080p frame): the finish tail's fixed latency dominates a small frame, and a
+    // third overlapping frame fills it (C3g per rank: 2-way split 4.52 -> 5.19, 8-way 2.30 -> 2.64
+    // Grays/s per GPU)
+    int nfl = 1;
+    if (wavefront && c->stream == c->own_stream && !wavefront_graph_mode()) {
+        const uint64_t frame_paths = (uint64_t)own * ts * ts * (uint64_t)std::max(U->samplesPerPixel, 1);
+        nfl = c->max_in_flight > 0 ? c->max_in_flight : (frame_paths < kSmallFrame ? 3 : 2);
+    }
     const int k = c->frame_no > 0 ? (c->last_slot + 1) % nfl : 0;
     FrameSlot& F = c->slot[k];
     const hipStream_t stream = slot_stream(c, k);
