@@ -2090,7 +2090,7 @@ bool run_wavefront(const DevScene& S, const FrameParams& P, WavefrontBuffers& W,
     Q.shade_min = shade_min;
     static const int drain_min = env_int("RT_DRAIN", 0);   // measured slower on C3g: off
     Q.drain_min = Q.finish_step == 1 ? drain_min : 0;
-    static const int prio = env_int("RT_PRIO", 0), fchunk = env_int("RT_FCHUNK", 64);
+    static const int prio = env_int("RT_PRIO", 0), fchunk = env_int("RT_FCHUNK", 32);
     Q.fchunk = max(1, fchunk);
     // frames in flight: 1 / in_flight of the machine for the tail, the rest for the other frames'
     // bulk rounds (C3g, 2 in flight: 5.94 -> 5.72 ms per frame at 50 %; 3 in flight: 33 %); one
