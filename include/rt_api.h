@@ -119,15 +119,15 @@ typedef struct rt_opts {
     int32_t pipeline;   /* RT_PIPELINE_* */
     int32_t tail_paths; /* wavefront: below this many live paths the rest of the frame runs in the
                            persistent finish kernel; 0 = default (4194304 one frame at a time,
-                           2097152 / 1048576 with 2 / 3 frames in flight), 1 = never */
+                           2097152 / 1048576 / 524288 with 2 / 3 / 4 frames in flight), 1 = never */
     int32_t sort_bins;  /* wavefront: hits are sorted into this many bins of BVH leaf order between
                            extend and shade (a power of two in [1024, 4096]); 0 = default (no
                            sort), < 0 = no sort.  Never changes the image, only memory locality. */
     int32_t frames_in_flight; /* wavefront on the context's own stream: frames rendered concurrently,
                                  each overlapping the previous one until it needs that frame's
-                                 accumulation / motion output; 0 = default (2, or 3 for frames of
+                                 accumulation / motion output; 0 = default (2, or 4 for frames of
                                  fewer than 6M paths, e.g. a multi-GPU rank's share), 1 = one at
-                                 a time, at most 3.
+                                 a time, at most 4.
                                  Images are identical either way. */
     int32_t reserved[3];
 } rt_opts;
@@ -165,7 +165,7 @@ typedef struct rt_stats {
     float trace_ms;         /* its summed device time (HIP events on the render stream) */
     uint64_t trace_closest_rays; /* the closest-hit (extend) share of trace_rays */
     int32_t finish_launches;     /* wavefront: persistent finish launches (their time: kernel_ms[5]) */
-    int32_t frames_in_flight;    /* frames the last rt_render_frame could overlap (1..3) */
+    int32_t frames_in_flight;    /* frames the last rt_render_frame could overlap (1..4) */
     /* running totals over every finished frame since rt_create (frames submitted back to back
        without rt_wait are each counted) */
     uint64_t frames_total;

@@ -59,10 +59,12 @@ struct Geo {
     DevBuf* all[9] = {&pos, &prev_pos, &nrm, &inst, &prev_inst, &tris, &nodes, &node_box, &tri_bin};
     uint32_t num_nodes8 = 0;
 };
-constexpr int kMaxSlots = 3;
-// default finish threshold with 2 / 3 frames in flight (C3g sweeps: 2M and 1M paths)
-constexpr int kTailInFlight[4] = {0, 0, 2097152, 1048576};
-constexpr uint64_t kSmallFrame = 6u << 20;   // paths: below, three frames in flight by default
+constexpr int kMaxSlots = 4;
+// default finish threshold with 2 / 3 / 4 frames in flight (C3g sweeps: 2M, 1M and 512K paths;
+// four slots serve the small frames of multi-GPU ranks: 8-way split 2.92 -> 3.46 Grays/s per rank
+// at 512K against 1M, with the finish kernel on 20 % of the grid)
+constexpr int kTailInFlight[kMaxSlots + 1] = {0, 0, 2097152, 1048576, 524288};
+constexpr uint64_t kSmallFrame = 6u << 20;   // paths: below, four frames in flight by default
 constexpr int kMotionTargets = kMaxSlots + 1;
 }  // namespace
 
@@ -929,14 +931,14 @@ rt_status rt_render_frame(rt_ctx* c, const Uniforms* U, const rt_tile_set* tiles
     bool wavefront = c->pipeline == RT_PIPELINE_WAVEFRONT && U->debugTextureMode != DebugTextureModeMotion;
     // Frames in flight (Renderer.swift:1406-1409): wavefront frames on the context's own stream
     // rotate over the frames-in-flight slots; a caller's stream, the megakernel and graph mode keep
-    // one.  By default two, three for frames of fewer than kSmallFrame paths (a multi-GPU rank's
-    // share of the 1080p frame): the finish tail's fixed latency dominates a small frame, and a
-    // third overlapping frame fills it (C3g per rank: 2-way split 4.52 -> 5.19, 8-way 2.30 -> 2.64
-    // Grays/s per GPU)
+    // one.  By default two, four for frames of fewer than kSmallFrame paths (a multi-GPU rank's
+    // share of the 1080p frame): the finish tail's fixed latency dominates a small frame, and more
+    // overlapping frames fill it (C3g per rank, 2 / 3 / 4 slots: 2-way split 4.52 / 5.15 / 5.49,
+    // 8-way 2.30 / 2.73 / 2.92 Grays/s per GPU; 5 and 6 slots measured slower)
     int nfl = 1;
     if (wavefront && c->stream == c->own_stream && !wavefront_graph_mode()) {
         const uint64_t frame_paths = (uint64_t)own * ts * ts * (uint64_t)std::max(U->samplesPerPixel, 1);
-        nfl = c->max_in_flight > 0 ? c->max_in_flight : (frame_paths < kSmallFrame ? 3 : 2);
+        nfl = c->max_in_flight > 0 ? c->max_in_flight : (frame_paths < kSmallFrame ? kMaxSlots : 2);
     }
     const int k = c->frame_no > 0 ? (c->last_slot + 1) % nfl : 0;
     FrameSlot& F = c->slot[k];

@@ -33,7 +33,7 @@ def test_bench_line_contract():
     assert r["bound"] == "hbm" and r["peak"] == 8000.0 and 0 < r["frac"] < 1
     cb = d["cpu_baseline"]
     assert cb["value"] > 0 and cb["kind"] == "port" and cb["cores"] >= 1
-    assert d["config"]["frames_in_flight"] == 3   # default for a small frame (< 6M paths)
+    assert d["config"]["frames_in_flight"] == 4   # default for a small frame (< 6M paths)
 
 
 def test_bench_emulated_rank_and_animation():

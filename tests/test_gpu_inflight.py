@@ -44,7 +44,7 @@ def _run(rt, sc, desc, pipeline, fif, frames, move_at=None, gbuffer=False):
     return R, img, depth, motion, gb, st
 
 
-@pytest.mark.parametrize("pipeline,fif", [(p, 2) for p in PIPELINES] + [("wavefront", 3), ("wavefront-mixed", 3)])
+@pytest.mark.parametrize("pipeline,fif", [(p, 2) for p in PIPELINES] + [("wavefront", 3), ("wavefront-mixed", 3), ("wavefront", 4), ("wavefront-mixed", 4)])
 def test_in_flight_matches_serial(rt, assets, pipeline, fif):
     sc = rt.Scene.preset("c2", assets)
     desc = sc.desc()

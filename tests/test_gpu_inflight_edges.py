@@ -118,13 +118,14 @@ def _animated(rt, assets, fif, frames=6, rebuild_at=None, move=False, rebuild_ev
 
 @pytest.mark.parametrize("kw", [dict(), dict(move=True), dict(rebuild_at=3), dict(rebuild_every="device"),
                                 dict(rebuild_every="host", move=True)])
-def test_animated_frames_in_flight(rt, assets, kw):
+@pytest.mark.parametrize("fif", [2, 4])
+def test_animated_frames_in_flight(rt, assets, kw, fif):
     """Per-frame skinning + refit (configs[4] shape) with frames in flight: the updates go to the
     other geometry generation while the previous frame still renders; bytes equal the serial run."""
     a = _animated(rt, assets, 1, **kw)
-    b = _animated(rt, assets, 2, **kw)
+    b = _animated(rt, assets, fif, **kw)
     for x, y in zip(a[:3], b[:3]):
         assert np.array_equal(x, y)
     assert np.abs(a[2]).max() > 0   # the robot moved: motion vectors exercised
     assert a[3].total_closest_rays == b[3].total_closest_rays
-    assert b[3].frames_in_flight == 2
+    assert b[3].frames_in_flight == fif

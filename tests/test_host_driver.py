@@ -34,7 +34,7 @@ def test_rtbench_renders(rt, assets, tmp_path):
                        capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr
     line = json.loads(r.stdout.strip().splitlines()[-1])
-    assert line["grays_per_s"] > 0 and line["frames_in_flight"] == 3   # default for a small frame
+    assert line["grays_per_s"] > 0 and line["frames_in_flight"] == 4   # default for a small frame
     img = rt.decode_png(png.read_bytes())
     assert img.shape == (96, 128, 4)
     # same frames through the Python mirror: identical display bytes
