@@ -94,7 +94,8 @@ def test_in_flight_then_megakernel_frame(rt, assets):
         assert np.array_equal(out[0][1], mot)
 
 
-def test_in_flight_tile_gather(rt, assets):
+@pytest.mark.parametrize("fif,expect", [(2, 2), (0, 4)])   # 0: the library default for a rank's small frame
+def test_in_flight_tile_gather(rt, assets, fif, expect):
     """Two ranks' renderers (tile split, frames in flight) with the per-frame gather enqueued on
     a separate stream without host waits (rank 1 packs, rank 0 unpacks, the pattern of
     TileGather.gather over RCCL): rank 0's image after the last frame equals the one-GPU image,
@@ -103,7 +104,7 @@ def test_in_flight_tile_gather(rt, assets):
     sc = rt.Scene.preset("c1", assets)
     W, H, T, K = 200, 136, 64, 5
     full = make_renderer(rt, sc, W, H, "wavefront", seed=5, frames_in_flight=1)
-    ranks = [make_renderer(rt, sc, W, H, "wavefront", seed=5, frames_in_flight=2) for _ in range(2)]
+    ranks = [make_renderer(rt, sc, W, H, "wavefront", seed=5, frames_in_flight=fif) for _ in range(2)]
     for R in [full] + ranks:
         R.maxBounces = 3
     cam0 = full.camera
@@ -123,5 +124,5 @@ def test_in_flight_tile_gather(rt, assets):
         keep.append(buf)
     ref = full.radiance()
     img = ranks[0].radiance()
-    assert ranks[0].stats().frames_in_flight == 2
+    assert ranks[0].stats().frames_in_flight == expect
     assert np.array_equal(img, ref)
