@@ -398,7 +398,12 @@ __global__ void __launch_bounds__(kBlock) RT_SHADE_ATTR wf_shade(DevScene S, con
             h.v = hv.w;
             if (h.id != 0xffffffffu) {                                           // miss -> path ends (:321-322)
                 uint4 meta = Q.W.p_meta[pid];
-                float4 c = Q.W.p_color[pid], a = Q.W.p_accum[pid];
+                float4 c = Q.W.p_color[pid];
+                // FULL=false: shade_step only adds color * emission to accum (:585), so it runs on a
+                // zero accumulator and the stored one is read and updated only when that term is
+                // non-zero (accum is never -0, so a + (0 + x) == a + x bit for bit); FULL (debug
+                // modes assign accum) reads it first
+                float4 a = FULL ? Q.W.p_accum[pid] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
                 PathRegs p;
                 p.color = mk3(c.x, c.y, c.z);
                 p.accum = mk3(a.x, a.y, a.z);
@@ -412,7 +417,15 @@ __global__ void __launch_bounds__(kBlock) RT_SHADE_ATTR wf_shade(DevScene S, con
                                  zero2, false, zero2, r);
                 write_pixel_outputs(P, meta.x, r, FULL);
                 if (r.next) Q.W.p_color[pid] = make_float4(p.color.x, p.color.y, p.color.z, 0.0f);
-                Q.W.p_accum[pid] = make_float4(p.accum.x, p.accum.y, p.accum.z, 0.0f);
+                // radiance only changes on emissive hits (:585-586): skip the store otherwise
+                if (__float_as_uint(p.accum.x) != __float_as_uint(a.x) || __float_as_uint(p.accum.y) != __float_as_uint(a.y) ||
+                    __float_as_uint(p.accum.z) != __float_as_uint(a.z)) {
+                    if (!FULL) {
+                        const float4 s = Q.W.p_accum[pid];
+                        p.accum = mk3(s.x + p.accum.x, s.y + p.accum.y, s.z + p.accum.z);
+                    }
+                    Q.W.p_accum[pid] = make_float4(p.accum.x, p.accum.y, p.accum.z, 0.0f);
+                }
                 if (r.next) Q.W.p_meta[pid] = make_uint4(meta.x, meta.y, pack_state(p.bounce, p.tpass, p.step), meta.w);
             }
         }
