@@ -202,3 +202,30 @@ def test_gpu_matches_golden_fixtures(rt, assets, name, pipeline):
     assert rep["n_bad"] == 0, rep
     assert np.array_equal(depth, g["depth"])
     assert [st.closest_rays, st.shadow_rays] == g["counts"].tolist()[:2]
+
+
+@pytest.mark.parametrize("pipeline", PIPELINES)
+def test_emissive_parity(rt, orc, assets, tmp_path, pipeline):
+    """An emissive untextured material (MTL Ke): the common shading kernels add color * emission
+    to the path radiance (:585), the only place shade changes it, over several frames (EMA)."""
+    import os
+    import shutil
+    shutil.copy(os.path.join(assets, "sphere.obj"), tmp_path / "sphere.obj")
+    (tmp_path / "sphere.mtl").write_text("newmtl None\nKd 0.6 0.7 0.5\nKe 1.5 0.75 0.25\nd 1\n")
+    scene = rt.Scene.preset("c1", assets)
+    scene.add_model(str(tmp_path / "sphere.obj"), (0.4, 0.6, 1.2), scale=0.5)
+    R = make_renderer(rt, scene, 72, 56, pipeline, seed=9)
+    R.samplesPerPixel, R.maxBounces = 2, 4
+    osc = orc.OracleScene(scene.desc())
+    prev = motion = None
+    for _ in range(3):
+        u = R.draw()
+        R.wait()
+        g = R.radiance()
+        st = R.stats()
+        o = osc.render(u, R.random, accum_in=prev, motion_in=motion)
+        prev, motion = o["radiance"], o["motion"]
+        rep = parity_report(g, o["radiance"])
+        assert rep["n_bad"] == 0, rep
+        assert st.closest_rays == o["closest_rays"] and st.shadow_rays == o["shadow_rays"]
+    assert float(np.max(g[..., :3])) > 0.5   # the emitter shows
