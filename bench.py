@@ -62,6 +62,7 @@ def parse():
     p.add_argument("--rebuild", action="store_true", help="with --animate: rebuild the BVH on the device instead of refitting")
     p.add_argument("--emulate-ranks", type=int, default=0,
                    help="tuning aid: one process renders rank 0's tiles of an N-way split (no gather)")
+    p.add_argument("--emulate-rank", type=int, default=0, help="with --emulate-ranks: which rank's tiles")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample time")
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--traffic-csv", default=None, help="rocprofv3 --pmc counter_collection.csv for traffic")
@@ -91,7 +92,7 @@ def main():
     R.maxBounces = a.bounces
     tiles = (a.tile, rank, n) if n > 1 else None
     if a.emulate_ranks > 1 and n == 1:
-        tiles = (a.tile, 0, a.emulate_ranks)
+        tiles = (a.tile, a.emulate_rank, a.emulate_ranks)
     T = a.tile
     dev = torch.device("cuda", local)
     gather = None
