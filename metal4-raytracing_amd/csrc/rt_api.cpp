@@ -428,7 +428,6 @@ rt_status rt_destroy(rt_ctx* c) {
             if (e) hipEventDestroy(e);
         for (auto& e : f.wft.ev)
             if (e) hipEventDestroy(e);
-        if (f.wft.exec) hipGraphExecDestroy(f.wft.exec);
         for (auto& e : f.wf.param_ev)
             if (e) hipEventDestroy(e);
         if (f.wf.h_params) hipHostFree(f.wf.h_params);
@@ -930,13 +929,13 @@ rt_status rt_render_frame(rt_ctx* c, const Uniforms* U, const rt_tile_set* tiles
     // (Raytracing.metal:483): only the per-pixel kernel orders samples that way.
     bool wavefront = c->pipeline == RT_PIPELINE_WAVEFRONT && U->debugTextureMode != DebugTextureModeMotion;
     // Frames in flight (Renderer.swift:1406-1409): wavefront frames on the context's own stream
-    // rotate over the frames-in-flight slots; a caller's stream, the megakernel and graph mode keep
-    // one.  By default two, four for frames of fewer than kSmallFrame paths (a multi-GPU rank's
+    // rotate over the frames-in-flight slots; a caller's stream and the megakernel keep one.
+    //  By default two, four for frames of fewer than kSmallFrame paths (a multi-GPU rank's
     // share of the 1080p frame): the finish tail's fixed latency dominates a small frame, and more
     // overlapping frames fill it (C3g per rank, 2 / 3 / 4 slots: 2-way split 4.52 / 5.15 / 5.49,
     // 8-way 2.30 / 2.73 / 2.92 Grays/s per GPU; 5 and 6 slots measured slower)
     int nfl = 1;
-    if (wavefront && c->stream == c->own_stream && !wavefront_graph_mode()) {
+    if (wavefront && c->stream == c->own_stream) {
         const uint64_t frame_paths = (uint64_t)own * ts * ts * (uint64_t)std::max(U->samplesPerPixel, 1);
         nfl = c->max_in_flight > 0 ? c->max_in_flight : (frame_paths < kSmallFrame ? kMaxSlots : 2);
     }

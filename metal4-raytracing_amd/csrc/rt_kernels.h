@@ -110,8 +110,8 @@ struct WavefrontBuffers {
     size_t cap_paths = 0;         // base + extra paths
     size_t cap_pixels = 0;
     hipEvent_t ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
-    // FrameParams of the frame in flight: one device copy the kernels read (so a captured frame
-    // graph replays with new uniforms), uploaded from a ring of pinned host slots
+    // FrameParams of the frame in flight: one device copy the kernels read, uploaded from a ring
+    // of pinned host slots
     static constexpr int kParamSlots = 4;
     FrameParams* d_params = nullptr;
     FrameParams* h_params = nullptr;
@@ -149,12 +149,6 @@ struct WfTimeline {
     Span spans[kMaxEv];
     int n_ev = 0, n_spans = 0;
     bool pending = false;
-    // the frame as a HIP graph (RT_GRAPH=1, default): replayed while `key` (everything the
-    // launches bake in) is unchanged, re-captured otherwise
-    hipGraphExec_t exec = nullptr;
-    std::vector<uint64_t> key;
-    int captures = 0;
-    bool in_graph = false;   // capturing: no event records
 };
 // Runs (host-driven: queue sizes read back every round; with RT_WF_LOG / RT_WF_DUMP /
 // RT_WF_HOST=1) or enqueues (device-driven, the default: `tl` receives the timeline, stats come
@@ -168,7 +162,6 @@ struct WfTimeline {
 bool run_wavefront(const DevScene& S, const FrameParams& P, WavefrontBuffers& W, int own_tiles, bool count,
                    int tail_paths, int sort_bins, bool extra_pass, int in_flight, hipStream_t stream,
                    hipEvent_t prev_done, WfTimeline* tl, WfFrameStats* fs, const char** err);
-bool wavefront_graph_mode();   // RT_GRAPH=1 (one frame in flight)
 bool wavefront_collect(const WavefrontBuffers& W, WfTimeline& T, WfFrameStats* fs, const char** err);
 size_t wavefront_queue_entries(size_t paths, int max_extra);
 

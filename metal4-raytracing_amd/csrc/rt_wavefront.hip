@@ -58,11 +58,6 @@ static int env_int(const char* name, int dflt) {  // tuning experiments
     return e ? atoi(e) : dflt;
 }
 
-static bool use_graph() {  // RT_GRAPH=1: the device-driven frame as a captured HIP graph
-    static const bool v = env_int("RT_GRAPH", 0) != 0;
-    return v;
-}
-
 static bool wf_log() {  // RT_WF_LOG=1: per-iteration queue sizes and stage times on stderr
     static const bool v = env_int("RT_WF_LOG", 0) != 0;
     return v;
@@ -275,7 +270,7 @@ __device__ __forceinline__ void write_pixel_outputs(const FrameParams& P, uint32
 
 // ---- generate -------------------------------------------------------------------------------------
 __global__ void __launch_bounds__(kBlock) wf_generate(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q) {
-    const FrameParams& P = *Pp;   // per-frame parameters in device memory (graph replay)
+    const FrameParams& P = *Pp;   // per-frame parameters in device memory
     __shared__ HaltonDim lds_halton[kHaltonLds];
     __shared__ BlockAlloc ba;
     const ShadeTabs halton = load_tabs(S, lds_halton, nullptr);   // no shading: Halton only
@@ -345,7 +340,7 @@ template <bool FULL, bool SORTED>
 #define RT_SHADE_ATTR
 #endif
 __global__ void __launch_bounds__(kBlock) RT_SHADE_ATTR wf_shade(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int cur) {
-    const FrameParams& P = *Pp;   // per-frame parameters in device memory (graph replay)
+    const FrameParams& P = *Pp;   // per-frame parameters in device memory
     __shared__ HaltonDim lds_halton[kHaltonLds];
     __shared__ MatRec lds_mat[kMatLds];
     __shared__ BlockAlloc ba_ray, ba_sh;
@@ -559,7 +554,7 @@ template <bool ANY, bool COUNT>
 #define RT_EXTEND_WAVES 7   // 70 VGPRs without scratch (8 waves: 64 VGPRs + 24 B/lane of spills)
 #endif
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ANY ? 8 : RT_EXTEND_WAVES, ANY ? 8 : RT_EXTEND_WAVES))) wf_trace(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int cur) {
-    const FrameParams& P = *Pp;   // per-frame parameters in device memory (graph replay)
+    const FrameParams& P = *Pp;   // per-frame parameters in device memory
     __shared__ int lds_stack[kStackSize * kBlock];
     constexpr int kTop = ANY ? RT_TOP_CONNECT : RT_TOP_EXTEND;
     __shared__ uint4 lds_top[kTop * 5];   // BVH top levels (BFS order: root, its children, ...)
@@ -790,7 +785,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ANY
 // ---- finish: run the remaining paths to completion --------------------------------------------------
 template <bool COUNT, bool FULL>
 __global__ void __launch_bounds__(kBlock) wf_finish(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int cur) {
-    const FrameParams& P = *Pp;   // per-frame parameters in device memory (graph replay)
+    const FrameParams& P = *Pp;   // per-frame parameters in device memory
     if (cur < 0) cur = (int)__builtin_amdgcn_readfirstlane(Q.W.counts[cslot(kCntFinishQ)]);   // dev_ctl
     // Persistent: every lane runs ONE path segment (closest hit, shade, shadow ray) per iteration
     // and picks up the next remaining path as soon as its own ends, so a wave waits for its
@@ -913,7 +908,7 @@ __global__ void __launch_bounds__(kBlock) wf_finish(DevScene S, const FrameParam
 template <bool COUNT, bool FULL, int WAVES>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES, WAVES)))
 wf_finish_step(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int cur) {
-    const FrameParams& P = *Pp;   // per-frame parameters in device memory (graph replay)
+    const FrameParams& P = *Pp;   // per-frame parameters in device memory
     if (cur < 0) cur = (int)__builtin_amdgcn_readfirstlane(Q.W.counts[cslot(kCntFinishQ)]);   // dev_ctl
     __shared__ int lds_stack[kStackSize * kBlock];
     __shared__ uint4 lds_top[RT_TOP_FINISH * 5];
@@ -1339,7 +1334,7 @@ constexpr int kWaveQ = 128;   // hit / ray queue entries per wave (LDS)
 template <bool COUNT, bool FULL>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 4)))
 wf_finish_q(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int cur) {
-    const FrameParams& P = *Pp;   // per-frame parameters in device memory (graph replay)
+    const FrameParams& P = *Pp;   // per-frame parameters in device memory
     if (cur < 0) cur = (int)__builtin_amdgcn_readfirstlane(Q.W.counts[cslot(kCntFinishQ)]);   // dev_ctl
     __shared__ int lds_stack[kStackSize * kBlock];
     __shared__ uint4 lds_top[kTopNodes * 5];
@@ -1536,7 +1531,7 @@ wf_finish_q(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int cur)
 
 // ---- motion-adaptive extra samples (:779-789) -----------------------------------------------------------
 __global__ void __launch_bounds__(kBlock) wf_extra(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int qidx) {
-    const FrameParams& P = *Pp;   // per-frame parameters in device memory (graph replay)
+    const FrameParams& P = *Pp;   // per-frame parameters in device memory
     __shared__ HaltonDim lds_halton[kHaltonLds];
     const ShadeTabs halton = load_tabs(S, lds_halton, nullptr);   // no shading: Halton only
     const Uniforms& U = P.U;
@@ -1587,7 +1582,7 @@ __global__ void __launch_bounds__(kBlock) wf_extra(DevScene S, const FrameParams
 
 // ---- resolve (:777, :792-819) -------------------------------------------------------------------------
 __global__ void __launch_bounds__(kBlock) wf_resolve(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int with_extra) {
-    const FrameParams& P = *Pp;   // per-frame parameters in device memory (graph replay)
+    const FrameParams& P = *Pp;   // per-frame parameters in device memory
     const Uniforms& U = P.U;
     uint32_t i = blockIdx.x * kBlock + threadIdx.x;
     if (i >= Q.own_pixels) return;
@@ -1871,7 +1866,6 @@ struct Enqueue {
     hipStream_t stream;
     int last = -1;
     bool mark(const char** err) {
-        if (T.in_graph) return true;   // events recorded by graph nodes carry no timestamps (HIP)
         if (T.n_ev >= WfTimeline::kMaxEv) {
             *err = "wavefront timeline: too many events";
             return false;
@@ -1886,7 +1880,6 @@ struct Enqueue {
     }
     // closes the span [previous mark, now) as `stage`
     bool span(int stage, const char** err) {
-        if (T.in_graph) return true;
         const int a = last;
         if (!mark(err)) return false;
         T.spans[T.n_spans++] = WfTimeline::Span{stage, a, last};
@@ -1936,19 +1929,14 @@ static bool enqueue_pass(const DevScene& S, const FrameParams& P, const WfParams
     return E.span(5, err);
 }
 
-// Issues one frame on `stream` (or into the graph being captured from it).  Everything the
-// launches bake in comes from S, Q and the buffer pointers in P; the per-frame values of P are
-// read by the kernels from Q.Pd.
-// h_stage: graph mode, the pinned copy of this frame's FrameParams the graph uploads first.
+// Issues one frame on `stream`.  Launch arguments come from S, Q and the buffer pointers in P;
+// the per-frame values of P are read by the kernels from Q.Pd.
 static bool record_frame(const DevScene& S, const FrameParams& P, WfParams& Q, bool count, bool full, int maxExtra,
-                         bool with_extra, const FrameParams* h_stage, hipStream_t stream, hipEvent_t prev_done,
-                         WfTimeline& T, const char** err) {
+                         bool with_extra, hipStream_t stream, hipEvent_t prev_done, WfTimeline& T, const char** err) {
     WavefrontBuffers& W = Q.W;
     T.n_ev = T.n_spans = 0;
     Enqueue E{T, stream};
     if (!E.mark(err)) return false;
-    if (h_stage)
-        WF_CHECK(hipMemcpyAsync(W.d_params, h_stage, sizeof(FrameParams), hipMemcpyHostToDevice, stream));
     WF_CHECK(hipMemsetAsync(W.counts, 0, kWfCountWords * sizeof(uint32_t), stream));
     const int rounds = rounds_for(Q.base_paths, Q.tail);
     Q.finish_q = rounds & 1;
@@ -1978,31 +1966,6 @@ static bool record_frame(const DevScene& S, const FrameParams& P, WfParams& Q, b
     return true;
 }
 
-// Everything a captured frame graph bakes in (launch arguments, buffer pointers, round counts).
-static std::vector<uint64_t> graph_key(const DevScene& S, const FrameParams& P, const WfParams& Q, bool count, bool full,
-                                       int maxExtra, bool with_extra) {
-    std::vector<uint64_t> k;
-    auto put = [&k](const auto& v) {
-        uint64_t w = 0;
-        static_assert(sizeof(v) <= 8, "key field");
-        std::memcpy(&w, &v, sizeof(v));
-        k.push_back(w);
-    };
-    put(S.tris); put(S.nodes8); put(S.tri_info); put(S.pos); put(S.prev_pos); put(S.nrm); put(S.inst);
-    put(S.prev_inst); put(S.materials); put(S.lights); put(S.halton); put(S.tri_bin); put(S.max_submeshes);
-    put(S.num_materials); put(S.num_tris); put(S.num_nodes8);
-    const WavefrontBuffers& W = Q.W;
-    put(W.queue_entries); put(W.p_color); put(W.p_accum); put(W.p_meta); put(W.q[0]); put(W.q[1]); put(W.hits);
-    put(W.sq); put(W.counts); put(W.h_counts); put(W.motion_prev); put(W.px_extra); put(W.sorted); put(W.sort_table);
-    put(W.sort_total); put(W.d_params);
-    put(Q.base_paths); put(Q.own_pixels); put(Q.seg_cap); put(Q.spp); put(Q.refill_min); put(Q.tri_vote);
-    put(Q.chunk); put(Q.tail); put(Q.sort_bins); put(Q.sort_xcd); put(Q.steal); put(Q.diag); put(Q.finish_step);
-    put(Q.shade_min); put(Q.drain_min); put(Q.dev_ctl); put(Q.Pd); put(Q.finish_frac); put(Q.fchunk); put(Q.prio);
-    put(P.motion); put(P.U.width); put(P.U.height);
-    put(count); put(full); put(maxExtra); put(with_extra);
-    return k;
-}
-
 static bool enqueue_wavefront(const DevScene& S, const FrameParams& P, WfParams& Q, bool count, bool full,
                               int maxExtra, bool extra_pass, hipStream_t stream, hipEvent_t prev_done, WfTimeline& T,
                               const char** err) {
@@ -2010,55 +1973,10 @@ static bool enqueue_wavefront(const DevScene& S, const FrameParams& P, WfParams&
     Q.drain_min = 0;
     Q.finish_q = 0;   // set by record_frame from the round count
     const bool with_extra = maxExtra > 0 && extra_pass;
-    if (!use_graph()) {
-        if (!record_frame(S, P, Q, count, full, maxExtra, with_extra, nullptr, stream, prev_done, T, err)) return false;
-        T.pending = true;
-        return true;
-    }
-    // HIP graph of the whole frame, captured once per configuration and replayed every frame.
-    // Its first node uploads the FrameParams from one pinned staging slot; the slot is rewritten
-    // only after the previous replay finished (one graph frame in flight per context).
-    WavefrontBuffers& W = Q.W;
-    WF_CHECK(hipEventSynchronize(W.param_ev[0]));
-    W.h_params[0] = P;
-    std::vector<uint64_t> key = graph_key(S, P, Q, count, full, maxExtra, with_extra);
-    if (!T.exec || key != T.key) {
-        if (T.exec) {
-            WF_CHECK(hipGraphExecDestroy(T.exec));
-            T.exec = nullptr;
-        }
-        T.key.clear();
-        WF_CHECK(hipStreamBeginCapture(stream, hipStreamCaptureModeRelaxed));
-        T.in_graph = true;
-        const bool ok = record_frame(S, P, Q, count, full, maxExtra, with_extra, &W.h_params[0], stream, nullptr, T, err);
-        T.in_graph = false;
-        hipGraph_t graph = nullptr;
-        const hipError_t e = hipStreamEndCapture(stream, &graph);
-        if (!ok || e != hipSuccess) {
-            if (graph) hipGraphDestroy(graph);
-            if (ok) *err = hipGetErrorString(e);
-            return false;
-        }
-        const hipError_t ei = hipGraphInstantiate(&T.exec, graph, nullptr, nullptr, 0);
-        hipGraphDestroy(graph);
-        if (ei != hipSuccess) {
-            T.exec = nullptr;
-            *err = hipGetErrorString(ei);
-            return false;
-        }
-        T.key = std::move(key);
-        ++T.captures;
-    }
-    // graph replay: per-stage times are not available (no timestamps on graph event nodes), only
-    // the whole frame (rt_stats.last_frame_ms, events around the replay)
-    T.n_ev = T.n_spans = 0;
-    WF_CHECK(hipGraphLaunch(T.exec, stream));
-    WF_CHECK(hipEventRecord(W.param_ev[0], stream));
+    if (!record_frame(S, P, Q, count, full, maxExtra, with_extra, stream, prev_done, T, err)) return false;
     T.pending = true;
     return true;
 }
-
-bool wavefront_graph_mode() { return use_graph(); }
 
 bool wavefront_collect(const WavefrontBuffers& W, WfTimeline& T, WfFrameStats* fs, const char** err) {
     if (!T.pending) return true;
@@ -2129,8 +2047,7 @@ bool run_wavefront(const DevScene& S, const FrameParams& P, WavefrontBuffers& W,
     // only bounded by maxBounces * (maxBounces + 1)
     const bool dev = tl && !host_ctl && !wf_log() && Q.drain_min == 0 && Q.tail > 1;
     Q.Pd = W.d_params;
-    if (!(dev && use_graph())) {   // this frame's parameters -> device (graph mode: inside the graph)
-        // the slot's previous upload has executed once its event has
+    {   // this frame's parameters -> device; the slot's previous upload has executed once its event has
         const int slot = W.param_slot;
         W.param_slot = (slot + 1) % WavefrontBuffers::kParamSlots;
         WF_CHECK(hipEventSynchronize(W.param_ev[slot]));
