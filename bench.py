@@ -37,8 +37,12 @@ B_TRI = 48
 B_HIT = 16 + 48 + 48
 B_PIXEL = 4 + 16 + 16 + 4 + 16
 B_QRAY = 48  # wf_trace queue entry: extend 32 B ray in + 16 B hit out; connect 48 B shadow entry in
-TRAFFIC_JSON_REL = "profiles/r01_traffic.json"
-TRAFFIC_JSON = os.path.join(os.path.dirname(os.path.abspath(__file__)), TRAFFIC_JSON_REL)
+_ROOT = os.path.dirname(os.path.abspath(__file__))
+# PMC traffic of the newest round (profiles/rNN_traffic.json, tools/gpurun_profile.sh)
+_TRAFFIC = sorted(f for f in os.listdir(os.path.join(_ROOT, "profiles")) if re.fullmatch(r"r\d+_traffic\.json", f)) \
+    if os.path.isdir(os.path.join(_ROOT, "profiles")) else []
+TRAFFIC_JSON_REL = "profiles/" + (_TRAFFIC[-1] if _TRAFFIC else "r01_traffic.json")
+TRAFFIC_JSON = os.path.join(_ROOT, TRAFFIC_JSON_REL)
 
 
 def parse():

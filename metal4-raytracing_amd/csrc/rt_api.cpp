@@ -49,22 +49,30 @@ struct FrameSlot {
     DevBuf* bufs[18] = {&color, &accum, &meta, &q0, &q1, &hits, &sq, &counts, &extra, &sorted,
                         &sort_table, &sort_total, &params, &pray, &psray, &depth, &gbuffer, &counters};
 };
-// Per-frame geometry (what skinning, instance transforms and refit rewrite between frames), in two
-// generations: frames read generation `gcur`; the first update after a frame copies it into the
-// other generation (once the frames still reading that one have finished) and every update until
-// the next frame writes there, so frames in flight keep their geometry while the next frame's is
-// built (Renderer.swift keeps per-frame position buffers for the same reason, :1290-1303).
+// Per-frame geometry (what skinning, instance transforms and refit rewrite between frames), in
+// kGens generations used round robin: frames read generation `gcur`; the first update after a frame
+// copies it into the next generation (once the frames still reading that one, kGens frames back,
+// have finished) and every update until the next frame writes there, so frames in flight keep
+// their geometry while the next frame's is built (Renderer.swift keeps per-frame position buffers
+// for the same reason, :1290-1303).  One generation per frame slot: with an update before every
+// frame (skinning, refit), all frames in flight still overlap.
 struct Geo {
     DevBuf pos, prev_pos, nrm, inst, prev_inst, tris, nodes, node_box, tri_bin;
     DevBuf* all[9] = {&pos, &prev_pos, &nrm, &inst, &prev_inst, &tris, &nodes, &node_box, &tri_bin};
     uint32_t num_nodes8 = 0;
 };
 constexpr int kMaxSlots = 4;
+constexpr int kGens = kMaxSlots;
 // default finish threshold with 2 / 3 / 4 frames in flight (C3g sweeps: 2M, 1M and 512K paths;
 // four slots serve the small frames of multi-GPU ranks: 8-way split 2.92 -> 3.46 Grays/s per rank
 // at 512K against 1M, with the finish kernel on 20 % of the grid)
 constexpr int kTailInFlight[kMaxSlots + 1] = {0, 0, 2097152, 1048576, 524288};
-constexpr uint64_t kSmallFrame = 6u << 20;   // paths: below, four frames in flight by default
+// paths a frame allocates (pixels x (spp + motion-adaptive extra samples), what ensure_wavefront
+// sizes a slot for): below, four frames in flight by default.  Every 1080p x 4 spp frame (8.29M
+// base paths) stays at two; a 2-way rank share of it with the default two extra samples (6.2M)
+// and the 720p x 4 frame of configs[1] (5.5M) take four.  A slot costs ~300 B per allocated path
+// (128 B path state and ray slots + 176 B of queues), 3.7 GB for 12.4M paths.
+constexpr uint64_t kSmallFrame = 8000000;
 constexpr int kMotionTargets = kMaxSlots + 1;
 }  // namespace
 
@@ -97,13 +105,14 @@ struct rt_ctx {
     std::vector<uint32_t> level_off;
 
     // device buffers
-    Geo geo[2];
+    Geo geo[kGens];
     int gcur = 0;            // generation new frames read
-    bool gdirty = false;     // updates since the last frame went into generation 1 - gcur
+    bool gdirty = false;     // updates since the last frame went into generation next_gen()
     hipStream_t ustream = nullptr;   // geometry updates (skin, transforms, refit)
     hipEvent_t uev = nullptr;        // end of the latest update batch; frames wait on it
     bool uev_valid = false;
-    Geo& G() { return geo[gdirty ? 1 - gcur : gcur]; }   // the generation updates and builds write
+    int next_gen() const { return (gcur + 1) % kGens; }
+    Geo& G() { return geo[gdirty ? next_gen() : gcur]; }   // the generation updates and builds write
     DevBuf d_rest_pos, d_rest_nrm, d_jidx, d_jw, d_joints;
     DevBuf d_tri_info, d_mat, d_lights, d_halton;
     DevBuf d_tex_texels, d_tex_info, d_mat_tex, d_uv, d_tex_lut;   // texture path (textured scenes)
@@ -316,7 +325,7 @@ static rt_status drain_frames(rt_ctx* c) {
 // stream; frames keep reading the current generation meanwhile).
 static rt_status begin_update(rt_ctx* c) {
     if (c->gdirty) return RT_OK;
-    const int w = 1 - c->gcur;
+    const int w = c->next_gen();
     for (const FrameSlot& f : c->slot)
         if (f.used && f.gen == w) HIPC(c, hipEventSynchronize(f.done));
     Geo& src = c->geo[c->gcur];
@@ -930,13 +939,16 @@ rt_status rt_render_frame(rt_ctx* c, const Uniforms* U, const rt_tile_set* tiles
     bool wavefront = c->pipeline == RT_PIPELINE_WAVEFRONT && U->debugTextureMode != DebugTextureModeMotion;
     // Frames in flight (Renderer.swift:1406-1409): wavefront frames on the context's own stream
     // rotate over the frames-in-flight slots; a caller's stream and the megakernel keep one.
-    //  By default two, four for frames of fewer than kSmallFrame paths (a multi-GPU rank's
-    // share of the 1080p frame): the finish tail's fixed latency dominates a small frame, and more
-    // overlapping frames fill it (C3g per rank, 2 / 3 / 4 slots: 2-way split 4.52 / 5.15 / 5.49,
-    // 8-way 2.30 / 2.73 / 2.92 Grays/s per GPU; 5 and 6 slots measured slower)
+    //  By default two, four for frames of fewer than kSmallFrame allocated paths (a multi-GPU
+    // rank's share of the 1080p frame, the 720p frame): the finish tail's fixed latency dominates a
+    // small frame, and more overlapping frames fill it (C3g per rank, 2 / 3 / 4 slots: 2-way split
+    // 4.52 / 5.15 / 5.49, 8-way 2.30 / 2.73 / 2.92 Grays/s per GPU; configs[1] 720p on one GPU,
+    // 3 / 4 slots: 5.95 / 7.38; 5 and 6 slots measured slower)
+    const int spp = std::max(U->samplesPerPixel, 1);
+    const int max_extra = U->enableMotionAdaptiveSampling ? std::max(U->motionSamplingMaxExtraSamples, 0) : 0;
     int nfl = 1;
     if (wavefront && c->stream == c->own_stream) {
-        const uint64_t frame_paths = (uint64_t)own * ts * ts * (uint64_t)std::max(U->samplesPerPixel, 1);
+        const uint64_t frame_paths = (uint64_t)own * ts * ts * (uint64_t)(spp + max_extra);
         nfl = c->max_in_flight > 0 ? c->max_in_flight : (frame_paths < kSmallFrame ? kMaxSlots : 2);
     }
     const int k = c->frame_no > 0 ? (c->last_slot + 1) % nfl : 0;
@@ -958,7 +970,7 @@ rt_status rt_render_frame(rt_ctx* c, const Uniforms* U, const rt_tile_set* tiles
     if (c->gdirty) {   // this frame reads the updated generation
         HIPC(c, hipEventRecord(c->uev, c->ustream));
         c->uev_valid = true;
-        c->gcur = 1 - c->gcur;
+        c->gcur = c->next_gen();
         c->gdirty = false;
     }
     if (c->uev_valid) HIPC(c, hipStreamWaitEvent(stream, c->uev, 0));
@@ -1007,8 +1019,6 @@ rt_status rt_render_frame(rt_ctx* c, const Uniforms* U, const rt_tile_set* tiles
     P.nranks = nranks;
     P.tiles_x = tiles_x;
     if (wavefront) {
-        int spp = std::max(U->samplesPerPixel, 1);
-        int max_extra = U->enableMotionAdaptiveSampling ? std::max(U->motionSamplingMaxExtraSamples, 0) : 0;
         if ((st = ensure_wavefront(c, F, (size_t)own * ts * ts, spp, max_extra))) return st;
         F.wf.motion_prev = (float2*)c->d_motion[m_prev].p;
     }

@@ -2024,12 +2024,13 @@ bool run_wavefront(const DevScene& S, const FrameParams& P, WavefrontBuffers& W,
     static const int prio = env_int("RT_PRIO", 0), fchunk = env_int("RT_FCHUNK", 32);
     Q.fchunk = max(1, fchunk);
     // frames in flight: 1 / in_flight of the machine for the tail, the rest for the other frames'
-    // bulk rounds (C3g, 2 in flight: 5.94 -> 5.72 ms per frame at 50 %; 3 in flight: 33 %; 4 in
-    // flight: 20 %, per-rank 4-way split 4.48 -> 4.69 Grays/s against 25 %); one frame at a time:
-    // all of it
+    // bulk rounds (C3g, 2 in flight: 5.94 -> 5.72 ms per frame at 50 %; 3 in flight: 33 %); one
+    // frame at a time: all of it.  Four frames of a small frame (below 6M base paths, a rank's
+    // share): 20 %, per-rank 4-way split 4.48 -> 4.69 Grays/s against 25 %; a large frame forced
+    // to four slots keeps 25 % (the 20 % sweep covered rank shares only)
     static const int finish_frac = env_int("RT_FINISH_FRAC", 0);
     Q.finish_frac = finish_frac > 0 ? min(finish_frac, 100)
-                  : in_flight >= 4 ? 20 : (in_flight > 1 ? 100 / in_flight : 100);
+                  : (in_flight >= 4 && Q.base_paths < (6u << 20)) ? 20 : (in_flight > 1 ? 100 / in_flight : 100);
     Q.prio = (prio && Q.finish_step == 1 && W.sorted) ? 1 : 0;
     if (Q.finish_step == 2 && (!W.p_ray || !W.p_sray)) {
         *err = "wave-queue finish kernel without its path ray slots";

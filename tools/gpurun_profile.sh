@@ -3,7 +3,7 @@
 #   1. the default bench line (with the CPU baseline)           -> gpurun_out/${TAG}_bench.json
 #   2. rocprofv3 --kernel-trace --stats of a bench run            -> gpurun_out/${TAG}_kernel_stats.csv
 #   3. three --pmc passes (FETCH_SIZE, WRITE_SIZE, TCC_HIT+TCC_MISS) -> gpurun_out/${TAG}_traffic.json gpurun_out/${TAG}_pmc_TCC_HIT_sum/run_counter_collection.csv
-TAG=${TAG:-r01}
+TAG=${TAG:-r02}
 R=$PWD
 mkdir -p gpurun_out
 export TMPDIR=/tmp

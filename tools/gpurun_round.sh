@@ -2,4 +2,4 @@ set -o pipefail
 mkdir -p gpurun_out
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1
 rc=$?; tail -3 gpurun_out/gpu_tests.log; [ $rc -ne 0 ] && exit $rc
-TAG=r01 bash tools/gpurun_profile.sh
+TAG=${TAG:-r02} bash tools/gpurun_profile.sh
