@@ -47,6 +47,22 @@ const char* rt_scene_last_error(const rt_scene* scene);
 rt_status rt_scene_add_obj(rt_scene* scene, const char* obj_path, const float position[3],
                            const float rotation[3], float scale, const rt_material_override* ov);
 
+/* Model(name:position:rotation:scale:materialOverride:) for a USD asset — the USDZ branch of
+ * Model.init (Model.swift:87-184).  `usd_path` is a .usdz package (its first .usd/.usda/.usdc
+ * entry is the root layer; textures are read from the package), a .usda text layer or a .usdc
+ * crate layer.  Every active UsdGeomMesh becomes one mesh in depth-first order, placed by the
+ * model's T*R*S only (the reference passes worldTransform to every mesh, Model.swift:162-170):
+ * fan-triangulated faces, one vertex per unique (point, normal, uv) corner, normals computed
+ * when absent, one submesh per materialBind GeomSubset, UsdPreviewSurface inputs mapped as
+ * Material(material:) does (SubMesh.swift:291-324) plus their texture maps.  The last Skeleton
+ * and SkelAnimation met in the walk are the model's (Model.swift:99-121); meshes carrying
+ * skel:jointIndices / jointWeights become skinned meshes (first four influences), their joint
+ * order (skel:joints or the skeleton's) mapped to the skeleton by path, unique suffix and tail
+ * (Model.swift:427-494).  Composition arcs (references, payloads, variants) are not followed.
+ * Fails with RT_ERR_IO when the file is missing or malformed. */
+rt_status rt_scene_add_usd(rt_scene* scene, const char* usd_path, const float position[3], const float rotation[3],
+                           float scale, const rt_material_override* ov);
+
 /* Deterministic procedural stand-ins for the assets missing from the reference snapshot
  * (.MISSING_LARGE_BLOBS): kind = "dragon" (871,414 tris), "bunny" (69,451 tris),
  * "robot" (skinned, for config 5). `mtl_path` may be NULL (built-in material). */
@@ -61,8 +77,8 @@ rt_status rt_scene_set_light_intensity(rt_scene* scene, float intensity);
 
 /* Benchmark / parity presets: "c1", "c2", "c3", "c3g", "c3d", "c5", "app".
  * `asset_dir` holds the OBJ/MTL files (plane.obj, sphere.obj, ...); a real dragon.obj /
- * bunny.obj found there is loaded instead of the procedural stand-in unless the preset name
- * ends in "_synthetic". *is_synthetic reports whether a stand-in was used. */
+ * bunny.obj / robot.usdz found there is loaded instead of the procedural stand-in unless the
+ * preset name ends in "_synthetic". *is_synthetic reports whether a stand-in was used. */
 rt_status rt_scene_preset(const char* name, const char* asset_dir, rt_scene** out, int32_t* is_synthetic);
 
 /* Flattened description. Pointers stay valid until the scene is modified or freed. */
@@ -92,7 +108,11 @@ uint64_t rt_scene_triangle_count(const rt_scene* scene);
 
 /* Skinned meshes (config 5): joint matrices for animation time t, already composed as
  * geomBind^-1 * (global * invBind) * geomBind (SkinningPass.swift:124-157, Model.swift:207-261).
- * `out` receives joint_count column-major float4x4. */
+ * For a USD model: Model.update's clip time fmod(t, duration), the animation's translations /
+ * rotations / scales sampled there (linear, rotations spherical; clamped outside the keys; time
+ * codes / timeCodesPerSecond), local = T * R(normalised q) * S over the rest transforms,
+ * global = parent global * local, skin = global * inverse bind, one matrix per mesh joint
+ * (identity for joints the skeleton lacks).  `out` receives joint_count column-major float4x4. */
 rt_status rt_scene_joint_matrices(rt_scene* scene, uint32_t mesh_index, double time_seconds,
                                   float* out, uint32_t capacity, uint32_t* joint_count);
 

@@ -162,6 +162,13 @@ class Scene:
         _check(lib().rt_scene_add_obj(self._h, obj_path.encode(), p, r, scale,
                                       C.byref(material_override) if material_override else None), scene=self._h)
 
+    def add_usd(self, usd_path, position, rotation=(0, 0, 0), scale=1.0, material_override=None):
+        """Model(name:...) for a .usdz / .usda / .usdc asset (Model.swift:87-184)."""
+        p = (C.c_float * 3)(*position)
+        r = (C.c_float * 3)(*rotation)
+        _check(lib().rt_scene_add_usd(self._h, usd_path.encode(), p, r, scale,
+                                      C.byref(material_override) if material_override else None), scene=self._h)
+
     def add_procedural(self, kind, position, rotation=(0, 0, 0), scale=1.0, material_override=None, mtl_path=None):
         p = (C.c_float * 3)(*position)
         r = (C.c_float * 3)(*rotation)

@@ -218,7 +218,7 @@ EXPORTED_SYMBOLS = [
     "rt_set_counting", "rt_get_stats", "rt_version", "rt_debug_trace_host",
     # rt_scene.h
     "rt_material_override_glass", "rt_scene_new", "rt_scene_free", "rt_scene_last_error",
-    "rt_scene_add_obj", "rt_scene_add_procedural", "rt_scene_set_lights", "rt_scene_set_light_intensity",
+    "rt_scene_add_obj", "rt_scene_add_usd", "rt_scene_add_procedural", "rt_scene_set_lights", "rt_scene_set_light_intensity",
     "rt_scene_preset", "rt_scene_get_desc", "rt_scene_triangle_count", "rt_scene_joint_matrices",
     "rt_scene_add_texture", "rt_scene_load_texture", "rt_scene_bind_texture", "rt_decode_png",
     "rt_camera_default", "rt_camera_orbit", "rt_uniforms_default", "rt_random_offsets",
@@ -265,6 +265,7 @@ def declare(lib):
         "rt_scene_free": (st, [vp]),
         "rt_scene_last_error": (C.c_char_p, [vp]),
         "rt_scene_add_obj": (st, [vp, C.c_char_p, P(C.c_float), P(C.c_float), C.c_float, P(MaterialOverride)]),
+        "rt_scene_add_usd": (st, [vp, C.c_char_p, P(C.c_float), P(C.c_float), C.c_float, P(MaterialOverride)]),
         "rt_scene_add_procedural": (st, [vp, C.c_char_p, C.c_char_p, P(C.c_float), P(C.c_float), C.c_float,
                                          P(MaterialOverride)]),
         "rt_scene_set_lights": (st, [vp, P(Light), C.c_uint32]),

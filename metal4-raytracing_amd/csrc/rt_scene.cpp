@@ -14,13 +14,16 @@
 // SubMesh.swift:309-311).  ModelIO itself is unvendored: its exact triangulation/dedup order
 // is parity-unpinned and documented in DESIGN.md.
 #include "../../include/rt_scene.h"
+#include "rt_usd.h"
 
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <map>
 #include <memory>
+#include <tuple>
 #include <string>
 #include <unordered_map>
 #include <vector>
@@ -102,6 +105,24 @@ struct Skin {
     double duration = 2.0;
 };
 
+// Model.skeleton / Model.animation of a USD asset (Model.swift:346-414): joint paths, parents
+// from the paths, rest transforms, inverse bind transforms, and the packed joint animation as
+// keyframe tracks (time in seconds, translations / rotations (x, y, z, w) / scales per joint).
+struct UsdSkel {
+    std::vector<std::string> joint_paths;
+    std::vector<int> parent;
+    std::vector<M4> rest, inverse_bind;
+    struct Track {
+        int comps = 3;
+        std::vector<double> t;
+        std::vector<std::vector<float>> v;   // per key: comps * joints
+    };
+    bool has_anim = false;
+    std::vector<std::string> anim_paths;
+    Track tr, rot, sc;
+    double duration = 0.0;
+};
+
 struct Mesh {
     std::string name;
     std::vector<rt_float3> positions, normals;
@@ -113,6 +134,11 @@ struct Mesh {
     M4 transform;
     uint32_t joint_count = 0;
     std::shared_ptr<Skin> skin;
+    // USD skinning (MeshSkinningInfo, Mesh.swift:10-15): the model's skeleton, this mesh's joint
+    // order mapped to skeleton indices, geometryBindTransform and its inverse
+    std::shared_ptr<UsdSkel> usd_skel;
+    std::vector<int> joint_to_skel;
+    M4 geom_bind, geom_bind_inv;
 };
 
 struct Model {
@@ -664,6 +690,512 @@ static rt_status load_png_file(rt_scene* s, const std::string& path, uint32_t* i
     return RT_OK;
 }
 
+// ---- USD assets: the USDZ branch of Model.init (Model.swift:87-184) -----------------------------
+namespace usdscene {
+
+using usd::Attr;
+using usd::Prim;
+using usd::Stage;
+using usd::Value;
+
+static rt_status texture_from_bytes(rt_scene* s, const std::string& key, const uint8_t* data, size_t n, uint32_t* id) {
+    for (size_t i = 0; i < s->textures.size(); ++i)
+        if (!s->textures[i].path.empty() && s->textures[i].path == key) {
+            *id = (uint32_t)i;
+            return RT_OK;
+        }
+    rt_scene::Texture t;
+    char eb[256] = {0};
+    rt_status st = rt_decode_png(data, n, nullptr, &t.w, &t.h, eb, sizeof eb);
+    if (!st) {
+        t.texels.resize((size_t)t.w * t.h * 4);
+        st = rt_decode_png(data, n, t.texels.data(), &t.w, &t.h, eb, sizeof eb);
+    }
+    if (st) return st;
+    t.path = key;
+    s->textures.push_back(std::move(t));
+    *id = (uint32_t)(s->textures.size() - 1);
+    return RT_OK;
+}
+
+// simd_inverse (Model.swift:361): general 4x4 inverse (cofactors in double, rounded once)
+static M4 m4_inverse(const M4& a) {
+    double m[16], inv[16];
+    for (int i = 0; i < 16; ++i) m[i] = a.m[i];
+    inv[0] = m[5] * m[10] * m[15] - m[5] * m[11] * m[14] - m[9] * m[6] * m[15] + m[9] * m[7] * m[14] + m[13] * m[6] * m[11] - m[13] * m[7] * m[10];
+    inv[4] = -m[4] * m[10] * m[15] + m[4] * m[11] * m[14] + m[8] * m[6] * m[15] - m[8] * m[7] * m[14] - m[12] * m[6] * m[11] + m[12] * m[7] * m[10];
+    inv[8] = m[4] * m[9] * m[15] - m[4] * m[11] * m[13] - m[8] * m[5] * m[15] + m[8] * m[7] * m[13] + m[12] * m[5] * m[11] - m[12] * m[7] * m[9];
+    inv[12] = -m[4] * m[9] * m[14] + m[4] * m[10] * m[13] + m[8] * m[5] * m[14] - m[8] * m[6] * m[13] - m[12] * m[5] * m[10] + m[12] * m[6] * m[9];
+    inv[1] = -m[1] * m[10] * m[15] + m[1] * m[11] * m[14] + m[9] * m[2] * m[15] - m[9] * m[3] * m[14] - m[13] * m[2] * m[11] + m[13] * m[3] * m[10];
+    inv[5] = m[0] * m[10] * m[15] - m[0] * m[11] * m[14] - m[8] * m[2] * m[15] + m[8] * m[3] * m[14] + m[12] * m[2] * m[11] - m[12] * m[3] * m[10];
+    inv[9] = -m[0] * m[9] * m[15] + m[0] * m[11] * m[13] + m[8] * m[1] * m[15] - m[8] * m[3] * m[13] - m[12] * m[1] * m[11] + m[12] * m[3] * m[9];
+    inv[13] = m[0] * m[9] * m[14] - m[0] * m[10] * m[13] - m[8] * m[1] * m[14] + m[8] * m[2] * m[13] + m[12] * m[1] * m[10] - m[12] * m[2] * m[9];
+    inv[2] = m[1] * m[6] * m[15] - m[1] * m[7] * m[14] - m[5] * m[2] * m[15] + m[5] * m[3] * m[14] + m[13] * m[2] * m[7] - m[13] * m[3] * m[6];
+    inv[6] = -m[0] * m[6] * m[15] + m[0] * m[7] * m[14] + m[4] * m[2] * m[15] - m[4] * m[3] * m[14] - m[12] * m[2] * m[7] + m[12] * m[3] * m[6];
+    inv[10] = m[0] * m[5] * m[15] - m[0] * m[7] * m[13] - m[4] * m[1] * m[15] + m[4] * m[3] * m[13] + m[12] * m[1] * m[7] - m[12] * m[3] * m[5];
+    inv[14] = -m[0] * m[5] * m[14] + m[0] * m[6] * m[13] + m[4] * m[1] * m[14] - m[4] * m[2] * m[13] - m[12] * m[1] * m[6] + m[12] * m[2] * m[5];
+    inv[3] = -m[1] * m[6] * m[11] + m[1] * m[7] * m[10] + m[5] * m[2] * m[11] - m[5] * m[3] * m[10] - m[9] * m[2] * m[7] + m[9] * m[3] * m[6];
+    inv[7] = m[0] * m[6] * m[11] - m[0] * m[7] * m[10] - m[4] * m[2] * m[11] + m[4] * m[3] * m[10] + m[8] * m[2] * m[7] - m[8] * m[3] * m[6];
+    inv[11] = -m[0] * m[5] * m[11] + m[0] * m[7] * m[9] + m[4] * m[1] * m[11] - m[4] * m[3] * m[9] - m[8] * m[1] * m[7] + m[8] * m[3] * m[5];
+    inv[15] = m[0] * m[5] * m[10] - m[0] * m[6] * m[9] - m[4] * m[1] * m[10] + m[4] * m[2] * m[9] + m[8] * m[1] * m[6] - m[8] * m[2] * m[5];
+    const double det = m[0] * inv[0] + m[1] * inv[4] + m[2] * inv[8] + m[3] * inv[12];
+    M4 r = m4_identity();
+    if (det == 0.0) return r;
+    for (int i = 0; i < 16; ++i) r.m[i] = (float)(inv[i] / det);
+    return r;
+}
+
+// a USD matrix4d (row-vector convention, translation in the last row) is the simd float4x4 whose
+// columns are its rows (ModelIO's conversion)
+static M4 m4_from_usd(const std::vector<double>& v, size_t off) {
+    M4 r;
+    for (int i = 0; i < 16; ++i) r.m[i] = (float)v[off + i];
+    return r;
+}
+
+// ---- joint paths (Model.swift:427-494) ----
+static std::vector<std::string> split_path(const std::string& p) {
+    std::vector<std::string> parts;
+    size_t i = 0;
+    while (i <= p.size()) {
+        size_t j = p.find('/', i);
+        if (j == std::string::npos) j = p.size();
+        if (j > i) parts.push_back(p.substr(i, j - i));
+        i = j + 1;
+    }
+    return parts;
+}
+static std::string join_path(const std::vector<std::string>& parts, size_t from) {
+    std::string r;
+    for (size_t k = from; k < parts.size(); ++k) r += (k > from ? "/" : "") + parts[k];
+    return r;
+}
+static std::string normalize_joint_path(const std::string& p) { return join_path(split_path(p), 0); }
+static std::string parent_joint_path(const std::string& p) {   // parentJointPath(for:)
+    const std::string n = normalize_joint_path(p);
+    const size_t s = n.find_last_of('/');
+    if (s == std::string::npos || s == 0) return std::string();
+    return n.substr(0, s);
+}
+static std::map<std::string, int> path_index_map(const std::vector<std::string>& paths) {   // buildPathIndexMap
+    std::vector<std::string> norm;
+    for (const auto& p : paths) norm.push_back(normalize_joint_path(p));
+    std::map<std::string, int> map;
+    for (size_t i = 0; i < norm.size(); ++i)
+        if (!norm[i].empty()) map[norm[i]] = (int)i;
+    std::map<std::string, int> suffix_count;
+    for (const auto& p : norm) {
+        if (p.empty()) continue;
+        const auto parts = split_path(p);
+        for (size_t st = 1; st < parts.size(); ++st) suffix_count[join_path(parts, st)]++;
+    }
+    for (size_t i = 0; i < norm.size(); ++i) {
+        if (norm[i].empty()) continue;
+        const auto parts = split_path(norm[i]);
+        for (size_t st = 1; st < parts.size(); ++st) {
+            const std::string suf = join_path(parts, st);
+            if (suffix_count[suf] == 1 && !map.count(suf)) map[suf] = (int)i;
+        }
+    }
+    return map;
+}
+static std::map<std::string, int> tail_index_map(const std::vector<std::string>& paths) {   // buildTailIndexMap
+    std::vector<std::string> tails;
+    for (const auto& p : paths) {
+        const auto parts = split_path(p);
+        tails.push_back(parts.empty() ? normalize_joint_path(p) : parts.back());
+    }
+    std::map<std::string, int> counts, map;
+    for (const auto& t : tails)
+        if (!t.empty()) counts[t]++;
+    for (size_t i = 0; i < tails.size(); ++i)
+        if (!tails[i].empty() && counts[tails[i]] == 1) map[tails[i]] = (int)i;
+    return map;
+}
+static int map_joint(const std::string& p, const std::map<std::string, int>& by_path, const std::map<std::string, int>& by_tail) {
+    const std::string n = normalize_joint_path(p);
+    auto it = by_path.find(n);
+    if (it != by_path.end()) return it->second;
+    const auto parts = split_path(n);
+    const std::string tail = parts.empty() ? n : parts.back();
+    auto jt = by_tail.find(tail);
+    return jt != by_tail.end() ? jt->second : -1;
+}
+
+// matrix_float4x4(simd_quatf) and matrix4x4_trs (Model.swift:496-501): T * R(q) * S
+static M4 m4_quat(const float q[4]) {   // q = (x, y, z, w)
+    const float x = q[0], y = q[1], z = q[2], w = q[3];
+    M4 r = m4_identity();
+    r.m[0] = w * w + x * x - y * y - z * z;
+    r.m[1] = 2.0f * (x * y + z * w);
+    r.m[2] = 2.0f * (x * z - y * w);
+    r.m[4] = 2.0f * (x * y - z * w);
+    r.m[5] = w * w - x * x + y * y - z * z;
+    r.m[6] = 2.0f * (y * z + x * w);
+    r.m[8] = 2.0f * (z * x + y * w);
+    r.m[9] = 2.0f * (y * z - x * w);
+    r.m[10] = w * w - x * x - y * y + z * z;
+    return r;
+}
+static M4 m4_trs(const float* t, const float* q, const float* sc) {
+    M4 S = m4_identity();
+    S.m[0] = sc[0];
+    S.m[5] = sc[1];
+    S.m[10] = sc[2];
+    return m4_mul(m4_mul(m4_translate(t), m4_quat(q)), S);
+}
+
+// MDLAnimatedValue sampling: clamped outside the keys, linear between them (spherical for
+// rotations, along the shorter arc)
+static void sample_track(const UsdSkel::Track& tr, double t, bool quat, std::vector<float>& out) {
+    out.clear();
+    if (tr.t.empty()) return;
+    if (t <= tr.t.front() || tr.t.size() == 1) { out = tr.v.front(); return; }
+    if (t >= tr.t.back()) { out = tr.v.back(); return; }
+    size_t k = 0;
+    while (k + 1 < tr.t.size() && tr.t[k + 1] <= t) ++k;
+    const std::vector<float>& a = tr.v[k];
+    const std::vector<float>& b = tr.v[k + 1];
+    const float u = (float)((t - tr.t[k]) / (tr.t[k + 1] - tr.t[k]));
+    const size_t n = std::min(a.size(), b.size());
+    out.resize(n);
+    if (!quat) {
+        for (size_t i = 0; i < n; ++i) out[i] = a[i] + (b[i] - a[i]) * u;
+        return;
+    }
+    for (size_t j = 0; j + 3 < n; j += 4) {
+        float q1[4] = {b[j], b[j + 1], b[j + 2], b[j + 3]};
+        float d = a[j] * q1[0] + a[j + 1] * q1[1] + a[j + 2] * q1[2] + a[j + 3] * q1[3];
+        if (d < 0.0f) { for (float& c : q1) c = -c; d = -d; }
+        float wa, wb;
+        if (d > 0.9995f) {
+            wa = 1.0f - u;
+            wb = u;
+        } else {
+            const float th = std::acos(d), st = std::sin(th);
+            wa = std::sin((1.0f - u) * th) / st;
+            wb = std::sin(u * th) / st;
+        }
+        float r[4], l = 0.0f;
+        for (int c = 0; c < 4; ++c) { r[c] = a[j + c] * wa + q1[c] * wb; l += r[c] * r[c]; }
+        l = std::sqrt(l);
+        for (int c = 0; c < 4; ++c) out[j + c] = l > 0.0f ? r[c] / l : r[c];
+    }
+}
+
+// Model.update(deltaTime:) at clip time t, then SkinningPass.updateSkinningJointMatrices
+// (SkinningPass.swift:124-157) for one mesh: geomBind^-1 * (global * invBind) * geomBind
+static void joint_matrices(const Mesh& m, double time_seconds, std::vector<M4>& out) {
+    const UsdSkel& S = *m.usd_skel;
+    const size_t J = S.joint_paths.size();
+    std::vector<M4> local = S.rest;
+    local.resize(J, m4_identity());
+    if (S.has_anim) {
+        const double t = S.duration > 0.0 ? std::fmod(time_seconds, S.duration) : 0.0;
+        std::vector<float> T, R, Sc;
+        sample_track(S.tr, t, false, T);
+        sample_track(S.rot, t, true, R);
+        sample_track(S.sc, t, false, Sc);
+        const size_t n = std::min(std::min(T.size() / 3, R.size() / 4), std::min(Sc.size() / 3, S.anim_paths.size()));
+        const auto by_path = path_index_map(S.joint_paths);
+        const auto by_tail = tail_index_map(S.joint_paths);
+        for (size_t i = 0; i < n; ++i) {
+            const int ji = map_joint(S.anim_paths[i], by_path, by_tail);
+            if (ji < 0 || (size_t)ji >= J) continue;
+            float q[4] = {R[4 * i + 1], R[4 * i + 2], R[4 * i + 3], R[4 * i]};   // stage order (w, x, y, z)
+            const float ql = std::sqrt(q[3] * q[3] + q[0] * q[0] + q[1] * q[1] + q[2] * q[2]);
+            if (ql > 0.0001f) for (float& c : q) c = c / ql;
+            else { q[0] = q[1] = q[2] = 0.0f; q[3] = 1.0f; }
+            local[ji] = m4_trs(&T[3 * i], q, &Sc[3 * i]);
+        }
+    }
+    std::vector<M4> global = local;   // Skeleton.computeGlobalTransforms
+    for (size_t i = 0; i < J; ++i) {
+        const int p = S.parent[i];
+        if (p >= 0 && (size_t)p < i) global[i] = m4_mul(global[p], local[i]);
+    }
+    std::vector<M4> skin(J);
+    for (size_t j = 0; j < J; ++j) skin[j] = m4_mul(global[j], j < S.inverse_bind.size() ? S.inverse_bind[j] : m4_identity());
+    const std::vector<int>& map = m.joint_to_skel;
+    const size_t count = map.empty() ? std::max<size_t>(1, J) : map.size();
+    out.assign(count, m4_identity());
+    if (skin.empty()) return;
+    for (size_t i = 0; i < count; ++i) {
+        const int k = map.empty() ? (int)i : map[i];
+        const M4 sm = k >= 0 && (size_t)k < J ? skin[k] : m4_identity();
+        out[i] = m4_mul(m.geom_bind_inv, m4_mul(sm, m.geom_bind));
+    }
+}
+
+static const Value* attr_value(const Prim& p, const std::string& name, const Attr** out = nullptr) {
+    const Attr* a = p.attr(name);
+    if (out) *out = a;
+    if (!a) return nullptr;
+    if (a->has_default) return &a->value;
+    if (!a->samples.empty()) return &a->samples.front();   // first time sample (rest pose)
+    return nullptr;
+}
+
+static bool read_skeleton(const Stage& st, const Prim& sk, const Prim* anim, UsdSkel& out) {
+    const Value* joints = attr_value(sk, "joints");
+    if (!joints || joints->kind != Value::kStr) return false;
+    out.joint_paths = joints->str;
+    const size_t J = out.joint_paths.size();
+    const auto by_path = path_index_map(out.joint_paths);
+    for (const auto& p : out.joint_paths) {
+        const std::string pp = parent_joint_path(p);
+        auto it = pp.empty() ? by_path.end() : by_path.find(pp);
+        out.parent.push_back(it == by_path.end() ? -1 : it->second);
+    }
+    const Value* bind = attr_value(sk, "bindTransforms");
+    if (bind && bind->kind == Value::kNum && bind->num.size() == 16 * J)
+        for (size_t j = 0; j < J; ++j) out.inverse_bind.push_back(m4_inverse(m4_from_usd(bind->num, 16 * j)));
+    else
+        out.inverse_bind.assign(J, m4_identity());
+    const Value* rest = attr_value(sk, "restTransforms");
+    if (rest && rest->kind == Value::kNum && rest->num.size() == 16 * J)
+        for (size_t j = 0; j < J; ++j) out.rest.push_back(m4_from_usd(rest->num, 16 * j));
+    else
+        out.rest.assign(J, m4_identity());
+    if (!anim) return true;
+    const Value* aj = attr_value(*anim, "joints");
+    if (!aj || aj->kind != Value::kStr) return true;
+    out.has_anim = true;
+    out.anim_paths = aj->str;
+    const double tcps = st.time_codes_per_second > 0.0 ? st.time_codes_per_second : 24.0;
+    double tmin = 0.0, tmax = 0.0;
+    bool any = false;
+    auto track = [&](const char* name, int comps, UsdSkel::Track& tr) {
+        tr.comps = comps;
+        const Attr* a = anim->attr(name);
+        if (!a) return;
+        auto push = [&](double t, const Value& v) {
+            if (v.kind != Value::kNum) return;
+            std::vector<float> f(v.num.begin(), v.num.end());
+            tr.t.push_back(t);
+            tr.v.push_back(std::move(f));
+        };
+        if (!a->samples.empty()) {
+            std::vector<size_t> order(a->times.size());
+            for (size_t i = 0; i < order.size(); ++i) order[i] = i;
+            std::sort(order.begin(), order.end(), [a](size_t x, size_t y) { return a->times[x] < a->times[y]; });
+            for (size_t i : order) push(a->times[i] / tcps, a->samples[i]);
+        } else if (a->has_default) {
+            push(0.0, a->value);
+        }
+        if (!tr.t.empty()) {
+            tmin = any ? std::min(tmin, tr.t.front()) : tr.t.front();
+            tmax = any ? std::max(tmax, tr.t.back()) : tr.t.back();
+            any = true;
+        }
+    };
+    track("translations", 3, out.tr);
+    track("rotations", 4, out.rot);
+    track("scales", 3, out.sc);
+    out.duration = any ? tmax - tmin : 0.0;   // AnimationClip.init (Model.swift:401-403)
+    return true;
+}
+
+// primvar value at (point, face-vertex corner, face) per its interpolation; -1 = none
+struct Primvar {
+    const Value* v = nullptr;
+    std::vector<int> idx;     // <name>:indices
+    std::string interp;
+    int comps = 0;
+    bool ok() const { return v && v->kind == Value::kNum && comps > 0; }
+    int key(int point, int corner, int face) const {
+        int k = interp == "faceVarying" ? corner : interp == "uniform" ? face : interp == "constant" ? 0 : point;
+        if (!idx.empty()) k = k < (int)idx.size() ? idx[k] : -1;
+        return k >= 0 && (size_t)(k + 1) * comps <= v->num.size() ? k : -1;
+    }
+};
+static Primvar primvar(const Prim& p, const std::string& name, const char* default_interp) {
+    Primvar pv;
+    const Attr* a = nullptr;
+    pv.v = attr_value(p, name, &a);
+    if (!pv.v || pv.v->kind != Value::kNum) { pv.v = nullptr; return pv; }
+    pv.comps = pv.v->comps;
+    pv.interp = a && !a->interpolation.empty() ? a->interpolation : default_interp;
+    if (const Value* iv = attr_value(p, name + ":indices"))
+        for (double d : iv->num) pv.idx.push_back((int)d);
+    return pv;
+}
+
+static int find_prim_up(const Stage& st, int id, const char* rel) {   // inherited relationship target
+    for (int k = id; k >= 0; k = st.prims[k].parent) {
+        const auto* r = st.prims[k].rel(rel);
+        if (r && !r->empty()) return st.find((*r)[0]);
+    }
+    return -1;
+}
+
+static bool load_tex(rt_scene* s, const std::string& file, const std::vector<usd::PackageFile>& files, const std::string& dir,
+                     uint32_t* id) {
+    std::string f = file;
+    while (f.size() > 2 && f[0] == '.' && f[1] == '/') f = f.substr(2);
+    for (const auto& pf : files)
+        if (pf.name == f) return texture_from_bytes(s, "usdz:" + dir + ":" + f, pf.data.data(), pf.data.size(), id) == RT_OK;
+    return load_png_file(s, file[0] == '/' ? file : dir + "/" + f, id) == RT_OK;
+}
+
+// Material(material:) (SubMesh.swift:291-324) + the texture slots (SubMesh.swift:117-166) from a
+// UsdPreviewSurface: diffuseColor -> baseColor / base color map, emissiveColor -> emission /
+// emission map, ior, opacity (clamped) / opacity map, specularColor -> specular, normal /
+// roughness / metallic / occlusion -> their maps
+static void usd_material(rt_scene* s, const Stage& st, int mat, const std::vector<usd::PackageFile>& files,
+                         const std::string& dir, Submesh& sm) {
+    sm.material = default_material();
+    if (mat < 0) return;
+    int shader = -1;
+    if (const Attr* out = st.prims[mat].attr("outputs:surface"))
+        if (!out->connections.empty()) shader = st.find(out->connections[0].substr(0, out->connections[0].find_last_of('.')));
+    if (shader < 0) {
+        std::function<void(int)> walk = [&](int k) {
+            const Value* id = attr_value(st.prims[k], "info:id");
+            if (shader < 0 && st.prims[k].type == "Shader" && id && !id->str.empty() && id->str[0] == "UsdPreviewSurface") shader = k;
+            for (int c : st.prims[k].children) walk(c);
+        };
+        walk(mat);
+    }
+    if (shader < 0) return;
+    const Prim& sh = st.prims[shader];
+    auto texture_of = [&](const char* input) -> std::string {   // connected UsdUVTexture's file
+        const Attr* a = sh.attr(input);
+        if (!a || a->connections.empty()) return std::string();
+        const int t = st.find(a->connections[0].substr(0, a->connections[0].find_last_of('.')));
+        if (t < 0) return std::string();
+        const Value* f = attr_value(st.prims[t], "inputs:file");
+        return f && f->kind == Value::kStr && !f->str.empty() ? f->str[0] : std::string("?");
+    };
+    auto vec3 = [&](const char* input, rt_float3& dst) {
+        const Value* v = attr_value(sh, input);
+        if (v && v->kind == Value::kNum && v->num.size() >= 3) dst = f3((float)v->num[0], (float)v->num[1], (float)v->num[2]);
+    };
+    vec3("inputs:diffuseColor", sm.material.baseColor);
+    vec3("inputs:emissiveColor", sm.material.emission);
+    vec3("inputs:specularColor", sm.material.specular);
+    if (const Value* v = attr_value(sh, "inputs:ior"))
+        if (v->kind == Value::kNum && !v->num.empty()) sm.material.refractionIndex = (float)v->num[0];
+    if (const Value* v = attr_value(sh, "inputs:opacity"))
+        if (v->kind == Value::kNum && !v->num.empty()) sm.material.opacity = std::min(std::max((float)v->num[0], 0.0f), 1.0f);
+    static const struct { const char* input; int slot; } kMaps[] = {
+        {"inputs:diffuseColor", 0}, {"inputs:normal", 1}, {"inputs:roughness", 2}, {"inputs:metallic", 3},
+        {"inputs:occlusion", 4}, {"inputs:emissiveColor", 5}, {"inputs:opacity", 6}};
+    for (const auto& m : kMaps) {
+        const std::string file = texture_of(m.input);
+        if (file.empty()) continue;
+        if (m.slot == 0) sm.material.baseColor = f3(1.0f, 1.0f, 1.0f);   // a texture-typed base color (SubMesh.swift:299-302)
+        uint32_t id;
+        if (file != "?" && load_tex(s, file, files, dir, &id)) bind_slot(sm, m.slot, id);
+    }
+}
+
+// One UsdGeomMesh -> Mesh: fan triangulation, one vertex per unique (point, normal, uv) corner,
+// one submesh per materialBind GeomSubset (+ the faces no subset claims)
+static bool build_mesh(rt_scene* s, const Stage& st, int id, const std::vector<usd::PackageFile>& files,
+                       const std::string& dir, Mesh& out, std::string& err) {
+    const Prim& p = st.prims[id];
+    const Value* pts = attr_value(p, "points");
+    const Value* fvc = attr_value(p, "faceVertexCounts");
+    const Value* fvi = attr_value(p, "faceVertexIndices");
+    if (!pts || !fvc || !fvi || pts->kind != Value::kNum || pts->comps != 3) { err = p.path + ": mesh without points / faces"; return false; }
+    const int np = (int)(pts->num.size() / 3);
+    size_t total = 0;
+    for (double c : fvc->num) total += (size_t)c;
+    if (total != fvi->num.size()) { err = p.path + ": faceVertexCounts do not match faceVertexIndices"; return false; }
+    for (double v : fvi->num)
+        if (v < 0 || v >= np) { err = p.path + ": face vertex index out of range"; return false; }
+    Primvar nrm = primvar(p, "primvars:normals", "vertex");
+    if (!nrm.ok()) nrm = primvar(p, "normals", "vertex");
+    Primvar uv = primvar(p, "primvars:st", "vertex");
+    if (!uv.ok())
+        for (const auto& kv : p.attrs)
+            if (kv.first.rfind("primvars:", 0) == 0 && kv.second.type.rfind("texCoord2", 0) == 0 &&
+                kv.first.find(":indices") == std::string::npos) {
+                uv = primvar(p, kv.first, "vertex");
+                break;
+            }
+    Primvar ji = primvar(p, "primvars:skel:jointIndices", "vertex");
+    Primvar jw = primvar(p, "primvars:skel:jointWeights", "vertex");
+    int es = 1;
+    if (const Attr* a = p.attr("primvars:skel:jointIndices")) es = std::max(1, a->element_size);
+    out.name = p.name;
+    out.transform = m4_identity();
+    const bool skinned = ji.ok() && jw.ok();
+    // faces -> submesh (GeomSubset "materialBind" family)
+    const int nf = (int)fvc->num.size();
+    std::vector<int> face_sub(nf, -1);
+    std::vector<int> sub_mat;
+    for (int c : p.children) {
+        const Prim& g = st.prims[c];
+        if (g.type != "GeomSubset") continue;
+        const Value* fam = attr_value(g, "familyName");
+        if (fam && (fam->str.empty() || fam->str[0] != "materialBind")) continue;
+        const Value* ix = attr_value(g, "indices");
+        if (!ix) continue;
+        const int sid = (int)sub_mat.size();
+        sub_mat.push_back(find_prim_up(st, c, "material:binding"));
+        for (double f : ix->num)
+            if (f >= 0 && f < nf && face_sub[(int)f] < 0) face_sub[(int)f] = sid;
+    }
+    const int rest_sub = (int)sub_mat.size();
+    sub_mat.push_back(find_prim_up(st, id, "material:binding"));
+    std::vector<Submesh> subs(sub_mat.size());
+    for (size_t k = 0; k < subs.size(); ++k) usd_material(s, st, sub_mat[k], files, dir, subs[k]);
+    std::map<std::tuple<int, int, int>, uint32_t> dedup;
+    std::vector<uint32_t> poly;
+    size_t corner = 0;
+    for (int f = 0; f < nf; ++f) {
+        const int cnt = (int)fvc->num[f];
+        poly.clear();
+        for (int c = 0; c < cnt; ++c, ++corner) {
+            const int pt = (int)fvi->num[corner];
+            const int nk = nrm.ok() ? nrm.key(pt, (int)corner, f) : -1, uk = uv.ok() ? uv.key(pt, (int)corner, f) : -1;
+            auto key = std::make_tuple(pt, nk, uk);
+            auto it = dedup.find(key);
+            if (it == dedup.end()) {
+                const uint32_t v = (uint32_t)out.positions.size();
+                dedup.emplace(key, v);
+                out.positions.push_back(f3((float)pts->num[3 * pt], (float)pts->num[3 * pt + 1], (float)pts->num[3 * pt + 2]));
+                out.normals.push_back(nk >= 0 ? f3((float)nrm.v->num[3 * nk], (float)nrm.v->num[3 * nk + 1], (float)nrm.v->num[3 * nk + 2])
+                                              : f3(0, 0, 0));
+                rt_float2 t{0.0f, 0.0f};
+                if (uk >= 0) { t.x = (float)uv.v->num[uv.comps * uk]; t.y = (float)uv.v->num[uv.comps * uk + 1]; out.has_uvs = true; }
+                out.uvs.push_back(t);
+                if (skinned) {   // first four influences; Model.vertexDescriptor defaults otherwise
+                    uint16_t jix[4] = {0, 0, 0, 0};
+                    float w[4] = {1.0f, 0.0f, 0.0f, 0.0f};
+                    const int src = ji.interp == "constant" ? 0 : pt;
+                    if ((size_t)(src + 1) * es <= ji.v->num.size() && (size_t)(src + 1) * es <= jw.v->num.size()) {
+                        w[0] = 0.0f;
+                        for (int k = 0; k < std::min(es, 4); ++k) {
+                            jix[k] = (uint16_t)std::max(0.0, ji.v->num[(size_t)src * es + k]);
+                            w[k] = (float)jw.v->num[(size_t)src * es + k];
+                        }
+                    }
+                    for (int k = 0; k < 4; ++k) { out.joint_indices.push_back(jix[k]); out.joint_weights.push_back(w[k]); }
+                }
+            }
+            poly.push_back(dedup[key]);
+        }
+        Submesh& sm = subs[face_sub[f] >= 0 ? face_sub[f] : rest_sub];
+        for (size_t k = 2; k < poly.size(); ++k) {
+            sm.indices.push_back(poly[0]);
+            sm.indices.push_back(poly[k - 1]);
+            sm.indices.push_back(poly[k]);
+        }
+    }
+    for (auto& sm : subs)
+        if (!sm.indices.empty()) out.submeshes.push_back(std::move(sm));
+    if (out.submeshes.empty()) { err = p.path + ": mesh without faces"; return false; }
+    if (!nrm.ok()) {   // addNormals(withAttributeNamed:creaseThreshold:) (Model.swift:136-138)
+        compute_vertex_normals(out);
+    }
+    return true;
+}
+
+}  // namespace usdscene
+
 static Light area_light_default() {  // Scene.setupLight (Scene.swift:161-169)
     Light l;
     std::memset(&l, 0, sizeof l);
@@ -734,6 +1266,80 @@ rt_status rt_scene_add_obj(rt_scene* s, const char* obj_path, const float positi
                 uint32_t id;
                 if (!sm.tex_path[k].empty() && load_png_file(s, sm.tex_path[k], &id) == RT_OK) bind_slot(sm, k, id);
             }
+    s->err.clear();
+    finish_model(s, std::move(model), ov);
+    return RT_OK;
+}
+
+rt_status rt_scene_add_usd(rt_scene* s, const char* path, const float position[3], const float rotation[3], float scale,
+                           const rt_material_override* ov) {
+    if (!s || !path || !position) return RT_ERR_INVALID_ARG;
+    usd::Stage st;
+    std::vector<usd::PackageFile> files;
+    std::string err;
+    if (!usd::load_stage(path, st, files, err)) {
+        s->err = std::string(path) + ": " + err;
+        return RT_ERR_IO;
+    }
+    Model model;
+    model.name = path;
+    for (int k = 0; k < 3; ++k) { model.position[k] = position[k]; model.rotation[k] = rotation ? rotation[k] : 0.0f; }
+    model.scale = scale;
+    // traverseAndFind (Model.swift:99-121): every MDLSkeleton / MDLPackedJointAnimation met on the
+    // depth-first walk replaces the previous one, so the last of each wins
+    std::vector<int> meshes;
+    int skel = -1, anim = -1;
+    std::function<void(int)> walk = [&](int k) {
+        const usd::Prim& p = st.prims[k];
+        if (!p.active) return;
+        if (p.type == "Skeleton") skel = k;
+        if (p.type == "SkelAnimation") anim = k;
+        if (p.type == "Mesh") meshes.push_back(k);
+        for (int c : p.children) walk(c);
+    };
+    walk(0);
+    if (anim < 0 && skel >= 0) anim = usdscene::find_prim_up(st, skel, "skel:animationSource");
+    std::shared_ptr<UsdSkel> sk;
+    if (skel >= 0) {
+        sk = std::make_shared<UsdSkel>();
+        if (!usdscene::read_skeleton(st, st.prims[skel], anim >= 0 ? &st.prims[anim] : nullptr, *sk)) sk.reset();
+    }
+    const std::string dir = dir_of(path);
+    for (int id : meshes) {
+        Mesh m;
+        if (!usdscene::build_mesh(s, st, id, files, dir, m, err)) {
+            s->err = std::string(path) + ": " + err;
+            return RT_ERR_IO;
+        }
+        const usd::Prim& p = st.prims[id];
+        // MeshSkinningInfo (Model.swift:143-160): the mesh's joint order (skel:joints, else the
+        // skeleton's) mapped to skeleton indices; geometryBindTransform and its inverse
+        if (sk && !m.joint_indices.empty()) {
+            const usd::Value* jv = usdscene::attr_value(p, "skel:joints");
+            const std::vector<std::string>& jp = jv && jv->kind == usd::Value::kStr && !jv->str.empty() ? jv->str : sk->joint_paths;
+            const auto by_path = usdscene::path_index_map(sk->joint_paths);
+            const auto by_tail = usdscene::tail_index_map(sk->joint_paths);
+            for (const auto& j : jp) m.joint_to_skel.push_back(usdscene::map_joint(j, by_path, by_tail));
+            const usd::Value* gb = usdscene::attr_value(p, "primvars:skel:geomBindTransform");
+            m.geom_bind = gb && gb->num.size() == 16 ? usdscene::m4_from_usd(gb->num, 0) : m4_identity();
+            m.geom_bind_inv = usdscene::m4_inverse(m.geom_bind);
+            m.usd_skel = sk;
+            m.joint_count = (uint32_t)std::max<size_t>(1, m.joint_to_skel.size());
+            for (size_t v = 0; v < m.joint_indices.size(); ++v)
+                if (m.joint_indices[v] >= m.joint_count) {
+                    s->err = std::string(path) + ": " + p.path + ": joint index beyond the mesh's joints";
+                    return RT_ERR_IO;
+                }
+        } else {
+            m.joint_indices.clear();
+            m.joint_weights.clear();
+        }
+        model.meshes.push_back(std::move(m));
+    }
+    if (model.meshes.empty()) {
+        s->err = std::string(path) + ": no meshes";
+        return RT_ERR_IO;
+    }
     s->err.clear();
     finish_model(s, std::move(model), ov);
     return RT_OK;
@@ -848,8 +1454,13 @@ rt_status rt_scene_preset(const char* name_c, const char* asset_dir_c, rt_scene*
             st = base();
     } else if (name == "c5" || name == "app") {
         float rp[3] = {-0.5f, 0.0f, 1.0f};
-        synth = 1;
-        st = rt_scene_add_procedural(s, "robot", nullptr, rp, zero, 0.5f, nullptr);
+        const std::string robot = dir + "/robot.usdz";
+        if (!force_synth && file_exists(robot)) {   // AppScene.swift:15: robot, scale 0.01
+            st = rt_scene_add_usd(s, robot.c_str(), rp, zero, 0.01f, nullptr);
+        } else {
+            synth = 1;
+            st = rt_scene_add_procedural(s, "robot", nullptr, rp, zero, 0.5f, nullptr);
+        }
         if (!st && name == "app") {
             if (!(st = hero("dragon", &glass))) {
                 if (!(st = obj("train", -0.3f, 0.0f, 0.4f, 0.5f))) st = obj("treefir", 0.5f, 0.0f, -0.2f, 0.7f);
@@ -981,7 +1592,15 @@ rt_status rt_scene_joint_matrices(rt_scene* s, uint32_t mesh_index, double time_
     Mesh* mesh = nullptr;
     for (auto& model : s->models)
         for (auto& m : model.meshes) { if (k == mesh_index) mesh = &m; ++k; }
-    if (!mesh || !mesh->skin) { s->err = "mesh is not skinned"; return RT_ERR_INVALID_ARG; }
+    if (!mesh || (!mesh->skin && !mesh->usd_skel)) { s->err = "mesh is not skinned"; return RT_ERR_INVALID_ARG; }
+    if (mesh->usd_skel) {
+        std::vector<M4> jm;
+        usdscene::joint_matrices(*mesh, time_seconds, jm);
+        if (capacity < jm.size()) return RT_ERR_INVALID_ARG;
+        for (size_t j = 0; j < jm.size(); ++j) std::memcpy(out + 16 * j, jm[j].m, sizeof jm[j].m);
+        if (joint_count) *joint_count = (uint32_t)jm.size();
+        return RT_OK;
+    }
     Skin& sk = *mesh->skin;
     uint32_t J = (uint32_t)sk.parent.size();
     if (capacity < J) return RT_ERR_INVALID_ARG;

@@ -43,6 +43,7 @@ def _desc_with(rt, desc, mesh, positions=None, normals=None, transform=None):
         C.memmove(C.byref(md.transform), np.ascontiguousarray(transform, np.float32).ctypes.data, 48)
     d = A.SceneDesc()
     d.mesh_count, d.light_count, d.meshes, d.lights = desc.mesh_count, desc.light_count, arr, desc.lights
+    d.texture_count, d.textures = desc.texture_count, desc.textures
     d._keep = (arr, positions, normals)
     return d
 

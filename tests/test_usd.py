@@ -1,0 +1,365 @@
+"""USD ingest (the USDZ branch of Model.init, Model.swift:87-184, with its
+skeleton / animation, Model.swift:207-414, and SkinningPass.updateSkinningJointMatrices,
+SkinningPass.swift:124-157).
+
+One skinned test asset is described once in Python (tests/usd_writers.py) and written as a .usda
+text layer, a .usdc crate layer and .usdz packages of either (stored and deflated entries, with
+a PNG texture inside).  The scene the library builds must be the same from every encoding, match
+the asset's declared geometry / materials / skin streams, and its joint matrices must equal a
+numpy restatement of Model.update + updateSkinningJointMatrices.  The reference's own robot.usdz
+is absent from the snapshot (.MISSING_LARGE_BLOBS) and no USD library is in the image, so parity
+with Pixar's / ModelIO's readers is unpinned; these tests pin our reader against independent
+writers of the published encodings."""
+import ctypes as C
+import math
+import os
+import shutil
+
+import numpy as np
+import pytest
+
+import usd_writers as W
+
+I4 = ((1, 0, 0, 0), (0, 1, 0, 0), (0, 0, 1, 0), (0, 0, 0, 1))
+
+
+def T(x, y, z):
+    return ((1, 0, 0, 0), (0, 1, 0, 0), (0, 0, 1, 0), (x, y, z, 1))
+
+
+def robot_prims():
+    # column of 4 rings (y = 0..3) of a 0.4-wide square: 12 side quads, a top quad, two bottom tris
+    pts = [(sx * 0.2, float(k), sz * 0.2) for k in range(4) for (sx, sz) in ((-1, -1), (1, -1), (1, 1), (-1, 1))]
+    counts, idx = [], []
+    for k in range(3):
+        for e in range(4):
+            a, b = 4 * k + e, 4 * k + (e + 1) % 4
+            counts.append(4)
+            idx += [a, b, b + 4, a + 4]
+    counts.append(4)
+    idx += [12, 13, 14, 15]
+    counts += [3, 3]
+    idx += [0, 2, 1, 0, 3, 2]
+    P = np.array(pts)
+    normals = []
+    c = 0
+    for n in counts:   # flat face normals per corner (faceVarying)
+        f = [P[i] for i in idx[c:c + n]]
+        nv = np.cross(f[1] - f[0], f[2] - f[0])
+        nv = nv / np.linalg.norm(nv)
+        normals += [tuple(float(W.f32(x)) for x in nv)] * n
+        c += n
+    st = [(0.0, 0.0), (1.0, 0.0), (1.0, 1.0), (0.0, 1.0)]
+    st_idx = [i % 4 for i in range(len(idx))]
+    ji, jw = [], []
+    for k in range(4):   # elementSize 2 influences per point
+        j, w = [((0, 1), (1.0, 0.0)), ((0, 1), (0.5, 0.5)), ((1, 2), (0.25, 0.75)), ((2, 0), (1.0, 0.0))][k]
+        for _ in range(4):
+            ji += list(j)
+            jw += list(w)
+    qz = W.quat_from_axis_angle((0, 0, 1), math.radians(60))
+    qx = W.quat_from_axis_angle((1, 0, 0), math.radians(90))
+    tok = lambda s: ("token", s)
+    prims = [
+        dict(path="/Robot", type="SkelRoot", api=["SkelBindingAPI"]),
+        dict(path="/Robot/Skel", type="Skeleton", attrs=[
+            dict(name="joints", type="token[]", uniform=True, value=[tok("root"), tok("root/arm"), tok("root/arm/hand")]),
+            dict(name="bindTransforms", type="matrix4d[]", uniform=True, value=[I4, T(0, 1, 0), T(0, 2, 0)]),
+            dict(name="restTransforms", type="matrix4d[]", uniform=True, value=[I4, T(0, 1, 0), T(0, 1, 0)]),
+        ], rels={"skel:animationSource": ["/Robot/Skel/Anim"]}),
+        dict(path="/Robot/Skel/Anim", type="SkelAnimation", attrs=[
+            dict(name="joints", type="token[]", uniform=True, value=[tok("root/arm"), tok("root/arm/hand")]),
+            dict(name="translations", type="float3[]", samples={0: [(0, 1, 0), (0, 1, 0)], 48: [(0, 1, 0), (0, 1.5, 0)]}),
+            dict(name="rotations", type="quatf[]", samples={0: [(1, 0, 0, 0), (1, 0, 0, 0)], 48: [qz, qx]}),
+            dict(name="scales", type="half3[]", value=[(1, 1, 1), (1, 1, 0.5)]),
+        ]),
+        dict(path="/Robot/Body", type="Mesh", api=["SkelBindingAPI", "MaterialBindingAPI"], attrs=[
+            dict(name="faceVertexCounts", type="int[]", value=counts),
+            dict(name="faceVertexIndices", type="int[]", value=idx),
+            dict(name="points", type="point3f[]", value=pts),
+            dict(name="normals", type="normal3f[]", value=normals, interpolation="faceVarying"),
+            dict(name="primvars:st", type="texCoord2f[]", value=st, interpolation="faceVarying"),
+            dict(name="primvars:st:indices", type="int[]", value=st_idx),
+            dict(name="primvars:skel:jointIndices", type="int[]", value=ji, interpolation="vertex", element_size=2),
+            dict(name="primvars:skel:jointWeights", type="float[]", value=jw, interpolation="vertex", element_size=2),
+            dict(name="primvars:skel:geomBindTransform", type="matrix4d", value=T(0, 0.1, 0)),
+            dict(name="skel:joints", type="token[]", uniform=True, value=[tok("root"), tok("arm"), tok("root/arm/hand")]),
+        ], rels={"skel:skeleton": ["/Robot/Skel"], "material:binding": ["/Robot/Looks/Red"]}),
+        dict(path="/Robot/Body/top", type="GeomSubset", attrs=[
+            dict(name="elementType", type="token", uniform=True, value=tok("face")),
+            dict(name="familyName", type="token", uniform=True, value=tok("materialBind")),
+            dict(name="indices", type="int[]", value=[12]),
+        ], rels={"material:binding": ["/Robot/Looks/Tex"]}),
+        dict(path="/Robot/Prop", type="Mesh", attrs=[
+            dict(name="faceVertexCounts", type="int[]", value=[4, 3]),
+            dict(name="faceVertexIndices", type="int[]", value=[0, 1, 2, 3, 0, 1, 2]),
+            dict(name="points", type="point3f[]", value=[(1, 0, 0), (2, 0, 0), (2, 0, 1), (1, 0, 1)]),
+        ]),
+        dict(path="/Robot/Looks", type="Scope"),
+        dict(path="/Robot/Looks/Red", type="Material", attrs=[
+            dict(name="outputs:surface", type="token", connect=["/Robot/Looks/Red/PBR.outputs:surface"])]),
+        dict(path="/Robot/Looks/Red/PBR", type="Shader", attrs=[
+            dict(name="info:id", type="token", uniform=True, value=tok("UsdPreviewSurface")),
+            dict(name="inputs:diffuseColor", type="color3f", value=(0.8, 0.1, 0.1)),
+            dict(name="inputs:emissiveColor", type="color3f", value=(0, 0, 0)),
+            dict(name="inputs:specularColor", type="color3f", value=(0.5, 0.5, 0.5)),
+            dict(name="inputs:ior", type="float", value=1.3),
+            dict(name="inputs:opacity", type="float", value=0.9),
+            dict(name="outputs:surface", type="token")]),
+        dict(path="/Robot/Looks/Tex", type="Material", attrs=[
+            dict(name="outputs:surface", type="token", connect=["/Robot/Looks/Tex/PBR.outputs:surface"])]),
+        dict(path="/Robot/Looks/Tex/PBR", type="Shader", attrs=[
+            dict(name="info:id", type="token", uniform=True, value=tok("UsdPreviewSurface")),
+            dict(name="inputs:diffuseColor", type="color3f", connect=["/Robot/Looks/Tex/Img.outputs:rgb"]),
+            dict(name="inputs:emissiveColor", type="color3f", value=(0.2, 0.3, 0.4)),
+            dict(name="outputs:surface", type="token")]),
+        dict(path="/Robot/Looks/Tex/Img", type="Shader", attrs=[
+            dict(name="info:id", type="token", uniform=True, value=tok("UsdUVTexture")),
+            dict(name="inputs:file", type="asset", value=("asset", "textures/tex.png")),
+            dict(name="outputs:rgb", type="float3")]),
+    ]
+    return prims, dict(pts=pts, counts=counts, idx=idx, normals=normals, st=st, st_idx=st_idx, ji=ji, jw=jw)
+
+
+TEX = W.png_rgba(2, 2, [255, 0, 0, 255, 0, 255, 0, 255, 0, 0, 255, 255, 255, 255, 255, 255])
+
+
+@pytest.fixture(scope="module")
+def files(tmp_path_factory):
+    d = tmp_path_factory.mktemp("usd")
+    prims, _ = robot_prims()
+    usda, usdc = W.write_usda(prims), W.write_usdc(prims)
+    out = {}
+    for name, data in [("robot.usda", usda), ("robot.usdc", usdc),
+                       ("robot_c.usdz", W.write_usdz("robot.usdc", usdc, [("textures/tex.png", TEX)])),
+                       ("robot_a.usdz", W.write_usdz("robot.usda", usda, [("textures/tex.png", TEX)], deflate=True))]:
+        (d / name).write_bytes(data)
+        out[name] = str(d / name)
+    os.makedirs(d / "textures", exist_ok=True)
+    (d / "textures" / "tex.png").write_bytes(TEX)   # bare layers resolve the texture next to them
+    return out
+
+
+def _scene(rt, path):
+    s = rt.Scene()
+    s.add_usd(path, (0.0, 0.0, 0.0))
+    return s
+
+
+def _mesh_arrays(desc, m):
+    md = desc.meshes[m]
+    n = md.vertex_count
+    f4 = lambda p: np.ctypeslib.as_array(C.cast(p, C.POINTER(C.c_float)), shape=(n, 4)).copy()
+    out = dict(pos=f4(md.positions), nrm=f4(md.normals), joints=md.joint_count,
+               uv=np.ctypeslib.as_array(C.cast(md.uvs, C.POINTER(C.c_float)), shape=(n, 2)).copy() if md.uvs else None)
+    if md.joint_count:
+        out["ji"] = np.ctypeslib.as_array(md.joint_indices, shape=(n, 4)).copy()
+        out["jw"] = np.ctypeslib.as_array(md.joint_weights, shape=(n, 4)).copy()
+    subs = []
+    for k in range(md.submesh_count):
+        sm = md.submeshes[k]
+        subs.append(dict(idx=np.ctypeslib.as_array(sm.indices, shape=(sm.index_count,)).copy(), mat=bytes(sm.material),
+                         tex=list(sm.textures)))
+    out["subs"] = subs
+    return out
+
+
+def test_usda_scene_matches_the_asset(rt, files):
+    _, A = robot_prims()
+    s = _scene(rt, files["robot.usda"])
+    desc = s.desc()
+    assert desc.mesh_count == 2
+    body = _mesh_arrays(desc, 0)
+    # faceVarying normals: every corner is its own vertex, in corner order
+    ncorner = len(A["idx"])
+    assert body["pos"].shape[0] == ncorner
+    np.testing.assert_array_equal(body["pos"][:, :3], np.array(A["pts"], np.float32)[A["idx"]])
+    np.testing.assert_array_equal(body["nrm"][:, :3], np.array(A["normals"], np.float32))
+    np.testing.assert_array_equal(body["uv"], np.array(A["st"], np.float32)[A["st_idx"]])
+    # skin streams: the point's two influences, then zeros
+    ji = np.array(A["ji"]).reshape(-1, 2)[A["idx"]]
+    jw = np.array(A["jw"], np.float32).reshape(-1, 2)[A["idx"]]
+    assert body["joints"] == 3
+    np.testing.assert_array_equal(body["ji"][:, :2], ji)
+    np.testing.assert_array_equal(body["ji"][:, 2:], 0)
+    np.testing.assert_array_equal(body["jw"][:, :2], jw)
+    # submesh 0 = the GeomSubset (face 12, the top quad), submesh 1 = the rest
+    assert len(body["subs"]) == 2
+    c0 = sum(A["counts"][:12])
+    np.testing.assert_array_equal(body["subs"][0]["idx"], [c0, c0 + 1, c0 + 2, c0, c0 + 2, c0 + 3])
+    tris = sum(n - 2 for n in A["counts"])
+    assert len(body["subs"][1]["idx"]) == 3 * (tris - 2)
+    from importlib import import_module
+    Mt = import_module("metal4-raytracing_amd._abi").Material
+    red = Mt.from_buffer_copy(body["subs"][1]["mat"])
+    assert (red.baseColor.x, red.baseColor.y, red.baseColor.z) == (W.f32(0.8), W.f32(0.1), W.f32(0.1))
+    assert (red.specular.x, red.refractionIndex, red.opacity) == (0.5, W.f32(1.3), W.f32(0.9))
+    assert red.textureFlags == 0
+    tex = Mt.from_buffer_copy(body["subs"][0]["mat"])
+    assert tex.textureFlags == 1 and (tex.baseColor.x, tex.baseColor.y, tex.baseColor.z) == (1.0, 1.0, 1.0)
+    assert (tex.emission.x, tex.emission.y, tex.emission.z) == (W.f32(0.2), W.f32(0.3), W.f32(0.4))
+    assert tex.refractionIndex == 1.0 and tex.opacity == 1.0   # Material(material:) defaults
+    assert desc.texture_count == 1 and body["subs"][0]["tex"][0] == 0
+    t = desc.textures[0]
+    assert (t.width, t.height) == (2, 2)
+    assert bytes(np.ctypeslib.as_array(C.cast(t.rgba8, C.POINTER(C.c_uint8)), shape=(16,))) == bytes([255, 0, 0, 255, 0, 255, 0, 255, 0, 0, 255, 255, 255, 255, 255, 255])
+    # the prop: 4 shared points, no normals authored -> computed unit normals (+-y), no skin
+    prop = _mesh_arrays(desc, 1)
+    assert prop["pos"].shape[0] == 4 and prop["joints"] == 0
+    np.testing.assert_allclose(np.abs(prop["nrm"][:, 1]), 1.0, rtol=1e-6)
+    assert s.triangle_count == tris + 3
+
+
+@pytest.mark.parametrize("name", ["robot.usdc", "robot_c.usdz", "robot_a.usdz"])
+def test_every_encoding_builds_the_same_scene(rt, files, name):
+    ref = _scene(rt, files["robot.usda"])
+    got = _scene(rt, files[name])
+    d0, d1 = ref.desc(), got.desc()
+    assert d0.mesh_count == d1.mesh_count
+    for m in range(d0.mesh_count):
+        a, b = _mesh_arrays(d0, m), _mesh_arrays(d1, m)
+        for k in ("pos", "nrm", "uv", "ji", "jw"):
+            if a.get(k) is None:
+                assert b.get(k) is None
+            else:
+                np.testing.assert_array_equal(a[k], b[k], err_msg=f"{name} mesh {m} {k}")
+        assert a["joints"] == b["joints"]
+        assert [(list(x["idx"]), x["mat"], x["tex"]) for x in a["subs"]] == [(list(x["idx"]), x["mat"], x["tex"]) for x in b["subs"]]
+    assert d0.texture_count == d1.texture_count
+    for t in (0.0, 0.7, 1.9, 2.6):
+        np.testing.assert_array_equal(ref.joint_matrices(0, t), got.joint_matrices(0, t))
+
+
+# ---- Model.update + SkinningPass.updateSkinningJointMatrices, restated in numpy -----------------
+def _quat_mat(q):   # (x, y, z, w) -> simd_matrix4x4 columns as a 4x4 column-major array
+    x, y, z, w = q
+    M = np.eye(4)
+    M[0, 0], M[1, 0], M[2, 0] = w * w + x * x - y * y - z * z, 2 * (x * y + z * w), 2 * (x * z - y * w)
+    M[0, 1], M[1, 1], M[2, 1] = 2 * (x * y - z * w), w * w - x * x + y * y - z * z, 2 * (y * z + x * w)
+    M[0, 2], M[1, 2], M[2, 2] = 2 * (z * x + y * w), 2 * (y * z - x * w), w * w - x * x - y * y + z * z
+    return M
+
+
+def _slerp(a, b, u):
+    a, b = np.array(a, float), np.array(b, float)
+    d = a @ b
+    if d < 0:
+        b, d = -b, -d
+    if d > 0.9995:
+        r = a * (1 - u) + b * u
+    else:
+        th = math.acos(d)
+        r = (math.sin((1 - u) * th) * a + math.sin(u * th) * b) / math.sin(th)
+    return r / np.linalg.norm(r)
+
+
+def _usd_mat(m):   # USD rows = simd columns
+    return np.array(m, float).T
+
+
+def expected_joint_matrices(t):
+    """Model.swift:207-261 and SkinningPass.swift:124-157 for the test asset at time t (s)."""
+    dur = 2.0                                       # keys at time codes 0 and 48, 24 per second
+    ct = math.fmod(t, dur)
+    u = min(max(ct / 2.0, 0.0), 1.0)
+    qz = W.quat_from_axis_angle((0, 0, 1), math.radians(60))
+    qx = W.quat_from_axis_angle((1, 0, 0), math.radians(90))
+    wxyz = [_slerp((1, 0, 0, 0), qz, u), _slerp((1, 0, 0, 0), qx, u)]
+    tr = [np.array([0, 1, 0]), np.array([0, 1, 0]) * (1 - u) + np.array([0, 1.5, 0]) * u]
+    sc = [np.array([1, 1, 1]), np.array([1, 1, 0.5])]
+    rest = [np.eye(4), _usd_mat(T(0, 1, 0)), _usd_mat(T(0, 1, 0))]
+    local = list(rest)
+    for i, j in enumerate((1, 2)):                  # animation joints root/arm, root/arm/hand
+        w, x, y, z = wxyz[i]
+        q = np.array([x, y, z, w]) / math.sqrt(w * w + x * x + y * y + z * z)
+        Tm = np.eye(4)
+        Tm[:3, 3] = tr[i]
+        local[j] = Tm @ _quat_mat(q) @ np.diag([*sc[i], 1.0])
+    glob = [local[0]]
+    glob.append(glob[0] @ local[1])
+    glob.append(glob[1] @ local[2])
+    inv_bind = [np.linalg.inv(_usd_mat(b)) for b in (I4, T(0, 1, 0), T(0, 2, 0))]
+    skin = [glob[j] @ inv_bind[j] for j in range(3)]
+    gb = _usd_mat(T(0, 0.1, 0))
+    return np.stack([np.linalg.inv(gb) @ skin[k] @ gb for k in (0, 1, 2)])   # mesh joints root, arm, hand
+
+
+@pytest.mark.parametrize("t", [0.0, 0.5, 1.0, 1.75, 2.5, 3.99])
+def test_joint_matrices_follow_model_update(rt, files, t):
+    s = _scene(rt, files["robot_c.usdz"])
+    got = s.joint_matrices(0, t).reshape(-1, 4, 4).transpose(0, 2, 1)   # column-major -> rows
+    np.testing.assert_allclose(got, expected_joint_matrices(t), rtol=2e-5, atol=2e-6)
+
+
+def test_joint_matrices_skin_the_rest_pose_at_bind(rt, files):
+    """At t = 0 the root and arm are in their rest pose = bind pose (identity joint matrices); the
+    hand's constant 0.5 z scale shows up as diag(1, 1, 0.5) around its bind point."""
+    s = _scene(rt, files["robot.usda"])
+    J = s.joint_matrices(0, 0.0).reshape(-1, 4, 4).transpose(0, 2, 1)
+    np.testing.assert_allclose(J[:2], np.broadcast_to(np.eye(4), (2, 4, 4)), atol=1e-6)
+    np.testing.assert_allclose(J[2][:3, :3], np.diag([1.0, 1.0, 0.5]), atol=1e-6)
+
+
+def test_usd_errors(rt, files, tmp_path):
+    s = rt.Scene()
+    with pytest.raises(rt.RTError, match="cannot open"):
+        s.add_usd(str(tmp_path / "missing.usdz"), (0, 0, 0))
+    bad = tmp_path / "bad.usda"
+    bad.write_text('#usda 1.0\ndef Mesh "m" {\n  int[] faceVertexCounts = [3\n}\n')
+    with pytest.raises(rt.RTError, match="usda line"):
+        s.add_usd(str(bad), (0, 0, 0))
+    data = open(files["robot.usdc"], "rb").read()
+    trunc = tmp_path / "trunc.usdc"
+    trunc.write_bytes(data[: len(data) // 2])
+    with pytest.raises(rt.RTError, match="usdc"):
+        s.add_usd(str(trunc), (0, 0, 0))
+    noise = tmp_path / "x.usd"
+    noise.write_bytes(b"not usd at all")
+    with pytest.raises(rt.RTError, match="not a USD layer"):
+        s.add_usd(str(noise), (0, 0, 0))
+    empty = tmp_path / "empty.usda"
+    empty.write_text('#usda 1.0\ndef Xform "x" {\n}\n')
+    with pytest.raises(rt.RTError, match="no meshes"):
+        s.add_usd(str(empty), (0, 0, 0))
+    assert s.triangle_count == 0
+
+
+def test_lz4_and_integer_coding_round_trips(rt, files, tmp_path):
+    """Long runs (LZ4 matches longer than 19 bytes, literal runs longer than 15) and large integer
+    deltas (all four integer codes) through the crate path."""
+    n = 5000
+    pts = [(float(i % 7), float(i // 7) * 0.001, 123456.0 if i % 1000 == 0 else 0.0) for i in range(n)]
+    counts = [3] * (n // 3)
+    idx = list(range(3 * (n // 3)))
+    idx[5] = 4000   # a large jump: medium / large delta codes
+    prims = [dict(path="/M", type="Mesh", attrs=[
+        dict(name="faceVertexCounts", type="int[]", value=counts),
+        dict(name="faceVertexIndices", type="int[]", value=idx),
+        dict(name="points", type="point3f[]", value=pts)])]
+    p = tmp_path / "big.usdc"
+    p.write_bytes(W.write_usdc(prims))
+    a = tmp_path / "big.usda"
+    a.write_bytes(W.write_usda(prims))
+    s1, s2 = _scene(rt, str(p)), _scene(rt, str(a))   # the descriptors point into the scenes
+    d1, d2 = s1.desc(), s2.desc()
+    m1, m2 = _mesh_arrays(d1, 0), _mesh_arrays(d2, 0)
+    np.testing.assert_array_equal(m1["pos"], m2["pos"])
+    np.testing.assert_array_equal(m1["subs"][0]["idx"], m2["subs"][0]["idx"])
+    assert m1["pos"].shape[0] == len(set(idx))
+
+
+def test_preset_c5_loads_a_real_robot_usdz(rt, assets, files, tmp_path):
+    """A robot.usdz in the asset directory replaces the procedural stand-in at AppScene's robot
+    slot (AppScene.swift:15, scale 0.01), like dragon.obj / bunny.obj do for theirs."""
+    for f in os.listdir(assets):
+        shutil.copy(os.path.join(assets, f), tmp_path / f)
+    shutil.copy(files["robot_c.usdz"], tmp_path / "robot.usdz")
+    s = rt.Scene.preset("c5", str(tmp_path))
+    assert not s.synthetic
+    d = s.desc()
+    assert d.meshes[0].joint_count == 3 and d.meshes[1].joint_count == 0
+    M = np.frombuffer(bytes(d.meshes[0].transform), np.float32).reshape(4, 3)
+    np.testing.assert_allclose(M[:3], np.eye(3) * 0.01, atol=1e-9)
+    np.testing.assert_allclose(M[3], [-0.5, 0.0, 1.0])
+    s2 = rt.Scene.preset("c5_synthetic", str(tmp_path))
+    assert s2.synthetic
