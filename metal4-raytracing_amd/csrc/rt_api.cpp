@@ -215,11 +215,14 @@ static std::vector<HaltonDim> halton_table() {
 
 // SAH build + 8-wide collapse whose group-stack depth fits the kStackSize LDS stack: the binned-SAH
 // builder falls back to median splits past its depth limit, so tighter limits bound the depth.
+// RT_BVH_COLLAPSE=greedy selects round 1's collapse (largest child opened first) for A/B runs.
 static bool build_bvh8_fit(const float* world, uint32_t n, BvhResult& b2, Bvh8Result& b8) {
+    static const bool greedy = getenv("RT_BVH_COLLAPSE") && !std::strcmp(getenv("RT_BVH_COLLAPSE"), "greedy");
+    static const float c_prim = getenv("RT_BVH_CPRIM") ? (float)atof(getenv("RT_BVH_CPRIM")) : 0.5f;
     for (int limit : {64, 48, 40, 32, 28, 24, 21}) {
-        static const int leaf = getenv("RT_BVH_LEAF") ? std::max(1, std::min(4, atoi(getenv("RT_BVH_LEAF")))) : 4;
+        static const int leaf = getenv("RT_BVH_LEAF") ? std::max(1, std::min(4, atoi(getenv("RT_BVH_LEAF")))) : (greedy ? 4 : 1);
         b2 = build_bvh2(world, n, leaf, limit);
-        b8 = collapse_bvh8(b2);
+        b8 = greedy ? collapse_bvh8(b2) : collapse_bvh8_dp(b2, 1.0f, c_prim);
         if (b8.max_depth <= kStackSize) return true;
     }
     return false;

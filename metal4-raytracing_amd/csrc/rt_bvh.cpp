@@ -3,6 +3,7 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <functional>
 #include <cmath>
 #include <cstring>
 
@@ -330,17 +331,40 @@ void quantize_bvh8_node(Bvh8Node& nd, const float clo[8][3], const float chi[8][
     }
 }
 
+namespace {
+struct Job { int b2node; uint32_t b8node; int depth; };
+
+// One 8-wide node from its child items (internal children are queued as new jobs).
+void emit_bvh8_node(const BvhResult& b2, const Job& job, std::vector<WItem>& items, std::vector<Job>& queue,
+                    Bvh8Result& out);
+
+// Subtree triangle range [start, start + count) of every BVH2 internal node: the builder
+// partitions index ranges, so a subtree's triangles are contiguous in tri_order.
+struct Range { uint32_t start, count; };
+std::vector<Range> subtree_ranges(const BvhResult& b2) {
+    std::vector<Range> r(b2.nodes.size(), Range{0xffffffffu, 0u});
+    for (int k = (int)b2.nodes.size() - 1; k >= 0; --k) {   // children after parents (pre-order)
+        const Bvh2Node& n = b2.nodes[k];
+        for (int s = 0; s < 2; ++s) {
+            if (n.child[s] < 0 && n.count[s] == 0) continue;
+            const Range c = n.child[s] < 0 ? Range{(uint32_t)~n.child[s], (uint32_t)n.count[s]} : r[n.child[s]];
+            r[k].start = std::min(r[k].start, c.start);
+            r[k].count += c.count;
+        }
+    }
+    return r;
+}
+}  // namespace
+
 Bvh8Result collapse_bvh8(const BvhResult& b2) {
     Bvh8Result out;
     out.pad = b2.pad;
-    struct Job { int b2node; uint32_t b8node; int depth; };
     std::vector<Job> queue;
     out.nodes.emplace_back();
     out.parent.push_back(-1);
     queue.push_back({0, 0u, 0});
     for (size_t qi = 0; qi < queue.size(); ++qi) {
         Job job = queue[qi];
-        out.max_depth = std::max(out.max_depth, job.depth + 1);
         std::vector<WItem> items;
         bvh2_children(b2, job.b2node, items);
         while (items.size() < 8) {
@@ -355,6 +379,159 @@ Bvh8Result collapse_bvh8(const BvhResult& b2) {
             items.erase(items.begin() + best);
             items.insert(items.end(), kids.begin(), kids.end());
         }
+        emit_bvh8_node(b2, job, items, queue, out);
+    }
+    out.node_box.resize(6 * out.nodes.size());
+    return out;
+}
+
+// SAH-optimal 8-wide collapse (after Ylitie, Karras, Laine, "Efficient Incoherent Ray Traversal
+// on GPUs Through Compressed Wide BVHs", HPG 2017, §4): dynamic programming over the BVH2 for
+// the cheapest way to represent every subtree with at most i (1..8) slots of its parent, a slot
+// being a leaf (<= 4 triangles, the meta field's limit) or an 8-wide child node:
+//   C(n, 1)  = min(A(n) * c_prim * tris(n)  [tris(n) <= 4],  A(n) * c_node + D(n, 8))
+//   C(n, i)  = min(C(n, i - 1), D(n, i)),   D(n, j) = min_k C(l, k) + C(r, j - k)
+// The greedy collapse (open the largest child until 8) leaves the bottom of the tree in nodes
+// with two used slots (C3g: 47 % of its nodes) whose box tests are mostly spent on empty slots.
+Bvh8Result collapse_bvh8_dp(const BvhResult& b2, float c_node, float c_prim) {
+    // DP nodes: BVH2 internal nodes keep their index; leaf slots are appended
+    struct DN { float area; uint32_t start, count; int kid[2]; bool leaf; WItem item; };
+    const size_t ni = b2.nodes.size();
+    std::vector<DN> dn(ni);
+    const std::vector<Range> ranges = subtree_ranges(b2);
+    for (size_t k = 0; k < ni; ++k) {
+        dn[k].leaf = false;
+        dn[k].start = ranges[k].start;
+        dn[k].count = ranges[k].count;
+    }
+    for (size_t k = 0; k < ni; ++k) {
+        std::vector<WItem> kids;
+        bvh2_children(b2, (int)k, kids);
+        dn[k].kid[0] = dn[k].kid[1] = -1;
+        for (size_t s = 0; s < kids.size(); ++s) {
+            int id;
+            if (kids[s].leaf) {
+                DN l;
+                l.leaf = true;
+                l.start = kids[s].start;
+                l.count = kids[s].count;
+                l.kid[0] = l.kid[1] = -1;
+                l.item = kids[s];
+                l.area = item_area(kids[s]);
+                dn.push_back(l);
+                id = (int)dn.size() - 1;
+            } else {
+                id = kids[s].node;
+                dn[id].item = kids[s];
+                dn[id].area = item_area(kids[s]);
+            }
+            dn[k].kid[s] = id;
+        }
+    }
+    {   // the root's box: the union of its slots
+        WItem r;
+        for (int a = 0; a < 3; ++a) { r.lo[a] = INFINITY; r.hi[a] = -INFINITY; }
+        for (int s = 0; s < 2; ++s) {
+            const int c = dn[0].kid[s];
+            if (c < 0) continue;
+            for (int a = 0; a < 3; ++a) { r.lo[a] = std::min(r.lo[a], dn[c].item.lo[a]); r.hi[a] = std::max(r.hi[a], dn[c].item.hi[a]); }
+        }
+        r.leaf = false;
+        r.node = 0;
+        dn[0].item = r;
+        dn[0].area = item_area(r);
+    }
+    const size_t nd = dn.size();
+    std::vector<float> C(nd * 9, INFINITY);           // C(n, i), i = 1..8
+    std::vector<int8_t> choice(nd * 9, 0);            // i = 1: 1 leaf / 2 node; i >= 2: 0 = C(n, i-1), k = split
+    std::vector<int8_t> split8(nd, 1);                // best k of D(n, 8) (the node's own slots)
+    constexpr uint32_t kLeafMax = 4;
+    auto cost_of = [&](int id) {
+        DN& n = dn[id];
+        const float leaf = n.count <= kLeafMax ? n.area * c_prim * (float)n.count : INFINITY;
+        if (n.leaf) {
+            for (int i = 1; i <= 8; ++i) { C[id * 9 + i] = leaf; choice[id * 9 + i] = 1; }
+            return;
+        }
+        float D[9];
+        int8_t K[9];
+        for (int j = 2; j <= 8; ++j) {
+            D[j] = INFINITY;
+            K[j] = 1;
+            const int l = n.kid[0], r = n.kid[1];
+            if (l < 0 || r < 0) {   // one-child node: the child alone
+                const int c = l >= 0 ? l : r;
+                D[j] = C[c * 9 + j - 1];
+                K[j] = (int8_t)(j - 1);
+                continue;
+            }
+            for (int k = 1; k < j; ++k) {
+                const float v = C[l * 9 + k] + C[r * 9 + j - k];
+                if (v < D[j]) { D[j] = v; K[j] = (int8_t)k; }
+            }
+        }
+        const float node = n.area * c_node + D[8];
+        split8[id] = K[8];
+        C[id * 9 + 1] = std::min(leaf, node);
+        choice[id * 9 + 1] = leaf <= node ? 1 : 2;
+        for (int i = 2; i <= 8; ++i) {
+            if (D[i] < C[id * 9 + i - 1]) { C[id * 9 + i] = D[i]; choice[id * 9 + i] = K[i]; }
+            else { C[id * 9 + i] = C[id * 9 + i - 1]; choice[id * 9 + i] = 0; }
+        }
+    };
+    for (size_t id = ni; id < nd; ++id) cost_of((int)id);          // leaves
+    for (int id = (int)ni - 1; id >= 0; --id) cost_of(id);        // internal, children first
+    // slots of subtree `id` with budget j
+    std::function<void(int, int, std::vector<WItem>&)> expand = [&](int id, int j, std::vector<WItem>& items) {
+        const DN& n = dn[id];
+        while (j >= 2 && choice[id * 9 + j] == 0) --j;
+        if (j >= 2 && !n.leaf) {
+            const int k = choice[id * 9 + j];
+            const int l = n.kid[0], r = n.kid[1];
+            if (l < 0 || r < 0) { expand(l >= 0 ? l : r, j - 1 > 0 ? j - 1 : 1, items); return; }
+            expand(l, k, items);
+            expand(r, j - k, items);
+            return;
+        }
+        WItem it = n.item;
+        if (n.leaf || choice[id * 9 + 1] == 1) {   // a leaf slot over the subtree's triangles
+            it.leaf = true;
+            it.node = -1;
+            it.start = n.start;
+            it.count = n.count;
+        } else {
+            it.leaf = false;
+            it.node = id;
+        }
+        items.push_back(it);
+    };
+    Bvh8Result out;
+    out.pad = b2.pad;
+    std::vector<Job> queue;
+    out.nodes.emplace_back();
+    out.parent.push_back(-1);
+    queue.push_back({0, 0u, 0});
+    for (size_t qi = 0; qi < queue.size(); ++qi) {
+        const Job job = queue[qi];
+        std::vector<WItem> items;
+        const DN& n = dn[job.b2node];
+        if (n.kid[0] >= 0 && n.kid[1] >= 0) {
+            const int k = split8[job.b2node];
+            expand(n.kid[0], k, items);
+            expand(n.kid[1], 8 - k, items);
+        } else {
+            bvh2_children(b2, job.b2node, items);
+        }
+        emit_bvh8_node(b2, job, items, queue, out);
+    }
+    out.node_box.resize(6 * out.nodes.size());
+    return out;
+}
+
+namespace {
+void emit_bvh8_node(const BvhResult& b2, const Job& job, std::vector<WItem>& items, std::vector<Job>& queue,
+                    Bvh8Result& out) {
+        out.max_depth = std::max(out.max_depth, job.depth + 1);
         // slot order: centroid along the longest axis of the node box
         float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
         for (auto& it : items)
@@ -402,9 +579,7 @@ Bvh8Result collapse_bvh8(const BvhResult& b2) {
             out.node_box[6 * job.b8node + a] = lo[a];
             out.node_box[6 * job.b8node + 3 + a] = hi[a];
         }
-    }
-    out.node_box.resize(6 * out.nodes.size());
-    return out;
 }
+}  // namespace
 
 }  // namespace rt

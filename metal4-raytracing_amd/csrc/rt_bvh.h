@@ -68,6 +68,11 @@ struct Bvh8Result {
 // with the largest surface area until a node has 8 children).
 Bvh8Result collapse_bvh8(const BvhResult& b2);
 
+// SAH-optimal collapse by dynamic programming over the BVH2 (Ylitie et al. 2017): every node
+// slot is a leaf of <= 4 triangles or a child node, chosen to minimise
+// sum(A(node) * c_node) + sum(A(leaf) * c_prim * triangles).  Best on a BVH2 with 1-triangle leaves.
+Bvh8Result collapse_bvh8_dp(const BvhResult& b2, float c_node, float c_prim);
+
 // Re-quantize node n from its children's boxes (children: node_box of internal children, leaf
 // triangle bounds from tri_verts in BVH8 triangle order, padded).  Host mirror of the refit kernel.
 void quantize_bvh8_node(Bvh8Node& node, const float child_lo[8][3], const float child_hi[8][3], const bool used[8]);
