@@ -728,6 +728,12 @@ rt_status rt_bvh_build_device(rt_ctx* c) {
     if ((st = dev_alloc(c, c->d_maxabs, 4))) return st;
     if (!c->h_lbvh) HIPC(c, hipHostMalloc((void**)&c->h_lbvh, 16, 0));
     LbvhInput in{(const float4*)g.pos.p, (const uint4*)c->d_tri_info.p, (const float*)g.inst.p, n};
+    // PLOC topology + SAH-DP collapse by default; RT_DEVICE_BVH=lbvh / RT_DEVICE_COLLAPSE=greedy
+    // select round 1's radix tree / greedy collapse (A/B runs)
+    static const bool lbvh_tree = getenv("RT_DEVICE_BVH") && !std::strcmp(getenv("RT_DEVICE_BVH"), "lbvh");
+    static const bool greedy = getenv("RT_DEVICE_COLLAPSE") && !std::strcmp(getenv("RT_DEVICE_COLLAPSE"), "greedy");
+    in.ploc = lbvh_tree ? 0 : 1;
+    in.dp = greedy ? 0 : 1;
     LbvhOutput out{(Bvh8Node*)g.nodes.p, (float*)g.node_box.p, (uint32_t*)c->d_slot_to_tri.p,
                    (uint16_t*)g.tri_bin.p, (uint32_t*)c->d_levels.p, c->h_lbvh};
     LbvhResult res;

@@ -184,6 +184,10 @@ struct LbvhInput {
     const uint4* tri_info;
     const float* inst;
     uint32_t n;
+    int ploc = 1;          // BVH2 topology: 1 = PLOC clustering, 0 = LBVH radix tree
+    int dp = 1;            // 8-wide collapse: 1 = SAH dynamic programming, 0 = greedy
+    float c_node = 1.0f;   // DP costs (as the host builder's)
+    float c_prim = 0.5f;
 };
 struct LbvhOutput {
     Bvh8Node* nodes8;

@@ -276,6 +276,277 @@ __global__ void __launch_bounds__(kThreads) lbvh_boxes_up_k(const unsigned long 
     }
 }
 
+// ---- 4b. PLOC (Meister, Bittner, "Parallel Locally-Ordered Clustering for Bounding Volume
+// Hierarchy Construction", TVCG 2018): clusters start as the Morton-sorted triangles; every round
+// each cluster finds the neighbour within +-kPlocR (in the current order) whose merged box has the
+// smallest surface area, mutual nearest neighbours merge into a new inner node (at the lower
+// position), and the survivors are compacted in order.  The globally cheapest neighbour pair is
+// always mutual (ties go to the smaller index), so every round makes progress.
+constexpr int kPlocR = 16;
+
+__device__ __forceinline__ float area6(const float* a, const float* b) {
+    const float d0 = fmaxf(a[3], b[3]) - fminf(a[0], b[0]);
+    const float d1 = fmaxf(a[4], b[4]) - fminf(a[1], b[1]);
+    const float d2 = fmaxf(a[5], b[5]) - fminf(a[2], b[2]);
+    return 2.0f * (d0 * d1 + d1 * d2 + d2 * d0);
+}
+
+__global__ void __launch_bounds__(kThreads) ploc_init_k(const unsigned long long* keys, const float* tri_box, uint32_t n,
+                                                        int* cref, float* cbox, uint32_t* m0) {
+    const uint32_t i = blockIdx.x * kThreads + threadIdx.x;
+    if (i == 0) *m0 = n;   // the first round's cluster count
+    if (i >= n) return;
+    cref[i] = ~(int)i;   // leaf at sorted position i
+    const uint32_t t = (uint32_t)keys[i];
+    for (int k = 0; k < 6; ++k) cbox[6 * (size_t)i + k] = tri_box[6 * (size_t)t + k];
+}
+
+// The round's cluster count comes from device memory (the previous round's scan): the host
+// launches rounds in batches with grids sized by its last known count and reads the count back
+// once per batch.
+__global__ void __launch_bounds__(kThreads) ploc_nn_k(const float* cbox, const uint32_t* mp, int* nn) {
+    const uint32_t m = *mp;
+    if (blockIdx.x * kThreads >= m) return;
+    __shared__ float sb[(kThreads + 2 * kPlocR) * 6];
+    const int base = (int)(blockIdx.x * kThreads) - kPlocR;
+    for (int t = threadIdx.x; t < kThreads + 2 * kPlocR; t += kThreads) {
+        const int g = base + t;
+        for (int k = 0; k < 6; ++k) sb[t * 6 + k] = (g >= 0 && g < (int)m) ? cbox[6 * (size_t)g + k] : 0.0f;
+    }
+    __syncthreads();
+    const int i = (int)(blockIdx.x * kThreads + threadIdx.x);
+    if (i >= (int)m) return;
+    const float* bi = &sb[(threadIdx.x + kPlocR) * 6];
+    float best = INFINITY;
+    int bj = -1;
+    for (int d = -kPlocR; d <= kPlocR; ++d) {   // ascending index: ties keep the smaller one
+        const int j = i + d;
+        if (d == 0 || j < 0 || j >= (int)m) continue;
+        const float a = area6(bi, &sb[(threadIdx.x + kPlocR + d) * 6]);
+        if (a < best) {
+            best = a;
+            bj = j;
+        }
+    }
+    nn[i] = bj;
+}
+
+// mutual pairs merge into a new inner node at the lower position; keep[i] = cluster i survives
+struct PlocMerge {
+    const int* nn;
+    const int* cref;
+    const float* cbox;
+    int* tref;          // this round's clusters before compaction
+    float* tbox;
+    uint32_t* keep;
+    int* child;
+    int* parent;
+    int* leaf_parent;
+    uint32_t* count;    // triangles under each inner node
+    float* node_box;
+    uint32_t* node_ctr;
+    uint32_t* err;
+    const uint32_t* mp;   // this round's cluster count
+    uint32_t n;
+};
+
+__global__ void __launch_bounds__(kThreads) ploc_merge_k(PlocMerge M) {
+    const int i = (int)(blockIdx.x * kThreads + threadIdx.x);
+    if (i >= (int)*M.mp) return;
+    const int j = M.nn[i];
+    const bool mutual = j >= 0 && M.nn[j] == i;
+    const int ri = M.cref[i];
+    if (mutual && i > j) {   // the partner at the lower position creates the node
+        M.keep[i] = 0u;
+        return;
+    }
+    M.keep[i] = 1u;
+    if (!mutual) {
+        M.tref[i] = ri;
+        for (int k = 0; k < 6; ++k) M.tbox[6 * (size_t)i + k] = M.cbox[6 * (size_t)i + k];
+        return;
+    }
+    const uint32_t id = atomicAdd(M.node_ctr, 1u);
+    if (id + 1 >= M.n) {   // guard: n - 1 inner nodes at most
+        atomicOr(M.err, 16u);
+        M.tref[i] = ri;
+        return;
+    }
+    const int rj = M.cref[j];
+    M.child[2 * id] = ri;
+    M.child[2 * id + 1] = rj;
+    uint32_t cnt = 0;
+    for (int s = 0; s < 2; ++s) {
+        const int r = s ? rj : ri;
+        if (r >= 0) {
+            M.parent[r] = (int)id;
+            cnt += M.count[r];
+        } else {
+            M.leaf_parent[~r] = (int)id;
+            cnt += 1u;
+        }
+    }
+    M.count[id] = cnt;
+    for (int k = 0; k < 3; ++k) {
+        const float lo = fminf(M.cbox[6 * (size_t)i + k], M.cbox[6 * (size_t)j + k]);
+        const float hi = fmaxf(M.cbox[6 * (size_t)i + 3 + k], M.cbox[6 * (size_t)j + 3 + k]);
+        M.node_box[6 * (size_t)id + k] = lo;
+        M.node_box[6 * (size_t)id + 3 + k] = hi;
+        M.tbox[6 * (size_t)i + k] = lo;
+        M.tbox[6 * (size_t)i + 3 + k] = hi;
+    }
+    M.tref[i] = (int)id;
+}
+
+// order-preserving compaction: per-block counts, one scan of the block counts, scatter
+__global__ void __launch_bounds__(kThreads) ploc_count_k(const uint32_t* keep, const uint32_t* mp, uint32_t* bsum) {
+    const uint32_t m = *mp;
+    __shared__ uint32_t w[kThreads / 64];
+    const uint32_t i = blockIdx.x * kThreads + threadIdx.x;
+    const unsigned long long b = __ballot(i < m && keep[i]);
+    if ((threadIdx.x & 63) == 0) w[threadIdx.x >> 6] = (uint32_t)__popcll(b);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t s = 0;
+        for (int k = 0; k < kThreads / 64; ++k) s += w[k];
+        bsum[blockIdx.x] = s;
+    }
+}
+
+__global__ void __launch_bounds__(1024) ploc_scan_k(uint32_t* bsum, uint32_t nb, uint32_t* total) {
+    __shared__ uint32_t part[1024];
+    const uint32_t per = (nb + 1023) / 1024;
+    const uint32_t b = min(threadIdx.x * per, nb), e = min(b + per, nb);
+    uint32_t s = 0;
+    for (uint32_t i = b; i < e; ++i) s += bsum[i];
+    part[threadIdx.x] = s;
+    __syncthreads();
+    for (uint32_t off = 1; off < 1024; off <<= 1) {
+        const uint32_t v = threadIdx.x >= off ? part[threadIdx.x - off] : 0u;
+        __syncthreads();
+        part[threadIdx.x] += v;
+        __syncthreads();
+    }
+    uint32_t run = part[threadIdx.x] - s;
+    for (uint32_t i = b; i < e; ++i) {
+        const uint32_t v = bsum[i];
+        bsum[i] = run;
+        run += v;
+    }
+    if (threadIdx.x == 1023) *total = part[1023];
+}
+
+__global__ void __launch_bounds__(kThreads) ploc_scatter_k(const uint32_t* keep, const uint32_t* mp, const uint32_t* bsum,
+                                                           const int* tref, const float* tbox, int* cref, float* cbox) {
+    const uint32_t m = *mp;
+    if (blockIdx.x * kThreads >= m) return;
+    __shared__ uint32_t w[kThreads / 64];
+    const uint32_t i = blockIdx.x * kThreads + threadIdx.x;
+    const bool k = i < m && keep[i];
+    const unsigned long long b = __ballot(k);
+    const int wave = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) w[wave] = (uint32_t)__popcll(b);
+    __syncthreads();
+    uint32_t off = bsum[blockIdx.x];
+    for (int q = 0; q < wave; ++q) off += w[q];
+    const uint32_t lane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+    if (k) {
+        const uint32_t o = off + (uint32_t)__popcll(b & ((1ull << lane) - 1ull));
+        cref[o] = tref[i];
+        for (int c = 0; c < 6; ++c) cbox[6 * (size_t)o + c] = tbox[6 * (size_t)i + c];
+    }
+}
+
+// ---- 5b. SAH dynamic programming over the BVH2 (the host builder's collapse_bvh8_dp, rt_bvh.cpp):
+// per inner node the cheapest cost with 1..8 slots and the choices that reach it, bottom-up (the
+// second child to finish computes its parent, as lbvh_boxes_up_k).  choice[10 * p + i]:
+// i = 1: 1 leaf / 2 node; i >= 2: 0 = as with i - 1 slots, k = k slots to the left child;
+// [10 * p + 9] = the left child's share of the node's own eight slots.
+struct DpArgs {
+    const unsigned long long* keys;   // low 32 bits = triangle id
+    const int* child;
+    const int* parent;
+    const int* leaf_parent;
+    const uint32_t* count;
+    const float* tri_box;
+    const float* node_box;
+    float* cost;        // 8 per inner node
+    uint8_t* choice;    // 10 per inner node
+    uint32_t* flag;
+    uint32_t n;
+    float c_node, c_prim;
+};
+
+__device__ __forceinline__ float box_area(const float* b) {
+    const float d0 = b[3] - b[0], d1 = b[4] - b[1], d2 = b[5] - b[2];
+    return 2.0f * (d0 * d1 + d1 * d2 + d2 * d0);
+}
+
+__device__ __forceinline__ void dp_child_costs(const DpArgs& A, int r, float* c) {
+    if (r < 0) {   // one triangle: a leaf whatever the budget
+        const float a = box_area(A.tri_box + 6 * (size_t)(uint32_t)A.keys[~r]) * A.c_prim;
+        for (int i = 0; i < 8; ++i) c[i] = a;
+    } else {   // plain loads after the acquire fence (independent, so they overlap)
+        const float4 a = *reinterpret_cast<const float4*>(A.cost + 8 * (size_t)r);
+        const float4 b = *reinterpret_cast<const float4*>(A.cost + 8 * (size_t)r + 4);
+        c[0] = a.x; c[1] = a.y; c[2] = a.z; c[3] = a.w;
+        c[4] = b.x; c[5] = b.y; c[6] = b.z; c[7] = b.w;
+    }
+}
+
+__global__ void __launch_bounds__(kThreads) lbvh_dp_up_k(DpArgs A) {
+    const uint32_t k = blockIdx.x * kThreads + threadIdx.x;
+    if (k >= A.n) return;
+    int p = A.leaf_parent[k];
+    while (p >= 0 && p < (int)A.n - 1) {
+        // release this thread's cost stores, count the arrival; the second arrival acquires (the
+        // fence invalidates this CU's L1, so the sibling's costs are read from L2).  Per-word
+        // agent-scope atomic loads here serialised into ~50 us per tree level (4.8 ms a build).
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        if (atomicAdd(&A.flag[p], 1u) == 0u) return;   // the sibling subtree is not finished yet
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        float cl[8], cr[8], D[9];
+        uint8_t K[9];
+        dp_child_costs(A, A.child[2 * p], cl);
+        dp_child_costs(A, A.child[2 * p + 1], cr);
+        for (int j = 2; j <= 8; ++j) {
+            D[j] = INFINITY;
+            K[j] = 1;
+            for (int q = 1; q < j; ++q) {
+                const float v = cl[q - 1] + cr[j - q - 1];
+                if (v < D[j]) {
+                    D[j] = v;
+                    K[j] = (uint8_t)q;
+                }
+            }
+        }
+        const float area = box_area(A.node_box + 6 * (size_t)p);
+        const uint32_t cnt = A.count[p];
+        const float leaf = cnt <= kLeafMax ? area * A.c_prim * (float)cnt : INFINITY;
+        const float node = area * A.c_node + D[8];
+        float c = fminf(leaf, node);
+        float C[8];
+        uint8_t ch[10];
+        ch[0] = 0;
+        ch[1] = leaf <= node ? 1 : 2;
+        ch[9] = K[8];
+        C[0] = c;
+        for (int i = 2; i <= 8; ++i) {
+            if (D[i] < c) {
+                c = D[i];
+                ch[i] = K[i];
+            } else {
+                ch[i] = 0;
+            }
+            C[i - 1] = c;
+        }
+        *reinterpret_cast<float4*>(A.cost + 8 * (size_t)p) = make_float4(C[0], C[1], C[2], C[3]);
+        *reinterpret_cast<float4*>(A.cost + 8 * (size_t)p + 4) = make_float4(C[4], C[5], C[6], C[7]);
+        for (int i = 0; i < 10; ++i) A.choice[10 * (size_t)p + i] = ch[i];
+        p = A.parent[p];
+    }
+}
+
 // 6. top-down collapse of one level into 8-wide nodes
 struct Item {
     float lo[3], hi[3];
@@ -300,6 +571,7 @@ struct CollapseArgs {
     const int2* jobs_in;              // (BVH2 reference, 8-wide node)
     uint32_t n_jobs;
     int2* jobs_out;
+    const uint8_t* choice;            // DP choices (lbvh_dp_up_k), null: greedy collapse
     uint32_t* counters;               // [0] 8-wide nodes allocated, [1] triangle slots, [2] next jobs,
                                       // [4] error flag (a capacity guard tripped)
     uint32_t n;                       // triangles = capacity of nodes8, tri_order, the job queues
@@ -383,20 +655,51 @@ __global__ void __launch_bounds__(kThreads) lbvh_collapse_k(CollapseArgs A) {
     }
     Item items[8];
     int n_items = 0;
-    items[n_items++] = make_item(A, A.child[2 * job.x], pad);
-    items[n_items++] = make_item(A, A.child[2 * job.x + 1], pad);
-    while (n_items < 8) {   // open the inner child with the largest surface area
-        int best = -1;
-        float ba = -1.0f;
-        for (int i = 0; i < n_items; ++i)
-            if (!items[i].leaf && item_area(items[i]) > ba) {
-                ba = item_area(items[i]);
-                best = i;
+    if (A.choice) {
+        // DP: the node's eight slots split between its children as chosen bottom-up; a subtree
+        // with budget j either splits again (choice k) or becomes one slot (leaf or node)
+        int2 st[16];
+        int sp = 0;
+        const int k8 = A.choice[10 * (size_t)job.x + 9];
+        st[sp++] = make_int2(A.child[2 * job.x + 1], 8 - k8);
+        st[sp++] = make_int2(A.child[2 * job.x], k8);
+        while (sp > 0) {
+            const int2 e = st[--sp];
+            const int r = e.x;
+            int b = e.y;
+            if (r >= 0 && (uint32_t)r + 1 < A.n) {
+                while (b >= 2 && A.choice[10 * (size_t)r + b] == 0) --b;
+                if (b >= 2 && sp + 2 <= 16) {
+                    const int k = A.choice[10 * (size_t)r + b];
+                    st[sp++] = make_int2(A.child[2 * r + 1], b - k);
+                    st[sp++] = make_int2(A.child[2 * r], k);
+                    continue;
+                }
             }
-        if (best < 0) break;
-        const int r = items[best].ref;
-        items[best] = make_item(A, A.child[2 * r], pad);
-        items[n_items++] = make_item(A, A.child[2 * r + 1], pad);
+            if (n_items >= 8) {   // guard: the budgets add up to 8
+                atomicOr(&A.counters[4], 32u);
+                return;
+            }
+            Item it = make_item(A, r, pad);
+            if (r >= 0) it.leaf = A.choice[10 * (size_t)r + 1] == 1 && it.count <= kLeafMax;
+            items[n_items++] = it;
+        }
+    } else {
+        items[n_items++] = make_item(A, A.child[2 * job.x], pad);
+        items[n_items++] = make_item(A, A.child[2 * job.x + 1], pad);
+        while (n_items < 8) {   // open the inner child with the largest surface area
+            int best = -1;
+            float ba = -1.0f;
+            for (int i = 0; i < n_items; ++i)
+                if (!items[i].leaf && item_area(items[i]) > ba) {
+                    ba = item_area(items[i]);
+                    best = i;
+                }
+            if (best < 0) break;
+            const int r = items[best].ref;
+            items[best] = make_item(A, A.child[2 * r], pad);
+            items[n_items++] = make_item(A, A.child[2 * r + 1], pad);
+        }
     }
     float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
     for (int i = 0; i < n_items; ++i)
@@ -442,7 +745,22 @@ __global__ void __launch_bounds__(kThreads) lbvh_collapse_k(CollapseArgs A) {
             ++rank;
         } else {
             nd.meta[i] = (uint8_t)(((it.count - 1u) << 5) | toff);
-            for (uint32_t t = 0; t < it.count; ++t) A.tri_order[nd.tri_base + toff + t] = (uint32_t)A.keys[it.first + t];
+            // the subtree's triangles (<= 4), left to right (PLOC subtrees are not contiguous in
+            // the sorted order)
+            int st[8];
+            int sp = 0;
+            uint32_t t = 0;
+            st[sp++] = it.ref;
+            while (sp > 0 && t < it.count) {
+                const int r = st[--sp];
+                if (r < 0) {
+                    A.tri_order[nd.tri_base + toff + t++] = (uint32_t)A.keys[~r];
+                } else if (sp + 2 <= 8) {
+                    st[sp++] = A.child[2 * r + 1];
+                    st[sp++] = A.child[2 * r];
+                }
+            }
+            if (t != it.count) atomicOr(&A.counters[4], 64u);
             toff += it.count;
         }
     }
@@ -482,7 +800,13 @@ size_t lbvh_scratch_bytes(uint32_t n) {
            + align256(24 * (size_t)n)       // inner boxes
            + align256(4 * (size_t)n)        // bottom-up flags
            + 2 * align256(8 * (size_t)n)    // job queues
-           + align256(64 * 4);              // bounds, maxabs, counters
+           + align256(64 * 4)               // bounds, maxabs, counters
+           + 2 * align256(4 * (size_t)n)    // PLOC cluster refs (current, merged)
+           + 2 * align256(24 * (size_t)n)   // PLOC cluster boxes
+           + 2 * align256(4 * (size_t)n)    // PLOC nearest neighbours, keep flags
+           + align256(4 * ((size_t)n / kThreads + 2))   // PLOC block counts
+           + align256(32 * (size_t)n)       // DP costs
+           + align256(10 * (size_t)n);      // DP choices
 }
 
 bool lbvh_build(const LbvhInput& in, const LbvhOutput& out, void* scratch, hipStream_t s, LbvhResult* res,
@@ -512,7 +836,17 @@ bool lbvh_build(const LbvhInput& in, const LbvhOutput& out, void* scratch, hipSt
     auto* flag = (uint32_t*)carve(4 * (size_t)n);
     auto* jobs_a = (int2*)carve(8 * (size_t)n);
     auto* jobs_b = (int2*)carve(8 * (size_t)n);
-    auto* misc = (uint32_t*)carve(64 * 4);   // [0..5] centroid bounds, [6] max |coord|, [8..10] counters
+    auto* misc = (uint32_t*)carve(64 * 4);   // [0..5] centroid bounds, [6] max |coord|, [8..12] counters,
+                                             // [14] PLOC inner nodes, [15] PLOC clusters left
+    auto* cref = (int*)carve(4 * (size_t)n);
+    auto* tref = (int*)carve(4 * (size_t)n);
+    auto* cbox = (float*)carve(24 * (size_t)n);
+    auto* tbox = (float*)carve(24 * (size_t)n);
+    auto* nn = (int*)carve(4 * (size_t)n);
+    auto* keep = (uint32_t*)carve(4 * (size_t)n);
+    auto* bsum = (uint32_t*)carve(4 * ((size_t)n / kThreads + 2));
+    auto* cost = (float*)carve(32 * (size_t)n);
+    auto* choice = (uint8_t*)carve(10 * (size_t)n);
 #define LB_CHECK(expr)                    \
     do {                                  \
         hipError_t e_ = (expr);           \
@@ -523,7 +857,7 @@ bool lbvh_build(const LbvhInput& in, const LbvhOutput& out, void* scratch, hipSt
     } while (0)
     // bounds start empty, max |coord| at 1.0 (as the host builder), node counter past the root
     static const uint32_t init[16] = {0xffffffffu, 0xffffffffu, 0xffffffffu, 0, 0, 0, 0x3f800000u, 0,
-                                      1u, 0, 0, 0, 0, 0, 0, 0};
+                                      1u, 0, 0, 0, 0, 0, 0, 0};   // [14] PLOC node counter = 0
     LB_CHECK(hipMemcpyAsync(misc, init, sizeof init, hipMemcpyHostToDevice, s));
     LB_CHECK(hipMemsetAsync(flag, 0, 4 * (size_t)n, s));
     LB_CHECK(hipMemsetAsync(parent, 0xff, 4 * (size_t)n, s));        // -1: unset
@@ -542,10 +876,83 @@ bool lbvh_build(const LbvhInput& in, const LbvhOutput& out, void* scratch, hipSt
         lbvh_scatter_k<<<tiles, kThreads, 0, s>>>(src, dst, n, shift, tiles, table);
         std::swap(src, dst);
     }
-    lbvh_tree_k<<<blocks(n - 1), kThreads, 0, s>>>(src, n, child, parent, leaf_parent, first, count);
-    lbvh_key_ids_k<<<blocks(n), kThreads, 0, s>>>(src, n, (1ull << id_bits) - 1ull);
-    lbvh_boxes_up_k<<<blocks(n), kThreads, 0, s>>>(src, n, child, parent, leaf_parent, tri_box, node_box, flag);
+    uint32_t* h_next = out.h_scratch;   // pinned
+    int2* jin = jobs_a;
+    int2* jout = jobs_b;
+    LB_CHECK(hipMemsetAsync(jobs_a, 0, sizeof(int2), s));   // the root job: (BVH2 root, 8-wide node 0)
+    if (in.ploc) {
+        lbvh_key_ids_k<<<blocks(n), kThreads, 0, s>>>(src, n, (1ull << id_bits) - 1ull);
+        ploc_init_k<<<blocks(n), kThreads, 0, s>>>(src, tri_box, n, cref, cbox, misc + 15);
+        PlocMerge M;
+        M.nn = nn;
+        M.cref = cref;
+        M.cbox = cbox;
+        M.tref = tref;
+        M.tbox = tbox;
+        M.keep = keep;
+        M.child = child;
+        M.parent = parent;
+        M.leaf_parent = leaf_parent;
+        M.count = count;
+        M.node_box = node_box;
+        M.node_ctr = misc + 14;
+        M.err = misc + 12;
+        M.n = n;
+        // cluster counts ping-pong between misc[15] and misc[16]: round r reads misc[15 + (r & 1)]
+        uint32_t m = n;
+        int round = 0;
+        while (m > 1) {
+            if (round >= 2000) {
+                *err = "ploc: no convergence";
+                return false;
+            }
+            const unsigned nb = blocks(m);   // an upper bound for every round of the batch
+            const int batch = m > 65536 ? 4 : 8;
+            for (int b = 0; b < batch; ++b, ++round) {
+                uint32_t* mc = misc + 15 + (round & 1);
+                uint32_t* mn = misc + 15 + ((round + 1) & 1);
+                M.mp = mc;
+                ploc_nn_k<<<nb, kThreads, 0, s>>>(cbox, mc, nn);
+                ploc_merge_k<<<nb, kThreads, 0, s>>>(M);
+                ploc_count_k<<<nb, kThreads, 0, s>>>(keep, mc, bsum);
+                ploc_scan_k<<<1, 1024, 0, s>>>(bsum, nb, mn);
+                ploc_scatter_k<<<nb, kThreads, 0, s>>>(keep, mc, bsum, tref, tbox, cref, cbox);
+            }
+            LB_CHECK(hipGetLastError());
+            LB_CHECK(hipMemcpyAsync(h_next, misc + 15 + (round & 1), 4, hipMemcpyDeviceToHost, s));
+            LB_CHECK(hipStreamSynchronize(s));
+            if (*h_next >= m || *h_next == 0) {
+                *err = "ploc: a batch of rounds merged nothing";
+                return false;
+            }
+            m = *h_next;
+        }
+        LB_CHECK(hipMemcpyAsync(jobs_a, cref, 4, hipMemcpyDeviceToDevice, s));   // root = the last cluster
+    } else {
+        lbvh_tree_k<<<blocks(n - 1), kThreads, 0, s>>>(src, n, child, parent, leaf_parent, first, count);
+        lbvh_key_ids_k<<<blocks(n), kThreads, 0, s>>>(src, n, (1ull << id_bits) - 1ull);
+        lbvh_boxes_up_k<<<blocks(n), kThreads, 0, s>>>(src, n, child, parent, leaf_parent, tri_box, node_box, flag);
+    }
     LB_CHECK(hipGetLastError());
+    if (in.dp) {
+        LB_CHECK(hipMemsetAsync(flag, 0, 4 * (size_t)n, s));
+        DpArgs D;
+        D.keys = src;
+        D.child = child;
+        D.parent = parent;
+        D.leaf_parent = leaf_parent;
+        D.count = count;
+        D.tri_box = tri_box;
+        D.node_box = node_box;
+        D.cost = cost;
+        D.choice = choice;
+        D.flag = flag;
+        D.n = n;
+        D.c_node = in.c_node;
+        D.c_prim = in.c_prim;
+        lbvh_dp_up_k<<<blocks(n), kThreads, 0, s>>>(D);
+        LB_CHECK(hipGetLastError());
+    }
     // collapse, one level per launch; the next level's job count comes back to the host
     CollapseArgs A;
     A.keys = src;
@@ -560,13 +967,9 @@ bool lbvh_build(const LbvhInput& in, const LbvhOutput& out, void* scratch, hipSt
     A.nodes8 = out.nodes8;
     A.node8_box = out.node_box;
     A.tri_order = out.tri_order;
-    static const int2 root = make_int2(0, 0);
-    LB_CHECK(hipMemcpyAsync(jobs_a, &root, sizeof root, hipMemcpyHostToDevice, s));
+    A.choice = in.dp ? choice : nullptr;
     res->level_off.assign(1, 0u);
     uint32_t n_jobs = 1, total = 1;
-    int2* jin = jobs_a;
-    int2* jout = jobs_b;
-    uint32_t* h_next = out.h_scratch;   // pinned
     while (n_jobs > 0) {
         if ((int)res->level_off.size() > kStackSize) {
             *err = "lbvh: 8-wide tree deeper than the traversal stack";
