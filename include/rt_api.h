@@ -226,10 +226,16 @@ rt_status rt_read_aux(rt_ctx* ctx, float* depth, float* motion, float* gbuffer);
  * nearest render pixel (the presenter's own path); SPATIAL resamples bilinearly; TEMPORAL blends
  * with the previous output reprojected through the motion vectors, clamped to the current
  * neighbourhood, rejected on depth jumps (MetalFX's scalers are unpublished: these are stand-ins
- * consuming the same inputs).  encode: RT_ENCODE_SRGB8 (default) or RT_ENCODE_LINEAR8. */
+ * consuming the same inputs).  DENOISED (MTLFXTemporalDenoisedScaler's place when
+ * useTemporalDenoiser is set, FramePresenter.swift:77-98,179-198) first filters the radiance at
+ * render size, guided by the G-buffer (enableDenoiseGBuffer must be on: RT_ERR_STATE otherwise):
+ * demodulation by diffuse + specular albedo, `denoise_passes` edge-avoiding a-trous passes over
+ * normals and depth, remodulation; then the TEMPORAL path.  DENOISED and TEMPORAL share one
+ * history.  encode: RT_ENCODE_SRGB8 (default) or RT_ENCODE_LINEAR8. */
 #define RT_SCALER_NONE 0
 #define RT_SCALER_SPATIAL 1
 #define RT_SCALER_TEMPORAL 2
+#define RT_SCALER_DENOISED 3
 #define RT_ENCODE_SRGB8 0
 #define RT_ENCODE_LINEAR8 1
 typedef struct rt_present_opts {
@@ -237,7 +243,8 @@ typedef struct rt_present_opts {
     int32_t out_height;  /* 0 = render height */
     int32_t scaler;
     int32_t encode;
-    int32_t reserved[4];
+    int32_t denoise_passes;   /* RT_SCALER_DENOISED: 0 = 3; at most 6 */
+    int32_t reserved[3];
 } rt_present_opts;
 rt_status rt_present(rt_ctx* ctx, const rt_present_opts* opts, uint8_t* host_rgba8);
 

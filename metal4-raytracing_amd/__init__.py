@@ -368,16 +368,18 @@ class Renderer:
         dev = (self.bvh_builder == "lbvh") if device is None else device
         _check((lib().rt_bvh_build_device if dev else lib().rt_bvh_build)(self._ctx), self._ctx)
 
-    def present(self, width=None, height=None, scaler="none", srgb=True):
+    def present(self, width=None, height=None, scaler="none", srgb=True, denoise_passes=0):
         """Display image of the newest frame (FramePresenter + Shaders.metal): resampled to
         width x height ('none' = nearest, 'spatial' = bilinear, 'temporal' = reprojected history
-        through the motion vectors), tone-mapped c / (1 + c), 8-bit sRGB (or linear) RGBA rows
+        through the motion vectors, 'denoised' = G-buffer-guided a-trous filter then 'temporal';
+        needs useTemporalDenoiser), tone-mapped c / (1 + c), 8-bit sRGB (or linear) RGBA rows
         top-down."""
         o = _abi.PresentOpts()
         o.out_width = int(width or 0)
         o.out_height = int(height or 0)
         o.scaler = _abi.SCALERS[scaler]
         o.encode = 0 if srgb else 1
+        o.denoise_passes = int(denoise_passes)
         out = np.empty((height or self.height, width or self.width, 4), dtype=np.uint8)
         _check(lib().rt_present(self._ctx, C.byref(o), out.ctypes.data), self._ctx)
         return out

@@ -133,10 +133,10 @@ class Opts(C.Structure):
 
 class PresentOpts(C.Structure):  # rt_present_opts
     _fields_ = [("out_width", C.c_int32), ("out_height", C.c_int32), ("scaler", C.c_int32), ("encode", C.c_int32),
-                ("reserved", C.c_int32 * 4)]
+                ("denoise_passes", C.c_int32), ("reserved", C.c_int32 * 3)]
 
 
-SCALERS = {"none": 0, "spatial": 1, "temporal": 2}
+SCALERS = {"none": 0, "spatial": 1, "temporal": 2, "denoised": 3}
 
 
 class TileSet(C.Structure):

@@ -133,6 +133,8 @@ struct rt_ctx {
     DevBuf d_hist[2], d_hdepth[2], d_present_out, d_present_thr;
     int hist_w = 0, hist_h = 0, hist_idx = 0;
     bool hist_valid = false;
+    DevBuf d_den[4];   // RT_SCALER_DENOISED scratch at render size: ping, pong, guide, albedo
+    size_t den_n = 0;
     rt_stats stats{};
 
     // frames in flight
@@ -240,7 +242,7 @@ static size_t ctx_bytes(const rt_ctx* c) {
                            &c->d_accum[0], &c->d_accum[1], &c->d_lbvh_scratch,
                            &c->d_tex_texels, &c->d_tex_info, &c->d_mat_tex, &c->d_uv, &c->d_tex_lut,
                            &c->d_hist[0], &c->d_hist[1], &c->d_hdepth[0], &c->d_hdepth[1], &c->d_present_out,
-                           &c->d_present_thr};
+                           &c->d_present_thr, &c->d_den[0], &c->d_den[1], &c->d_den[2], &c->d_den[3]};
     size_t s = 0;
     for (auto* b : all) s += b->bytes;
     for (const DevBuf& b : c->d_motion) s += b.bytes;
@@ -423,7 +425,8 @@ rt_status rt_destroy(rt_ctx* c) {
                      &c->d_slot_to_tri, &c->d_levels, &c->d_maxabs, &c->d_random, &c->d_accum[0],
                      &c->d_accum[1], &c->d_lbvh_scratch, &c->d_tex_texels, &c->d_tex_info,
                      &c->d_mat_tex, &c->d_uv, &c->d_tex_lut, &c->d_hist[0], &c->d_hist[1], &c->d_hdepth[0],
-                     &c->d_hdepth[1], &c->d_present_out, &c->d_present_thr};
+                     &c->d_hdepth[1], &c->d_present_out, &c->d_present_thr, &c->d_den[0], &c->d_den[1],
+                     &c->d_den[2], &c->d_den[3]};
     for (auto* b : all) dev_free(*b);
     for (DevBuf& b : c->d_motion) dev_free(b);
     for (Geo& g : c->geo)
@@ -1154,8 +1157,10 @@ rt_status rt_present(rt_ctx* c, const rt_present_opts* o, uint8_t* host_rgba8) {
     const int oh = (o && o->out_height > 0) ? o->out_height : c->height;
     const int scaler = o ? o->scaler : RT_SCALER_NONE;
     const int encode = o ? o->encode : RT_ENCODE_SRGB8;
-    if (scaler < RT_SCALER_NONE || scaler > RT_SCALER_TEMPORAL || (encode != RT_ENCODE_SRGB8 && encode != RT_ENCODE_LINEAR8))
+    const int passes = (o && o->denoise_passes > 0) ? o->denoise_passes : 3;
+    if (scaler < RT_SCALER_NONE || scaler > RT_SCALER_DENOISED || (encode != RT_ENCODE_SRGB8 && encode != RT_ENCODE_LINEAR8))
         FAIL(c, RT_ERR_INVALID_ARG, "bad scaler / encode");
+    if (scaler == RT_SCALER_DENOISED && passes > 6) FAIL(c, RT_ERR_INVALID_ARG, "denoise_passes > 6");
     if ((int64_t)ow * oh > (1ll << 28)) FAIL(c, RT_ERR_INVALID_ARG, "output too large");
     HIPC(c, hipSetDevice(c->device));
     rt_status st;
@@ -1170,7 +1175,8 @@ rt_status rt_present(rt_ctx* c, const rt_present_opts* o, uint8_t* host_rgba8) {
         if ((st = dev_upload(c, c->d_present_thr, thr, sizeof thr))) return st;
     }
     if ((st = dev_alloc(c, c->d_present_out, n * 4))) return st;
-    if (scaler == RT_SCALER_TEMPORAL && (c->hist_w != ow || c->hist_h != oh || !c->d_hist[0].p)) {
+    const bool temporal = scaler == RT_SCALER_TEMPORAL || scaler == RT_SCALER_DENOISED;
+    if (temporal && (c->hist_w != ow || c->hist_h != oh || !c->d_hist[0].p)) {
         for (int i = 0; i < 2; ++i) {
             if ((st = dev_alloc(c, c->d_hist[i], n * 16))) return st;
             if ((st = dev_alloc(c, c->d_hdepth[i], n * 4))) return st;
@@ -1182,14 +1188,28 @@ rt_status rt_present(rt_ctx* c, const rt_present_opts* o, uint8_t* host_rgba8) {
     // after the newest frame (and any pack / unpack of it)
     FrameSlot& f = c->slot[c->last_slot];
     if (!f.used) FAIL(c, RT_ERR_STATE, "rt_present before the first frame");
+    const float4* color = (const float4*)c->d_accum[c->read_idx].p;
+    if (scaler == RT_SCALER_DENOISED) {   // render-size scratch: two ping-pong images, guide, albedo
+        if (!f.gbuffer.p) FAIL(c, RT_ERR_STATE, "RT_SCALER_DENOISED needs the G-buffer (enableDenoiseGBuffer)");
+        const size_t rn = (size_t)c->width * c->height;
+        if (c->den_n != rn || !c->d_den[0].p) {
+            for (int i = 0; i < 4; ++i)
+                if ((st = dev_alloc(c, c->d_den[i], rn * 16))) return st;
+            c->den_n = rn;
+        }
+    }
     HIPC(c, hipStreamWaitEvent(c->stream, f.done, 0));
-    const bool temporal = scaler == RT_SCALER_TEMPORAL;
+    if (scaler == RT_SCALER_DENOISED)
+        color = launch_denoise(color, (const float*)f.depth.p, (const float4*)f.gbuffer.p, (float4*)c->d_den[0].p,
+                               (float4*)c->d_den[1].p, (float4*)c->d_den[2].p, (float4*)c->d_den[3].p, c->width,
+                               c->height, passes, c->stream);
     const int hi = c->hist_idx;
-    launch_present((const float4*)c->d_accum[c->read_idx].p, (const float*)f.depth.p,
+    launch_present(color, (const float*)f.depth.p,
                    (const float2*)c->d_motion[c->motion_cur].p, temporal ? (const float4*)c->d_hist[hi].p : nullptr,
                    temporal ? (const float*)c->d_hdepth[hi].p : nullptr,
                    temporal ? (float4*)c->d_hist[1 - hi].p : nullptr, temporal ? (float*)c->d_hdepth[1 - hi].p : nullptr,
-                   (uchar4*)c->d_present_out.p, (const float*)c->d_present_thr.p, c->width, c->height, ow, oh, scaler,
+                   (uchar4*)c->d_present_out.p, (const float*)c->d_present_thr.p, c->width, c->height, ow, oh,
+                   temporal ? RT_SCALER_TEMPORAL : scaler,
                    encode == RT_ENCODE_SRGB8 ? 1 : 0, (temporal && c->hist_valid && c->last_frame_index > 0) ? 1 : 0,
                    c->stream);
     HIPC(c, hipGetLastError());

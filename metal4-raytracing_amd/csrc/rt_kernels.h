@@ -208,6 +208,10 @@ bool lbvh_build(const LbvhInput& in, const LbvhOutput& out, void* scratch, hipSt
                 const char** err);
 
 // Utility kernels (rt_util.hip)
+// G-buffer-guided denoise for RT_SCALER_DENOISED (rt_present.hip); returns tmp0 or tmp1, whichever
+// holds the result (passes = 0 returns the demodulated radiance unremodulated: callers pass >= 1)
+const float4* launch_denoise(const float4* accum, const float* depth, const float4* gbuf, float4* tmp0, float4* tmp1,
+                             float4* guide, float4* alb, int w, int h, int passes, hipStream_t stream);
 void launch_present(const float4* accum, const float* depth, const float2* motion, const float4* hist_in,
                     const float* hdepth_in, float4* hist_out, float* hdepth_out, uchar4* out, const float* thr, int w,
                     int h, int ow, int oh, int scaler, int srgb, int use_hist, hipStream_t stream);

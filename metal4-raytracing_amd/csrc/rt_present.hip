@@ -119,7 +119,102 @@ __global__ void __launch_bounds__(256) present_k(const float4* __restrict__ accu
     out[(size_t)oyd * ow + ox] = r;
 }
 
+// ---- RT_SCALER_DENOISED: G-buffer-guided denoise ahead of the temporal scaler ----------------
+// Stand-in for MTLFXTemporalDenoisedScaler (FramePresenter.swift:77-98,179-198), which consumes
+// colour, depth, motion and the four G-buffer planes of Raytracing.metal:506-515 with an
+// unpublished algorithm.  Here: demodulate the radiance by diffuse + specular albedo, run
+// `passes` edge-avoiding a-trous passes (5x5 B3-spline taps at step 1, 2, 4, ...; weights
+// max(0, n.n')^16 from the decoded G-buffer normals and 1 / (1 + (dz / (0.05 step z))^2) from
+// the depth; background only with background), remodulate, then the TEMPORAL path above.  All
+// arithmetic is written in a fixed order without contraction (tests/test_gpu_present.py
+// restates it in numpy byte for byte).
+
+// illum = radiance / albedo, guide = (normal, depth) on hits, (0, 0, 0, -1) on background,
+// alb = the demodulation albedo (1 where diffuse + specular albedo <= 1e-3 or no hit)
+__global__ void __launch_bounds__(256) denoise_prep_k(const float4* __restrict__ accum, const float* __restrict__ depth,
+                                                      const float4* __restrict__ gbuf, float4* __restrict__ illum,
+                                                      float4* __restrict__ guide, float4* __restrict__ alb, int n) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const float4 c = accum[i], g0 = gbuf[i], g1 = gbuf[(size_t)n + i], g2 = gbuf[2 * (size_t)n + i];
+    const bool hit = g2.w > 0.5f;
+    float ax = g0.x + g1.x, ay = g0.y + g1.y, az = g0.z + g1.z;
+    ax = (hit && ax > 1e-3f) ? ax : 1.0f;
+    ay = (hit && ay > 1e-3f) ? ay : 1.0f;
+    az = (hit && az > 1e-3f) ? az : 1.0f;
+    illum[i] = make_float4(c.x / ax, c.y / ay, c.z / az, c.w);
+    guide[i] = hit ? make_float4(g2.x * 2.0f - 1.0f, g2.y * 2.0f - 1.0f, g2.z * 2.0f - 1.0f, depth[i])
+                   : make_float4(0.0f, 0.0f, 0.0f, -1.0f);
+    alb[i] = make_float4(ax, ay, az, 1.0f);
+}
+
+__global__ void __launch_bounds__(256) denoise_atrous_k(const float4* __restrict__ in, const float4* __restrict__ guide,
+                                                        const float4* __restrict__ alb, float4* __restrict__ out, int w,
+                                                        int h, int step, int last) {
+    const int x = blockIdx.x * 16 + (threadIdx.x & 15), y = blockIdx.y * 16 + (threadIdx.x >> 4);
+    if (x >= w || y >= h) return;
+    const size_t i = (size_t)y * w + x;
+    const float4 p = guide[i];
+    const float kern[5] = {0.0625f, 0.25f, 0.375f, 0.25f, 0.0625f};
+    const float zs = 0.05f * (float)step * p.w;
+    float sx = 0.0f, sy = 0.0f, sz = 0.0f, sw = 0.0f;
+    for (int dy = -2; dy <= 2; ++dy) {
+        const int yy = y + dy * step;
+        if (yy < 0 || yy >= h) continue;
+        for (int dx = -2; dx <= 2; ++dx) {
+            const int xx = x + dx * step;
+            if (xx < 0 || xx >= w) continue;
+            const size_t j = (size_t)yy * w + xx;
+            const float4 q = guide[j];
+            float wgt = kern[dy + 2] * kern[dx + 2];
+            if (p.w < 0.0f || q.w < 0.0f) {
+                if (p.w >= 0.0f || q.w >= 0.0f) continue;   // hit next to background: no weight
+            } else {
+                float t = fmaxf(p.x * q.x + p.y * q.y + p.z * q.z, 0.0f);
+                t = t * t;
+                t = t * t;
+                t = t * t;
+                t = t * t;
+                const float dz = fabsf(p.w - q.w) / zs;
+                wgt = (wgt * t) / (1.0f + dz * dz);
+            }
+            const float4 c = in[j];
+            sx = sx + c.x * wgt;
+            sy = sy + c.y * wgt;
+            sz = sz + c.z * wgt;
+            sw = sw + wgt;
+        }
+    }
+    const float4 c0 = in[i];
+    float4 r = sw > 0.0f ? make_float4(sx / sw, sy / sw, sz / sw, c0.w) : c0;
+    if (last) {
+        const float4 a = alb[i];
+        r.x = r.x * a.x;
+        r.y = r.y * a.y;
+        r.z = r.z * a.z;
+    }
+    out[i] = r;
+}
+
 }  // namespace
+
+const float4* launch_denoise(const float4* accum, const float* depth, const float4* gbuf, float4* tmp0, float4* tmp1,
+                             float4* guide, float4* alb, int w, int h, int passes, hipStream_t stream) {
+    const int n = w * h;
+    hipLaunchKernelGGL(denoise_prep_k, dim3((n + 255) / 256), dim3(256), 0, stream, accum, depth, gbuf, tmp0, guide,
+                       alb, n);
+    float4* src = tmp0;
+    float4* dst = tmp1;
+    dim3 grid((w + 15) / 16, (h + 15) / 16);
+    for (int k = 0; k < passes; ++k) {
+        hipLaunchKernelGGL(denoise_atrous_k, grid, dim3(256), 0, stream, src, guide, alb, dst, w, h, 1 << k,
+                           k == passes - 1 ? 1 : 0);
+        float4* t = src;
+        src = dst;
+        dst = t;
+    }
+    return src;
+}
 
 void launch_present(const float4* accum, const float* depth, const float2* motion, const float4* hist_in,
                     const float* hdepth_in, float4* hist_out, float* hdepth_out, uchar4* out, const float* thr, int w,

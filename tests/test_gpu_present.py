@@ -4,8 +4,9 @@ reprojection through the motion vectors and depth), tone-maps color / (1 + color
 8-bit sRGB or linear rows top-down.  The kernel is byte work on float inputs with a fixed
 operation order, so a numpy float32 restatement (below) reproduces its bytes exactly; the
 radiance, depth and motion it reads are the library's own (pinned elsewhere against the oracle).
-MetalFX's scalers are unpublished, so the spatial / temporal modes are parity unpinned against
-the reference and pinned here against this restatement."""
+MetalFX's scalers are unpublished, so the spatial / temporal / denoised modes are parity unpinned
+against the reference and pinned here against this restatement; the denoised mode is also checked
+to bring a 1-spp frame closer to a converged one."""
 import os
 
 import numpy as np
@@ -97,6 +98,60 @@ def present_np(acc, depth, motion, ow, oh, scaler, srgb, hist=None, hdepth=None,
     return out[::-1], nh, nd
 
 
+def denoise_np(acc, depth, gb, passes=3):
+    """RT_SCALER_DENOISED's render-size filter (rt_present.hip denoise_prep_k / denoise_atrous_k):
+    demodulate by diffuse + specular albedo, `passes` a-trous passes weighted by the B3 spline,
+    max(0, n.n')^16 and 1 / (1 + (dz / (0.05 step z))^2), background only with background,
+    remodulate.  Same operation order as the kernels."""
+    h, w = acc.shape[:2]
+    hit = gb[2][..., 3] > f32(0.5)
+    a = gb[0][..., :3] + gb[1][..., :3]
+    a = np.where(hit[..., None] & (a > f32(1e-3)), a, f32(1)).astype(f32)
+    src = acc.astype(f32).copy()
+    src[..., :3] = acc[..., :3] / a
+    guide = np.zeros((h, w, 4), f32)
+    guide[..., 3] = -1
+    guide[hit, :3] = gb[2][hit, :3] * f32(2) - f32(1)
+    guide[hit, 3] = depth[hit]
+    kern = np.array([0.0625, 0.25, 0.375, 0.25, 0.0625], f32)
+    ys, xs = np.meshgrid(np.arange(h), np.arange(w), indexing="ij")
+    p = guide
+    pb = p[..., 3] < 0
+    for k in range(passes):
+        step = 1 << k
+        zs = f32(0.05) * f32(step) * p[..., 3]
+        s = np.zeros((h, w, 3), f32)
+        sw = np.zeros((h, w), f32)
+        for dy in range(-2, 3):
+            for dx in range(-2, 3):
+                yy, xx = ys + dy * step, xs + dx * step
+                inb = (yy >= 0) & (yy < h) & (xx >= 0) & (xx < w)
+                yc, xc = np.clip(yy, 0, h - 1), np.clip(xx, 0, w - 1)
+                q = guide[yc, xc]
+                qb = q[..., 3] < 0
+                w0 = kern[dy + 2] * kern[dx + 2]
+                t = np.maximum(p[..., 0] * q[..., 0] + p[..., 1] * q[..., 1] + p[..., 2] * q[..., 2], f32(0))
+                t = t * t
+                t = t * t
+                t = t * t
+                t = t * t
+                with np.errstate(invalid="ignore", divide="ignore", over="ignore"):
+                    dz = np.abs(p[..., 3] - q[..., 3]) / zs
+                    wv = (w0 * t) / (f32(1) + dz * dz)
+                wgt = np.where(pb | qb, w0, wv).astype(f32)
+                use = inb & ~(pb ^ qb)
+                c = src[yc, xc][..., :3]
+                s = np.where(use[..., None], s + c * wgt[..., None], s)
+                sw = np.where(use, sw + wgt, sw)
+        r = src.copy()
+        with np.errstate(invalid="ignore", divide="ignore"):
+            r[..., :3] = np.where((sw > 0)[..., None], s / sw[..., None], src[..., :3])
+        if k == passes - 1:
+            r[..., :3] = r[..., :3] * a
+        src = r
+    return src
+
+
 def _renderer(rt, assets, fif=2):
     sc = rt.Scene.preset("c1", assets)
     R = make_renderer(rt, sc, 80, 56, "wavefront", seed=4, frames_in_flight=fif)
@@ -156,3 +211,56 @@ def test_present_orientation(rt, assets):
     acc = R.radiance()
     assert np.array_equal(got[0, :, :3], _encode(acc[-1, :, :3], False))
     assert np.array_equal(got[-1, :, :3], _encode(acc[0, :, :3], False))
+
+
+@pytest.mark.parametrize("passes", [1, 3, 5])
+def test_present_denoised_sequence(rt, assets, passes):
+    """RT_SCALER_DENOISED over four moving-camera frames (G-buffer on): the G-buffer-guided filter
+    and the temporal history match the restatement byte for byte, at a resampled output size."""
+    R = _renderer(rt, assets)
+    R.useTemporalDenoiser = True
+    cam0 = R.camera
+    ow, oh = (80, 56) if passes == 3 else (100, 70)
+    hist = hdepth = None
+    for i in range(4):
+        c = rt.Camera()
+        c.position = type(cam0.position)(cam0.position.x - 0.02 * i, cam0.position.y, cam0.position.z, 0.0)
+        c.right, c.up, c.forward = cam0.right, cam0.up, cam0.forward
+        R.camera = c
+        u = R.draw()
+        got = R.present(ow, oh, scaler="denoised", denoise_passes=passes)
+        acc = R.radiance()
+        depth, motion, gb = R.aux(gbuffer=True)
+        den = denoise_np(acc, depth, gb, passes)
+        use = hist is not None and u.frameIndex > 0
+        exp, hist, hdepth = present_np(den, depth, motion, ow, oh, "temporal", True, hist, hdepth, use)
+        assert np.array_equal(got, exp), (i, np.argwhere(got != exp)[:5])
+
+
+def test_present_denoised_needs_gbuffer(rt, assets):
+    R = _renderer(rt, assets)
+    R.draw()
+    with pytest.raises(RuntimeError, match="G-buffer"):
+        R.present(scaler="denoised")
+    R.useTemporalDenoiser = True
+    R.draw()
+    with pytest.raises(RuntimeError):
+        R.present(scaler="denoised", denoise_passes=7)
+    assert R.present(scaler="denoised").shape == (56, 80, 4)
+
+
+def test_present_denoised_reduces_noise(rt, assets):
+    """One 1-spp frame: the denoised display is closer to a 64-spp frame's than the raw one."""
+    R = _renderer(rt, assets)
+    R.useTemporalDenoiser = True
+    R.samplesPerPixel = 1
+    R.draw()
+    raw = R.present(scaler="none", srgb=False).astype(np.float64)
+    den = R.present(scaler="denoised", srgb=False).astype(np.float64)
+    Q = _renderer(rt, assets)
+    Q.samplesPerPixel = 64
+    Q.draw()
+    ref = Q.present(scaler="none", srgb=False).astype(np.float64)
+    e_raw = np.abs(raw - ref)[..., :3].mean()
+    e_den = np.abs(den - ref)[..., :3].mean()
+    assert e_den < 0.7 * e_raw, (e_den, e_raw)
