@@ -20,6 +20,8 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <climits>
+#include <cstdint>
 #include <functional>
 #include <map>
 #include <memory>
@@ -1017,7 +1019,7 @@ static Primvar primvar(const Prim& p, const std::string& name, const char* defau
     pv.comps = pv.v->comps;
     pv.interp = a && !a->interpolation.empty() ? a->interpolation : default_interp;
     if (const Value* iv = attr_value(p, name + ":indices"))
-        for (double d : iv->num) pv.idx.push_back((int)d);
+        for (double d : iv->num) pv.idx.push_back(d >= 0.0 && d < 2147483647.0 ? (int)d : -1);
     return pv;
 }
 
@@ -1050,12 +1052,13 @@ static void usd_material(rt_scene* s, const Stage& st, int mat, const std::vecto
     if (const Attr* out = st.prims[mat].attr("outputs:surface"))
         if (!out->connections.empty()) shader = st.find(out->connections[0].substr(0, out->connections[0].find_last_of('.')));
     if (shader < 0) {
-        std::function<void(int)> walk = [&](int k) {
+        for (int k : st.preorder(mat, false)) {
             const Value* id = attr_value(st.prims[k], "info:id");
-            if (shader < 0 && st.prims[k].type == "Shader" && id && !id->str.empty() && id->str[0] == "UsdPreviewSurface") shader = k;
-            for (int c : st.prims[k].children) walk(c);
-        };
-        walk(mat);
+            if (st.prims[k].type == "Shader" && id && !id->str.empty() && id->str[0] == "UsdPreviewSurface") {
+                shader = k;
+                break;
+            }
+        }
     }
     if (shader < 0) return;
     const Prim& sh = st.prims[shader];
@@ -1101,12 +1104,16 @@ static bool build_mesh(rt_scene* s, const Stage& st, int id, const std::vector<u
     if (!pts || !fvc || !fvi || pts->kind != Value::kNum || pts->comps != 3) { err = p.path + ": mesh without points / faces"; return false; }
     const int np = (int)(pts->num.size() / 3);
     size_t total = 0;
-    for (double c : fvc->num) total += (size_t)c;
+    for (double c : fvc->num) {   // NaN-safe: every count an integer within the index array
+        if (!(c >= 0.0 && c <= (double)fvi->num.size()) || c != std::floor(c)) { total = SIZE_MAX; break; }
+        total += (size_t)c;
+    }
     if (total != fvi->num.size()) { err = p.path + ": faceVertexCounts do not match faceVertexIndices"; return false; }
     for (double v : fvi->num)
-        if (v < 0 || v >= np) { err = p.path + ": face vertex index out of range"; return false; }
+        if (!(v >= 0 && v < np)) { err = p.path + ": face vertex index out of range"; return false; }
     Primvar nrm = primvar(p, "primvars:normals", "vertex");
-    if (!nrm.ok()) nrm = primvar(p, "normals", "vertex");
+    if (!nrm.ok() || nrm.comps < 3) nrm = primvar(p, "normals", "vertex");
+    if (nrm.comps < 3) nrm.v = nullptr;   // normals need three components
     Primvar uv = primvar(p, "primvars:st", "vertex");
     if (!uv.ok())
         for (const auto& kv : p.attrs)
@@ -1115,6 +1122,7 @@ static bool build_mesh(rt_scene* s, const Stage& st, int id, const std::vector<u
                 uv = primvar(p, kv.first, "vertex");
                 break;
             }
+    if (uv.comps < 2) uv.v = nullptr;   // texture coordinates need two components
     Primvar ji = primvar(p, "primvars:skel:jointIndices", "vertex");
     Primvar jw = primvar(p, "primvars:skel:jointWeights", "vertex");
     int es = 1;
@@ -1169,7 +1177,8 @@ static bool build_mesh(rt_scene* s, const Stage& st, int id, const std::vector<u
                     if ((size_t)(src + 1) * es <= ji.v->num.size() && (size_t)(src + 1) * es <= jw.v->num.size()) {
                         w[0] = 0.0f;
                         for (int k = 0; k < std::min(es, 4); ++k) {
-                            jix[k] = (uint16_t)std::max(0.0, ji.v->num[(size_t)src * es + k]);
+                            const double j = ji.v->num[(size_t)src * es + k];
+                            jix[k] = (uint16_t)(j >= 0.0 && j <= 65535.0 ? j : 0.0);
                             w[k] = (float)jw.v->num[(size_t)src * es + k];
                         }
                     }
@@ -1289,15 +1298,12 @@ rt_status rt_scene_add_usd(rt_scene* s, const char* path, const float position[3
     // depth-first walk replaces the previous one, so the last of each wins
     std::vector<int> meshes;
     int skel = -1, anim = -1;
-    std::function<void(int)> walk = [&](int k) {
+    for (int k : st.preorder(0, true)) {
         const usd::Prim& p = st.prims[k];
-        if (!p.active) return;
         if (p.type == "Skeleton") skel = k;
         if (p.type == "SkelAnimation") anim = k;
         if (p.type == "Mesh") meshes.push_back(k);
-        for (int c : p.children) walk(c);
-    };
-    walk(0);
+    }
     if (anim < 0 && skel >= 0) anim = usdscene::find_prim_up(st, skel, "skel:animationSource");
     std::shared_ptr<UsdSkel> sk;
     if (skel >= 0) {

@@ -38,6 +38,25 @@ int Stage::add_prim(int parent, const std::string& name) {
     return id;
 }
 
+// primvar elementSize from a file number (1 when absent, NaN or out of range)
+static int element_size(double d) { return d >= 1.0 && d <= 65536.0 ? (int)d : 1; }
+
+std::vector<int> Stage::preorder(int root, bool active_only) const {
+    std::vector<int> out, todo{root};
+    std::vector<char> seen(prims.size(), 0);
+    while (!todo.empty()) {
+        const int k = todo.back();
+        todo.pop_back();
+        if (k < 0 || (size_t)k >= prims.size() || seen[k]) continue;
+        seen[k] = 1;
+        if (active_only && !prims[k].active) continue;
+        out.push_back(k);
+        const std::vector<int>& ch = prims[k].children;
+        for (size_t i = ch.size(); i-- > 0;) todo.push_back(ch[i]);
+    }
+    return out;
+}
+
 static float half_to_float(uint16_t h) {
     const uint32_t s = (uint32_t)(h >> 15) << 31, e = (h >> 10) & 0x1fu, m = h & 0x3ffu;
     uint32_t bits;
@@ -229,7 +248,18 @@ private:
         return true;
     }
 
+    // nesting of values and prims is bounded: hostile input must not exhaust the stack
+    static constexpr int kMaxDepth = 64;
+    int depth_ = 0;
+    struct Nest {
+        int& d;
+        explicit Nest(int& d_) : d(d_) { ++d; }
+        ~Nest() { --d; }
+    };
+
     bool value(Value& v) {
+        Nest nest(depth_);
+        if (depth_ > kMaxDepth) { msg_ = "values nested too deeply"; return false; }
         const Tok& t = lx_.peek();
         if (t.t == Tok::kPunct && t.s == "[") {
             lx_.next();
@@ -323,6 +353,8 @@ private:
     bool tcps_set_ = false;
 
     bool prim(int parent) {
+        Nest nest(depth_);
+        if (depth_ > kMaxDepth) { msg_ = "prims nested too deeply"; return false; }
         lx_.next();   // specifier
         std::string type;
         if (lx_.peek().t == Tok::kIdent) type = lx_.next().s;
@@ -437,7 +469,7 @@ private:
         if (is_punct("(")) {
             if (!meta_entries([&a](const std::string& k, const Value& v) {
                     if (k == "interpolation" && v.kind == Value::kStr && !v.str.empty()) a.interpolation = v.str[0];
-                    if (k == "elementSize" && v.kind == Value::kNum && !v.num.empty()) a.element_size = (int)v.num[0];
+                    if (k == "elementSize" && v.kind == Value::kNum && !v.num.empty()) a.element_size = element_size(v.num[0]);
                 }))
                 return false;
         }
@@ -544,6 +576,7 @@ bool read_zip(const uint8_t* data, size_t n, std::vector<PackageFile>& files, st
         if (method == 0) {
             f.data.assign(data + off, data + off + csize);
         } else if (method == 8) {
+            if ((uint64_t)usize > 1032ull * csize + 1024) { err = "zip: implausible size of " + f.name; return false; }
             f.data.resize(usize);
             z_stream zs;
             std::memset(&zs, 0, sizeof zs);
@@ -660,6 +693,13 @@ private:
 
     bool fail(const std::string& m) { if (msg_.empty()) msg_ = m; return false; }
     bool has(uint64_t off, uint64_t len) const { return off <= n_ && len <= n_ - off; }
+    // `count` elements of `elem` bytes at `off` (overflow-safe: counts come from the file)
+    bool has_n(uint64_t off, uint64_t count, uint64_t elem) const {
+        return off <= n_ && (elem == 0 || count <= (n_ - off) / elem);
+    }
+    // a decoded element count a file of this size can carry (compressed integers take at least
+    // two bits each before TfFastCompression, whose ratio is below 256:1)
+    bool plausible(uint64_t count) const { return count <= (1ull << 28) && count <= 1024 * (uint64_t)n_ + 1024; }
     bool u64(uint64_t off, uint64_t& v) { if (!has(off, 8)) return fail("read past the end"); std::memcpy(&v, d_ + off, 8); return true; }
     bool u32(uint64_t off, uint32_t& v) { if (!has(off, 4)) return fail("read past the end"); std::memcpy(&v, d_ + off, 4); return true; }
     bool at_least(int a, int b, int c) const {
@@ -717,7 +757,8 @@ private:
                 else { int64_t v; std::memcpy(&v, vp, 8); delta = (SInt)v; }
                 vp += sz;
             }
-            prev = (SInt)((Int)prev + (Int)delta);   // wrapping (uint32 fieldset terminators)
+            typedef typename std::make_unsigned<Int>::type UInt;
+            prev = (SInt)((UInt)prev + (UInt)delta);   // wrapping (uint32 fieldset terminators)
             out[i] = (Int)prev;
         }
         return true;
@@ -729,6 +770,7 @@ private:
         if (!u64(pos, csize)) return false;
         pos += 8;
         if (!has(pos, csize)) return fail("compressed integers past the end");
+        if (!plausible(count)) return fail("implausible integer count");
         if (count == 0) { out.clear(); pos += csize; return true; }
         std::vector<uint8_t> w(sizeof(Int) + (count * 2 + 7) / 8 + count * sizeof(Int) + 64);
         size_t got = 0;
@@ -761,7 +803,7 @@ private:
         if (!s) return fail("no STRINGS section");
         uint64_t count;
         if (!u64(s->start, count)) return false;
-        if (!has(s->start + 8, count * 4)) return fail("bad STRINGS section");
+        if (!has_n(s->start + 8, count, 4)) return fail("bad STRINGS section");
         strings_.resize(count);
         if (count) std::memcpy(strings_.data(), d_ + s->start + 8, count * 4);
         return true;
@@ -775,7 +817,7 @@ private:
         uint64_t rsize;
         if (!u64(pos, rsize)) return false;
         pos += 8;
-        if (!has(pos, rsize)) return fail("bad FIELDS reps");
+        if (!has(pos, rsize) || !plausible(count)) return fail("bad FIELDS reps");
         field_rep_.resize(count);
         size_t got = 0;
         if (!fast_decompress(d_ + pos, rsize, (uint8_t*)field_rep_.data(), count * 8, &got) || got != count * 8)
@@ -799,6 +841,7 @@ private:
         if (!compressed_ints<uint32_t>(pos, count, idx) || !compressed_ints<int32_t>(pos, count, elem) ||
             !compressed_ints<int32_t>(pos, count, jump))
             return false;
+        if (!plausible(total)) return fail("implausible path count");
         paths_.assign(total, std::string());
         // _BuildDecompressedPathsImpl: depth-first, children follow their parent, a positive
         // jump points at the sibling subtree
@@ -851,7 +894,7 @@ private:
     bool index_vector(uint64_t& pos, std::vector<uint32_t>& out) {
         uint64_t count;
         if (!u64(pos, count)) return false;
-        if (!has(pos + 8, count * 4)) return fail("vector past the end");
+        if (!has_n(pos + 8, count, 4)) return fail("vector past the end");
         out.resize(count);
         if (count) std::memcpy(out.data(), d_ + pos + 8, count * 4);
         pos += 8 + count * 4;
@@ -929,7 +972,7 @@ private:
             return fail("unknown float array code");
         }
         const uint64_t eb = (uint64_t)nt.comps * nt.bytes;
-        if (!has(pos, count * eb)) return fail("array past the end");
+        if (!has_n(pos, count, eb)) return fail("array past the end");
         v.num.reserve(count * nt.comps);
         for (uint64_t i = 0; i < count * nt.comps; ++i) v.num.push_back(read_num(d_ + pos + i * nt.bytes, nt.k));
         if (nt.quat) reorder_quats(v);
@@ -1000,7 +1043,7 @@ public:
             uint64_t count, pos = payload;
             if (at_least(0, 7, 0)) { if (!u64(pos, count)) return false; pos += 8; }
             else { uint32_t c; if (!u32(pos, c)) return false; count = c; pos += 4; }
-            if (!has(pos, count * 4)) return fail("token array past the end");
+            if (!has_n(pos, count, 4)) return fail("token array past the end");
             for (uint64_t k = 0; k < count; ++k) {
                 uint32_t i;
                 std::memcpy(&i, d_ + pos + 4 * k, 4);
@@ -1032,7 +1075,7 @@ public:
         case kDoubleVector: {
             uint64_t count;
             if (!u64(payload, count)) return false;
-            if (!has(payload + 8, count * 8)) return fail("double vector past the end");
+            if (!has_n(payload + 8, count, 8)) return fail("double vector past the end");
             v.kind = Value::kNum;
             v.array = true;
             for (uint64_t i = 0; i < count; ++i) v.num.push_back(read_num(d_ + payload + 8 + 8 * i, 'd'));
@@ -1064,7 +1107,7 @@ public:
         if (!unpack(times_rep, times)) return false;
         const uint64_t b = o + ja;
         if (!u64(b, jb) || !u64(b + 8, n)) return false;
-        if (times.num.size() != n || !has(b + 16, n * 8)) return fail("bad time samples");
+        if (times.num.size() != n || !has_n(b + 16, n, 8)) return fail("bad time samples");
         for (uint64_t i = 0; i < n; ++i) {
             uint64_t r;
             std::memcpy(&r, d_ + b + 16 + 8 * i, 8);
@@ -1077,14 +1120,17 @@ public:
     }
 
 private:
+    // the prim at an absolute path, creating missing ancestors (iteratively: paths may be deep)
     static int ensure_prim(Stage& st, const std::string& path) {
-        if (path == "/") return 0;
-        const int have = st.find(path);
-        if (have >= 0) return have;
-        const size_t s = path.find_last_of('/');
-        const std::string parent = s == 0 ? "/" : path.substr(0, s);
-        const int pid = ensure_prim(st, parent);
-        return st.add_prim(pid, path.substr(s + 1));
+        int id = 0;
+        size_t b = 1;
+        while (b < path.size()) {
+            size_t e = path.find('/', b);
+            if (e == std::string::npos) e = path.size();
+            if (e > b) id = st.add_prim(id, path.substr(b, e - b));
+            b = e + 1;
+        }
+        return id;
     }
 
     bool build(Stage& st) {
@@ -1147,7 +1193,7 @@ private:
                     else if (kv.first == "default" && v.kind != Value::kNone) { a.value = v; a.has_default = true; }
                     else if (kv.first == "variability" && !v.num.empty()) a.uniform = v.num[0] == 1.0;
                     else if (kv.first == "interpolation" && !v.str.empty()) a.interpolation = v.str[0];
-                    else if (kv.first == "elementSize" && !v.num.empty()) a.element_size = (int)v.num[0];
+                    else if (kv.first == "elementSize" && !v.num.empty()) a.element_size = element_size(v.num[0]);
                     else if (kv.first == "connectionPaths") a.connections = v.str;
                 }
             }

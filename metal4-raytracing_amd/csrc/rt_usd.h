@@ -76,6 +76,10 @@ struct Stage {
         return it == by_path.end() ? -1 : it->second;
     }
     int add_prim(int parent, const std::string& name);   // returns the existing prim for a repeated path
+    // depth-first pre-order of the subtree at `root` in children order, each prim once (an
+    // explicit stack: a hostile file's path tree may be deep); inactive prims and their subtrees
+    // are left out when active_only
+    std::vector<int> preorder(int root, bool active_only) const;
 };
 
 // One file of a .usdz package.

@@ -14,6 +14,7 @@ import ctypes as C
 import math
 import os
 import shutil
+import struct
 
 import numpy as np
 import pytest
@@ -322,6 +323,58 @@ def test_usd_errors(rt, files, tmp_path):
     with pytest.raises(rt.RTError, match="no meshes"):
         s.add_usd(str(empty), (0, 0, 0))
     assert s.triangle_count == 0
+
+
+def test_hostile_inputs_are_rejected(rt, files, tmp_path):
+    """Input classes tools/fuzz_host.sh (AddressSanitizer + UBSan mutation fuzzing) found crashing
+    the readers: deep prim / value nesting (stack), huge element counts (allocation), a zip entry
+    claiming a huge inflated size, NaN and fractional face counts / indices, two-component
+    normals.  Each must be an error or a clean load, never a crash."""
+    s = rt.Scene()
+    deep = tmp_path / "deep.usda"
+    deep.write_text("#usda 1.0\n" + 'def Xform "x" {\n' * 5000 + "}\n" * 5000)
+    with pytest.raises(rt.RTError, match="nested too deeply"):
+        s.add_usd(str(deep), (0, 0, 0))
+    nest = tmp_path / "nest.usda"
+    nest.write_text('#usda 1.0\ndef Mesh "m" {\n  int[] faceVertexCounts = ' + "(" * 5000 + "3" + ")" * 5000 + "\n}\n")
+    with pytest.raises(rt.RTError, match="nested too deeply"):
+        s.add_usd(str(nest), (0, 0, 0))
+    mesh = '#usda 1.0\ndef Mesh "m" {\n  int[] faceVertexCounts = [%s]\n  int[] faceVertexIndices = [%s]\n' \
+           '  point3f[] points = [(0, 0, 0), (1, 0, 0), (0, 1, 0)]\n%s}\n'
+    for counts, idx in [("3.5", "0, 1, 2"), ("nan", "0, 1, 2"), ("-3", "0, 1, 2"), ("3", "0, 1, nan"),
+                        ("3", "0, 1, 1e300")]:
+        bad = tmp_path / "bad_counts.usda"
+        bad.write_text(mesh % (counts, idx, ""))
+        with pytest.raises(rt.RTError, match="faceVertex|face vertex"):
+            s.add_usd(str(bad), (0, 0, 0))
+    n2 = tmp_path / "n2.usda"   # normals of two components: ignored, computed from the faces
+    n2.write_text(mesh % ("3", "0, 1, 2", '  float2[] primvars:normals = [(0, 1), (0, 1), (0, 1)] (\n'
+                          '    interpolation = "vertex"\n  )\n  texCoord2f[] primvars:st = [1, 2, 3] (\n'
+                          '    interpolation = "vertex"\n  )\n'))
+    s2 = rt.Scene()
+    s2.add_usd(str(n2), (0, 0, 0))
+    assert s2.triangle_count == 1
+    # a crate whose PATHS count claims 2^40 entries
+    data = bytearray(open(files["robot.usdc"], "rb").read())
+    toc = struct.unpack_from("<Q", data, 16)[0]
+    nsec = struct.unpack_from("<Q", data, toc)[0]
+    for k in range(nsec):
+        name = bytes(data[toc + 8 + 32 * k: toc + 24 + 32 * k]).rstrip(b"\0")
+        start = struct.unpack_from("<Q", data, toc + 24 + 32 * k)[0]
+        if name == b"PATHS":
+            struct.pack_into("<Q", data, start, 1 << 40)
+    huge = tmp_path / "huge.usdc"
+    huge.write_bytes(bytes(data))
+    with pytest.raises(rt.RTError, match="implausible"):
+        s.add_usd(str(huge), (0, 0, 0))
+    # a deflated zip entry claiming 4 GB
+    z = bytearray(W.write_usdz("robot.usdc", open(files["robot.usdc"], "rb").read(), deflate=True))
+    cd = z.rfind(b"PK\x01\x02")
+    struct.pack_into("<I", z, cd + 24, 0xFFFFFFF0)
+    zf = tmp_path / "huge.usdz"
+    zf.write_bytes(bytes(z))
+    with pytest.raises(rt.RTError, match="implausible"):
+        s.add_usd(str(zf), (0, 0, 0))
 
 
 def test_lz4_and_integer_coding_round_trips(rt, files, tmp_path):

@@ -1,0 +1,42 @@
+"""Seed inputs for tools/fuzz_host.cpp: the skinned test asset of tests/test_usd.py as .usda,
+.usdc and .usdz (crate + PNG texture), and the test PNG.  Usage: python tools/fuzz_seeds.py DIR"""
+import os
+import sys
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "tests"))
+import usd_writers as W  # noqa: E402
+from test_usd import TEX, robot_prims  # noqa: E402
+
+out = sys.argv[1]
+os.makedirs(out, exist_ok=True)
+prims, _ = robot_prims()
+crate = W.write_usdc(prims)
+files = {
+    "seed.usda": W.write_usda(prims).encode() if isinstance(W.write_usda(prims), str) else W.write_usda(prims),
+    "seed.usdc": crate,
+    "seed.usdz": W.write_usdz("robot.usdc", crate, [("textures/tex.png", TEX)]),
+    "seed.png": TEX,
+    # a quad and a triangle with normals, texture coordinates, negative indices and a polygon
+    "seed.obj": b"""# fuzz seed
+o quad
+v 0 0 0
+v 1 0 0
+v 1 1 0
+v 0 1 0
+v 0.5 1.5 0.2
+vn 0 0 1
+vt 0 0
+vt 1 0
+vt 1 1
+vt 0 1
+f 1/1/1 2/2/1 3/3/1 4/4/1
+f -1 -2 -3
+usemtl none
+f 1//1 3//1 5//1
+f 2/2 3/3 5/1
+""",
+}
+for k, v in files.items():
+    with open(os.path.join(out, k), "wb") as f:
+        f.write(v)
+print(" ".join(sorted(files)))
