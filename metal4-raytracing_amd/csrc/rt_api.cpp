@@ -37,6 +37,7 @@ struct MeshInfo {
 struct FrameSlot {
     DevBuf color, accum, meta, q0, q1, hits, sq, counts, extra, sorted, sort_table, sort_total, params, pray, psray;
     DevBuf depth, gbuffer, counters;
+    DevBuf prim_hit;   // wavefront: per pixel, sample 0's last bounce-0 hit (id, u, v) for wf_motion
     WavefrontBuffers wf;
     WfTimeline wft;
     WfFrameStats wfs{};
@@ -46,8 +47,8 @@ struct FrameSlot {
     bool pending = false, wavefront = false, used = false;
     uint64_t seq = 0;                           // frame number (harvest order)
     int gen = 0;                                // geometry generation the frame reads
-    DevBuf* bufs[18] = {&color, &accum, &meta, &q0, &q1, &hits, &sq, &counts, &extra, &sorted,
-                        &sort_table, &sort_total, &params, &pray, &psray, &depth, &gbuffer, &counters};
+    DevBuf* bufs[19] = {&color, &accum, &meta, &q0, &q1, &hits, &sq, &counts, &extra, &sorted,
+                        &sort_table, &sort_total, &params, &pray, &psray, &depth, &gbuffer, &counters, &prim_hit};
 };
 // Per-frame geometry (what skinning, instance transforms and refit rewrite between frames), in
 // kGens generations used round robin: frames read generation `gcur`; the first update after a frame
@@ -843,6 +844,7 @@ rt_status rt_resize(rt_ctx* c, int32_t w, int32_t h, const uint32_t* offsets) {
         if ((st = dev_alloc(c, f.depth, n * 4))) return st;
         HIPC(c, hipMemsetAsync(f.depth.p, 0, n * 4, c->stream));
         dev_free(f.gbuffer);
+        dev_free(f.prim_hit);
         f.used = false;
         f.pending = false;
     }
@@ -1025,6 +1027,7 @@ rt_status rt_render_frame(rt_ctx* c, const Uniforms* U, const rt_tile_set* tiles
     P.depth = (float*)F.depth.p;
     P.motion = (float2*)c->d_motion[m_out].p;
     P.gbuffer = U->enableDenoiseGBuffer ? (float4*)F.gbuffer.p : nullptr;
+    P.prim_hit = nullptr;
     P.counters = (unsigned long long*)F.counters.p;
     P.tile_size = ts;
     P.rank = rank;
@@ -1032,6 +1035,8 @@ rt_status rt_render_frame(rt_ctx* c, const Uniforms* U, const rt_tile_set* tiles
     P.tiles_x = tiles_x;
     if (wavefront) {
         if ((st = ensure_wavefront(c, F, (size_t)own * ts * ts, spp, max_extra))) return st;
+        if ((st = dev_alloc(c, F.prim_hit, n * 16))) return st;
+        P.prim_hit = (uint4*)F.prim_hit.p;
         F.wf.motion_prev = (float2*)c->d_motion[m_prev].p;
     }
     HIPC(c, hipMemsetAsync(F.counters.p, 0, sizeof(unsigned long long) * kCounterWords, stream));

@@ -24,6 +24,7 @@ struct FrameParams {
     float* depth;
     float2* motion;            // read (previous frame) + write, in place
     float4* gbuffer;           // 4 planes or null
+    uint4* prim_hit;           // wavefront: sample 0's last bounce-0 hit per pixel (wf_motion input)
     unsigned long long* counters;
     int tile_size, rank, nranks, tiles_x;
 };

@@ -124,11 +124,49 @@ __host__ __device__ __forceinline__ bool needs_full(const Uniforms& U, const Dev
     return U.debugTextureMode != DebugTextureModeNone || U.enableDenoiseGBuffer != 0 || S.textured != 0;
 }
 
+// Depth and motion vector of a bounce-0 hit of sample 0 (Raytracing.metal:342-389): the hit
+// point through this frame's and the previous frame's instance transforms and cameras.  Inline in
+// the per-pixel kernel; the wavefront kernels record the hit and wf_motion evaluates this once
+// per pixel after the pass (the last bounce-0 hit of sample 0 wins either way).
+__device__ __forceinline__ void primary_outputs(const DevScene& S, const Uniforms& U, uint32_t id, float bu, float bv,
+                                                float& depth_out, f2& motion_out) {
+    const uint4 ti = S.tri_info[id];
+    const int instanceIndex = (int)(ti.w >> 8);
+    const float* M = S.inst + 12 * instanceIndex;
+    const float bw = (1.0f - bu) - bv;
+    const Camera& cam = U.camera;
+    const f3 cright = ldf3(cam.right), cup = ldf3(cam.up), cfwd = ldf3(cam.forward);
+    f3 op = (bu * ld3(S.pos[ti.y]) + bv * ld3(S.pos[ti.z])) + bw * ld3(S.pos[ti.x]);
+    f3 pp = (bu * ld3(S.prev_pos[ti.y]) + bv * ld3(S.prev_pos[ti.z])) + bw * ld3(S.prev_pos[ti.x]);
+    f3 worldPos = xform(M, op, 1.0f);
+    f3 prevWorldPos = xform(S.prev_inst + 12 * instanceIndex, pp, 1.0f);
+    f3 viewPos = worldPos - ldf3(cam.position);
+    float sx = dot(viewPos, cright), sy = dot(viewPos, cup);
+    float depth = dot(viewPos, cfwd);
+    depth_out = fmaxf(depth, 1.0e-3f);
+    float dd = fmaxf(depth, 0.001f);
+    sx = sx / dd;
+    sy = sy / dd;
+    const Camera& pc = U.previousCamera;
+    f3 pv = prevWorldPos - ldf3(pc.position);
+    float psx = dot(pv, ldf3(pc.right)), psy = dot(pv, ldf3(pc.up));
+    float pd = fmaxf(dot(pv, ldf3(pc.forward)), 0.001f);
+    psx = psx / pd;
+    psy = psy / pd;
+    float mnx = sx - psx, mny = sy - psy;
+    float rightScale = fmaxf(length(cright), 1e-5f);
+    float upScale = fmaxf(length(cup), 1e-5f);
+    float mpx = mnx * ((float)U.width / (2.0f * rightScale));
+    float mpy = mny * ((float)U.height / (2.0f * upScale));
+    motion_out.x = mpx;
+    motion_out.y = -mpy;
+}
+
 // prevMotion / hadPrimaryHit / motionVector: only read by DebugTextureModeMotion.
 // FULL = false compiles out the texture maps, the debug-visualisation and the G-buffer branches
 // (the caller selects FULL = true whenever the scene is textured, uniforms.debugTextureMode != 0
 // or enableDenoiseGBuffer != 0).
-template <bool FULL>
+template <bool FULL, bool INLINE_PRIMARY = true>
 __device__ __forceinline__ void shade_step(const DevScene& S, const Uniforms& U, const ShadeTabs& halton, int hidx,
                                            int sampleIndex, f3& rayO, f3& rayD, const Hit& h, PathRegs& p,
                                            bool gbuf_pending, f2 prevMotion, bool hadPrimaryHit, f2 motionVector,
@@ -148,31 +186,8 @@ __device__ __forceinline__ void shade_step(const DevScene& S, const Uniforms& U,
     f3 cright = ldf3(cam.right), cup = ldf3(cam.up), cfwd = ldf3(cam.forward);
 
     if (p.bounce == 0 && sampleIndex == 0) {                                            // :342-389
-        f3 op = (bu * ld3(S.pos[ti.y]) + bv * ld3(S.pos[ti.z])) + bw * ld3(S.pos[ti.x]);
-        f3 pp = (bu * ld3(S.prev_pos[ti.y]) + bv * ld3(S.prev_pos[ti.z])) + bw * ld3(S.prev_pos[ti.x]);
-        f3 worldPos = xform(M, op, 1.0f);
-        f3 prevWorldPos = xform(S.prev_inst + 12 * instanceIndex, pp, 1.0f);
-        f3 viewPos = worldPos - ldf3(cam.position);
-        float sx = dot(viewPos, cright), sy = dot(viewPos, cup);
-        float depth = dot(viewPos, cfwd);
-        r.depth = fmaxf(depth, 1.0e-3f);
-        float dd = fmaxf(depth, 0.001f);
-        sx = sx / dd;
-        sy = sy / dd;
-        const Camera& pc = U.previousCamera;
-        f3 pv = prevWorldPos - ldf3(pc.position);
-        float psx = dot(pv, ldf3(pc.right)), psy = dot(pv, ldf3(pc.up));
-        float pd = fmaxf(dot(pv, ldf3(pc.forward)), 0.001f);
-        psx = psx / pd;
-        psy = psy / pd;
-        float mnx = sx - psx, mny = sy - psy;
-        float rightScale = fmaxf(length(cright), 1e-5f);
-        float upScale = fmaxf(length(cup), 1e-5f);
-        float mpx = mnx * ((float)U.width / (2.0f * rightScale));
-        float mpy = mny * ((float)U.height / (2.0f * upScale));
-        r.motion.x = mpx;
-        r.motion.y = -mpy;
-        r.primary = true;
+        if (INLINE_PRIMARY) primary_outputs(S, U, h.id, bu, bv, r.depth, r.motion);
+        r.primary = true;   // deferred: the caller records the hit for wf_motion
     }
 
     f3 objN = (bu * ld3(S.nrm[ti.y]) + bv * ld3(S.nrm[ti.z])) + bw * ld3(S.nrm[ti.x]); // :391

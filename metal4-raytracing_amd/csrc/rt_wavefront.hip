@@ -252,11 +252,10 @@ __device__ __forceinline__ void flush_counters(const FrameParams& P, uint32_t cl
 }
 
 // per-pixel outputs of a shade step (depth / motion / G-buffer, :342-389, :506-515)
-__device__ __forceinline__ void write_pixel_outputs(const FrameParams& P, uint32_t pix, const StepResult& r, bool full) {
-    if (r.primary) {
-        P.depth[pix] = r.depth;
-        P.motion[pix] = make_float2(r.motion.x, r.motion.y);
-    }
+// (depth and motion: the hit is recorded and wf_motion evaluates it after the pass)
+__device__ __forceinline__ void write_pixel_outputs(const FrameParams& P, uint32_t pix, const StepResult& r, const Hit& h,
+                                                    bool full) {
+    if (r.primary) P.prim_hit[pix] = make_uint4(h.id, __float_as_uint(h.u), __float_as_uint(h.v), 0u);
     if (full && r.gbuf && P.gbuffer) {
         size_t plane = (size_t)P.U.width * P.U.height;
         P.gbuffer[pix] = r.g0;
@@ -304,6 +303,7 @@ __global__ void __launch_bounds__(kBlock) wf_generate(DevScene S, const FramePar
             if (s == 0) {  // per-pixel defaults (:252-261)
                 P.depth[pix] = 1.0e8f;
                 P.motion[pix] = make_float2(0.0f, 0.0f);
+                P.prim_hit[pix] = make_uint4(0xffffffffu, 0u, 0u, 0u);
                 if (P.gbuffer) {
                     size_t plane = (size_t)U.width * U.height;
                     float4 z = make_float4(0, 0, 0, 0);
@@ -408,9 +408,9 @@ __global__ void __launch_bounds__(kBlock) RT_SHADE_ATTR wf_shade(DevScene S, con
                 int sample = (int)meta.y;
                 rayO = ld3(o);
                 rayD = ld3(d);
-                shade_step<FULL>(S, U, halton, (int)meta.w, sample, rayO, rayD, h, p, sample == 0 && p.step == 0,
+                shade_step<FULL, false>(S, U, halton, (int)meta.w, sample, rayO, rayD, h, p, sample == 0 && p.step == 0,
                                  zero2, false, zero2, r);
-                write_pixel_outputs(P, meta.x, r, FULL);
+                write_pixel_outputs(P, meta.x, r, h, FULL);
                 if (r.next) Q.W.p_color[pid] = make_float4(p.color.x, p.color.y, p.color.z, 0.0f);
                 // radiance only changes on emissive hits (:585-586): skip the store otherwise
                 if (__float_as_uint(p.accum.x) != __float_as_uint(a.x) || __float_as_uint(p.accum.y) != __float_as_uint(a.y) ||
@@ -866,9 +866,9 @@ __global__ void __launch_bounds__(kBlock) wf_finish(DevScene S, const FrameParam
         if (trace8<false, COUNT>(S, rayO, rayD, 0.0f, INFINITY, h, stack, tc, overflow)) {
             const int sample = (int)meta.y;
             StepResult r;
-            shade_step<FULL>(S, U, halton, (int)meta.w, sample, rayO, rayD, h, p, sample == 0 && p.step == 0, zero2,
+            shade_step<FULL, false>(S, U, halton, (int)meta.w, sample, rayO, rayD, h, p, sample == 0 && p.step == 0, zero2,
                              false, zero2, r);
-            write_pixel_outputs(P, meta.x, r, FULL);
+            write_pixel_outputs(P, meta.x, r, h, FULL);
             if (r.shadow) {
                 Hit sh;
                 n_shadow++;
@@ -905,6 +905,9 @@ __global__ void __launch_bounds__(kBlock) wf_finish(DevScene S, const FrameParam
 // shadow ray, its next ray, or the next path of the queue.  A wave therefore costs the sum of its
 // own lanes' steps, not the sum over segments of the slowest lane's traversal: the glass paths
 // left at the tail (up to ~20 segments) no longer wait for their wave's worst ray every segment.
+#ifndef RT_FINISH_REBUILD
+#define RT_FINISH_REBUILD 1
+#endif
 template <bool COUNT, bool FULL, int WAVES>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES, WAVES)))
 wf_finish_step(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int cur) {
@@ -914,6 +917,9 @@ wf_finish_step(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int c
     __shared__ uint4 lds_top[RT_TOP_FINISH * 5];
     __shared__ HaltonDim lds_halton[kHaltonLds];
     __shared__ MatRec lds_mat[kMatLds];
+#if RT_FINISH_REBUILD
+    __shared__ float lds_sray[6][kBlock];   // each lane's shadow ray (origin, direction)
+#endif
     int* stack = &lds_stack[threadIdx.x];
     const uint32_t n_top = (uint32_t)min(S.num_nodes8, RT_TOP_FINISH);
     for (uint32_t i = threadIdx.x; i < n_top * 5; i += kBlock) lds_top[i] = reinterpret_cast<const uint4*>(S.nodes8)[i];
@@ -1154,13 +1160,21 @@ wf_finish_step(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int c
                 h.v = bv;
                 const int sample = (int)meta.y;
                 StepResult r;
-                shade_step<FULL>(S, U, halton, (int)meta.w, sample, rayO, rayD, h, p, sample == 0 && p.step == 0,
+                shade_step<FULL, false>(S, U, halton, (int)meta.w, sample, rayO, rayD, h, p, sample == 0 && p.step == 0,
                                  zero2, false, zero2, r);
-                write_pixel_outputs(P, meta.x, r, FULL);
+                write_pixel_outputs(P, meta.x, r, h, FULL);
                 next = r.next;
                 if (r.shadow) {
                     contrib = r.contrib;
                     start_trace(r.so, r.sd, r.stmax);
+#if RT_FINISH_REBUILD
+                    lds_sray[0][threadIdx.x] = r.so.x;
+                    lds_sray[1][threadIdx.x] = r.so.y;
+                    lds_sray[2][threadIdx.x] = r.so.z;
+                    lds_sray[3][threadIdx.x] = r.sd.x;
+                    lds_sray[4][threadIdx.x] = r.sd.y;
+                    lds_sray[5][threadIdx.x] = r.sd.z;
+#endif
                     mode = kShadow;
                     n_shadow++;
                 } else if (r.next) {
@@ -1172,6 +1186,17 @@ wf_finish_step(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int c
                     end_path();
                 }
             }
+#if RT_FINISH_REBUILD
+            // Every lane's ray setup is rebuilt from its ray (a pure function of it, so bit for bit
+            // the one start_trace made): the ~19 registers of the traversing lanes' setups are
+            // then dead while the shading code runs, which sets the kernel's register peak.
+            if (mode == kShadow) {
+                R = ray_setup(mk3(lds_sray[0][threadIdx.x], lds_sray[1][threadIdx.x], lds_sray[2][threadIdx.x]),
+                              mk3(lds_sray[3][threadIdx.x], lds_sray[4][threadIdx.x], lds_sray[5][threadIdx.x]));
+            } else {
+                R = ray_setup(rayO, rayD);
+            }
+#endif
         }
     }
     if (Q.diag) {
@@ -1500,9 +1525,9 @@ wf_finish_q(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int cur)
                 f3 rayO = ld3(o), rayD = ld3(d);
                 const int sample = (int)meta.y;
                 StepResult r;
-                shade_step<FULL>(S, U, halton, (int)meta.w, sample, rayO, rayD, h, pr, sample == 0 && pr.step == 0,
+                shade_step<FULL, false>(S, U, halton, (int)meta.w, sample, rayO, rayD, h, pr, sample == 0 && pr.step == 0,
                                  zero2, false, zero2, r);
-                write_pixel_outputs(P, meta.x, r, FULL);
+                write_pixel_outputs(P, meta.x, r, h, FULL);
                 Q.W.p_accum[spid] = make_float4(pr.accum.x, pr.accum.y, pr.accum.z, 0.0f);
                 if (r.next) {
                     Q.W.p_color[spid] = make_float4(pr.color.x, pr.color.y, pr.color.z, 0.0f);
@@ -1578,6 +1603,29 @@ __global__ void __launch_bounds__(kBlock) wf_extra(DevScene S, const FrameParams
     if (i < Q.own_pixels) Q.W.px_extra[i] = make_uint2(start, (uint32_t)e);
     TraceCounters tc{0, 0};
     flush_counters(P, 0, 0, (uint32_t)e, tc, false, false);
+}
+
+// ---- depth + motion (:342-389) ----------------------------------------------------------------------
+// After the base pass: every own pixel whose sample 0 had a bounce-0 hit gets the depth and motion
+// vector of the last such hit (the value the per-pixel kernel leaves, since each of those hits
+// overwrites it), evaluated here once instead of inside every shading launch, where it would
+// hold ~25 VGPRs of transforms and cameras.
+__global__ void __launch_bounds__(kBlock) wf_motion(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q) {
+    const FrameParams& P = *Pp;
+    const Uniforms& U = P.U;
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= Q.own_pixels) return;
+    int px, py;
+    own_pixel(P, i, px, py);
+    if (px >= U.width || py >= U.height) return;
+    const size_t pix = (size_t)py * U.width + px;
+    const uint4 ph = P.prim_hit[pix];
+    if (ph.x == 0xffffffffu) return;   // no bounce-0 hit: generate's defaults stay
+    float depth;
+    f2 mv;
+    primary_outputs(S, U, ph.x, __uint_as_float(ph.y), __uint_as_float(ph.z), depth, mv);
+    P.depth[pix] = depth;
+    P.motion[pix] = make_float2(mv.x, mv.y);
 }
 
 // ---- resolve (:777, :792-819) -------------------------------------------------------------------------
@@ -1666,7 +1714,14 @@ static void launch_finish(const DevScene& S, const FrameParams& P, const WfParam
     static const int waves = env_int("RT_FINISH_WAVES", 4);
     // Q.finish_frac < 100: the finish kernel takes that share of the resident grid, the rest of
     // the machine stays free for the next frame's kernels (frames in flight)
-    if (STEP && Q.finish_frac < 100 && waves == 3) {
+    if (STEP && Q.finish_frac < 100 && waves == 5) {
+        static const unsigned full_cap = resident_grid(wf_finish_step<COUNT, FULL, 5>, 2);
+        const unsigned cap = std::max(1u, full_cap * (unsigned)Q.finish_frac / 100u);
+        hipLaunchKernelGGL((wf_finish_step<COUNT, FULL, 5>), dim3(grid_for(n, cap)), dim3(kBlock), 0, stream, S, Q.Pd, Q, cur);
+    } else if (STEP && waves == 5) {
+        static const unsigned cap = resident_grid(wf_finish_step<COUNT, FULL, 5>, 2);
+        hipLaunchKernelGGL((wf_finish_step<COUNT, FULL, 5>), dim3(grid_for(n, cap)), dim3(kBlock), 0, stream, S, Q.Pd, Q, cur);
+    } else if (STEP && Q.finish_frac < 100 && waves == 3) {
         static const unsigned full_cap = resident_grid(wf_finish_step<COUNT, FULL, 3>, 2);
         const unsigned cap = std::max(1u, full_cap * (unsigned)Q.finish_frac / 100u);
         hipLaunchKernelGGL((wf_finish_step<COUNT, FULL, 3>), dim3(grid_for(n, cap)), dim3(kBlock), 0, stream, S, Q.Pd, Q, cur);
@@ -1944,6 +1999,9 @@ static bool record_frame(const DevScene& S, const FrameParams& P, WfParams& Q, b
     WF_CHECK(hipGetLastError());
     if (!E.span(0, err)) return false;
     if (!enqueue_pass(S, P, Q, rounds, count, full, E, err)) return false;
+    hipLaunchKernelGGL(wf_motion, dim3(grid_for(Q.own_pixels, 1u << 30)), dim3(kBlock), 0, stream, S, Q.Pd, Q);
+    WF_CHECK(hipGetLastError());
+    if (!E.span(4, err)) return false;
     if (prev_done) WF_CHECK(hipStreamWaitEvent(stream, prev_done, 0));
     if (with_extra) {
         // second pass over the motion-adaptive extra samples (:779-789), appended to queue 0
@@ -2078,6 +2136,8 @@ bool run_wavefront(const DevScene& S, const FrameParams& P, WavefrontBuffers& W,
 
     if (prev_done) WF_CHECK(hipStreamWaitEvent(stream, prev_done, 0));
     WF_CHECK(hipEventRecord(W.ev[0], stream));
+    hipLaunchKernelGGL(wf_motion, dim3(grid_for(Q.own_pixels, 1u << 30)), dim3(kBlock), 0, stream, S, Q.Pd, Q);
+    WF_CHECK(hipGetLastError());
     if (maxExtra > 0) {
         // the extra-sample pass appends primary rays to queue `cur` (reset here)
         WF_CHECK(hipMemsetAsync(W.counts + cslot(cur * kShards), 0, cslot(kShards) * sizeof(uint32_t), stream));
