@@ -119,7 +119,7 @@ typedef struct rt_opts {
     int32_t pipeline;   /* RT_PIPELINE_* */
     int32_t tail_paths; /* wavefront: below this many live paths the rest of the frame runs in the
                            persistent finish kernel; 0 = default (4194304 one frame at a time,
-                           1572864 / 1048576 / 524288 with 2 / 3 / 4 frames in flight), 1 = never */
+                           1310720 / 1048576 / 524288 with 2 / 3 / 4 frames in flight), 1 = never */
     int32_t sort_bins;  /* wavefront: hits are sorted into this many bins of BVH leaf order between
                            extend and shade (a power of two in [1024, 4096]); 0 = default (no
                            sort), < 0 = no sort.  Never changes the image, only memory locality. */

@@ -64,12 +64,13 @@ struct Geo {
 };
 constexpr int kMaxSlots = 4;
 constexpr int kGens = kMaxSlots;
-// default finish threshold with 2 / 3 / 4 frames in flight (C3g sweeps: 1.5M, 1M and 512K paths;
+// default finish threshold with 2 / 3 / 4 frames in flight (C3g sweeps: 1.25M, 1M and 512K paths;
 // round 2, with the DP-collapsed tree and the lighter shading kernels, two slots: 2M 5.88 / 5.89,
+// 1.57M 5.90 (C3g enters the finish one round earlier between 1.5M and 1.57M live paths),
 // 1.5M 5.97 / 6.02, 1M 6.02 / 6.00 Grays/s; four slots serve the small frames of multi-GPU ranks:
 // 8-way split 2.92 -> 3.46 Grays/s per rank at 512K against 1M in round 1, 256K-786K within noise
 // in round 2, with the finish kernel on 20 % of the grid)
-constexpr int kTailInFlight[kMaxSlots + 1] = {0, 0, 1572864, 1048576, 524288};
+constexpr int kTailInFlight[kMaxSlots + 1] = {0, 0, 1310720, 1048576, 524288};
 // paths a frame allocates (pixels x (spp + motion-adaptive extra samples), what ensure_wavefront
 // sizes a slot for): below, four frames in flight by default.  Every 1080p x 4 spp frame (8.29M
 // base paths) stays at two; a 2-way rank share of it with the default two extra samples (6.2M)
@@ -1054,7 +1055,7 @@ rt_status rt_render_frame(rt_ctx* c, const Uniforms* U, const rt_tile_set* tiles
         F.wfs = WfFrameStats{};
         // finish threshold: with frames in flight the next frames' bulk rounds overlap this
         // frame's tail, so more bulk rounds and a shorter tail pay (kTailInFlight: C3g, 2 in
-        // flight 1.5M paths against the one-frame-at-a-time optimum of 4M; 3 in flight 1M)
+        // flight 1.25M paths against the one-frame-at-a-time optimum of 4M; 3 in flight 1M)
         static const bool tail_env = getenv("RT_TAIL_RAYS") != nullptr;
         const int tail = c->tail_paths ? c->tail_paths : (nfl > 1 && !tail_env ? kTailInFlight[nfl] : 0);
         if (own > 0 && !run_wavefront(S, P, F.wf, own, c->counting, tail, c->sort_bins, extra_pass, nfl, stream,

@@ -2087,8 +2087,11 @@ bool run_wavefront(const DevScene& S, const FrameParams& P, WavefrontBuffers& W,
     // share): 20 %, per-rank 4-way split 4.48 -> 4.69 Grays/s against 25 %; a large frame forced
     // to four slots keeps 25 % (the 20 % sweep covered rank shares only)
     static const int finish_frac = env_int("RT_FINISH_FRAC", 0);
+    // (round 2, two slots at the 1.25M threshold: 30 % 5.88 / 5.84, 35 % 5.97 / 6.00, 40 % 6.03 /
+    // 6.01, 45 % 6.07 / 5.99, 50 % 5.93 / 5.90 Grays/s)
     Q.finish_frac = finish_frac > 0 ? min(finish_frac, 100)
-                  : (in_flight >= 4 && Q.base_paths < (6u << 20)) ? 20 : (in_flight > 1 ? 100 / in_flight : 100);
+                  : (in_flight >= 4 && Q.base_paths < (6u << 20)) ? 20
+                  : in_flight == 2 ? 40 : (in_flight > 1 ? 100 / in_flight : 100);
     Q.prio = (prio && Q.finish_step == 1 && W.sorted) ? 1 : 0;
     if (Q.finish_step == 2 && (!W.p_ray || !W.p_sray)) {
         *err = "wave-queue finish kernel without its path ray slots";
