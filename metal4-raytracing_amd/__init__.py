@@ -272,7 +272,7 @@ class Renderer:
         opts.pipeline = {"megakernel": 0, "wavefront": 1}[pipeline]
         opts.tail_paths = int(tail_paths)
         opts.sort_bins = int(sort_bins)   # 0 = default hit sort, < 0 = none
-        opts.frames_in_flight = int(frames_in_flight)   # 0 = default (2, or 4 below 6M paths per frame), 1 = one frame at a time
+        opts.frames_in_flight = int(frames_in_flight)   # 0 = default (2; below 8M paths per frame 4, or 8 with GPU_MAX_HW_QUEUES >= 8), 1 = one frame at a time
         ctx = C.c_void_p()
         _check(lib().rt_create(C.byref(opts), C.byref(ctx)))
         object.__setattr__(self, "_ctx", ctx)

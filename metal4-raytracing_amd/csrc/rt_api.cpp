@@ -62,7 +62,7 @@ struct Geo {
     DevBuf* all[9] = {&pos, &prev_pos, &nrm, &inst, &prev_inst, &tris, &nodes, &node_box, &tri_bin};
     uint32_t num_nodes8 = 0;
 };
-constexpr int kMaxSlots = 4;
+constexpr int kMaxSlots = 8;
 constexpr int kGens = kMaxSlots;
 // default finish threshold with 2 / 3 / 4 frames in flight (C3g sweeps: 1.25M, 1M and 512K paths;
 // round 2, with the DP-collapsed tree and the lighter shading kernels, two slots: 2M 5.88 / 5.89,
@@ -70,14 +70,26 @@ constexpr int kGens = kMaxSlots;
 // 1.5M 5.97 / 6.02, 1M 6.02 / 6.00 Grays/s; four slots serve the small frames of multi-GPU ranks:
 // 8-way split 2.92 -> 3.46 Grays/s per rank at 512K against 1M in round 1, 256K-786K within noise
 // in round 2, with the finish kernel on 20 % of the grid)
-constexpr int kTailInFlight[kMaxSlots + 1] = {0, 0, 1310720, 1048576, 524288};
+constexpr int kTailInFlight[kMaxSlots + 1] = {0, 0, 1310720, 1048576, 524288, 524288, 524288, 524288, 524288};
 // paths a frame allocates (pixels x (spp + motion-adaptive extra samples), what ensure_wavefront
-// sizes a slot for): below, four frames in flight by default.  Every 1080p x 4 spp frame (8.29M
+// sizes a slot for): below, four or eight frames in flight by default (small_frame_slots).  Every 1080p x 4 spp frame (8.29M
 // base paths) stays at two; a 2-way rank share of it with the default two extra samples (6.2M)
 // and the 720p x 4 frame of configs[1] (5.5M) take four.  A slot costs ~300 B per allocated path
 // (128 B path state and ray slots + 176 B of queues), 3.7 GB for 12.4M paths.
 constexpr uint64_t kSmallFrame = 8000000;
 constexpr int kMotionTargets = kMaxSlots + 1;
+// Slots for a small frame: eight when the HIP runtime gives the process at least eight hardware
+// queues (GPU_MAX_HW_QUEUES, read once; HIP's default is 4), so every slot's stream has a queue of
+// its own; four otherwise (more streams than queues serialise unrelated frames: eight slots on
+// four queues measured 2.85 against 3.54 Grays/s per rank).  8-way rank share of C3g, eight
+// queues: 4 slots 3.54 / 3.52, 8 slots 3.71 / 3.69; 4-way 4.73 / 4.70 -> 4.76 / 4.86.
+static int small_frame_slots() {
+    static const int n = [] {
+        const char* e = getenv("GPU_MAX_HW_QUEUES");
+        return (e && atoi(e) >= 8) ? 8 : 4;
+    }();
+    return n;
+}
 }  // namespace
 
 struct rt_ctx {
@@ -966,7 +978,7 @@ rt_status rt_render_frame(rt_ctx* c, const Uniforms* U, const rt_tile_set* tiles
     int nfl = 1;
     if (wavefront && c->stream == c->own_stream) {
         const uint64_t frame_paths = (uint64_t)own * ts * ts * (uint64_t)(spp + max_extra);
-        nfl = c->max_in_flight > 0 ? c->max_in_flight : (frame_paths < kSmallFrame ? kMaxSlots : 2);
+        nfl = c->max_in_flight > 0 ? c->max_in_flight : (frame_paths < kSmallFrame ? small_frame_slots() : 2);
     }
     const int k = c->frame_no > 0 ? (c->last_slot + 1) % nfl : 0;
     FrameSlot& F = c->slot[k];

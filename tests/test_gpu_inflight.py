@@ -4,6 +4,8 @@ one until its extra-sample pass and resolve, which read that frame's accumulatio
 outputs.  The images, auxiliary targets and ray counts must be bit-identical to rendering one
 frame at a time, through camera motion (EMA history, motion vectors, motion-adaptive extra
 samples) and through scene updates between frames (which drain the frames in flight)."""
+import os
+
 import numpy as np
 import pytest
 
@@ -44,7 +46,7 @@ def _run(rt, sc, desc, pipeline, fif, frames, move_at=None, gbuffer=False):
     return R, img, depth, motion, gb, st
 
 
-@pytest.mark.parametrize("pipeline,fif", [(p, 2) for p in PIPELINES] + [("wavefront", 3), ("wavefront-mixed", 3), ("wavefront", 4), ("wavefront-mixed", 4)])
+@pytest.mark.parametrize("pipeline,fif", [(p, 2) for p in PIPELINES] + [("wavefront", 3), ("wavefront-mixed", 3), ("wavefront", 4), ("wavefront-mixed", 4), ("wavefront", 8)])
 def test_in_flight_matches_serial(rt, assets, pipeline, fif):
     sc = rt.Scene.preset("c2", assets)
     desc = sc.desc()
@@ -94,7 +96,8 @@ def test_in_flight_then_megakernel_frame(rt, assets):
         assert np.array_equal(out[0][1], mot)
 
 
-@pytest.mark.parametrize("fif,expect", [(2, 2), (0, 4)])   # 0: the library default for a rank's small frame
+# 0: the library default for a rank's small frame (eight slots with eight hardware queues)
+@pytest.mark.parametrize("fif,expect", [(2, 2), (0, 8 if int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) >= 8 else 4)])
 def test_in_flight_tile_gather(rt, assets, fif, expect):
     """Two ranks' renderers (tile split, frames in flight) with the per-frame gather enqueued on
     a separate stream without host waits (rank 1 packs, rank 0 unpacks, the pattern of
