@@ -133,6 +133,36 @@ def test_tiles_bitwise(rt, assets, pipeline):
 
 
 @pytest.mark.parametrize("pipeline", PIPELINES)
+def test_tiles_depth_motion(rt, assets, pipeline):
+    """A rank's depth and motion vectors (evaluated per own pixel by wf_motion after the pass)
+    equal the full frame's on its tiles, after a camera move."""
+    scene = rt.Scene.preset("c1", assets)
+    W, H, T, n = 200, 136, 64, 3
+    rs = [make_renderer(rt, scene, W, H, pipeline, seed=5) for _ in range(n + 1)]
+    cam0 = rs[0].camera
+    for i in range(2):
+        for k, R in enumerate(rs):
+            R.maxBounces = 3
+            c = rt.Camera()
+            c.position = type(cam0.position)(cam0.position.x + 0.04 * i, cam0.position.y, cam0.position.z, 0.0)
+            c.right, c.up, c.forward = cam0.right, cam0.up, cam0.forward
+            R.camera = c
+            R.draw() if k == 0 else R.draw(tiles=(T, k - 1, n))
+    ref_d, ref_m, _ = rs[0].aux()
+    assert np.abs(ref_m).max() > 0
+    tx = (W + T - 1) // T
+    seen = np.zeros((H, W), bool)
+    for rank in range(n):
+        d, m, _ = rs[rank + 1].aux()
+        for tid in range(rank, tx * ((H + T - 1) // T), n):
+            x0, y0 = (tid % tx) * T, (tid // tx) * T
+            sl = (slice(y0, min(y0 + T, H)), slice(x0, min(x0 + T, W)))
+            assert np.array_equal(d[sl], ref_d[sl]) and np.array_equal(m[sl], ref_m[sl]), (rank, tid)
+            seen[sl] = True
+    assert seen.all()
+
+
+@pytest.mark.parametrize("pipeline", PIPELINES)
 def test_counting_frame_matches(rt, assets, pipeline):
     """Counting frames produce the same image; node/triangle counters are populated."""
     scene = rt.Scene.preset("c1", assets)
