@@ -85,7 +85,10 @@ constexpr int kWfDiagHist = 50 * kCntStride;        // 64 words: wf_finish wave 
 constexpr int kWfDiagSteps = kWfDiagHist + 64;        // 66 words: wf_trace steps-per-ray histograms + max
 constexpr int kWfStat = kWfDiagSteps + 66;              // 3 words: rounds, wf_trace launches, their rays
 constexpr int kStatRounds = 0, kStatTraceLaunches = 1, kStatTraceRays = 2, kStatExtendRays = 3, kStatFinish = 4;
-constexpr int kWfCountWords = 50 * kCntStride + 64 + 66 + 5;
+// wf_finish_step diagnostics (RT_WF_LOG): summed over waves, s_memrealtime ticks (10 ns) spent in
+// shading passes and in total, shading passes and lanes shaded
+constexpr int kStatDiagShadeT = 5, kStatDiagTotalT = 6, kStatDiagPasses = 7, kStatDiagShaded = 8;
+constexpr int kWfCountWords = 50 * kCntStride + 64 + 66 + 9;
 __host__ __device__ constexpr uint32_t cslot(int c) { return (uint32_t)c * kCntStride; }
 struct WavefrontBuffers {
     size_t queue_entries = 0;     // kShards segments of queue_entries / kShards

@@ -974,6 +974,8 @@ wf_finish_step(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int c
     // time (s_memrealtime, 100 MHz) of the slowest wave
     uint32_t segs = 0, max_segs = 0, iters = 0;
     const uint64_t t_start = Q.diag ? __builtin_amdgcn_s_memrealtime() : 0;
+    uint64_t t_shade = 0;
+    uint32_t n_pass = 0, n_shaded = 0;
     auto end_path = [&]() {
         Q.W.p_accum[pid] = make_float4(p.accum.x, p.accum.y, p.accum.z, 0.0f);
         mode = kIdle;
@@ -1152,6 +1154,11 @@ wf_finish_step(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int c
         const unsigned long long ready = __ballot(mode == kReady);
         if (ready != 0ull &&
             (__popcll(ready) >= Q.shade_min || __ballot(mode == kClosest || mode == kShadow) == 0ull)) {
+            const uint64_t ts0 = Q.diag ? __builtin_amdgcn_s_memrealtime() : 0;
+            if (Q.diag) {
+                ++n_pass;
+                n_shaded += (uint32_t)__popcll(ready);
+            }
             if (mode == kReady) {
                 Hit h;
                 h.t = best;
@@ -1197,10 +1204,17 @@ wf_finish_step(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int c
                 R = ray_setup(rayO, rayD);
             }
 #endif
+            if (Q.diag) t_shade += __builtin_amdgcn_s_memrealtime() - ts0;
         }
     }
     if (Q.diag) {
         const uint32_t dt = (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_start);
+        if (lane_id() == 0) {
+            atomicAdd(&Q.W.counts[kWfStat + kStatDiagShadeT], (uint32_t)t_shade);
+            atomicAdd(&Q.W.counts[kWfStat + kStatDiagTotalT], dt);
+            atomicAdd(&Q.W.counts[kWfStat + kStatDiagPasses], n_pass);
+            atomicAdd(&Q.W.counts[kWfStat + kStatDiagShaded], n_shaded);
+        }
         for (int off = 32; off > 0; off >>= 1) max_segs = max(max_segs, (uint32_t)__shfl_xor((int)max_segs, off, 64));
         if (lane_id() == 0) {
             atomicMax(&Q.W.counts[cslot(kCntDiagSegs)], max_segs);
@@ -1832,6 +1846,12 @@ static bool iterate(const DevScene& S, const FrameParams& P, WfParams& Q, int& c
                             "slowest wave %u iterations in %.3f ms\n", it, n, n_next, a,
                             W.h_counts[cslot(kCntDiagSegs)], W.h_counts[cslot(kCntDiagIters)],
                             W.h_counts[cslot(kCntDiagTime)] * 1e-5);
+                    {
+                        const double st = W.h_counts[kWfStat + kStatDiagShadeT], tt = W.h_counts[kWfStat + kStatDiagTotalT];
+                        const double np = W.h_counts[kWfStat + kStatDiagPasses], ns = W.h_counts[kWfStat + kStatDiagShaded];
+                        fprintf(stderr, "[wf] finish: %.1f %% of wave time in shading passes, %.0f passes, %.1f lanes per pass\n",
+                                tt > 0 ? 100.0 * st / tt : 0.0, np, np > 0 ? ns / np : 0.0);
+                    }
                     fprintf(stderr, "[wf] finish wave end times (50 us bins):");
                     for (int b = 0; b < 64; ++b)
                         if (W.h_counts[kWfDiagHist + b]) fprintf(stderr, " %d:%u", b, W.h_counts[kWfDiagHist + b]);
