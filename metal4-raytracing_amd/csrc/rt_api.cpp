@@ -364,7 +364,7 @@ static rt_status begin_update(rt_ctx* c) {
 extern "C" {
 
 const char* rt_version(void) {
-    return "rt_hip 0.3 (gfx950, compressed 8-wide BVH, wavefront with frames in flight + megakernel)";
+    return "rt_hip 0.4 (gfx950, SAH-DP compressed 8-wide BVH, PLOC device build, wavefront with frames in flight + megakernel, USD + PNG ingest, denoised present)";
 }
 
 const char* rt_last_error(const rt_ctx* ctx) { return ctx ? ctx->err.c_str() : g_err.c_str(); }
