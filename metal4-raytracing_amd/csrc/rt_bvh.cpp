@@ -1,4 +1,6 @@
-// rt_bvh.cpp — binned-SAH BVH2 builder over world-space triangles (see rt_bvh.h).
+// rt_bvh.cpp — SAH BVH2 builder over world-space triangles (see rt_bvh.h): 256-bin binned SAH
+// over all three axes for ranges above 1,024 triangles, an exact sweep over the sorted centroids
+// below (C3g: extend nodes per ray 4.40 at 32 bins -> 3.93, 6.04 -> 6.15 Grays/s).
 #include "rt_bvh.h"
 
 #include <algorithm>
@@ -29,7 +31,14 @@ struct TmpNode {
     uint32_t start = 0, count = 0;
 };
 
-constexpr int kBins = 32;
+#ifndef RT_SAH_BINS
+#define RT_SAH_BINS 256
+#endif
+constexpr int kBins = RT_SAH_BINS;   // binned-SAH buckets per axis
+#ifndef RT_SAH_SWEEP
+#define RT_SAH_SWEEP 1024
+#endif
+constexpr uint32_t kSweepMax = RT_SAH_SWEEP;   // ranges up to this size: exact SAH sweep over sorted centroids
 
 struct Builder {
     const std::vector<Box>& tri_box;
@@ -71,7 +80,39 @@ struct Builder {
             if (n <= (uint32_t)max_leaf) return make_leaf(s, e, b);
             median = true;
         }
-        if (!median) {
+        if (!median && n <= kSweepMax) {
+            // exact SAH: every split of the centroid order on each axis (ties by triangle index)
+            std::vector<uint32_t> ord[3];
+            std::vector<float> rarea(n);
+            float best_cost = INFINITY;
+            int best_axis = -1;
+            uint32_t best_i = 0;
+            for (int a = 0; a < 3; ++a) {
+                ord[a].assign(idx.begin() + s, idx.begin() + e);
+                std::sort(ord[a].begin(), ord[a].end(), [&](uint32_t x, uint32_t y) {
+                    const float cx = cen[3 * x + a], cy = cen[3 * y + a];
+                    return cx < cy || (cx == cy && x < y);
+                });
+                Box acc; acc.reset();
+                for (uint32_t i = n; i-- > 1;) { acc.grow(tri_box[ord[a][i]]); rarea[i] = acc.area(); }
+                acc.reset();
+                for (uint32_t i = 1; i < n; ++i) {
+                    acc.grow(tri_box[ord[a][i - 1]]);
+                    const float cost = acc.area() * (float)i + rarea[i] * (float)(n - i);
+                    if (cost < best_cost) { best_cost = cost; best_axis = a; best_i = i; }
+                }
+            }
+            float pa = b.area();
+            static const float c_trav_s = getenv("RT_BVH_CTRAV") ? (float)atof(getenv("RT_BVH_CTRAV")) : 1.0f;
+            float split_cost = c_trav_s + (pa > 0 ? best_cost / pa : INFINITY);
+            if (best_axis >= 0 && (split_cost < (float)n || n > (uint32_t)max_leaf)) {
+                std::copy(ord[best_axis].begin(), ord[best_axis].end(), idx.begin() + s);
+                mid = s + best_i;
+                split_found = true;
+            } else if (n <= (uint32_t)max_leaf) {
+                return make_leaf(s, e, b);
+            }
+        } else if (!median) {
             // binned SAH over all three axes
             float best_cost = INFINITY;
             int best_axis = -1, best_bin = -1;
