@@ -133,9 +133,11 @@ __host__ __device__ __forceinline__ NodeWords load_node8(const Bvh8Node* nodes, 
 }
 
 template <bool PK = false>
+// nearest (optional): the rank of the hit internal child with the smallest entry distance, -1 if
+// none (callers visit it first; the rest of the group follows the slot order)
 __host__ __device__ __forceinline__ void test_node8_words(const NodeWords& W, const RaySetup& R, float tmin, float tmax,
                                                           uint32_t& ihits, uint32_t& tmask, uint32_t& child_base,
-                                                          uint32_t& tri_base, bool& flip) {
+                                                          uint32_t& tri_base, bool& flip, int* nearest = nullptr) {
     const float4 h0 = W.h0;
     const uint4 h1 = W.h1, qx = W.qx, qy = W.qy, qz = W.qz;
     const uint32_t ew = __builtin_bit_cast(uint32_t, h0.w);
@@ -156,6 +158,8 @@ __host__ __device__ __forceinline__ void test_node8_words(const NodeWords& W, co
     const uint32_t fz0 = R.iz >= 0.0f ? qz.z : qz.x, fz1 = R.iz >= 0.0f ? qz.w : qz.y;
     const float tf_max = tmax * 1.0000004f;
     uint32_t ih = 0, tm = 0;
+    float near_t = INFINITY;
+    int near_r = -1;
     if (PK) {
         // children c and c + 4 in one packed FMA per plane (v_pk_fma_f32): the byte words of a
         // plane hold children 0..3 and 4..7.  Fewer VALU instructions, more register pairs.
@@ -175,8 +179,15 @@ __host__ __device__ __forceinline__ void test_node8_words(const NodeWords& W, co
                 const float tf = fminf(fminf(tfx[h], tfy[h]), fminf(tfz[h], tf_max));
                 if (tn <= tf) {
                     const uint32_t m = ((h == 0 ? h1.z : h1.w) >> (8 * b)) & 0xffu;
-                    if (m & 0x80u) ih |= 1u << (m & 7u);
-                    else tm |= ((1u << ((m >> 5) + 1u)) - 1u) << (m & 31u);
+                    if (m & 0x80u) {
+                        ih |= 1u << (m & 7u);
+                        if (nearest && tn < near_t) {
+                            near_t = tn;
+                            near_r = (int)(m & 7u);
+                        }
+                    } else {
+                        tm |= ((1u << ((m >> 5) + 1u)) - 1u) << (m & 31u);
+                    }
                 }
             }
         }
@@ -194,13 +205,21 @@ __host__ __device__ __forceinline__ void test_node8_words(const NodeWords& W, co
             const float tf = fminf(fminf(tfx, tfy), fminf(tfz, tf_max));
             if (tn <= tf) {
                 const uint32_t m = ((c < 4 ? h1.z : h1.w) >> (8 * b)) & 0xffu;
-                if (m & 0x80u) ih |= 1u << (m & 7u);
-                else tm |= ((1u << ((m >> 5) + 1u)) - 1u) << (m & 31u);
+                if (m & 0x80u) {
+                    ih |= 1u << (m & 7u);
+                    if (nearest && tn < near_t) {
+                        near_t = tn;
+                        near_r = (int)(m & 7u);
+                    }
+                } else {
+                    tm |= ((1u << ((m >> 5) + 1u)) - 1u) << (m & 31u);
+                }
             }
         }
     }
     ihits = ih;
     tmask = tm;
+    if (nearest) *nearest = near_r;
     child_base = h1.x;
     tri_base = h1.y;
     flip = (R.dneg >> axis) & 1u;   // bit select: a dynamic pick of R.d lowers to a scratch access

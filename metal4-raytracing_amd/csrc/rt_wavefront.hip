@@ -267,6 +267,12 @@ __device__ __forceinline__ void write_pixel_outputs(const FrameParams& P, uint32
 
 }  // namespace
 
+// Node order: after a node test the nearest hit internal child (smallest entry distance) is
+// visited first, the rest of the group in the node's slot order (RT_NEAREST_FIRST=0: slot order only).
+#ifndef RT_NEAREST_FIRST
+#define RT_NEAREST_FIRST 1
+#endif
+
 // ---- generate -------------------------------------------------------------------------------------
 __global__ void __launch_bounds__(kBlock) wf_generate(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q) {
     const FrameParams& P = *Pp;   // per-frame parameters in device memory
@@ -632,6 +638,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ANY
     uint32_t best_id = 0xffffffffu, g_base = 0, g_hits = 0, t_base = 0, t_mask = 0;
     int sp = 0;
     uint32_t steps = 0;   // COUNT: iterations the current ray has taken
+    int g_near = -1;      // RT_NEAREST_FIRST: rank of the nearest hit child of the last node test
 
     while (true) {
         // refill idle lanes from the wave's range
@@ -662,6 +669,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ANY
                     g_base = 0;
                     g_hits = 1;   // virtual group holding the root
                     g_flip = false;
+                    g_near = -1;
                     t_mask = 0;
                     sp = 0;
                     hit_any = false;
@@ -734,7 +742,12 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ANY
                 g_flip = (ent >> 8) & 1u;
                 g_hits = ent & 0xffu;
             }
+#if RT_NEAREST_FIRST
+            const int r = g_near >= 0 ? g_near : (g_flip ? highest_bit(g_hits) : lowest_bit(g_hits));
+            g_near = -1;
+#else
             const int r = g_flip ? highest_bit(g_hits) : lowest_bit(g_hits);
+#endif
             g_hits &= ~(1u << r);
             if (g_hits) {
                 if (sp < kStackSize) {
@@ -757,7 +770,11 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ANY
             } else {
                 w = load_node8(S.nodes8, ni);
             }
+#if RT_NEAREST_FIRST
+            test_node8_words(w, R, 0.0f, best, g_hits, t_mask, g_base, t_base, g_flip, &g_near);
+#else
             test_node8_words(w, R, 0.0f, best, g_hits, t_mask, g_base, t_base, g_flip);
+#endif
         }
         if (!done && !t_mask && !g_hits && sp == 0) done = true;
         if (done) {
@@ -958,6 +975,7 @@ wf_finish_step(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int c
     uint32_t best_id = 0xffffffffu, g_base = 0, g_hits = 0, t_base = 0, t_mask = 0;
     bool g_flip = false;
     int sp = 0;
+    int g_near = -1;   // RT_NEAREST_FIRST: rank of the nearest hit child of the last node test
     auto start_trace = [&](f3 o, f3 d, float tmax) {
         R = ray_setup(o, d);
         best = tmax;
@@ -966,6 +984,7 @@ wf_finish_step(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int c
         g_base = 0;
         g_hits = 1;   // virtual group holding the root
         g_flip = false;
+        g_near = -1;
         t_mask = 0;
         sp = 0;
         hit_any = false;
@@ -1105,7 +1124,12 @@ wf_finish_step(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int c
                     g_flip = (ent >> 8) & 1u;
                     g_hits = ent & 0xffu;
                 }
+#if RT_NEAREST_FIRST
+                const int r = g_near >= 0 ? g_near : (g_flip ? highest_bit(g_hits) : lowest_bit(g_hits));
+                g_near = -1;
+#else
                 const int r = g_flip ? highest_bit(g_hits) : lowest_bit(g_hits);
+#endif
                 g_hits &= ~(1u << r);
                 if (g_hits) {
                     if (sp < kStackSize) {
@@ -1128,7 +1152,11 @@ wf_finish_step(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int c
                 } else {
                     w = load_node8(S.nodes8, ni);
                 }
+#if RT_NEAREST_FIRST
+                test_node8_words<kFinishPk>(w, R, 0.0f, best, g_hits, t_mask, g_base, t_base, g_flip, &g_near);
+#else
                 test_node8_words<kFinishPk>(w, R, 0.0f, best, g_hits, t_mask, g_base, t_base, g_flip);
+#endif
             }
             if (!tdone && !t_mask && !g_hits && sp == 0) tdone = true;
             if (tdone) {
