@@ -53,8 +53,8 @@ TRAFFIC_JSON = os.path.join(_ROOT, TRAFFIC_JSON_REL)
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=16)
-    p.add_argument("--warmup", type=int, default=2)
+    p.add_argument("--steps", type=int, default=32)
+    p.add_argument("--warmup", type=int, default=4)
     p.add_argument("--scene", default="c3g")
     p.add_argument("--width", type=int, default=1920)
     p.add_argument("--height", type=int, default=1080)
