@@ -189,7 +189,7 @@ struct rt_ctx {
 
 static rt_status dev_alloc(rt_ctx* c, DevBuf& b, size_t bytes) {
     if (b.p && b.bytes >= bytes && bytes > 0) return RT_OK;
-    if (b.p) { hipFree(b.p); b.p = nullptr; b.bytes = 0; }
+    if (b.p) { (void)hipFree(b.p); b.p = nullptr; b.bytes = 0; }
     if (bytes == 0) return RT_OK;
     HIPC(c, hipMalloc(&b.p, bytes));
     b.bytes = bytes;
@@ -202,7 +202,7 @@ static rt_status dev_upload(rt_ctx* c, DevBuf& b, const void* src, size_t bytes,
     return RT_OK;
 }
 static void dev_free(DevBuf& b) {
-    if (b.p) hipFree(b.p);
+    if (b.p) (void)hipFree(b.p);
     b.p = nullptr;
     b.bytes = 0;
 }
@@ -431,11 +431,11 @@ rt_status rt_create(const rt_opts* opts, rt_ctx** out) {
 
 rt_status rt_destroy(rt_ctx* c) {
     if (!c) return RT_OK;
-    hipSetDevice(c->device);
-    if (c->stream) hipStreamSynchronize(c->stream);
-    if (c->ustream) hipStreamSynchronize(c->ustream);
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    if (c->ustream) (void)hipStreamSynchronize(c->ustream);
     for (FrameSlot& f : c->slot)
-        if (f.own_stream) hipStreamSynchronize(f.own_stream);
+        if (f.own_stream) (void)hipStreamSynchronize(f.own_stream);
     DevBuf* all[] = {&c->d_rest_pos, &c->d_rest_nrm, &c->d_jidx, &c->d_jw,
                      &c->d_joints, &c->d_tri_info, &c->d_mat, &c->d_lights, &c->d_halton,
                      &c->d_slot_to_tri, &c->d_levels, &c->d_maxabs, &c->d_random, &c->d_accum[0],
@@ -447,26 +447,26 @@ rt_status rt_destroy(rt_ctx* c) {
     for (DevBuf& b : c->d_motion) dev_free(b);
     for (Geo& g : c->geo)
         for (DevBuf* b : g.all) dev_free(*b);
-    if (c->uev) hipEventDestroy(c->uev);
-    if (c->ustream) hipStreamDestroy(c->ustream);
-    if (c->h_lbvh) hipHostFree(c->h_lbvh);
-    if (c->scene_ev) hipEventDestroy(c->scene_ev);
+    if (c->uev) (void)hipEventDestroy(c->uev);
+    if (c->ustream) (void)hipStreamDestroy(c->ustream);
+    if (c->h_lbvh) (void)hipHostFree(c->h_lbvh);
+    if (c->scene_ev) (void)hipEventDestroy(c->scene_ev);
     for (FrameSlot& f : c->slot) {
         for (DevBuf* b : f.bufs) dev_free(*b);
-        if (f.h_counters) hipHostFree(f.h_counters);
-        if (f.wf.h_counts) hipHostFree(f.wf.h_counts);
+        if (f.h_counters) (void)hipHostFree(f.h_counters);
+        if (f.wf.h_counts) (void)hipHostFree(f.wf.h_counts);
         for (auto& e : f.wf.ev)
-            if (e) hipEventDestroy(e);
+            if (e) (void)hipEventDestroy(e);
         for (auto& e : f.wft.ev)
-            if (e) hipEventDestroy(e);
+            if (e) (void)hipEventDestroy(e);
         for (auto& e : f.wf.param_ev)
-            if (e) hipEventDestroy(e);
-        if (f.wf.h_params) hipHostFree(f.wf.h_params);
+            if (e) (void)hipEventDestroy(e);
+        if (f.wf.h_params) (void)hipHostFree(f.wf.h_params);
         for (hipEvent_t ev : {f.ev0, f.ev1, f.done})
-            if (ev) hipEventDestroy(ev);
-        if (f.own_stream) hipStreamDestroy(f.own_stream);
+            if (ev) (void)hipEventDestroy(ev);
+        if (f.own_stream) (void)hipStreamDestroy(f.own_stream);
     }
-    if (c->own_stream) hipStreamDestroy(c->own_stream);
+    if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
     delete c;
     return RT_OK;
 }
