@@ -582,29 +582,30 @@ void emit_bvh8_node(const BvhResult& b2, const Job& job, std::vector<WItem>& ite
         std::stable_sort(items.begin(), items.end(), [&](const WItem& x, const WItem& y) {
             return x.lo[axis] + x.hi[axis] < y.lo[axis] + y.hi[axis];
         });
+        // internal children first (slot = rank), then the leaves, each kind in centroid order
+        std::stable_partition(items.begin(), items.end(), [](const WItem& x) { return !x.leaf; });
         Bvh8Node nd;
         std::memset(&nd, 0, sizeof nd);
-        nd.axis = (uint8_t)axis;
         uint32_t n_internal = 0, n_tris = 0;
         for (auto& it : items) { if (!it.leaf) ++n_internal; else n_tris += it.count; }
+        nd.axis_k = (uint8_t)(axis | (n_internal << 4));
         nd.child_base = (uint32_t)out.nodes.size();
         nd.tri_base = (uint32_t)out.tri_order.size();
         float clo[8][3], chi[8][3];
         bool used[8] = {false, false, false, false, false, false, false, false};
-        uint32_t rank = 0, toff = 0;
+        uint32_t rank = 0;
         for (size_t c = 0; c < items.size(); ++c) {
             const WItem& it = items[c];
             used[c] = true;
             for (int a = 0; a < 3; ++a) { clo[c][a] = it.lo[a]; chi[c][a] = it.hi[a]; }
             if (!it.leaf) {
-                nd.meta[c] = (uint8_t)(0x80 | rank);
                 uint32_t child = nd.child_base + rank;
                 ++rank;
                 queue.push_back({it.node, child, job.depth + 1});
             } else {
-                nd.meta[c] = (uint8_t)(((it.count - 1) << 5) | toff);
+                const uint32_t j = (uint32_t)c - n_internal;
+                nd.tri_valid |= ((1u << it.count) - 1u) << (4 * j);
                 for (uint32_t t = 0; t < it.count; ++t) out.tri_order.push_back(b2.tri_order[it.start + t]);
-                toff += it.count;
             }
         }
         (void)n_tris;

@@ -38,19 +38,25 @@ struct BvhResult {
 // Child boxes are quantized to 8 bits per plane against the node's origin p and per-axis
 // power-of-two scale 2^e, rounded outward, so the dequantized box p + q * 2^e always encloses
 // the (padded) BVH2 box it came from: traversal stays conservative and exact.
-//   meta[c]: 0x80 | rank  — internal child, node index = child_base + rank (slot order)
-//            (count-1) << 5 | offset — leaf with `count` (1..4) triangles at tri_base + offset
-//            0 with an empty box (qlo = 255 > qhi = 0) — unused slot
-//   axis: children are sorted by centroid along `axis`; rays with d[axis] < 0 visit them in
-//   reverse slot order (approximate front-to-back order for closest-hit culling).
+//   slots: the k internal children first (slot r = rank r, node index child_base + r), then the
+//            leaves (leaf j in slot k + j), then unused slots with an empty box (qlo = 255 > qhi = 0)
+//   k:       bits 4..7 of axis_k (bits 0..1: the sort axis)
+//   tri_valid: one nibble per leaf, bit 4j + i set when leaf j has a triangle i (1..4 triangles);
+//            the leaves' triangles are contiguous from tri_base in slot order, so triangle (j, i)
+//            is tri_base + popcount(tri_valid & ((1 << (4j + i)) - 1)).  A node test turns its
+//            hit slots into internal ranks (the low k bits) and a triangle mask in nibble space
+//            (the leaf bits spread to nibbles, & tri_valid) without per-child branches.
+//   axis: children of each kind are sorted by centroid along `axis`; rays with d[axis] < 0 visit
+//   them in reverse slot order (approximate front-to-back order for closest-hit culling).
 // Byte order of q: [qlo.x 0..7][qhi.x 0..7][qlo.y ..][qhi.y ..][qlo.z ..][qhi.z ..].
 struct alignas(16) Bvh8Node {
     float p[3];
-    uint8_t e[3];   // biased exponents (e + 127): scale = 2^(e - 127)
-    uint8_t axis;
+    uint8_t e[3];     // biased exponents (e + 127): scale = 2^(e - 127)
+    uint8_t axis_k;   // sort axis | k << 4
     uint32_t child_base;
     uint32_t tri_base;
-    uint8_t meta[8];
+    uint32_t tri_valid;
+    uint32_t reserved;
     uint8_t q[48];
 };
 static_assert(sizeof(Bvh8Node) == 80, "wide node is 80 B");
@@ -72,6 +78,17 @@ Bvh8Result collapse_bvh8(const BvhResult& b2);
 // slot is a leaf of <= 4 triangles or a child node, chosen to minimise
 // sum(A(node) * c_node) + sum(A(leaf) * c_prim * triangles).  Best on a BVH2 with 1-triangle leaves.
 Bvh8Result collapse_bvh8_dp(const BvhResult& b2, float c_node, float c_prim);
+
+#if defined(__HIPCC__)
+#define RT_BVH_HD __host__ __device__
+#else
+#define RT_BVH_HD
+#endif
+// Leaf j of a node: its first triangle slot (relative to tri_base) and its triangle count.
+RT_BVH_HD inline uint32_t bvh8_leaf_first(uint32_t tri_valid, int j) {
+    return (uint32_t)__builtin_popcount(j ? tri_valid & ((1u << (4 * j)) - 1u) : 0u);
+}
+RT_BVH_HD inline uint32_t bvh8_leaf_count(uint32_t tri_valid, int j) { return (uint32_t)__builtin_popcount((tri_valid >> (4 * j)) & 15u); }
 
 // Re-quantize node n from its children's boxes (children: node_box of internal children, leaf
 // triangle bounds from tri_verts in BVH8 triangle order, padded).  Host mirror of the refit kernel.

@@ -132,12 +132,31 @@ __host__ __device__ __forceinline__ NodeWords load_node8(const Bvh8Node* nodes, 
     return w;
 }
 
-template <bool PK = false>
-// nearest (optional): the rank of the hit internal child with the smallest entry distance, -1 if
-// none (callers visit it first; the rest of the group follows the slot order)
+// Leaf bits j (j < 8) -> nibbles 4j..4j+3 (the triangle space of Bvh8Node::tri_valid).
+__host__ __device__ __forceinline__ uint32_t spread_nibbles(uint32_t x) {
+    x = (x | (x << 12)) & 0x000F000Fu;
+    x = (x | (x << 6)) & 0x03030303u;
+    x = (x | (x << 3)) & 0x11111111u;
+    return x * 15u;
+}
+// Triangle slot of bit k of a node test's triangle mask (nibble space): tri_base + the valid bits below k.
+__host__ __device__ __forceinline__ uint32_t tri_slot(uint32_t tri_base, uint32_t tri_valid, int k) {
+    return tri_base + (uint32_t)__builtin_popcount(tri_valid & ((1u << k) - 1u));
+}
+
+// Slab-test the 8 children of a node.  Outputs: the internal children hit (bit r = internal rank r
+// = slot r), the triangles to test (nibble space: bit 4j + i = triangle i of leaf j, see
+// tri_slot), the node's tri_valid word, and the traversal direction of the slot order.
+// Branch-free over the children: each child only sets its bit of the hit-slot mask (and, with
+// `nearest`, competes for the nearest internal child); the internal / leaf split and the
+// triangle mask follow from the node's k and tri_valid once per node.
+// nearest (optional): the rank of the hit internal child with the smallest entry distance (ties:
+// the entry distances' low three mantissa bits are replaced by the slot), -1 if none (callers
+// visit it first; the rest of the group follows the slot order)
 __host__ __device__ __forceinline__ void test_node8_words(const NodeWords& W, const RaySetup& R, float tmin, float tmax,
-                                                          uint32_t& ihits, uint32_t& tmask, uint32_t& child_base,
-                                                          uint32_t& tri_base, bool& flip, int* nearest = nullptr) {
+                                                          uint32_t& ihits, uint32_t& tmask, uint32_t& tvalid,
+                                                          uint32_t& child_base, uint32_t& tri_base, bool& flip,
+                                                          int* nearest = nullptr) {
     const float4 h0 = W.h0;
     const uint4 h1 = W.h1, qx = W.qx, qy = W.qy, qz = W.qz;
     const uint32_t ew = __builtin_bit_cast(uint32_t, h0.w);
@@ -145,6 +164,7 @@ __host__ __device__ __forceinline__ void test_node8_words(const NodeWords& W, co
     const float sy = __builtin_bit_cast(float, ((ew >> 8) & 0xffu) << 23);
     const float sz = __builtin_bit_cast(float, ((ew >> 16) & 0xffu) << 23);
     const int axis = (int)((ew >> 24) & 3u);
+    const uint32_t k_int = ew >> 28;   // internal children: slots 0 .. k_int - 1
     const float ax = sx * R.ix, ay = sy * R.iy, az = sz * R.iz;
     const float bx = __builtin_fmaf(h0.x, R.ix, -R.ox);
     const float by = __builtin_fmaf(h0.y, R.iy, -R.oy);
@@ -157,78 +177,39 @@ __host__ __device__ __forceinline__ void test_node8_words(const NodeWords& W, co
     const uint32_t nz0 = R.iz >= 0.0f ? qz.x : qz.z, nz1 = R.iz >= 0.0f ? qz.y : qz.w;
     const uint32_t fz0 = R.iz >= 0.0f ? qz.z : qz.x, fz1 = R.iz >= 0.0f ? qz.w : qz.y;
     const float tf_max = tmax * 1.0000004f;
-    uint32_t ih = 0, tm = 0;
-    float near_t = INFINITY;
-    int near_r = -1;
-    if (PK) {
-        // children c and c + 4 in one packed FMA per plane (v_pk_fma_f32): the byte words of a
-        // plane hold children 0..3 and 4..7.  Fewer VALU instructions, more register pairs.
-        typedef float f2v __attribute__((ext_vector_type(2)));
-        const f2v ax2 = {ax, ax}, ay2 = {ay, ay}, az2 = {az, az}, bx2 = {bx, bx}, by2 = {by, by}, bz2 = {bz, bz};
-        #pragma unroll
-        for (int b = 0; b < 4; ++b) {
-            const f2v qnx = {byte_f(nx0, b), byte_f(nx1, b)}, qfx = {byte_f(fx0, b), byte_f(fx1, b)};
-            const f2v qny = {byte_f(ny0, b), byte_f(ny1, b)}, qfy = {byte_f(fy0, b), byte_f(fy1, b)};
-            const f2v qnz = {byte_f(nz0, b), byte_f(nz1, b)}, qfz = {byte_f(fz0, b), byte_f(fz1, b)};
-            const f2v tnx = __builtin_elementwise_fma(qnx, ax2, bx2), tfx = __builtin_elementwise_fma(qfx, ax2, bx2);
-            const f2v tny = __builtin_elementwise_fma(qny, ay2, by2), tfy = __builtin_elementwise_fma(qfy, ay2, by2);
-            const f2v tnz = __builtin_elementwise_fma(qnz, az2, bz2), tfz = __builtin_elementwise_fma(qfz, az2, bz2);
-            #pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                const float tn = fmaxf(fmaxf(tnx[h], tny[h]), fmaxf(tnz[h], tmin));
-                const float tf = fminf(fminf(tfx[h], tfy[h]), fminf(tfz[h], tf_max));
-                if (tn <= tf) {
-                    const uint32_t m = ((h == 0 ? h1.z : h1.w) >> (8 * b)) & 0xffu;
-                    if (m & 0x80u) {
-                        ih |= 1u << (m & 7u);
-                        if (nearest && tn < near_t) {
-                            near_t = tn;
-                            near_r = (int)(m & 7u);
-                        }
-                    } else {
-                        tm |= ((1u << ((m >> 5) + 1u)) - 1u) << (m & 31u);
-                    }
-                }
-            }
-        }
-    } else {
-        #pragma unroll
-        for (int c = 0; c < 8; ++c) {
-            const int b = c & 3;
-            const uint32_t wnx = c < 4 ? nx0 : nx1, wfx = c < 4 ? fx0 : fx1;
-            const uint32_t wny = c < 4 ? ny0 : ny1, wfy = c < 4 ? fy0 : fy1;
-            const uint32_t wnz = c < 4 ? nz0 : nz1, wfz = c < 4 ? fz0 : fz1;
-            const float tnx = __builtin_fmaf(byte_f(wnx, b), ax, bx), tfx = __builtin_fmaf(byte_f(wfx, b), ax, bx);
-            const float tny = __builtin_fmaf(byte_f(wny, b), ay, by), tfy = __builtin_fmaf(byte_f(wfy, b), ay, by);
-            const float tnz = __builtin_fmaf(byte_f(wnz, b), az, bz), tfz = __builtin_fmaf(byte_f(wfz, b), az, bz);
-            const float tn = fmaxf(fmaxf(tnx, tny), fmaxf(tnz, tmin));
-            const float tf = fminf(fminf(tfx, tfy), fminf(tfz, tf_max));
-            if (tn <= tf) {
-                const uint32_t m = ((c < 4 ? h1.z : h1.w) >> (8 * b)) & 0xffu;
-                if (m & 0x80u) {
-                    ih |= 1u << (m & 7u);
-                    if (nearest && tn < near_t) {
-                        near_t = tn;
-                        near_r = (int)(m & 7u);
-                    }
-                } else {
-                    tm |= ((1u << ((m >> 5) + 1u)) - 1u) << (m & 31u);
-                }
-            }
+    uint32_t hm = 0, nkey = 0xffffffffu;
+    #pragma unroll
+    for (int c = 0; c < 8; ++c) {
+        const int b = c & 3;
+        const uint32_t wnx = c < 4 ? nx0 : nx1, wfx = c < 4 ? fx0 : fx1;
+        const uint32_t wny = c < 4 ? ny0 : ny1, wfy = c < 4 ? fy0 : fy1;
+        const uint32_t wnz = c < 4 ? nz0 : nz1, wfz = c < 4 ? fz0 : fz1;
+        const float tnx = __builtin_fmaf(byte_f(wnx, b), ax, bx), tfx = __builtin_fmaf(byte_f(wfx, b), ax, bx);
+        const float tny = __builtin_fmaf(byte_f(wny, b), ay, by), tfy = __builtin_fmaf(byte_f(wfy, b), ay, by);
+        const float tnz = __builtin_fmaf(byte_f(wnz, b), az, bz), tfz = __builtin_fmaf(byte_f(wfz, b), az, bz);
+        const float tn = fmaxf(fmaxf(tnx, tny), fmaxf(tnz, tmin));
+        const float tf = fminf(fminf(tfx, tfy), fminf(tfz, tf_max));
+        const bool hit = tn <= tf;
+        hm |= hit ? (1u << c) : 0u;
+        if (nearest) {
+            // entry distance (>= tmin >= 0: unsigned order = float order) with the slot in its low bits
+            const uint32_t key = (__builtin_bit_cast(uint32_t, tn) & ~7u) | (uint32_t)c;
+            nkey = (hit && (uint32_t)c < k_int && key < nkey) ? key : nkey;
         }
     }
-    ihits = ih;
-    tmask = tm;
-    if (nearest) *nearest = near_r;
+    ihits = hm & ((1u << k_int) - 1u);
+    tmask = spread_nibbles(hm >> k_int) & h1.z;
+    tvalid = h1.z;
+    if (nearest) *nearest = nkey == 0xffffffffu ? -1 : (int)(nkey & 7u);
     child_base = h1.x;
     tri_base = h1.y;
     flip = (R.dneg >> axis) & 1u;   // bit select: a dynamic pick of R.d lowers to a scratch access
 }
 
 __host__ __device__ __forceinline__ void test_node8(const Bvh8Node* nodes, uint32_t ni, const RaySetup& R, float tmin,
-                                                    float tmax, uint32_t& ihits, uint32_t& tmask,
+                                                    float tmax, uint32_t& ihits, uint32_t& tmask, uint32_t& tvalid,
                                                     uint32_t& child_base, uint32_t& tri_base, bool& flip) {
-    test_node8_words(load_node8(nodes, ni), R, tmin, tmax, ihits, tmask, child_base, tri_base, flip);
+    test_node8_words(load_node8(nodes, ni), R, tmin, tmax, ihits, tmask, tvalid, child_base, tri_base, flip);
 }
 
 __host__ __device__ __forceinline__ int lowest_bit(uint32_t m) { return __builtin_ctz(m); }
@@ -247,14 +228,14 @@ __host__ __device__ __forceinline__ bool trace8(const DevScene& S, f3 o, f3 d, f
     const RaySetup R = ray_setup(o, d);
     float best = tmax, bu = 0.0f, bv = 0.0f;
     uint32_t best_id = 0xffffffffu;
-    uint32_t g_base = 0, g_hits = 1, t_base = 0, t_mask = 0;  // virtual group holding the root
+    uint32_t g_base = 0, g_hits = 1, t_base = 0, t_mask = 0, t_valid = 0;  // virtual group holding the root
     bool g_flip = false;
     int sp = 0;
     while (true) {
         if (t_mask) {
             const int k = lowest_bit(t_mask);
             t_mask &= t_mask - 1u;
-            const float4* tp = S.tris + 3 * (size_t)(t_base + (uint32_t)k);
+            const float4* tp = S.tris + 3 * (size_t)tri_slot(t_base, t_valid, k);
             const float4 v0 = tp[0], v1 = tp[1], v2 = tp[2];
             if (COUNT) cnt.tris++;
             float t, u, v;
@@ -287,7 +268,7 @@ __host__ __device__ __forceinline__ bool trace8(const DevScene& S, f3 o, f3 d, f
             }
         }
         if (COUNT) cnt.nodes++;
-        test_node8(S.nodes8, g_base + (uint32_t)r, R, tmin, best, g_hits, t_mask, g_base, t_base, g_flip);
+        test_node8(S.nodes8, g_base + (uint32_t)r, R, tmin, best, g_hits, t_mask, t_valid, g_base, t_base, g_flip);
     }
     hit.t = best; hit.id = best_id; hit.u = bu; hit.v = bv;
     return best_id != 0xffffffffu;

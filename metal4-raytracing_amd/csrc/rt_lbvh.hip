@@ -720,14 +720,24 @@ __global__ void __launch_bounds__(kThreads) lbvh_collapse_k(CollapseArgs A) {
         }
         items[q + 1] = x;
     }
+    {   // internal children first (slot = rank), then the leaves, each kind in centroid order
+        Item sorted[8];
+        int m = 0;
+        for (int i = 0; i < n_items; ++i)
+            if (!items[i].leaf) sorted[m++] = items[i];
+        for (int i = 0; i < n_items; ++i)
+            if (items[i].leaf) sorted[m++] = items[i];
+        for (int i = 0; i < n_items; ++i) items[i] = sorted[i];
+    }
     uint32_t n_internal = 0, n_tris = 0;
     for (int i = 0; i < n_items; ++i) {
         if (items[i].leaf) n_tris += items[i].count;
         else ++n_internal;
     }
     Bvh8Node nd;
-    for (int c = 0; c < 8; ++c) nd.meta[c] = 0;
-    nd.axis = (uint8_t)axis;
+    nd.tri_valid = 0u;
+    nd.reserved = 0u;
+    nd.axis_k = (uint8_t)(axis | (n_internal << 4));
     nd.child_base = n_internal ? atomicAdd(&A.counters[0], n_internal) : 0u;
     nd.tri_base = n_tris ? atomicAdd(&A.counters[1], n_tris) : 0u;
     if (nd.child_base + n_internal > A.n || nd.tri_base + n_tris > A.n) {
@@ -738,13 +748,12 @@ __global__ void __launch_bounds__(kThreads) lbvh_collapse_k(CollapseArgs A) {
     for (int i = 0; i < n_items; ++i) {
         const Item& it = items[i];
         if (!it.leaf) {
-            nd.meta[i] = (uint8_t)(0x80u | rank);
             const uint32_t slot = atomicAdd(&A.counters[2], 1u);
             if (slot < A.n) A.jobs_out[slot] = make_int2(it.ref, (int)(nd.child_base + rank));
             else atomicOr(&A.counters[4], 4u);
             ++rank;
         } else {
-            nd.meta[i] = (uint8_t)(((it.count - 1u) << 5) | toff);
+            nd.tri_valid |= ((1u << it.count) - 1u) << (4u * ((uint32_t)i - n_internal));
             // the subtree's triangles (<= 4), left to right (PLOC subtrees are not contiguous in
             // the sorted order)
             int st[8];

@@ -137,13 +137,14 @@ __global__ void refit8_level_k(Bvh8Node* __restrict__ nodes, float* __restrict__
         // unused slots carry an empty quantized box (qlo = 255 > qhi = 0 on x)
         used[c] = !(nd.q[c] == 255 && nd.q[8 + c] == 0);
         if (!used[c]) continue;
-        const uint32_t m = nd.meta[c];
+        const uint32_t k_int = (uint32_t)nd.axis_k >> 4;
         float l[3] = {INFINITY, INFINITY, INFINITY}, h[3] = {-INFINITY, -INFINITY, -INFINITY};
-        if (m & 0x80u) {
-            const float* b = node_box + 6 * (size_t)(nd.child_base + (m & 7u));
+        if ((uint32_t)c < k_int) {
+            const float* b = node_box + 6 * (size_t)(nd.child_base + (uint32_t)c);
             for (int a = 0; a < 3; ++a) { l[a] = b[a]; h[a] = b[3 + a]; }
         } else {
-            const uint32_t first = nd.tri_base + (m & 31u), n = (m >> 5) + 1u;
+            const int j = c - (int)k_int;
+            const uint32_t first = nd.tri_base + bvh8_leaf_first(nd.tri_valid, j), n = bvh8_leaf_count(nd.tri_valid, j);
             for (uint32_t t = 0; t < n; ++t)
                 for (int q = 0; q < 3; ++q) {
                     float4 v = tris[3 * (size_t)(first + t) + q];

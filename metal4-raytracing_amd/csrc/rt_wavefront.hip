@@ -24,10 +24,6 @@
 // contribution, then step s+1), and samples are summed per pixel in sample order.
 #include "rt_shade.h"
 
-#ifndef RT_FINISH_PK
-#define RT_FINISH_PK 0   // packed variant measured slower (3.37 -> 3.5 ms finish)
-#endif
-
 #include <cstdio>
 #include <cstring>
 #include <vector>
@@ -37,7 +33,6 @@ namespace rt {
 namespace {
 
 constexpr uint32_t kTailRaysDefault = 4194304;
-constexpr bool kFinishPk = RT_FINISH_PK;   // packed-FMA node test in the finish kernels (build flag)
 static uint32_t tail_rays() {  // RT_TAIL_RAYS overrides (tuning experiments)
     static uint32_t v = [] { const char* e = getenv("RT_TAIL_RAYS"); return e ? (uint32_t)atol(e) : kTailRaysDefault; }();
     return v;
@@ -635,7 +630,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ANY
     uint32_t e = 0;
     RaySetup R = ray_setup(mk3(0, 0, 0), mk3(1, 0, 0));
     float best = 0.0f, bu = 0.0f, bv = 0.0f;
-    uint32_t best_id = 0xffffffffu, g_base = 0, g_hits = 0, t_base = 0, t_mask = 0;
+    uint32_t best_id = 0xffffffffu, g_base = 0, g_hits = 0, t_base = 0, t_mask = 0, t_valid = 0;
     int sp = 0;
     uint32_t steps = 0;   // COUNT: iterations the current ray has taken
     int g_near = -1;      // RT_NEAREST_FIRST: rank of the nearest hit child of the last node test
@@ -703,8 +698,8 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ANY
             const bool two = t_mask != 0u;
             const int k1 = two ? lowest_bit(t_mask) : k0;
             if (two) t_mask &= t_mask - 1u;
-            const float4* tp0 = S.tris + 3 * (size_t)(t_base + (uint32_t)k0);
-            const float4* tp1 = S.tris + 3 * (size_t)(t_base + (uint32_t)k1);
+            const float4* tp0 = S.tris + 3 * (size_t)tri_slot(t_base, t_valid, k0);
+            const float4* tp1 = S.tris + 3 * (size_t)tri_slot(t_base, t_valid, k1);
             const float4 a0 = tp0[0], a1 = tp0[1], a2 = tp0[2];
             const float4 b0 = tp1[0], b1 = tp1[1], b2 = tp1[2];
             if (COUNT) tc.tris += two ? 2u : 1u;
@@ -771,9 +766,9 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ANY
                 w = load_node8(S.nodes8, ni);
             }
 #if RT_NEAREST_FIRST
-            test_node8_words(w, R, 0.0f, best, g_hits, t_mask, g_base, t_base, g_flip, &g_near);
+            test_node8_words(w, R, 0.0f, best, g_hits, t_mask, t_valid, g_base, t_base, g_flip, &g_near);
 #else
-            test_node8_words(w, R, 0.0f, best, g_hits, t_mask, g_base, t_base, g_flip);
+            test_node8_words(w, R, 0.0f, best, g_hits, t_mask, t_valid, g_base, t_base, g_flip);
 #endif
         }
         if (!done && !t_mask && !g_hits && sp == 0) done = true;
@@ -972,7 +967,7 @@ wf_finish_step(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int c
     // traversal
     RaySetup R = ray_setup(mk3(0, 0, 0), mk3(1, 0, 0));
     float best = 0.0f, bu = 0.0f, bv = 0.0f;
-    uint32_t best_id = 0xffffffffu, g_base = 0, g_hits = 0, t_base = 0, t_mask = 0;
+    uint32_t best_id = 0xffffffffu, g_base = 0, g_hits = 0, t_base = 0, t_mask = 0, t_valid = 0;
     bool g_flip = false;
     int sp = 0;
     int g_near = -1;   // RT_NEAREST_FIRST: rank of the nearest hit child of the last node test
@@ -1086,8 +1081,8 @@ wf_finish_step(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int c
                 const bool two = t_mask != 0u;
                 const int k1 = two ? lowest_bit(t_mask) : k0;
                 if (two) t_mask &= t_mask - 1u;
-                const float4* tp0 = S.tris + 3 * (size_t)(t_base + (uint32_t)k0);
-                const float4* tp1 = S.tris + 3 * (size_t)(t_base + (uint32_t)k1);
+                const float4* tp0 = S.tris + 3 * (size_t)tri_slot(t_base, t_valid, k0);
+                const float4* tp1 = S.tris + 3 * (size_t)tri_slot(t_base, t_valid, k1);
                 const float4 a0 = tp0[0], a1 = tp0[1], a2 = tp0[2];
                 const float4 b0 = tp1[0], b1 = tp1[1], b2 = tp1[2];
                 if (COUNT) tc.tris += two ? 2u : 1u;
@@ -1153,9 +1148,9 @@ wf_finish_step(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int c
                     w = load_node8(S.nodes8, ni);
                 }
 #if RT_NEAREST_FIRST
-                test_node8_words<kFinishPk>(w, R, 0.0f, best, g_hits, t_mask, g_base, t_base, g_flip, &g_near);
+                test_node8_words(w, R, 0.0f, best, g_hits, t_mask, t_valid, g_base, t_base, g_flip, &g_near);
 #else
-                test_node8_words<kFinishPk>(w, R, 0.0f, best, g_hits, t_mask, g_base, t_base, g_flip);
+                test_node8_words(w, R, 0.0f, best, g_hits, t_mask, t_valid, g_base, t_base, g_flip);
 #endif
             }
             if (!tdone && !t_mask && !g_hits && sp == 0) tdone = true;
@@ -1301,7 +1296,7 @@ __global__ void __launch_bounds__(kBlock) wf_prio(WfParams Q, int cur) {
 struct TravState {
     RaySetup R;
     float best, bu, bv;
-    uint32_t best_id, g_base, g_hits, t_base, t_mask;
+    uint32_t best_id, g_base, g_hits, t_base, t_mask, t_valid;
     bool g_flip, hit_any;
     int sp;
 };
@@ -1330,8 +1325,8 @@ __device__ __forceinline__ bool trav_step(const DevScene& S, TravState& T, bool 
         const bool two = T.t_mask != 0u;
         const int k1 = two ? lowest_bit(T.t_mask) : k0;
         if (two) T.t_mask &= T.t_mask - 1u;
-        const float4* tp0 = S.tris + 3 * (size_t)(T.t_base + (uint32_t)k0);
-        const float4* tp1 = S.tris + 3 * (size_t)(T.t_base + (uint32_t)k1);
+        const float4* tp0 = S.tris + 3 * (size_t)tri_slot(T.t_base, T.t_valid, k0);
+        const float4* tp1 = S.tris + 3 * (size_t)tri_slot(T.t_base, T.t_valid, k1);
         const float4 a0 = tp0[0], a1 = tp0[1], a2 = tp0[2];
         const float4 b0 = tp1[0], b1 = tp1[1], b2 = tp1[2];
         if (COUNT) tc.tris += two ? 2u : 1u;
@@ -1391,7 +1386,7 @@ __device__ __forceinline__ bool trav_step(const DevScene& S, TravState& T, bool 
         } else {
             w = load_node8(S.nodes8, ni);
         }
-        test_node8_words<kFinishPk>(w, T.R, 0.0f, T.best, T.g_hits, T.t_mask, T.g_base, T.t_base, T.g_flip);
+        test_node8_words(w, T.R, 0.0f, T.best, T.g_hits, T.t_mask, T.t_valid, T.g_base, T.t_base, T.g_flip);
     }
     return tdone || (!T.t_mask && !T.g_hits && T.sp == 0);
 }
