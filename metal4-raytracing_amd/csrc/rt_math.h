@@ -194,5 +194,34 @@ RT_HD bool intersect_triangle(const RayPre& p, f3 o, f3 v0, f3 v1, f3 v2, float 
     *v_out = W / det;
     return true;
 }
+// The same test, leaving the barycentric divisions to the caller: writes t and the unnormalised
+// (V, W, det), so u = V / det and v = W / det (bit for bit the values above) are formed once for
+// the closest hit instead of for every candidate.
+RT_HD bool intersect_triangle_vw(const RayPre& p, f3 o, f3 v0, f3 v1, f3 v2, float tmin, float tmax,
+                                 float* t_out, float* V_out, float* W_out, float* det_out) {
+    f3 A = v0 - o, B = v1 - o, C = v2 - o;
+    float Akz = comp(A, p.kz), Bkz = comp(B, p.kz), Ckz = comp(C, p.kz);
+    float Ax = comp(A, p.kx) - p.Sx * Akz;
+    float Ay = comp(A, p.ky) - p.Sy * Akz;
+    float Bx = comp(B, p.kx) - p.Sx * Bkz;
+    float By = comp(B, p.ky) - p.Sy * Bkz;
+    float Cx = comp(C, p.kx) - p.Sx * Ckz;
+    float Cy = comp(C, p.ky) - p.Sy * Ckz;
+    float U = Cx * By - Cy * Bx;
+    float V = Ax * Cy - Ay * Cx;
+    float W = Bx * Ay - By * Ax;
+    if ((U < 0.0f || V < 0.0f || W < 0.0f) && (U > 0.0f || V > 0.0f || W > 0.0f)) return false;
+    float det = (U + V) + W;
+    if (det == 0.0f) return false;
+    float Az = p.Sz * Akz, Bz = p.Sz * Bkz, Cz = p.Sz * Ckz;
+    float T = (U * Az + V * Bz) + W * Cz;
+    float t = T / det;
+    if (!(t >= tmin && t <= tmax)) return false;
+    *t_out = t;
+    *V_out = V;
+    *W_out = W;
+    *det_out = det;
+    return true;
+}
 
 }  // namespace rt

@@ -264,6 +264,9 @@ __device__ __forceinline__ void write_pixel_outputs(const FrameParams& P, uint32
 
 // Node order: after a node test the nearest hit internal child (smallest entry distance) is
 // visited first, the rest of the group in the node's slot order (RT_NEAREST_FIRST=0: slot order only).
+#ifndef RT_TRI_THEN_NODE
+#define RT_TRI_THEN_NODE 1   // a lane may run its last triangle step and its next node step in one iteration
+#endif
 #ifndef RT_NEAREST_FIRST
 #define RT_NEAREST_FIRST 1
 #endif
@@ -629,7 +632,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ANY
     bool active = false, hit_any = false, g_flip = false;
     uint32_t e = 0;
     RaySetup R = ray_setup(mk3(0, 0, 0), mk3(1, 0, 0));
-    float best = 0.0f, bu = 0.0f, bv = 0.0f;
+    float best = 0.0f, bu = 0.0f, bv = 0.0f, bdet = 1.0f;   // closest hit: u = bu / bdet, v = bv / bdet
     uint32_t best_id = 0xffffffffu, g_base = 0, g_hits = 0, t_base = 0, t_mask = 0, t_valid = 0;
     int sp = 0;
     uint32_t steps = 0;   // COUNT: iterations the current ray has taken
@@ -661,6 +664,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ANY
                     best = ANY ? d4.w : INFINITY;
                     best_id = 0xffffffffu;
                     bu = bv = 0.0f;
+                    bdet = 1.0f;
                     g_base = 0;
                     g_hits = 1;   // virtual group holding the root
                     g_flip = false;
@@ -703,8 +707,8 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ANY
             const float4 a0 = tp0[0], a1 = tp0[1], a2 = tp0[2];
             const float4 b0 = tp1[0], b1 = tp1[1], b2 = tp1[2];
             if (COUNT) tc.tris += two ? 2u : 1u;
-            float t, u, v;
-            if (intersect_triangle(R.pre, R.o, ld3(a0), ld3(a1), ld3(a2), 0.0f, best, &t, &u, &v)) {
+            float t, u, v, dt;
+            if (intersect_triangle_vw(R.pre, R.o, ld3(a0), ld3(a1), ld3(a2), 0.0f, best, &t, &u, &v, &dt)) {
                 const uint32_t id = __float_as_uint(a0.w);
                 if (ANY) {
                     hit_any = true;
@@ -713,10 +717,11 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ANY
                     best = t;
                     best_id = id;
                     bu = u;
+                    bdet = dt;
                     bv = v;
                 }
             }
-            if (two && !done && intersect_triangle(R.pre, R.o, ld3(b0), ld3(b1), ld3(b2), 0.0f, best, &t, &u, &v)) {
+            if (two && !done && intersect_triangle_vw(R.pre, R.o, ld3(b0), ld3(b1), ld3(b2), 0.0f, best, &t, &u, &v, &dt)) {
                 const uint32_t id = __float_as_uint(b0.w);
                 if (ANY) {
                     hit_any = true;
@@ -725,10 +730,17 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ANY
                     best = t;
                     best_id = id;
                     bu = u;
+                    bdet = dt;
                     bv = v;
                 }
             }
-        } else if (do_node) {
+        }
+#if RT_TRI_THEN_NODE
+        // a lane whose triangles ran out in this step takes its next node in the same iteration
+        // (the node block is issued anyway for the wave's other lanes)
+        if (Q.tri_vote == 0) do_node = !done && t_mask == 0u && (g_hits != 0u || sp > 0);
+#endif
+        if (do_node && !(do_tri && !RT_TRI_THEN_NODE)) {
             // ---- one 8-wide node
             if (!g_hits) {  // sp > 0 here (checked at the end of the previous iteration)
                 --sp;
@@ -787,7 +799,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ANY
                     Q.W.p_accum[pid] = make_float4(a.x + c.x, a.y + c.y, a.z + c.z, 0.0f);
                 }
             } else {
-                Q.W.hits[e] = make_float4(best, __uint_as_float(best_id), bu, bv);
+                Q.W.hits[e] = make_float4(best, __uint_as_float(best_id), bu / bdet, bv / bdet);
             }
         }
     }
@@ -966,7 +978,7 @@ wf_finish_step(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int c
     uint32_t* qout_cnt = Q.W.counts + cslot((1 - cur) * kShards + (int)(blockIdx.x & (kShards - 1)));
     // traversal
     RaySetup R = ray_setup(mk3(0, 0, 0), mk3(1, 0, 0));
-    float best = 0.0f, bu = 0.0f, bv = 0.0f;
+    float best = 0.0f, bu = 0.0f, bv = 0.0f, bdet = 1.0f;   // closest hit: u = bu / bdet, v = bv / bdet
     uint32_t best_id = 0xffffffffu, g_base = 0, g_hits = 0, t_base = 0, t_mask = 0, t_valid = 0;
     bool g_flip = false;
     int sp = 0;
@@ -976,6 +988,7 @@ wf_finish_step(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int c
         best = tmax;
         best_id = 0xffffffffu;
         bu = bv = 0.0f;
+        bdet = 1.0f;
         g_base = 0;
         g_hits = 1;   // virtual group holding the root
         g_flip = false;
@@ -1074,7 +1087,8 @@ wf_finish_step(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int c
         if (mode == kClosest || mode == kShadow) {
             const bool any = mode == kShadow;
             bool tdone = false;
-            if (t_mask) {
+            const bool tri_step = t_mask != 0u;
+            if (tri_step) {
                 // up to two triangles, both fetched before either is tested, tested in mask order
                 const int k0 = lowest_bit(t_mask);
                 t_mask &= t_mask - 1u;
@@ -1086,8 +1100,8 @@ wf_finish_step(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int c
                 const float4 a0 = tp0[0], a1 = tp0[1], a2 = tp0[2];
                 const float4 b0 = tp1[0], b1 = tp1[1], b2 = tp1[2];
                 if (COUNT) tc.tris += two ? 2u : 1u;
-                float t, u, v;
-                if (intersect_triangle(R.pre, R.o, ld3(a0), ld3(a1), ld3(a2), 0.0f, best, &t, &u, &v)) {
+                float t, u, v, dt;
+                if (intersect_triangle_vw(R.pre, R.o, ld3(a0), ld3(a1), ld3(a2), 0.0f, best, &t, &u, &v, &dt)) {
                     const uint32_t id = __float_as_uint(a0.w);
                     if (any) {
                         hit_any = true;
@@ -1096,10 +1110,11 @@ wf_finish_step(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int c
                         best = t;
                         best_id = id;
                         bu = u;
+                        bdet = dt;
                         bv = v;
                     }
                 }
-                if (two && !tdone && intersect_triangle(R.pre, R.o, ld3(b0), ld3(b1), ld3(b2), 0.0f, best, &t, &u, &v)) {
+                if (two && !tdone && intersect_triangle_vw(R.pre, R.o, ld3(b0), ld3(b1), ld3(b2), 0.0f, best, &t, &u, &v, &dt)) {
                     const uint32_t id = __float_as_uint(b0.w);
                     if (any) {
                         hit_any = true;
@@ -1108,10 +1123,14 @@ wf_finish_step(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int c
                         best = t;
                         best_id = id;
                         bu = u;
+                        bdet = dt;
                         bv = v;
                     }
                 }
-            } else {
+            }
+            // a lane whose triangles ran out in this step takes its next node in the same
+            // iteration (RT_TRI_THEN_NODE; the node block is issued anyway for other lanes)
+            if (RT_TRI_THEN_NODE ? (!tdone && t_mask == 0u && (g_hits != 0u || sp > 0)) : !tri_step) {
                 if (!g_hits) {   // sp > 0 here (checked at the end of the previous step)
                     --sp;
                     const uint32_t ent = (uint32_t)stack[sp * kBlock];
@@ -1186,8 +1205,8 @@ wf_finish_step(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int c
                 Hit h;
                 h.t = best;
                 h.id = best_id;
-                h.u = bu;
-                h.v = bv;
+                h.u = bu / bdet;
+                h.v = bv / bdet;
                 const int sample = (int)meta.y;
                 StepResult r;
                 shade_step<FULL, false>(S, U, halton, (int)meta.w, sample, rayO, rayD, h, p, sample == 0 && p.step == 0,
