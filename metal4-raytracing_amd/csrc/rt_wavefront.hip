@@ -267,6 +267,9 @@ __device__ __forceinline__ void write_pixel_outputs(const FrameParams& P, uint32
 #ifndef RT_TRI_THEN_NODE
 #define RT_TRI_THEN_NODE 1   // a lane may run its last triangle step and its next node step in one iteration
 #endif
+#ifndef RT_TRAV_SCHED
+#define RT_TRAV_SCHED 1   // wf_trace iteration: 1 = triangle step, node step; 2 = + a second node step; 3 = + a second triangle step
+#endif
 #ifndef RT_NEAREST_FIRST
 #define RT_NEAREST_FIRST 1
 #endif
@@ -694,9 +697,9 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ANY
             do_tri = do_tri && tri_phase;
             do_node = do_node && !tri_phase;
         }
-        if (do_tri) {
-            // ---- up to two triangles: both fetched before either is tested (one memory
-            // latency), tested in mask order so closest-hit updates are those of the serial loop
+        // ---- up to two triangles: both fetched before either is tested (one memory latency),
+        // tested in mask order so closest-hit updates are those of the serial loop
+        auto tri_step = [&]() {
             const int k0 = lowest_bit(t_mask);
             t_mask &= t_mask - 1u;
             const bool two = t_mask != 0u;
@@ -734,14 +737,9 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ANY
                     bv = v;
                 }
             }
-        }
-#if RT_TRI_THEN_NODE
-        // a lane whose triangles ran out in this step takes its next node in the same iteration
-        // (the node block is issued anyway for the wave's other lanes)
-        if (Q.tri_vote == 0) do_node = !done && t_mask == 0u && (g_hits != 0u || sp > 0);
-#endif
-        if (do_node && !(do_tri && !RT_TRI_THEN_NODE)) {
-            // ---- one 8-wide node
+        };
+        // ---- one 8-wide node
+        auto node_step = [&]() {
             if (!g_hits) {  // sp > 0 here (checked at the end of the previous iteration)
                 --sp;
                 const uint32_t ent = (uint32_t)stack[sp * kBlock];
@@ -782,7 +780,21 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ANY
 #else
             test_node8_words(w, R, 0.0f, best, g_hits, t_mask, t_valid, g_base, t_base, g_flip);
 #endif
-        }
+        };
+        if (do_tri) tri_step();
+#if RT_TRI_THEN_NODE
+        // a lane whose triangles ran out in this step takes its next node in the same iteration
+        // (the node block is issued anyway for the wave's other lanes)
+        if (Q.tri_vote == 0) do_node = !done && t_mask == 0u && (g_hits != 0u || sp > 0);
+#endif
+        if (do_node && !(do_tri && !RT_TRI_THEN_NODE)) node_step();
+#if RT_TRAV_SCHED == 2
+        // a second node step for lanes whose node test found no triangles
+        if (Q.tri_vote == 0 && !done && t_mask == 0u && (g_hits != 0u || sp > 0)) node_step();
+#elif RT_TRAV_SCHED == 3
+        // the first triangle step of the leaves the node test just found
+        if (Q.tri_vote == 0 && !done && t_mask != 0u) tri_step();
+#endif
         if (!done && !t_mask && !g_hits && sp == 0) done = true;
         if (done) {
             active = false;
