@@ -22,10 +22,11 @@ import time
 
 import numpy as np
 
-# Eight hardware queues per process (HIP's default is 4) before anything initialises HIP: small
-# frames (a multi-GPU rank's share) keep eight frames in flight, one stream and queue each
-# (rt_api.cpp small_frame_slots); more streams than queues would serialise unrelated frames.
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+# Eight hardware queues per process (HIP's default is 4, and the GPU boxes export 4) before
+# anything initialises HIP: small frames (a multi-GPU rank's share) keep eight frames in flight,
+# one stream and queue each (rt_api.cpp small_frame_slots); more streams than queues would
+# serialise unrelated frames.  RT_HW_QUEUES overrides (tuning runs).
+os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("RT_HW_QUEUES", "8")
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
