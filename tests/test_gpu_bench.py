@@ -33,7 +33,9 @@ def test_bench_line_contract():
     assert r["bound"] == "hbm" and r["peak"] == 8000.0 and 0 < r["frac"] < 1
     cb = d["cpu_baseline"]
     assert cb["value"] > 0 and cb["kind"] == "port" and cb["cores"] >= 1
-    assert d["config"]["frames_in_flight"] == 4   # default for a small frame (< 6M paths)
+    # a small frame (< 8M allocated paths) keeps eight frames in flight: bench.py asks HIP for
+    # eight hardware queues (rt_api.cpp small_frame_slots)
+    assert d["config"]["frames_in_flight"] == 8
 
 
 def test_bench_emulated_rank_and_animation():
