@@ -22,11 +22,13 @@ import time
 
 import numpy as np
 
-# Eight hardware queues per process (HIP's default is 4, and the GPU boxes export 4) before
-# anything initialises HIP: small frames (a multi-GPU rank's share) keep eight frames in flight,
-# one stream and queue each (rt_api.cpp small_frame_slots); more streams than queues would
-# serialise unrelated frames.  RT_HW_QUEUES overrides (tuning runs).
-os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("RT_HW_QUEUES", "8")
+# Hardware queues per process, fixed before anything initialises HIP so every run sees the same
+# count: four (HIP's default, also what the GPU boxes export).  Small frames (a multi-GPU rank's
+# share) keep as many frames in flight as there are queues, up to eight (rt_api.cpp
+# small_frame_slots).  Final round-2 kernels, 8-way rank share: four queues / four slots 4.21 /
+# 4.24 Grays/s against eight / eight 4.11 / 4.10 (round 1's slower kernels preferred eight).
+# RT_HW_QUEUES overrides (tuning runs).
+os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("RT_HW_QUEUES", "4")
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
@@ -66,7 +68,7 @@ def parse():
     p.add_argument("--sort-bins", type=int, default=0, help="hit-sort bins (0 = library default, -1 = no sort)")
     p.add_argument("--bvh", default="sah", choices=["sah", "lbvh"], help="host binned-SAH or on-device LBVH build")
     p.add_argument("--frames-in-flight", type=int, default=0,
-                   help="frames the renderer overlaps (0 = library default: 2; below 8M allocated paths per frame 8 with the 8 hardware queues set here, else 4; 1 = one at a time)")
+                   help="frames the renderer overlaps (0 = library default: 2; below 8M allocated paths per frame 4 with the 4 hardware queues set here, 8 with RT_HW_QUEUES=8; 1 = one at a time)")
     p.add_argument("--animate", action="store_true",
                    help="configs[4] shape: skin every skinned mesh at t = frame/60 s and refit the BVH before each frame")
     p.add_argument("--rebuild", action="store_true", help="with --animate: rebuild the BVH on the device instead of refitting")

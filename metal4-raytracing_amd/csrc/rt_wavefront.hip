@@ -270,6 +270,9 @@ __device__ __forceinline__ void write_pixel_outputs(const FrameParams& P, uint32
 #ifndef RT_TRAV_SCHED
 #define RT_TRAV_SCHED 1   // wf_trace iteration: 1 = triangle step, node step; 2 = + a second node step; 3 = + a second triangle step
 #endif
+#ifndef RT_NEAREST_ANY
+#define RT_NEAREST_ANY 1   // nearest-child-first for the shadow (any-hit) queue too
+#endif
 #ifndef RT_NEAREST_FIRST
 #define RT_NEAREST_FIRST 1
 #endif
@@ -776,7 +779,8 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ANY
                 w = load_node8(S.nodes8, ni);
             }
 #if RT_NEAREST_FIRST
-            test_node8_words(w, R, 0.0f, best, g_hits, t_mask, t_valid, g_base, t_base, g_flip, &g_near);
+            test_node8_words(w, R, 0.0f, best, g_hits, t_mask, t_valid, g_base, t_base, g_flip,
+                             (ANY && !RT_NEAREST_ANY) ? nullptr : &g_near);
 #else
             test_node8_words(w, R, 0.0f, best, g_hits, t_mask, t_valid, g_base, t_base, g_flip);
 #endif
