@@ -70,7 +70,9 @@ constexpr int kGens = kMaxSlots;
 // 1.5M 5.97 / 6.02, 1M 6.02 / 6.00 Grays/s; four slots serve the small frames of multi-GPU ranks:
 // 8-way split 2.92 -> 3.46 Grays/s per rank at 512K against 1M in round 1, 256K-786K within noise
 // in round 2, with the finish kernel on 20 % of the grid)
-constexpr int kTailInFlight[kMaxSlots + 1] = {0, 0, 1310720, 1048576, 524288, 524288, 524288, 524288, 524288};
+// Final round-2 kernels, 8-way share with four slots: 256K 4.14 / 4.13, 512K 4.25 / 4.26, 768K
+// 4.32 / 4.30 Grays/s per rank -> 768K for four slots.
+constexpr int kTailInFlight[kMaxSlots + 1] = {0, 0, 1310720, 1048576, 786432, 524288, 524288, 524288, 524288};
 // paths a frame allocates (pixels x (spp + motion-adaptive extra samples), what ensure_wavefront
 // sizes a slot for): below, four or eight frames in flight by default (small_frame_slots).  Every 1080p x 4 spp frame (8.29M
 // base paths) stays at two; a 2-way rank share of it with the default two extra samples (6.2M)
