@@ -171,7 +171,7 @@ typedef struct rt_stats {
     float trace_ms;         /* its summed device time (HIP events on the render stream) */
     uint64_t trace_closest_rays; /* the closest-hit (extend) share of trace_rays */
     int32_t finish_launches;     /* wavefront: persistent finish launches (their time: kernel_ms[5]) */
-    int32_t frames_in_flight;    /* frames the last rt_render_frame could overlap (1..4) */
+    int32_t frames_in_flight;    /* frames the last rt_render_frame could overlap (1..8) */
     /* running totals over every finished frame since rt_create (frames submitted back to back
        without rt_wait are each counted) */
     uint64_t frames_total;
