@@ -567,7 +567,7 @@ __global__ void __launch_bounds__(kSortThreads) wf_sort_scatter(DevScene S, WfPa
 // (slowest ray) x (rays per lane).
 template <bool ANY, bool COUNT>
 #ifndef RT_EXTEND_WAVES
-#define RT_EXTEND_WAVES 7   // 70 VGPRs without scratch (8 waves: 64 VGPRs + 24 B/lane of spills)
+#define RT_EXTEND_WAVES 8   // 64 VGPRs, no scratch (final round-2 node test; at 70 VGPRs it took 7 waves)
 #endif
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ANY ? 8 : RT_EXTEND_WAVES, ANY ? 8 : RT_EXTEND_WAVES))) wf_trace(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int cur) {
     const FrameParams& P = *Pp;   // per-frame parameters in device memory
