@@ -273,6 +273,9 @@ __device__ __forceinline__ void write_pixel_outputs(const FrameParams& P, uint32
 #ifndef RT_TRAV_SCHED
 #define RT_TRAV_SCHED 1   // wf_trace iteration: 1 = triangle step, node step; 2 = + a second node step; 3 = + a second triangle step
 #endif
+#ifndef RT_PRIO_LOADS
+#define RT_PRIO_LOADS 0   // raise the wave priority (s_setprio) while a traversal step issues its loads
+#endif
 #ifndef RT_TRI_B_MASKED
 #define RT_TRI_B_MASKED 0   // 1: branch around the second triangle's loads (measured 1-2 % slower: 7.07 -> 6.97 Grays/s)
 #endif
@@ -693,6 +696,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ANY
         }
         if (__ballot(active) == 0ull) break;
         if (!active) continue;
+        if (RT_PRIO_LOADS) __builtin_amdgcn_s_setprio(2);   // the wave about to issue its triangle loads goes first
         if (COUNT) ++steps;
 
         bool done = false;
@@ -729,6 +733,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ANY
             b1 = tp1[1];
             b2 = tp1[2];
 #endif
+            if (RT_PRIO_LOADS) __builtin_amdgcn_s_setprio(0);
             if (COUNT) tc.tris += two ? 2u : 1u;
             float t, u, v, dt;
             if (intersect_triangle_vw(R.pre, R.o, ld3(a0), ld3(a1), ld3(a2), 0.0f, best, &t, &u, &v, &dt)) {
@@ -760,6 +765,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ANY
         };
         // ---- one 8-wide node
         auto node_step = [&]() {
+            if (RT_PRIO_LOADS) __builtin_amdgcn_s_setprio(2);   // the wave about to issue its node loads goes first
             if (!g_hits) {  // sp > 0 here (checked at the end of the previous iteration)
                 --sp;
                 const uint32_t ent = (uint32_t)stack[sp * kBlock];
@@ -795,6 +801,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ANY
             } else {
                 w = load_node8(S.nodes8, ni);
             }
+            if (RT_PRIO_LOADS) __builtin_amdgcn_s_setprio(0);
 #if RT_NEAREST_FIRST
             test_node8_words(w, R, 0.0f, best, g_hits, t_mask, t_valid, g_base, t_base, g_flip,
                              (ANY && !RT_NEAREST_ANY) ? nullptr : &g_near);
