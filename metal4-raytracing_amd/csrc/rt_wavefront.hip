@@ -651,7 +651,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ANY
     uint32_t best_id = 0xffffffffu, g_base = 0, g_hits = 0, t_base = 0, t_mask = 0, t_valid = 0;
     int sp = 0;
     uint32_t steps = 0;   // COUNT: iterations the current ray has taken
-    int g_near = -1;      // RT_NEAREST_FIRST: rank of the nearest hit child of the last node test
+    [[maybe_unused]] int g_near = -1;   // RT_NEAREST_FIRST: rank of the nearest hit child of the last node test
 
     while (true) {
         // refill idle lanes from the wave's range
@@ -1022,7 +1022,7 @@ wf_finish_step(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int c
     uint32_t best_id = 0xffffffffu, g_base = 0, g_hits = 0, t_base = 0, t_mask = 0, t_valid = 0;
     bool g_flip = false;
     int sp = 0;
-    int g_near = -1;   // RT_NEAREST_FIRST: rank of the nearest hit child of the last node test
+    [[maybe_unused]] int g_near = -1;   // RT_NEAREST_FIRST: rank of the nearest hit child of the last node test
     auto start_trace = [&](f3 o, f3 d, float tmax) {
         R = ray_setup(o, d);
         best = tmax;
@@ -1807,7 +1807,7 @@ static unsigned trace_grid_cap() {
     static unsigned cap = 0;
     if (!cap) {
         int dev = 0, cus = 256, per = 0;
-        if (hipGetDevice(&dev) == hipSuccess) hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, wf_trace<false, false>, kBlock, 0) != hipSuccess || per < 1)
             per = 4;
         cap = (unsigned)(cus * per);
@@ -1819,7 +1819,7 @@ static unsigned trace_grid_cap() {
 template <typename K>
 static unsigned resident_grid(K kernel, int fallback_per_cu) {
     int dev = 0, cus = 256, per = 0;
-    if (hipGetDevice(&dev) == hipSuccess) hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, kBlock, 0) != hipSuccess || per < 1)
         per = fallback_per_cu;
     return (unsigned)(cus * per);
