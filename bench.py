@@ -8,6 +8,12 @@ N GPUs (one process per GPU, torch.distributed over RCCL): the frame is tile-par
 gathers the packed radiance over RCCL/xGMI and unpacks it into the full frame ("strong"
 scaling: the frame is fixed, N GPUs share it).
 
+`python bench.py --gpus N` with no WORLD_SIZE in the environment starts the N ranks itself: the
+parent never touches the GPU (it does not import torch); it starts N child processes of this
+script with RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT set, passes rank 0's JSON
+line through (the children share its stdout) and exits non-zero if any child fails.  Under
+torch.distributed.run (WORLD_SIZE set) the process is one rank.
+
 Grays/s = (closest-hit + shadow rays traced, all ranks) / wall time of the K timed frames
 (barrier + device sync on both sides, max over ranks).  Inputs (scene, BVH, random offsets)
 are resident in HBM before the timed region.
@@ -17,43 +23,49 @@ import importlib
 import json
 import os
 import re
+import socket
+import subprocess
 import sys
 import time
 
 import numpy as np
 
 # Hardware queues per process, fixed before anything initialises HIP so every run sees the same
-# count: four (HIP's default, also what the GPU boxes export).  Small frames (a multi-GPU rank's
-# share) keep as many frames in flight as there are queues, up to eight (rt_api.cpp
-# small_frame_slots).  Final round-2 kernels, 8-way rank share: four queues / four slots 4.21 /
-# 4.24 Grays/s against eight / eight 4.11 / 4.10 (round 1's slower kernels preferred eight).
-# RT_HW_QUEUES overrides (tuning runs).
-os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("RT_HW_QUEUES", "4")
+# count: RT_HW_QUEUES if set, else the caller's GPU_MAX_HW_QUEUES, else four (HIP's default, also
+# what the GPU boxes export).  Small frames (a multi-GPU rank's share) keep as many frames in
+# flight as there are queues, up to eight (rt_api.cpp small_frame_slots); with the final round-2
+# kernels four queues / four slots measured 4.21 / 4.24 Grays/s per rank against eight / eight
+# 4.11 / 4.10.
+os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("RT_HW_QUEUES") or os.environ.get("GPU_MAX_HW_QUEUES") or "4"
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: 8.0 TB/s spec
 
-# Algorithmic bytes: per traced ray 32 B in (o, tmin, d, tmax) + 16 B hit out;
-# per BVH node fetched 64 B; per triangle tested 48 B; per closest hit shading 16 B tri record
-# + 3x16 B normals + 48 B instance transform; per pixel 4 B offset + 16 B history read +
-# 16 B accumulation write + 4 B depth + 8+8 B motion read/write.
+# Algorithmic bytes (DESIGN.md §6 'Roofline'): per traced ray its 48-B queue entry (extend: 32 B ray
+# in + 16 B hit out; connect: 48 B shadow entry in); per 8-wide node fetched from memory 80 B; per
+# triangle tested 48 B; per closest hit shaded inside the finish kernel 16 B triangle record +
+# 3 x 16 B normals + 48 B instance transform.  Node tests served from the LDS copy of the BVH's top
+# levels move no memory per visit: they are charged once per block (the staging read, B_NODE x
+# kTopNodes per block).
 B_RAY = 48
 B_NODE = 80  # compressed 8-wide node (Bvh8Node)
 B_TRI = 48
 B_HIT = 16 + 48 + 48
 B_PIXEL = 4 + 16 + 16 + 4 + 16
-B_QRAY = 48  # wf_trace queue entry: extend 32 B ray in + 16 B hit out; connect 48 B shadow entry in
-_ROOT = os.path.dirname(os.path.abspath(__file__))
+B_QRAY = 48
+TOP_NODES = 32          # rt_device.h kTopNodes
+TRACE_BLOCKS_PER_CU = 8   # wf_trace: 256-thread blocks at 8 waves / SIMD
+FINISH_BLOCKS_PER_CU = 4  # wf_finish_step: 4 waves / SIMD
 # PMC traffic of the newest round (profiles/rNN_traffic.json, tools/gpurun_profile.sh)
-_TRAFFIC = sorted(f for f in os.listdir(os.path.join(_ROOT, "profiles")) if re.fullmatch(r"r\d+_traffic\.json", f)) \
-    if os.path.isdir(os.path.join(_ROOT, "profiles")) else []
+_TRAFFIC = sorted(f for f in os.listdir(os.path.join(ROOT, "profiles")) if re.fullmatch(r"r\d+_traffic\.json", f)) \
+    if os.path.isdir(os.path.join(ROOT, "profiles")) else []
 TRAFFIC_JSON_REL = "profiles/" + (_TRAFFIC[-1] if _TRAFFIC else "r01_traffic.json")
-TRAFFIC_JSON = os.path.join(_ROOT, TRAFFIC_JSON_REL)
+TRAFFIC_JSON = os.path.join(ROOT, TRAFFIC_JSON_REL)
 
 
-def parse():
+def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=32)
@@ -78,27 +90,134 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample time")
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--traffic-csv", default=None, help="rocprofv3 --pmc counter_collection.csv for traffic")
-    return p.parse_args()
+    p.add_argument("--dry-run", action="store_true",
+                   help="launcher / collective test on the CPU: gloo instead of RCCL, a stub frame instead of the renderer")
+    return p.parse_args(argv)
+
+
+# ---- launcher -----------------------------------------------------------------------------------
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch(n, argv):
+    """Starts n ranks of this script (one process per GPU) and waits for them; returns the exit
+    status (the first failing rank's, after stopping the others).  Touches no GPU itself."""
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env))
+    status = 0
+    try:
+        while procs:
+            for p in list(procs):
+                rc = p.poll()
+                if rc is None:
+                    continue
+                procs.remove(p)
+                if rc != 0 and status == 0:
+                    status = rc if rc > 0 else 1
+                    for q in procs:   # a failed rank leaves the collectives hanging: stop the others
+                        q.terminate()
+            time.sleep(0.2)
+    finally:
+        for p in procs:
+            p.kill()
+            p.wait()
+    return status
+
+
+# ---- one rank -----------------------------------------------------------------------------------
+class StubFrames:
+    """--dry-run: a constant 'frame' per rank with fixed ray counts, so the launcher, barriers,
+    max-over-ranks timing and the tile gather run without a GPU."""
+
+    RAYS = 1000
+
+    def __init__(self, a, rank, n):
+        from importlib import import_module
+        tiles = import_module("metal4-raytracing_amd.tiles")
+        self.gather = tiles.TileGather(a.width, a.height, a.tile, rank, n, "cpu") if n > 1 else None
+        self.img = np.full((a.height, a.width, 4), float(rank + 1), np.float32)
+        self.frames = 0
+
+    def submit(self):
+        self.frames += 1
+        if self.gather is not None:
+            out = self.gather.gather(self.img)
+            if out is not None:   # rank 0: every rank's tiles arrived
+                assert np.all(out[..., 0] >= 1.0)
+
+    def totals(self):
+        return dict(frames=self.frames, closest=self.frames * self.RAYS, shadow=self.frames * self.RAYS // 2)
 
 
 def main():
-    a = parse()
+    argv = sys.argv[1:]
+    a = parse(argv)
+    world_env = int(os.environ.get("WORLD_SIZE") or 0)
+    if a.gpus > 1 and world_env == 0:
+        sys.exit(launch(a.gpus, argv))
     import torch
     import torch.distributed as dist
-    rt = importlib.import_module("metal4-raytracing_amd")
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    world = max(world_env, 1)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    n = world
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    n = max(world, 1)
+        if a.dry_run:
+            dist.init_process_group("gloo")
+        else:
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        assert dist.get_world_size() == world
 
+    def barrier():
+        if n > 1:
+            dist.barrier()
+        if not a.dry_run:
+            torch.cuda.synchronize()
+
+    if a.dry_run:
+        stub = StubFrames(a, rank, n)
+        for _ in range(a.warmup):
+            stub.submit()
+        barrier()
+        t0 = time.perf_counter()
+        for _ in range(a.steps):
+            stub.submit()
+        barrier()
+        dt = time.perf_counter() - t0
+        tot = torch.tensor([dt, float(a.steps * (StubFrames.RAYS + StubFrames.RAYS // 2))], dtype=torch.float64)
+        if n > 1:
+            mx, sm = tot.clone(), tot.clone()
+            dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+            dist.all_reduce(sm, op=dist.ReduceOp.SUM)
+            dt, rays = float(mx[0]), float(sm[1])
+        else:
+            dt, rays = float(tot[0]), float(tot[1])
+        if rank == 0:
+            print(json.dumps({"metric": "dry-run (stub frames, gloo)", "value": rays / dt / 1e9, "unit": "Grays/s",
+                              "n_gpus": n, "world_size": n, "steps": a.steps, "warmup": a.warmup,
+                              "ms_per_step": dt / a.steps * 1e3, "higher_is_better": True, "scaling": "strong",
+                              "vs_baseline": None, "dtype": "f32", "data": "stub", "config": {"workload": "dry-run"}}),
+                  flush=True)
+        if n > 1:
+            dist.destroy_process_group()
+        return
+
+    rt = importlib.import_module("metal4-raytracing_amd")
     scene = rt.Scene.preset(a.scene)
     t0 = time.time()
     R = rt.Renderer(scene, a.width, a.height, device=local, pipeline=a.pipeline, seed=3, sort_bins=a.sort_bins,
-                   bvh=a.bvh, frames_in_flight=a.frames_in_flight)
+                    bvh=a.bvh, frames_in_flight=a.frames_in_flight)
     setup_s = time.time() - t0
     R.samplesPerPixel = a.spp
     R.maxBounces = a.bounces
@@ -111,14 +230,6 @@ def main():
     if n > 1:
         tiles_mod = importlib.import_module("metal4-raytracing_amd.tiles")
         gather = tiles_mod.TileGather(a.width, a.height, T, rank, n, dev, renderer=R)
-
-    def frame():
-        R.draw(tiles=tiles)
-        R.wait()
-        st = R.stats()
-        if gather is not None:
-            gather.gather()   # packed tiles -> rank 0 over RCCL, unpacked into its radiance target
-        return st
 
     skinned = []
     if a.animate:
@@ -136,35 +247,30 @@ def main():
             R.skin(m, scene.joint_matrices(m, t))
         R.rebuild(device=True) if a.rebuild else R.refit()
 
-    def submit():
+    gather_events = []
+
+    def submit(timed=False):
         # one step: the frame is submitted and, multi-GPU, its tiles packed, gathered to rank 0
-        # over RCCL and unpacked there, all enqueued without a host wait (the renderer keeps two
-        # frames in flight and waits for a slot's previous frame itself)
+        # over RCCL and unpacked there, all enqueued without a host wait (the renderer keeps
+        # frames in flight and waits for a slot's previous frame itself).  Timed steps bracket
+        # the collective (after the pack, through the unpack) with events on torch's stream.
         animate()
         R.draw(tiles=tiles)
         if gather is not None:
-            gather.gather()
-
-    def barrier():
-        if n > 1:
-            dist.barrier()
-        torch.cuda.synchronize()
+            ev = None
+            if timed:
+                ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            gather.gather(events=ev)
+            if ev is not None:
+                gather_events.append(ev)
 
     # counting frame (untimed): node visits / triangle tests per ray for the roofline numerator
     R.set_counting(True)
     R.frameIndex = 0
-    cst = frame()
+    R.draw(tiles=tiles)
+    R.wait()
+    cst = R.stats()
     R.set_counting(False)
-    rays_c = cst.closest_rays + cst.shadow_rays
-    nodes_per_ray = cst.node_visits / max(rays_c, 1)
-    tris_per_ray = cst.tri_tests / max(rays_c, 1)
-    # the queue traversal kernel alone (wavefront): its own node / triangle visits per traced ray
-    q_nodes_per_ray = cst.trace_nodes / max(cst.trace_rays, 1)
-    q_tris_per_ray = cst.trace_tris / max(cst.trace_rays, 1)
-    # the persistent finish kernel: the rest of the visits, over the rays it traced
-    f_rays_c = rays_c - cst.trace_rays
-    f_nodes_per_ray = (cst.node_visits - cst.trace_nodes) / max(f_rays_c, 1)
-    f_tris_per_ray = (cst.tri_tests - cst.trace_tris) / max(f_rays_c, 1)
     R.samplesPerPixel = a.spp  # resets frameIndex (didSet)
 
     for _ in range(a.warmup):
@@ -176,97 +282,41 @@ def main():
     t_host = 0.0
     for _ in range(a.steps):
         th = time.perf_counter()
-        submit()
+        submit(timed=True)
         t_host += time.perf_counter() - th
     R.wait()
     barrier()
     dt = time.perf_counter() - t0
     # the running totals of every frame of the timed region (HIP events per stage on the
     # renderer's streams, ray counters read back per frame)
-    last_st = s1 = R.stats()
+    s1 = R.stats()
     assert s1.frames_total - s0.frames_total == a.steps
+    gather_ms = sum(e0.elapsed_time(e1) for e0, e1 in gather_events) / a.steps if gather_events else 0.0
     d = lambda f: getattr(s1, f) - getattr(s0, f)
     closest = d("total_closest_rays")
     rays = closest + d("total_shadow_rays")
-    trace_rays, trace_launches, trace_ms = d("total_trace_rays"), d("total_trace_launches"), d("total_trace_ms")
-    trace_closest, finish_launches = d("total_trace_closest_rays"), d("total_finish_launches")
-    stage_ms = np.array(list(s1.total_kernel_ms)) - np.array(list(s0.total_kernel_ms))
-    kernel_ms = [d("total_frame_ms") / a.steps]
+    kms_local = d("total_frame_ms") / a.steps
 
-    rays_local, closest_local = rays, closest   # this rank's, for the per-kernel roofline
-    tot = torch.tensor([dt, float(rays), float(closest), float(np.mean(kernel_ms))], dtype=torch.float64, device=dev)
+    tot = torch.tensor([dt, float(rays), float(closest), kms_local, gather_ms], dtype=torch.float64, device=dev)
     if n > 1:
         mx = tot.clone()
         dist.all_reduce(mx, op=dist.ReduceOp.MAX)
         sm = tot.clone()
         dist.all_reduce(sm, op=dist.ReduceOp.SUM)
-        dt, rays, closest, kms = float(mx[0]), float(sm[1]), float(sm[2]), float(mx[3])
+        dt, rays_all, kms, gather_ms = float(mx[0]), float(sm[1]), float(mx[3]), float(mx[4])
     else:
-        kms = float(tot[3])
+        rays_all, kms = float(rays), kms_local
     if rank != 0:
         dist.destroy_process_group()
         return
 
-    value = rays / dt / 1e9
+    value = rays_all / dt / 1e9
     ms_per_step = dt / a.steps * 1e3
-    kernels = []
-    if last_st.pipeline == 1 and trace_launches > 0:
-        # wf_trace (extend + connect launches), per launch.  Algorithmic bytes per traced ray: 48 B
-        # queue entry in (+ hit record out) + 80 B per 8-wide node fetched + 48 B per triangle
-        # tested (DESIGN.md 'Roofline').
-        rpl = trace_rays / trace_launches
-        kernels.append(dict(
-            kernel="rt::wf_trace<{false,true}, false> (extend + connect)", launches=trace_launches / a.steps,
-            launch_ms=trace_ms / trace_launches, rays_per_launch=rpl, nodes_per_ray=q_nodes_per_ray,
-            tris_per_ray=q_tris_per_ray,
-            bytes_per_launch=rpl * (B_QRAY + q_nodes_per_ray * B_NODE + q_tris_per_ray * B_TRI)))
-    if last_st.pipeline == 1 and finish_launches > 0:
-        # wf_finish_step: the tail paths to completion.  Per ray 48 B (ray + hit) + nodes + triangles
-        # as above; per closest hit the shading gathers (B_HIT); the path state in and out (48 B x 2)
-        # once per path is left out (not counted per ray).
-        f_rays = (rays_local - trace_rays) / finish_launches
-        f_closest = (closest_local - trace_closest) / finish_launches
-        kernels.append(dict(
-            kernel="rt::wf_finish_step<false, false, 4>", launches=finish_launches / a.steps,
-            launch_ms=float(stage_ms[5]) / finish_launches, rays_per_launch=f_rays, nodes_per_ray=f_nodes_per_ray,
-            tris_per_ray=f_tris_per_ray,
-            bytes_per_launch=f_rays * (B_RAY + f_nodes_per_ray * B_NODE + f_tris_per_ray * B_TRI) + f_closest * B_HIT))
-    if not kernels:
-        # megakernel: the whole frame is one launch
-        rpl = rays_local / a.steps
-        kernels.append(dict(
-            kernel="rt::megakernel<false, false>", launches=1, launch_ms=kms, rays_per_launch=rpl,
-            nodes_per_ray=nodes_per_ray, tris_per_ray=tris_per_ray,
-            bytes_per_launch=(rpl * (B_RAY + nodes_per_ray * B_NODE + tris_per_ray * B_TRI)
-                              + closest_local / a.steps * B_HIT + a.width * a.height / n * B_PIXEL)))
-    for k in kernels:
-        k["achieved"] = k["bytes_per_launch"] / (k["launch_ms"] * 1e-3) / 1e9
-        k["ms_per_frame"] = k["launch_ms"] * k["launches"]
-    # the dominant kernel: the most device time per frame
-    dom = max(kernels, key=lambda k: k["ms_per_frame"])
-    # the whole frame: every timed kernel's algorithmic bytes over the wall time per frame (with
-    # frames in flight the kernels of two frames share the GPU, so per-launch durations stretch
-    # while the aggregate rate rises)
-    job_bytes = sum(k["bytes_per_launch"] * k["launches"] for k in kernels)
-    job_achieved = job_bytes / (dt / a.steps) / 1e9   # per GPU (rank 0's kernels)
-    kernel, launch_ms, bytes_per_launch = dom["kernel"], dom["launch_ms"], dom["bytes_per_launch"]
-    rays_per_launch, npr, tpr, achieved = dom["rays_per_launch"], dom["nodes_per_ray"], dom["tris_per_ray"], dom["achieved"]
-    traffic, traffic_src, l2_hit = None, None, None
-    if a.traffic_csv:
-        traffic = read_traffic(a.traffic_csv.split(","), traffic_key(kernel))
-        traffic_src = "live: " + a.traffic_csv
-    elif os.path.exists(TRAFFIC_JSON):
-        with open(TRAFFIC_JSON) as f:
-            tj = json.load(f)
-        if tj.get("config") == [a.scene, a.width, a.height, a.spp, a.bounces]:
-            by_kernel = tj.get("bytes_per_launch_by_kernel") or {}
-            if tj.get("kernel") == kernel:
-                by_kernel.setdefault(kernel, tj["bytes_per_launch"])
-            if by_kernel.get(kernel) is not None:
-                traffic, traffic_src = by_kernel[kernel], TRAFFIC_JSON_REL + " (" + tj.get("source", "") + ")"
-            # TCC hit rates (rocprofv3 TCC_HIT/TCC_MISS pass) of the traversal, shade and finish kernels
-            hits = tj.get("l2_hit") or {}
-            l2_hit = {k: v for k, v in hits.items() if re.search(r"wf_(trace|shade|finish)", k)} or None
+    try:
+        cus = torch.cuda.get_device_properties(local).multi_processor_count
+    except Exception:
+        cus = 256
+    roof = roofline(a, cst, s0, s1, rays, closest, kms_local, ms_per_step, cus)
 
     cpu = None
     if not a.no_cpu and n == 1:
@@ -277,6 +327,7 @@ def main():
         "value": round(value, 4),
         "unit": "Grays/s",
         "n_gpus": n,
+        "world_size": n,
         "steps": a.steps,
         "warmup": a.warmup,
         "ms_per_step": round(ms_per_step, 3),
@@ -290,39 +341,132 @@ def main():
         "config": {
             "workload": f"{a.scene}: glass dragon scene (configs[2]) {a.width}x{a.height}x{a.spp}spp, {a.bounces} bounces, "
                         f"one frame per step, {'tile-split ' + str(T) + 'px + RCCL gather' if n > 1 else 'single GPU'}"
-                        f"{', frames submitted back to back (overlapping frames in flight)' if n == 1 else ''}",
+                        f", frames submitted back to back (overlapping frames in flight)",
             "scene": a.scene, "triangles": scene.triangle_count, "width": a.width, "height": a.height,
             "spp": a.spp, "max_bounces": a.bounces, "pipeline": a.pipeline, "parallelism": f"tiles{n}",
-            "rays_per_frame": int(rays / a.steps), "kernel_ms_per_frame": round(kms, 3),
+            "rays_per_frame": int(rays_all / a.steps), "kernel_ms_per_frame": round(kms, 3),
             "setup_s": round(setup_s, 2),
             # [generate, extend, shade, connect, resolve, finish, hit sort]
-            "stage_ms": [round(x / a.steps, 3) for x in stage_ms[:7]], "sort_bins": a.sort_bins, "bvh": a.bvh,
-            "pipeline_used": ["megakernel", "wavefront"][last_st.pipeline], "iterations": last_st.iterations,
-            "frames_in_flight": last_st.frames_in_flight, "animate": bool(skinned),
+            "stage_ms": [round(x, 3) for x in roof.pop("_stage_ms")], "sort_bins": a.sort_bins, "bvh": a.bvh,
+            "pipeline_used": ["megakernel", "wavefront"][s1.pipeline], "iterations": s1.iterations,
+            "frames_in_flight": s1.frames_in_flight, "animate": bool(skinned),
             # host time inside the submit calls per step (includes waiting for a free frame slot)
             "host_submit_ms": round(t_host / a.steps * 1e3, 3),
+            # multi-GPU: device time per step from the end of the pack through the unpack on rank 0's
+            # side of the RCCL gather (max over ranks), and its share of the step
+            "gather_ms_per_step": round(gather_ms, 4) if n > 1 else None,
+            "gather_share": round(gather_ms / ms_per_step, 4) if n > 1 else None,
         },
-        "roofline": {
-            "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": traffic_src,
-            # measured HBM bytes of one launch (PMC) over the launch time: what actually crossed HBM
-            "hbm_GBs": round(traffic / (launch_ms * 1e-3) / 1e9, 1) if traffic else None,
-            "l2_hit": l2_hit,
-            "job_achieved": round(job_achieved, 1), "job_frac": round(job_achieved / HBM_PEAK_GBS, 4),
-            "job_bytes_per_frame": int(job_bytes),
-            "kernel": kernel, "launch_ms": round(launch_ms, 4), "bytes_per_launch": int(bytes_per_launch),
-            "rays_per_launch": int(rays_per_launch), "nodes_per_ray": round(npr, 3), "tris_per_ray": round(tpr, 3),
-            # every timed kernel of the frame with its own roofline, for comparison
-            "kernels": [{"kernel": k["kernel"], "ms_per_frame": round(k["ms_per_frame"], 3),
-                         "launch_ms": round(k["launch_ms"], 4), "achieved_GBs": round(k["achieved"], 1),
-                         "frac": round(k["achieved"] / HBM_PEAK_GBS, 4), "nodes_per_ray": round(k["nodes_per_ray"], 3),
-                         "tris_per_ray": round(k["tris_per_ray"], 3)} for k in kernels],
-        },
+        "roofline": roof,
         "cpu_baseline": cpu,
     }
     print(json.dumps(line), flush=True)
     if n > 1:
         dist.destroy_process_group()
+
+
+def roofline(a, cst, s0, s1, rays_local, closest_local, kms_local, ms_per_step, cus):
+    """The dominant kernel's algorithmic bytes per launch over its average launch time (HIP events
+    around each launch on its render stream), with node bytes counted for the nodes fetched from
+    memory only."""
+    d = lambda f: getattr(s1, f) - getattr(s0, f)
+    steps = a.steps
+    trace_rays, trace_launches, trace_ms = d("total_trace_rays"), d("total_trace_launches"), d("total_trace_ms")
+    trace_closest, finish_launches = d("total_trace_closest_rays"), d("total_finish_launches")
+    stage_ms = np.array(list(s1.total_kernel_ms)) - np.array(list(s0.total_kernel_ms))
+    # per-ray visits of the counting frame: wf_trace's own, and the finish kernel's (the rest)
+    rays_c = cst.closest_rays + cst.shadow_rays
+    q_nodes = cst.trace_nodes / max(cst.trace_rays, 1)
+    q_nodes_lds = cst.trace_nodes_lds / max(cst.trace_rays, 1)
+    q_tris = cst.trace_tris / max(cst.trace_rays, 1)
+    f_rays_c = rays_c - cst.trace_rays
+    f_nodes = (cst.node_visits - cst.trace_nodes) / max(f_rays_c, 1)
+    f_nodes_lds = (cst.node_visits_lds - cst.trace_nodes_lds) / max(f_rays_c, 1)
+    f_tris = (cst.tri_tests - cst.trace_tris) / max(f_rays_c, 1)
+    kernels = []
+    if s1.pipeline == 1 and trace_launches > 0:
+        rpl = trace_rays / trace_launches
+        blocks = cus * TRACE_BLOCKS_PER_CU
+        kernels.append(dict(
+            kernel="rt::wf_trace<{false,true}, false> (extend + connect)", launches=trace_launches / steps,
+            launch_ms=trace_ms / trace_launches, rays_per_launch=rpl, nodes_per_ray=q_nodes,
+            lds_nodes_per_ray=q_nodes_lds, tris_per_ray=q_tris,
+            bytes_per_launch=rpl * (B_QRAY + (q_nodes - q_nodes_lds) * B_NODE + q_tris * B_TRI)
+            + blocks * TOP_NODES * B_NODE,
+            bytes_all_nodes=rpl * (B_QRAY + q_nodes * B_NODE + q_tris * B_TRI)))
+    if s1.pipeline == 1 and finish_launches > 0:
+        # wf_finish_step: its rays (48 B ray + hit) + nodes + triangles as above, + the shading
+        # gathers per closest hit (B_HIT); the path state in and out once per path is left out
+        f_rays = (rays_local - trace_rays) / finish_launches
+        f_closest = (closest_local - trace_closest) / finish_launches
+        blocks = cus * FINISH_BLOCKS_PER_CU
+        kernels.append(dict(
+            kernel="rt::wf_finish_step<false, false>", launches=finish_launches / steps,
+            launch_ms=float(stage_ms[5]) / finish_launches, rays_per_launch=f_rays, nodes_per_ray=f_nodes,
+            lds_nodes_per_ray=f_nodes_lds, tris_per_ray=f_tris,
+            bytes_per_launch=f_rays * (B_RAY + (f_nodes - f_nodes_lds) * B_NODE + f_tris * B_TRI) + f_closest * B_HIT
+            + blocks * TOP_NODES * B_NODE,
+            bytes_all_nodes=f_rays * (B_RAY + f_nodes * B_NODE + f_tris * B_TRI) + f_closest * B_HIT))
+    if not kernels:
+        # megakernel: the whole frame is one launch; every node comes from memory
+        rpl = rays_local / steps
+        npr = cst.node_visits / max(rays_c, 1)
+        tpr = cst.tri_tests / max(rays_c, 1)
+        b = (rpl * (B_RAY + npr * B_NODE + tpr * B_TRI) + closest_local / steps * B_HIT
+             + a.width * a.height / max(1, int(os.environ.get("WORLD_SIZE", "1"))) * B_PIXEL)
+        kernels.append(dict(kernel="rt::megakernel<false, false>", launches=1, launch_ms=kms_local, rays_per_launch=rpl,
+                            nodes_per_ray=npr, lds_nodes_per_ray=0.0, tris_per_ray=tpr, bytes_per_launch=b,
+                            bytes_all_nodes=b))
+    for k in kernels:
+        k["achieved"] = k["bytes_per_launch"] / (k["launch_ms"] * 1e-3) / 1e9
+        k["achieved_all_nodes"] = k["bytes_all_nodes"] / (k["launch_ms"] * 1e-3) / 1e9
+        k["ms_per_frame"] = k["launch_ms"] * k["launches"]
+    dom = max(kernels, key=lambda k: k["ms_per_frame"])
+    # the whole frame: every timed kernel's algorithmic bytes over the wall time per frame
+    job_bytes = sum(k["bytes_per_launch"] * k["launches"] for k in kernels)
+    job_achieved = job_bytes / (ms_per_step * 1e-3) / 1e9
+    traffic, traffic_src, l2_hit = None, None, None
+    if a.traffic_csv:
+        traffic = read_traffic(a.traffic_csv.split(","), traffic_key(dom["kernel"]))
+        traffic_src = "live: " + a.traffic_csv
+    elif os.path.exists(TRAFFIC_JSON):
+        with open(TRAFFIC_JSON) as f:
+            tj = json.load(f)
+        if tj.get("config") == [a.scene, a.width, a.height, a.spp, a.bounces]:
+            by_kernel = tj.get("bytes_per_launch_by_kernel") or {}
+            if by_kernel.get(dom["kernel"]) is not None:
+                traffic, traffic_src = by_kernel[dom["kernel"]], TRAFFIC_JSON_REL + " (" + tj.get("source", "") + ")"
+            # TCC hit rates (rocprofv3 TCC_HIT/TCC_MISS pass) of the traversal, shade and finish kernels
+            hits = tj.get("l2_hit") or {}
+            l2_hit = {k: v for k, v in hits.items() if re.search(r"wf_(trace|shade|finish)", k)} or None
+    r = {
+        "bound": "hbm", "achieved": round(dom["achieved"], 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+        "frac": round(dom["achieved"] / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": traffic_src,
+        # the same launch with every node visit charged 80 B (round-2 accounting: LDS-served top
+        # nodes counted as memory bytes)
+        "frac_all_nodes": round(dom["achieved_all_nodes"] / HBM_PEAK_GBS, 4),
+        # measured HBM bytes of one launch (PMC) over the launch time: what actually crossed HBM
+        "hbm_GBs": round(traffic / (dom["launch_ms"] * 1e-3) / 1e9, 1) if traffic else None,
+        "l2_hit": l2_hit,
+        "job_achieved": round(job_achieved, 1), "job_frac": round(job_achieved / HBM_PEAK_GBS, 4),
+        "job_bytes_per_frame": int(job_bytes),
+        "kernel": dom["kernel"], "launch_ms": round(dom["launch_ms"], 4), "bytes_per_launch": int(dom["bytes_per_launch"]),
+        "rays_per_launch": int(dom["rays_per_launch"]), "nodes_per_ray": round(dom["nodes_per_ray"], 3),
+        "lds_nodes_per_ray": round(dom["lds_nodes_per_ray"], 3), "tris_per_ray": round(dom["tris_per_ray"], 3),
+        # every timed kernel of the frame with its own roofline, for comparison
+        "kernels": [{"kernel": k["kernel"], "ms_per_frame": round(k["ms_per_frame"], 3),
+                     "launch_ms": round(k["launch_ms"], 4), "achieved_GBs": round(k["achieved"], 1),
+                     "frac": round(k["achieved"] / HBM_PEAK_GBS, 4), "nodes_per_ray": round(k["nodes_per_ray"], 3),
+                     "lds_nodes_per_ray": round(k["lds_nodes_per_ray"], 3),
+                     "tris_per_ray": round(k["tris_per_ray"], 3)} for k in kernels],
+        "_stage_ms": list(stage_ms[:7] / steps),
+    }
+    if dom["ms_per_frame"] > ms_per_step:
+        # with frames in flight the HIP-event pairs of a launch also count the time it waits for
+        # CUs held by the other frames: the dominant kernel's summed event time exceeds the step,
+        # so achieved / frac are not a kernel measurement (rocprof's kernel durations are)
+        r["not_a_kernel_measurement"] = True
+    return r
 
 
 TRAFFIC_KEYS = {"rt::wf_trace": r"wf_trace<(true|false),false>", "rt::wf_finis": r"wf_finish_step<false,false"}
@@ -360,10 +504,39 @@ def read_traffic(paths, kernel_key):
     return int((2 * fetch / nf + write / nw) * 1024)
 
 
+def host_cpu():
+    """nproc, the CPUs this process may use, the cgroup's CPU quota and the CPU model."""
+    info = {"nproc": os.cpu_count()}
+    try:
+        info["affinity"] = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        info["affinity"] = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        info["cgroup_cpus"] = None if q == "max" else round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        info["cgroup_cpus"] = None
+    model = None
+    try:
+        for ln in open("/proc/cpuinfo"):
+            if ln.startswith("model name"):
+                model = ln.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    info["model"] = model
+    return info
+
+
 def cpu_baseline(rt, scene, R, a):
-    """The C oracle (oracle/, a port) on a bounded row subset of the same frame, host cores."""
+    """The C oracle (oracle/, a port: binned-SAH BVH2, nearer child first) built -O3 -march=native
+    on this host, on a bounded row subset of the same frame, on the host CPUs this process may use
+    (at most 16: the CPU share of one GPU on the GPU boxes, whose nproc is the whole machine)."""
     import oracle
-    threads = min(16, os.cpu_count() or 1)
+    native = oracle.build_native()
+    if native:
+        oracle.use_library(native)
+    threads = oracle.default_threads()
     osc = oracle.OracleScene(scene.desc())
     u = R.uniforms()
     u.frameIndex = 0
@@ -381,9 +554,12 @@ def cpu_baseline(rt, scene, R, a):
         o = osc.render(u, R.random, row_start=0, row_step=step, threads=threads)
         t += time.perf_counter() - t0
         rays += o["closest_rays"] + o["shadow_rays"]
+    hc = host_cpu()
     return {"value": round(rays / t / 1e9, 6), "unit": "Grays/s", "cores": threads, "kind": "port",
+            "build": "gcc -O3 -march=native -ffp-contract=off" if native else "gcc -O3 -ffp-contract=off (portable)",
+            "host": hc,
             "sample": f"every {step}th row of frame 0 ({(a.height + step - 1) // step} rows x {a.width} px x "
-                      f"{a.spp} spp) x {reps}, {rays} rays in {t:.1f} s"}
+                      f"{a.spp} spp) x {reps}, {rays} rays in {t:.1f} s on {threads} threads"}
 
 
 if __name__ == "__main__":

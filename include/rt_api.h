@@ -133,8 +133,8 @@ typedef struct rt_opts {
                                  on a frame of 6M+ base paths give the finish tail 25 % of the
                                  grid (20 % below: the rank-share sweep).
                                  Geometry updates (skinning, transforms, refit, builds) rotate
-                                 over eight generations, so per-frame updates keep every slot's
-                                 overlap.  Images are identical either way. */
+                                 over max(2, frames in flight) generations, so per-frame updates
+                                 keep every slot's overlap.  Images are identical either way. */
     int32_t reserved[3];
 } rt_opts;
 
@@ -151,7 +151,8 @@ typedef struct rt_tile_set {
 typedef struct rt_stats {
     uint64_t closest_rays;  /* closest-hit queries traced in the last frame (incl. primary) */
     uint64_t shadow_rays;   /* any-hit shadow queries traced in the last frame */
-    uint64_t node_visits;   /* BVH nodes fetched (counting frames only, see rt_set_counting) */
+    uint64_t node_visits;   /* BVH node tests (counting frames only, see rt_set_counting; the LDS-served
+                               share is node_visits_lds) */
     uint64_t tri_tests;     /* triangles tested (counting frames only) */
     uint64_t paths;         /* pixel samples started */
     uint64_t bvh_nodes;     /* nodes in the current BVH */
@@ -185,6 +186,10 @@ typedef struct rt_stats {
     double total_trace_ms;
     uint64_t total_trace_launches;
     uint64_t total_finish_launches;
+    /* counting frames: the node visits served from the LDS copy of the BVH's top levels (no
+       memory traffic); included in node_visits / trace_nodes */
+    uint64_t node_visits_lds;
+    uint64_t trace_nodes_lds;
 } rt_stats;
 
 rt_status rt_create(const rt_opts* opts, rt_ctx** out);

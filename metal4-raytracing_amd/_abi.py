@@ -176,6 +176,8 @@ class Stats(C.Structure):
         ("total_trace_ms", C.c_double),
         ("total_trace_launches", C.c_uint64),
         ("total_finish_launches", C.c_uint64),
+        ("node_visits_lds", C.c_uint64),
+        ("trace_nodes_lds", C.c_uint64),
     ]
 
 

@@ -8,6 +8,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <exception>
 #include <string>
 #include <vector>
 
@@ -35,7 +36,7 @@ struct MeshInfo {
 // the slots and overlap except where frame f needs frame f-1's results (the history target and
 // the previous motion vectors: the extra-sample pass and the resolve).
 struct FrameSlot {
-    DevBuf color, accum, meta, q0, q1, hits, sq, counts, extra, sorted, sort_table, sort_total, params, pray, psray;
+    DevBuf color, accum, meta, q0, q1, hits, sq, counts, extra, sorted, sort_table, sort_total, params;
     DevBuf depth, gbuffer, counters;
     DevBuf prim_hit;   // wavefront: per pixel, sample 0's last bounce-0 hit (id, u, v) for wf_motion
     WavefrontBuffers wf;
@@ -45,25 +46,27 @@ struct FrameSlot {
     hipStream_t own_stream = nullptr;           // slots 1..; slot 0 renders on rt_ctx::stream
     hipEvent_t ev0 = nullptr, ev1 = nullptr, done = nullptr;
     bool pending = false, wavefront = false, used = false;
+    bool gbuf_written = false;                  // the slot's last frame wrote the G-buffer (enableDenoiseGBuffer)
     uint64_t seq = 0;                           // frame number (harvest order)
     int gen = 0;                                // geometry generation the frame reads
-    DevBuf* bufs[19] = {&color, &accum, &meta, &q0, &q1, &hits, &sq, &counts, &extra, &sorted,
-                        &sort_table, &sort_total, &params, &pray, &psray, &depth, &gbuffer, &counters, &prim_hit};
+    DevBuf* bufs[17] = {&color, &accum, &meta, &q0, &q1, &hits, &sq, &counts, &extra, &sorted,
+                        &sort_table, &sort_total, &params, &depth, &gbuffer, &counters, &prim_hit};
 };
 // Per-frame geometry (what skinning, instance transforms and refit rewrite between frames), in
-// kGens generations used round robin: frames read generation `gcur`; the first update after a frame
-// copies it into the next generation (once the frames still reading that one, kGens frames back,
+// generations used round robin: frames read generation `gcur`; the first update after a frame
+// copies it into the next generation (once the frames still reading that one, ngens frames back,
 // have finished) and every update until the next frame writes there, so frames in flight keep
 // their geometry while the next frame's is built (Renderer.swift keeps per-frame position buffers
-// for the same reason, :1290-1303).  One generation per frame slot: with an update before every
-// frame (skinning, refit), all frames in flight still overlap.
+// for the same reason, :1290-1303).  ngens = max(2, frames in flight): with an update before every
+// frame (skinning, refit), all frames in flight still overlap, and no more copies exist than
+// frames can read.
 struct Geo {
     DevBuf pos, prev_pos, nrm, inst, prev_inst, tris, nodes, node_box, tri_bin;
     DevBuf* all[9] = {&pos, &prev_pos, &nrm, &inst, &prev_inst, &tris, &nodes, &node_box, &tri_bin};
     uint32_t num_nodes8 = 0;
 };
 constexpr int kMaxSlots = 8;
-constexpr int kGens = kMaxSlots;
+constexpr int kGens = kMaxSlots;   // generations allocated at most (ngens of them in use)
 // default finish threshold with 2 / 3 / 4 frames in flight (C3g sweeps: 1.25M, 1M and 512K paths;
 // round 2, with the DP-collapsed tree and the lighter shading kernels, two slots: 2M 5.88 / 5.89,
 // 1.57M 5.90 (C3g enters the finish one round earlier between 1.5M and 1.57M live paths),
@@ -125,11 +128,13 @@ struct rt_ctx {
     // device buffers
     Geo geo[kGens];
     int gcur = 0;            // generation new frames read
+    int ngens = 2;           // generations in rotation: max(2, frames in flight)
+    int cur_nfl = 0;         // frames in flight of the newest frame (a change drains and re-sizes the rotation)
     bool gdirty = false;     // updates since the last frame went into generation next_gen()
     hipStream_t ustream = nullptr;   // geometry updates (skin, transforms, refit)
     hipEvent_t uev = nullptr;        // end of the latest update batch; frames wait on it
     bool uev_valid = false;
-    int next_gen() const { return (gcur + 1) % kGens; }
+    int next_gen() const { return (gcur + 1) % ngens; }
     Geo& G() { return geo[gdirty ? next_gen() : gcur]; }   // the generation updates and builds write
     DevBuf d_rest_pos, d_rest_nrm, d_jidx, d_jw, d_joints;
     DevBuf d_tri_info, d_mat, d_lights, d_halton;
@@ -233,17 +238,19 @@ static std::vector<HaltonDim> halton_table() {
     return t;
 }
 
-// SAH build + 8-wide collapse whose group-stack depth fits the kStackSize LDS stack: the binned-SAH
+// SAH build (one triangle per BVH2 leaf) + SAH-DP 8-wide collapse (c_node 1, c_prim 0.5: the C3g
+// sweep of DESIGN.md §3) whose group-stack depth fits the kStackSize LDS stack: the binned-SAH
 // builder falls back to median splits past its depth limit, so tighter limits bound the depth.
-// RT_BVH_COLLAPSE=greedy selects round 1's collapse (largest child opened first) for A/B runs.
+// false on failure (no depth limit fits, or the builder threw: allocation, internal checks);
+// nothing is thrown across the C-ABI.
 static bool build_bvh8_fit(const float* world, uint32_t n, BvhResult& b2, Bvh8Result& b8) {
-    static const bool greedy = getenv("RT_BVH_COLLAPSE") && !std::strcmp(getenv("RT_BVH_COLLAPSE"), "greedy");
-    static const float c_prim = getenv("RT_BVH_CPRIM") ? (float)atof(getenv("RT_BVH_CPRIM")) : 0.5f;
-    for (int limit : {64, 48, 40, 32, 28, 24, 21}) {
-        static const int leaf = getenv("RT_BVH_LEAF") ? std::max(1, std::min(4, atoi(getenv("RT_BVH_LEAF")))) : (greedy ? 4 : 1);
-        b2 = build_bvh2(world, n, leaf, limit);
-        b8 = greedy ? collapse_bvh8(b2) : collapse_bvh8_dp(b2, 1.0f, c_prim);
-        if (b8.max_depth <= kStackSize) return true;
+    try {
+        for (int limit : {64, 48, 40, 32, 28, 24, 21}) {
+            b2 = build_bvh2(world, n, 1, limit);
+            b8 = collapse_bvh8_dp(b2, 1.0f, 0.5f);
+            if (b8.max_depth <= kStackSize) return true;
+        }
+    } catch (const std::exception&) {
     }
     return false;
 }
@@ -282,14 +289,12 @@ static rt_status ensure_wavefront(rt_ctx* c, FrameSlot& fs, size_t own_px, int s
         if ((st = dev_alloc(c, fs.color, paths * 16))) return st;
         if ((st = dev_alloc(c, fs.accum, paths * 16))) return st;
         if ((st = dev_alloc(c, fs.meta, paths * 16))) return st;
-        if ((st = dev_alloc(c, fs.pray, paths * 32))) return st;
-        if ((st = dev_alloc(c, fs.psray, paths * 48))) return st;
         if ((st = dev_alloc(c, fs.q0, qe * 32))) return st;
         if ((st = dev_alloc(c, fs.q1, qe * 32))) return st;
         if ((st = dev_alloc(c, fs.hits, qe * 16))) return st;
         if ((st = dev_alloc(c, fs.sq, qe * 48))) return st;
-        // hit sort output (3 float4 per hit) / finish input in priority order (2 per ray)
-        if ((st = dev_alloc(c, fs.sorted, qe * 48))) return st;
+        // hit sort output (3 float4 per hit), only with the sort on
+        if (c->sort_bins && (st = dev_alloc(c, fs.sorted, qe * 48))) return st;
         W.cap_paths = paths;
         W.queue_entries = qe;
     }
@@ -315,8 +320,6 @@ static rt_status ensure_wavefront(rt_ctx* c, FrameSlot& fs, size_t own_px, int s
     W.p_color = (float4*)fs.color.p;
     W.p_accum = (float4*)fs.accum.p;
     W.p_meta = (uint4*)fs.meta.p;
-    W.p_ray = (float4*)fs.pray.p;
-    W.p_sray = (float4*)fs.psray.p;
     W.q[0] = (float4*)fs.q0.p;
     W.q[1] = (float4*)fs.q1.p;
     W.hits = (float4*)fs.hits.p;
@@ -384,7 +387,6 @@ rt_status rt_create(const rt_opts* opts, rt_ctx** out) {
         c->tail_paths = opts->tail_paths;
         c->sort_bins = opts->sort_bins == 0 ? kSortBinsDefault : std::max(opts->sort_bins, 0);
     }
-    if (const char* e = getenv("RT_SORT_BINS")) c->sort_bins = std::max(0, atoi(e));  // tuning experiments
     if (c->device < 0 || c->device >= ndev) { delete c; FAIL((rt_ctx*)nullptr, RT_ERR_INVALID_ARG, "bad device ordinal"); }
     if (c->pipeline != RT_PIPELINE_MEGAKERNEL && c->pipeline != RT_PIPELINE_WAVEFRONT) {
         delete c;
@@ -749,12 +751,11 @@ rt_status rt_bvh_build_device(rt_ctx* c) {
     if ((st = dev_alloc(c, c->d_maxabs, 4))) return st;
     if (!c->h_lbvh) HIPC(c, hipHostMalloc((void**)&c->h_lbvh, 16, 0));
     LbvhInput in{(const float4*)g.pos.p, (const uint4*)c->d_tri_info.p, (const float*)g.inst.p, n};
-    // PLOC topology + SAH-DP collapse by default; RT_DEVICE_BVH=lbvh / RT_DEVICE_COLLAPSE=greedy
-    // select round 1's radix tree / greedy collapse (A/B runs)
+    // PLOC topology + SAH-DP collapse by default; RT_DEVICE_BVH=lbvh selects the radix tree, whose
+    // faster build wins for a small scene rebuilt every frame
     static const bool lbvh_tree = getenv("RT_DEVICE_BVH") && !std::strcmp(getenv("RT_DEVICE_BVH"), "lbvh");
-    static const bool greedy = getenv("RT_DEVICE_COLLAPSE") && !std::strcmp(getenv("RT_DEVICE_COLLAPSE"), "greedy");
     in.ploc = lbvh_tree ? 0 : 1;
-    in.dp = greedy ? 0 : 1;
+    in.dp = 1;
     LbvhOutput out{(Bvh8Node*)g.nodes.p, (float*)g.node_box.p, (uint32_t*)c->d_slot_to_tri.p,
                    (uint16_t*)g.tri_bin.p, (uint32_t*)c->d_levels.p, c->h_lbvh};
     LbvhResult res;
@@ -932,10 +933,12 @@ static rt_status harvest(rt_ctx* c, int k) {
     S.closest_rays = total(kCntClosest);
     S.shadow_rays = total(kCntShadow);
     S.node_visits = total(kCntNodes);
+    S.node_visits_lds = total(kCntNodesLds);
     S.tri_tests = total(kCntTris);
     S.paths = total(kCntPaths);
     S.trace_nodes = f.wavefront ? total(kCntTraceNodes) : 0;
     S.trace_tris = f.wavefront ? total(kCntTraceTris) : 0;
+    S.trace_nodes_lds = f.wavefront ? total(kCntTraceNodesLds) : 0;
     rt_stats& T = c->totals;
     T.frames_total += 1;
     T.total_closest_rays += S.closest_rays;
@@ -1004,6 +1007,15 @@ rt_status rt_render_frame(rt_ctx* c, const Uniforms* U, const rt_tile_set* tiles
         c->gcur = c->next_gen();
         c->gdirty = false;
     }
+    if (nfl != c->cur_nfl) {
+        // a different number of frames in flight (a new frame size or tile set): finish the frames
+        // in flight, then rotate the geometry over max(2, nfl) generations (from the current one)
+        if (c->cur_nfl != 0 && (st = drain_frames(c))) return st;
+        c->ngens = std::max(std::max(2, nfl), c->gcur + 1);
+        for (int g = c->ngens; g < kGens; ++g)
+            for (DevBuf* b : c->geo[g].all) dev_free(*b);
+        c->cur_nfl = nfl;
+    }
     if (c->uev_valid) HIPC(c, hipStreamWaitEvent(stream, c->uev, 0));
     const Geo& geo = c->geo[c->gcur];
     if (U->enableDenoiseGBuffer && !F.gbuffer.p) {
@@ -1057,6 +1069,7 @@ rt_status rt_render_frame(rt_ctx* c, const Uniforms* U, const rt_tile_set* tiles
         F.wf.motion_prev = (float2*)c->d_motion[m_prev].p;
     }
     HIPC(c, hipMemsetAsync(F.counters.p, 0, sizeof(unsigned long long) * kCounterWords, stream));
+    F.gbuf_written = U->enableDenoiseGBuffer != 0;
     // extra samples can only be non-zero when something moved in this frame or the previous one
     const bool moving = c->inst_moved || c->skin_moved ||
                         std::memcmp(&U->camera, &U->previousCamera, sizeof(Camera)) != 0;
@@ -1138,7 +1151,7 @@ rt_status rt_read_aux(rt_ctx* c, float* depth, float* motion, float* gbuffer) {
     if (depth) HIPC(c, hipMemcpy(depth, f.depth.p, n * 4, hipMemcpyDeviceToHost));
     if (motion) HIPC(c, hipMemcpy(motion, c->d_motion[c->motion_cur].p, n * 8, hipMemcpyDeviceToHost));
     if (gbuffer) {
-        if (!f.gbuffer.p) FAIL(c, RT_ERR_STATE, "G-buffer was never enabled");
+        if (!f.gbuffer.p || !f.gbuf_written) FAIL(c, RT_ERR_STATE, "the newest frame wrote no G-buffer (enableDenoiseGBuffer off)");
         HIPC(c, hipMemcpy(gbuffer, f.gbuffer.p, 4 * n * 16, hipMemcpyDeviceToHost));
     }
     return RT_OK;
@@ -1211,7 +1224,8 @@ rt_status rt_present(rt_ctx* c, const rt_present_opts* o, uint8_t* host_rgba8) {
     if (!f.used) FAIL(c, RT_ERR_STATE, "rt_present before the first frame");
     const float4* color = (const float4*)c->d_accum[c->read_idx].p;
     if (scaler == RT_SCALER_DENOISED) {   // render-size scratch: two ping-pong images, guide, albedo
-        if (!f.gbuffer.p) FAIL(c, RT_ERR_STATE, "RT_SCALER_DENOISED needs the G-buffer (enableDenoiseGBuffer)");
+        if (!f.gbuffer.p || !f.gbuf_written)
+            FAIL(c, RT_ERR_STATE, "RT_SCALER_DENOISED needs the newest frame's G-buffer (enableDenoiseGBuffer)");
         const size_t rn = (size_t)c->width * c->height;
         if (c->den_n != rn || !c->d_den[0].p) {
             for (int i = 0; i < 4; ++i)
@@ -1370,7 +1384,7 @@ rt_status rt_debug_trace_host(const rt_scene_desc* sd, const float* rays, const 
         f3 o = mk3(q[0], q[1], q[2]), d = mk3(q[3], q[4], q[5]);
         float tm = tmax ? tmax[r] : INFINITY;
         Hit h;
-        TraceCounters tc{0, 0};
+        TraceCounters tc{0, 0, 0};
         bool overflow = false;
         bool hit = any ? trace8<true, true>(S, o, d, 0.0f, tm, h, stack.data(), tc, overflow)
                        : trace8<false, true>(S, o, d, 0.0f, tm, h, stack.data(), tc, overflow);

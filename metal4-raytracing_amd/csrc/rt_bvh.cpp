@@ -6,6 +6,7 @@
 #include <algorithm>
 #include <cstdlib>
 #include <functional>
+#include <stdexcept>
 #include <cmath>
 #include <cstring>
 
@@ -103,8 +104,7 @@ struct Builder {
                 }
             }
             float pa = b.area();
-            static const float c_trav_s = getenv("RT_BVH_CTRAV") ? (float)atof(getenv("RT_BVH_CTRAV")) : 1.0f;
-            float split_cost = c_trav_s + (pa > 0 ? best_cost / pa : INFINITY);
+            float split_cost = 1.0f + (pa > 0 ? best_cost / pa : INFINITY);   // C_trav = 1
             if (best_axis >= 0 && (split_cost < (float)n || n > (uint32_t)max_leaf)) {
                 std::copy(ord[best_axis].begin(), ord[best_axis].end(), idx.begin() + s);
                 mid = s + best_i;
@@ -146,8 +146,7 @@ struct Builder {
             }
             float pa = b.area();
             float leaf_cost = (float)n;                             // C_isect = 1
-            static const float c_trav = getenv("RT_BVH_CTRAV") ? (float)atof(getenv("RT_BVH_CTRAV")) : 1.0f;
-            float split_cost = c_trav + (pa > 0 ? best_cost / pa : INFINITY);  // C_trav (default 1)
+            float split_cost = 1.0f + (pa > 0 ? best_cost / pa : INFINITY);  // C_trav = 1
             if (best_axis >= 0 && (split_cost < leaf_cost || n > (uint32_t)max_leaf)) {
                 float scale = kBins / ext[best_axis];
                 auto it = std::partition(idx.begin() + s, idx.begin() + e, [&](uint32_t t) {
@@ -514,7 +513,9 @@ Bvh8Result collapse_bvh8_dp(const BvhResult& b2, float c_node, float c_prim) {
         const float node = n.area * c_node + D[8];
         split8[id] = K[8];
         C[id * 9 + 1] = std::min(leaf, node);
-        choice[id * 9 + 1] = leaf <= node ? 1 : 2;
+        // a leaf slot holds at most kLeafMax triangles (the tri_valid nibble): with both costs
+        // infinite (box areas overflowing) a larger subtree must stay a node
+        choice[id * 9 + 1] = (n.count <= kLeafMax && leaf <= node) ? 1 : 2;
         for (int i = 2; i <= 8; ++i) {
             if (D[i] < C[id * 9 + i - 1]) { C[id * 9 + i] = D[i]; choice[id * 9 + i] = K[i]; }
             else { C[id * 9 + i] = C[id * 9 + i - 1]; choice[id * 9 + i] = 0; }
@@ -604,6 +605,7 @@ void emit_bvh8_node(const BvhResult& b2, const Job& job, std::vector<WItem>& ite
                 queue.push_back({it.node, child, job.depth + 1});
             } else {
                 const uint32_t j = (uint32_t)c - n_internal;
+                if (it.count > 4) throw std::runtime_error("bvh8: leaf slot with more than 4 triangles");
                 nd.tri_valid |= ((1u << it.count) - 1u) << (4 * j);
                 for (uint32_t t = 0; t < it.count; ++t) out.tri_order.push_back(b2.tri_order[it.start + t]);
             }

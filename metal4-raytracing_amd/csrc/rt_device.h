@@ -73,8 +73,9 @@ __host__ __device__ __forceinline__ f3 xform(const float* m, f3 p, float w) {
 }
 
 struct TraceCounters {
-    uint32_t nodes;
-    uint32_t tris;
+    uint32_t nodes;       // 8-wide nodes fetched from global memory
+    uint32_t tris;        // triangles tested
+    uint32_t lds_nodes;   // node tests served from the LDS copy of the top levels (no memory traffic)
 };
 
 // ---- compressed 8-wide BVH traversal (rt_bvh.h Bvh8Node) --------------------------------------
@@ -147,16 +148,11 @@ __host__ __device__ __forceinline__ uint32_t tri_slot(uint32_t tri_base, uint32_
 // Slab-test the 8 children of a node.  Outputs: the internal children hit (bit r = internal rank r
 // = slot r), the triangles to test (nibble space: bit 4j + i = triangle i of leaf j, see
 // tri_slot), the node's tri_valid word, and the traversal direction of the slot order.
-// Branch-free over the children: each child only sets its bit of the hit-slot mask (and, with
-// `nearest`, competes for the nearest internal child); the internal / leaf split and the
-// triangle mask follow from the node's k and tri_valid once per node.
-// nearest (optional): the rank of the hit internal child with the smallest entry distance (ties:
-// the entry distances' low three mantissa bits are replaced by the slot), -1 if none (callers
-// visit it first; the rest of the group follows the slot order)
+// Branch-free over the children: each child only sets its bit of the hit-slot mask; the
+// internal / leaf split and the triangle mask follow from the node's k and tri_valid once per node.
 __host__ __device__ __forceinline__ void test_node8_words(const NodeWords& W, const RaySetup& R, float tmin, float tmax,
                                                           uint32_t& ihits, uint32_t& tmask, uint32_t& tvalid,
-                                                          uint32_t& child_base, uint32_t& tri_base, bool& flip,
-                                                          int* nearest = nullptr) {
+                                                          uint32_t& child_base, uint32_t& tri_base, bool& flip) {
     const float4 h0 = W.h0;
     const uint4 h1 = W.h1, qx = W.qx, qy = W.qy, qz = W.qz;
     const uint32_t ew = __builtin_bit_cast(uint32_t, h0.w);
@@ -177,7 +173,7 @@ __host__ __device__ __forceinline__ void test_node8_words(const NodeWords& W, co
     const uint32_t nz0 = R.iz >= 0.0f ? qz.x : qz.z, nz1 = R.iz >= 0.0f ? qz.y : qz.w;
     const uint32_t fz0 = R.iz >= 0.0f ? qz.z : qz.x, fz1 = R.iz >= 0.0f ? qz.w : qz.y;
     const float tf_max = tmax * 1.0000004f;
-    uint32_t hm = 0, nkey = 0xffffffffu;
+    uint32_t hm = 0;
     #pragma unroll
     for (int c = 0; c < 8; ++c) {
         const int b = c & 3;
@@ -191,16 +187,10 @@ __host__ __device__ __forceinline__ void test_node8_words(const NodeWords& W, co
         const float tf = fminf(fminf(tfx, tfy), fminf(tfz, tf_max));
         const bool hit = tn <= tf;
         hm |= hit ? (1u << c) : 0u;
-        if (nearest) {
-            // entry distance (>= tmin >= 0: unsigned order = float order) with the slot in its low bits
-            const uint32_t key = (__builtin_bit_cast(uint32_t, tn) & ~7u) | (uint32_t)c;
-            nkey = (hit && (uint32_t)c < k_int && key < nkey) ? key : nkey;
-        }
     }
     ihits = hm & ((1u << k_int) - 1u);
     tmask = spread_nibbles(hm >> k_int) & h1.z;
     tvalid = h1.z;
-    if (nearest) *nearest = nkey == 0xffffffffu ? -1 : (int)(nkey & 7u);
     child_base = h1.x;
     tri_base = h1.y;
     flip = (R.dneg >> axis) & 1u;   // bit select: a dynamic pick of R.d lowers to a scratch access

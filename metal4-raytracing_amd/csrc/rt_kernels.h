@@ -10,10 +10,11 @@ namespace rt {
 
 constexpr int kHaltonLds = 64;   // first Halton dimensions staged in LDS per block
 
-// kCntTraceNodes / kCntTraceTris: the share of node / triangle visits made by wf_trace launches
+// kCntNodes: every node test; kCntNodesLds: those served from the LDS copy of the top levels.
+// kCntTrace*: the share of the visits made by wf_trace launches.
 enum CounterSlot {
     kCntClosest = 0, kCntShadow = 1, kCntNodes = 2, kCntTris = 3, kCntPaths = 4, kCntOverflow = 5,
-    kCntTraceNodes = 6, kCntTraceTris = 7, kCntSlots = 8
+    kCntTraceNodes = 6, kCntTraceTris = 7, kCntNodesLds = 8, kCntTraceNodesLds = 9, kCntSlots = 10
 };
 
 struct FrameParams {
@@ -47,15 +48,17 @@ __host__ __device__ constexpr uint32_t cnt_word(int slot, int rep) {
 }
 
 // Block-wide flush of the per-thread statistics; every thread of the block must call it.
+// nodes: global node fetches, lds_nodes: node tests served from LDS (both count as node visits).
 // trace_kernel: the node / triangle visits are also added to the kCntTrace* slots.
 __device__ __forceinline__ void block_flush_counters(unsigned long long* counters, uint32_t closest, uint32_t shadow,
                                                      uint32_t nodes, uint32_t tris, uint32_t paths, bool overflow,
-                                                     bool trace_kernel = false) {
+                                                     bool trace_kernel = false, uint32_t lds_nodes = 0) {
     __shared__ unsigned long long red[kBlock / 64][kCntSlots];
-    const unsigned long long n = wave_sum(nodes), t = wave_sum(tris);
+    const unsigned long long l = wave_sum(lds_nodes), n = wave_sum(nodes) + l, t = wave_sum(tris);
     const unsigned long long v[kCntSlots] = {wave_sum(closest), wave_sum(shadow), n, t, wave_sum(paths),
                                              __ballot(overflow) != 0ull ? 1ull : 0ull,
-                                             trace_kernel ? n : 0ull, trace_kernel ? t : 0ull};
+                                             trace_kernel ? n : 0ull, trace_kernel ? t : 0ull, l,
+                                             trace_kernel ? l : 0ull};
     const int wave = threadIdx.x >> 6;
     if ((threadIdx.x & 63) == 0) {
         #pragma unroll
@@ -102,10 +105,6 @@ struct WavefrontBuffers {
     uint32_t* h_counts = nullptr; // pinned host mirror
     float2* motion_prev = nullptr;   // the previous frame's motion target (set per frame)
     uint2* px_extra = nullptr;    // per own pixel: (first extra path - base_paths, count)
-    // wf_finish_q: per path, its next closest ray (o, d) and its shadow query (o; d, tmax;
-    // contribution, continues)
-    float4* p_ray = nullptr;
-    float4* p_sray = nullptr;
     // per-bounce hit sort (wf_sort_*): the hits reordered by key as {o, d, hit} float4 triples,
     // per-(bin, block) counts, per-bin totals
     float4* sorted = nullptr;
@@ -154,8 +153,7 @@ struct WfTimeline {
     int n_ev = 0, n_spans = 0;
     bool pending = false;
 };
-// Runs (host-driven: queue sizes read back every round; with RT_WF_LOG / RT_WF_DUMP /
-// RT_WF_HOST=1) or enqueues (device-driven, the default: `tl` receives the timeline, stats come
+// Runs (host-driven: queue sizes read back every round; with RT_WF_LOG / RT_WF_HOST=1) or enqueues (device-driven, the default: `tl` receives the timeline, stats come
 // from wavefront_collect after the stream finished) one frame; false on a HIP error (*err).
 // sort_bins: hit-sort bins (0 = no sort).  extra_pass: the motion-adaptive extra samples can be
 // non-zero this frame (something moved in this or the previous frame); the device-driven mode

@@ -34,7 +34,7 @@ megakernel(DevScene S, FrameParams P) {
     int py = tile_y * P.tile_size + (sub / sub_w) * 16 + (wave >> 1) * 8 + (lane >> 3);
 
     int* stack = &lds_stack[threadIdx.x];
-    TraceCounters tc{0, 0};
+    TraceCounters tc{0, 0, 0};
     uint32_t n_closest = 0, n_shadow = 0, n_paths = 0;
     bool overflow = false;
 

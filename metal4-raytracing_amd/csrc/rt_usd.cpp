@@ -844,8 +844,10 @@ private:
         if (!plausible(total)) return fail("implausible path count");
         paths_.assign(total, std::string());
         // _BuildDecompressedPathsImpl: depth-first, children follow their parent, a positive
-        // jump points at the sibling subtree
+        // jump points at the sibling subtree.  Every entry is visited at most once (a crafted jump table that reaches an entry
+        // twice would otherwise make the walk exponential): a second visit fails the file.
         std::vector<std::pair<size_t, std::string>> todo{{0, std::string()}};
+        std::vector<uint8_t> visited(count, 0);
         while (!todo.empty()) {
             size_t cur = todo.back().first;
             std::string parent = todo.back().second;
@@ -854,6 +856,8 @@ private:
             do {
                 if (cur >= count) return fail("bad path tree");
                 const size_t me = cur++;
+                if (visited[me]) return fail("bad path tree (entry reached twice)");
+                visited[me] = 1;
                 if (idx[me] >= total) return fail("bad path index");
                 std::string path;
                 if (parent.empty()) {

@@ -71,10 +71,12 @@ class TileGather:
         self.packed = torch.zeros((self.max_own, tile, tile, 4), dtype=torch.float32, device=device)
         self.recv = ([torch.empty_like(self.packed) for _ in range(nranks)] if rank == dst else None)
 
-    def gather(self, image=None):
+    def gather(self, image=None, events=None):
         """Gathers this frame's tiles on the dst rank. Device path: enqueued without a host wait;
-        after the dst renderer's wait() its target holds the full frame (returns None). Host path: returns the full (H, W, 4) image on dst,
-        None elsewhere."""
+        after the dst renderer's wait() its target holds the full frame (returns None). Host path:
+        returns the full (H, W, 4) image on dst, None elsewhere.  events (device path, optional): a
+        pair of torch.cuda.Event recorded on the current stream after the pack and after the
+        unpack (dst) / the gather (other ranks), i.e. around the collective."""
         import torch
         import torch.distributed as dist
         if self.R is not None:
@@ -82,16 +84,22 @@ class TileGather:
             # next frame overlaps the pack and the gather
             self.R.pack_tiles(self.T, self.rank, self.n, self.packed.data_ptr(),
                               stream=torch.cuda.current_stream().cuda_stream)
+            if events is not None:
+                events[0].record()
         else:
             self.packed.copy_(torch.from_numpy(pack_host(image, self.T, self.rank, self.n, self.max_own)))
         dist.gather(self.packed, self.recv, dst=self.dst)
         if self.rank != self.dst:
+            if events is not None and self.R is not None:
+                events[1].record()
             return None
         if self.R is not None:
             s = torch.cuda.current_stream().cuda_stream
             for r in range(self.n):
                 if r != self.rank:
                     self.R.unpack_tiles(self.T, r, self.n, self.recv[r].data_ptr(), stream=s)
+            if events is not None:
+                events[1].record()
             return None
         out = np.zeros((self.h, self.w, 4), np.float32)
         for r in range(self.n):

@@ -10,7 +10,8 @@ import subprocess
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "_build", "librt_oracle.so")
+# RT_ORACLE_LIB selects another build of the same source (e.g. _build/librt_oracle_native.so)
+LIB_PATH = os.environ.get("RT_ORACLE_LIB") or os.path.join(_HERE, "_build", "librt_oracle.so")
 _lib = None
 
 
@@ -31,7 +32,9 @@ class Frame(C.Structure):
         ("row_start", C.c_int32),
         ("row_step", C.c_int32),
         ("threads", C.c_int32),
-        ("_pad", C.c_int32),
+        ("tile_size", C.c_int32),
+        ("rank", C.c_int32),
+        ("nranks", C.c_int32),
         ("closest_rays", C.c_uint64),
         ("shadow_rays", C.c_uint64),
         ("paths", C.c_uint64),
@@ -40,6 +43,52 @@ class Frame(C.Structure):
 
 def build():
     subprocess.run(["make", "-s", "-C", _HERE], check=True)
+
+
+def _cpu_key():
+    """A short key of this host's CPU (model + feature flags): a -march=native build is only ever
+    loaded on a CPU with the same key (the tree travels between machines)."""
+    import hashlib
+    text = ""
+    try:
+        for ln in open("/proc/cpuinfo"):
+            if ln.startswith(("model name", "flags")):
+                text += ln
+                if ln.startswith("flags"):
+                    break
+    except OSError:
+        pass
+    return hashlib.sha1(text.encode()).hexdigest()[:12]
+
+
+def build_native():
+    """Builds the -march=native variant for this machine's CPU (CPU baseline); returns its path or
+    None."""
+    path = os.path.join(_HERE, "_build", "librt_oracle_native_%s.so" % _cpu_key())
+    try:
+        subprocess.run(["make", "-s", "-C", _HERE, "native", "NATIVE=" + os.path.relpath(path, _HERE)], check=True,
+                       capture_output=True, timeout=120)
+    except (OSError, subprocess.SubprocessError):
+        return None
+    return path if os.path.exists(path) else None
+
+
+def use_library(path):
+    """Selects the oracle build to load (before the first call into it)."""
+    global LIB_PATH
+    if _lib is not None and path != LIB_PATH:
+        raise RuntimeError("oracle library already loaded from " + LIB_PATH)
+    LIB_PATH = path
+
+
+def default_threads():
+    """Worker threads for oracle renders: the CPUs this process may run on, capped at 16 (the CPU
+    share of one GPU on the GPU boxes, whose nproc counts the whole machine)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        n = os.cpu_count() or 1
+    return max(1, min(n, 16))
 
 
 def lib():
@@ -131,8 +180,10 @@ class OracleScene:
             raise RuntimeError("set_previous failed")
 
     def render(self, uniforms, random, accum_in=None, motion_in=None, gbuffer=False, row_start=0, row_step=1,
-               threads=None):
-        """Render one frame; returns dict(radiance HxWx4, depth, motion, gbuffer, counts)."""
+               threads=None, tiles=None):
+        """Render one frame (rows row_start + k * row_step; tiles = (tile_size, rank, nranks): only that
+        rank's tiles); returns dict(radiance HxWx4, depth, motion, gbuffer, counts).  Pixels not
+        rendered stay zero (motion: the motion_in value)."""
         W, H = uniforms.width, uniforms.height
         accum_out = np.zeros((H, W, 4), np.float32)
         depth = np.zeros((H, W), np.float32)
@@ -151,7 +202,9 @@ class OracleScene:
         f.gbuffer = gb.ctypes.data_as(FP) if gb is not None else None
         f.row_start = row_start
         f.row_step = row_step
-        f.threads = threads or min(os.cpu_count() or 1, 16)
+        f.threads = threads or default_threads()
+        if tiles is not None:
+            f.tile_size, f.rank, f.nranks = tiles
         st = lib().rt_oracle_render(self._h, C.byref(f))
         if st != 0:
             raise RuntimeError(f"oracle render failed: {st}")

@@ -1,7 +1,7 @@
 /*
  * rt_oracle.c — CPU restatement of raytracingKernel (Raytracing.metal:220-831).
  * TEST INFRASTRUCTURE ONLY (see rt_oracle.h).  Build: oracle/Makefile
- * (gcc -O2 -std=c11 -ffp-contract=off -fno-fast-math -pthread).
+ * (gcc -O3 -std=gnu11 -ffp-contract=off -fno-fast-math -pthread).
  *
  * Every function cites the reference lines it restates.  Arithmetic is written with explicit
  * evaluation order; DESIGN.md §4 is the shared specification with the HIP path.
@@ -129,6 +129,34 @@ static inline V3 oxform(const float* m, V3 p, float w) {
     return vadd(vadd(vadd(vscl(c0, p.x), vscl(c1, p.y)), vscl(c2, p.z)), vscl(c3, w));
 }
 
+/* Binned-SAH BVH over triangle centroids (16 bins per axis, all three axes), leaves of <= 4
+ * triangles, iterative.  Its own builder, independent of the product's (rt_bvh.cpp): boxes are
+ * padded by 1e-5 * max |coordinate|, so hits do not depend on the tree. */
+#define OBINS 16
+#define OMEDIAN_DEPTH 48   /* below this depth: object-median splits (bounds the traversal stack) */
+typedef struct { float lo[3], hi[3]; uint32_t n; } OBin;
+
+static void bin_grow(OBin* b, const float* w) {
+    for (int q = 0; q < 3; ++q)
+        for (int a = 0; a < 3; ++a) {
+            b->lo[a] = fminf(b->lo[a], w[3 * q + a]);
+            b->hi[a] = fmaxf(b->hi[a], w[3 * q + a]);
+        }
+}
+static void bin_merge(OBin* d, const OBin* b) {
+    for (int a = 0; a < 3; ++a) { d->lo[a] = fminf(d->lo[a], b->lo[a]); d->hi[a] = fmaxf(d->hi[a], b->hi[a]); }
+    d->n += b->n;
+}
+static float bin_area(const OBin* b) {
+    if (b->n == 0) return 0.0f;
+    float dx = b->hi[0] - b->lo[0], dy = b->hi[1] - b->lo[1], dz = b->hi[2] - b->lo[2];
+    return dx * dy + dy * dz + dz * dx;
+}
+static void bin_clear(OBin* b) {
+    for (int a = 0; a < 3; ++a) { b->lo[a] = INFINITY; b->hi[a] = -INFINITY; }
+    b->n = 0;
+}
+
 static int cmp_axis;
 static const float* cmp_cen;
 static int cmp_c(const void* a, const void* b) {
@@ -139,7 +167,6 @@ static int cmp_c(const void* a, const void* b) {
     return x < y ? -1 : (x > y);
 }
 
-/* object-median BVH, leaves <= 4 (iterative) */
 static void build_bvh(rt_oracle_scene* s) {
     uint32_t n = s->ntri;
     float* cen = (float*)malloc(sizeof(float) * 3 * (n ? n : 1));
@@ -157,40 +184,83 @@ static void build_bvh(rt_oracle_scene* s) {
     uint32_t cap = 2 * (n ? n : 1) + 1;
     s->nodes = (ONode*)malloc(sizeof(ONode) * cap);
     s->nnodes = 1;
-    /* work stack of (node, start, end) */
-    uint32_t* st = (uint32_t*)malloc(sizeof(uint32_t) * 3 * (64 + 2 * (n ? n : 1)));
+    /* work stack of (node, start, end, depth) */
+    uint32_t* st = (uint32_t*)malloc(sizeof(uint32_t) * 4 * (64 + 2 * (n ? n : 1)));
     int sp = 0;
-    st[0] = 0; st[1] = 0; st[2] = n; sp = 1;
+    st[0] = 0; st[1] = 0; st[2] = n; st[3] = 0; sp = 1;
     while (sp) {
         --sp;
-        uint32_t ni = st[3 * sp], s0 = st[3 * sp + 1], e0 = st[3 * sp + 2];
+        uint32_t ni = st[4 * sp], s0 = st[4 * sp + 1], e0 = st[4 * sp + 2], depth = st[4 * sp + 3];
         ONode* nd = &s->nodes[ni];
-        float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+        OBin all;
+        bin_clear(&all);
         float clo[3] = {INFINITY, INFINITY, INFINITY}, chi[3] = {-INFINITY, -INFINITY, -INFINITY};
         for (uint32_t k = s0; k < e0; ++k) {
             uint32_t t = s->order[k];
-            for (int q = 0; q < 3; ++q)
-                for (int a = 0; a < 3; ++a) {
-                    lo[a] = fminf(lo[a], s->world[9 * t + 3 * q + a]);
-                    hi[a] = fmaxf(hi[a], s->world[9 * t + 3 * q + a]);
-                }
+            bin_grow(&all, &s->world[9 * (size_t)t]);
             for (int a = 0; a < 3; ++a) { clo[a] = fminf(clo[a], cen[3 * t + a]); chi[a] = fmaxf(chi[a], cen[3 * t + a]); }
         }
-        for (int a = 0; a < 3; ++a) { nd->lo[a] = lo[a] - s->pad; nd->hi[a] = hi[a] + s->pad; }
+        for (int a = 0; a < 3; ++a) { nd->lo[a] = all.lo[a] - s->pad; nd->hi[a] = all.hi[a] + s->pad; }
         if (e0 - s0 <= 4) {
             nd->left = -1; nd->right = -1; nd->start = s0; nd->count = e0 - s0;
             continue;
         }
-        int axis = 0;
-        for (int a = 1; a < 3; ++a) if (chi[a] - clo[a] > chi[axis] - clo[axis]) axis = a;
-        cmp_axis = axis; cmp_cen = cen;
-        qsort(s->order + s0, e0 - s0, sizeof(uint32_t), cmp_c);
-        uint32_t mid = s0 + (e0 - s0) / 2;
+        /* best binned split over the three axes: cost = A(left) * n(left) + A(right) * n(right) */
+        int best_axis = -1, best_b = 0;
+        float best_cost = INFINITY;
+        for (int a = 0; a < 3 && depth < OMEDIAN_DEPTH; ++a) {
+            float ext = chi[a] - clo[a];
+            if (!(ext > 0.0f)) continue;
+            OBin bins[OBINS];
+            for (int b = 0; b < OBINS; ++b) bin_clear(&bins[b]);
+            float scale = (float)OBINS / ext;
+            for (uint32_t k = s0; k < e0; ++k) {
+                uint32_t t = s->order[k];
+                int b = (int)((cen[3 * t + a] - clo[a]) * scale);
+                if (b >= OBINS) b = OBINS - 1;
+                if (b < 0) b = 0;
+                bin_grow(&bins[b], &s->world[9 * (size_t)t]);
+                bins[b].n++;
+            }
+            float right_cost[OBINS];
+            OBin acc;
+            bin_clear(&acc);
+            for (int b = OBINS - 1; b > 0; --b) {
+                bin_merge(&acc, &bins[b]);
+                right_cost[b] = bin_area(&acc) * (float)acc.n;
+            }
+            bin_clear(&acc);
+            for (int b = 1; b < OBINS; ++b) {   /* split before bin b */
+                bin_merge(&acc, &bins[b - 1]);
+                if (acc.n == 0 || acc.n == e0 - s0) continue;
+                float c = bin_area(&acc) * (float)acc.n + right_cost[b];
+                if (c < best_cost) { best_cost = c; best_axis = a; best_b = b; }
+            }
+        }
+        uint32_t mid;
+        if (best_axis >= 0) {   /* partition by bin index */
+            int a = best_axis;
+            float scale = (float)OBINS / (chi[a] - clo[a]);
+            uint32_t i = s0, j = e0;
+            while (i < j) {
+                uint32_t t = s->order[i];
+                int b = (int)((cen[3 * t + a] - clo[a]) * scale);
+                if (b >= OBINS) b = OBINS - 1;
+                if (b < best_b) { ++i; } else { --j; s->order[i] = s->order[j]; s->order[j] = t; }
+            }
+            mid = i;
+        } else {                /* deep (or all centroids coincide): object median on the longest axis */
+            int axis = 0;
+            for (int a = 1; a < 3; ++a) if (chi[a] - clo[a] > chi[axis] - clo[axis]) axis = a;
+            cmp_axis = axis; cmp_cen = cen;
+            qsort(s->order + s0, e0 - s0, sizeof(uint32_t), cmp_c);
+            mid = s0 + (e0 - s0) / 2;
+        }
         uint32_t l = s->nnodes++, r = s->nnodes++;
         nd = &s->nodes[ni];
         nd->left = (int32_t)l; nd->right = (int32_t)r; nd->start = 0; nd->count = 0;
-        st[3 * sp] = r; st[3 * sp + 1] = mid; st[3 * sp + 2] = e0; ++sp;
-        st[3 * sp] = l; st[3 * sp + 1] = s0; st[3 * sp + 2] = mid; ++sp;
+        st[4 * sp] = r; st[4 * sp + 1] = mid; st[4 * sp + 2] = e0; st[4 * sp + 3] = depth + 1; ++sp;
+        st[4 * sp] = l; st[4 * sp + 1] = s0; st[4 * sp + 2] = mid; st[4 * sp + 3] = depth + 1; ++sp;
     }
     free(st);
     free(cen);
@@ -323,16 +393,18 @@ static int otri(const OPre* p, V3 o, const float* w, float tmin, float tmax, flo
 
 static float safe_inv(float x) { return 1.0f / (fabsf(x) < 1e-30f ? copysignf(1e-30f, x) : x); }
 
-static int obox(const ONode* n, V3 o, V3 inv, float tmin, float tmax) {
+/* slab test; returns the entry distance, or -1 on a miss */
+static float obox(const ONode* n, V3 o, V3 inv, float tmin, float tmax) {
     float tx0 = (n->lo[0] - o.x) * inv.x, tx1 = (n->hi[0] - o.x) * inv.x;
     float ty0 = (n->lo[1] - o.y) * inv.y, ty1 = (n->hi[1] - o.y) * inv.y;
     float tz0 = (n->lo[2] - o.z) * inv.z, tz1 = (n->hi[2] - o.z) * inv.z;
     float tn = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), tmin));
     float tf = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), tmax * 1.000001f));
-    return tn <= tf;
+    return tn <= tf ? tn : -1.0f;
 }
 
-/* closest hit over the whole BVH; ties broken by the smaller original triangle id */
+/* closest hit over the whole BVH (nearer child first); ties broken by the smaller original
+ * triangle id, so the result does not depend on the visiting order */
 static int otrace(const rt_oracle_scene* s, V3 o, V3 d, float tmin, float tmax, int any,
                   float* to, uint32_t* ido, float* uo, float* vo) {
     if (s->ntri == 0) return 0;
@@ -340,12 +412,18 @@ static int otrace(const rt_oracle_scene* s, V3 o, V3 d, float tmin, float tmax, 
     V3 inv = v3(safe_inv(d.x), safe_inv(d.y), safe_inv(d.z));
     float best = tmax, bu = 0, bv = 0;
     uint32_t bid = 0xffffffffu;
-    uint32_t stack[128];
+    /* (node, entry distance) pairs; a popped node whose entry lies beyond the closest hit so far
+     * is skipped (the same margin as the slab test) */
+    uint32_t stack[256];
+    float tent[256];
     int sp = 0;
-    stack[sp++] = 0;
+    float t0 = obox(&s->nodes[0], o, inv, tmin, best);
+    if (t0 < 0.0f) return 0;
+    stack[sp] = 0; tent[sp++] = t0;
     while (sp) {
-        const ONode* n = &s->nodes[stack[--sp]];
-        if (!obox(n, o, inv, tmin, best)) continue;
+        --sp;
+        if (tent[sp] > best * 1.000001f) continue;
+        const ONode* n = &s->nodes[stack[sp]];
         if (n->left < 0) {
             for (uint32_t k = 0; k < n->count; ++k) {
                 uint32_t t = s->order[n->start + k];
@@ -356,8 +434,17 @@ static int otrace(const rt_oracle_scene* s, V3 o, V3 d, float tmin, float tmax, 
                 }
             }
         } else {
-            stack[sp++] = (uint32_t)n->right;
-            stack[sp++] = (uint32_t)n->left;
+            float tl = obox(&s->nodes[n->left], o, inv, tmin, best);
+            float tr = obox(&s->nodes[n->right], o, inv, tmin, best);
+            if (tl >= 0.0f && tr >= 0.0f) {
+                int near_left = tl <= tr;
+                stack[sp] = (uint32_t)(near_left ? n->right : n->left); tent[sp++] = near_left ? tr : tl;
+                stack[sp] = (uint32_t)(near_left ? n->left : n->right); tent[sp++] = near_left ? tl : tr;
+            } else if (tl >= 0.0f) {
+                stack[sp] = (uint32_t)n->left; tent[sp++] = tl;
+            } else if (tr >= 0.0f) {
+                stack[sp] = (uint32_t)n->right; tent[sp++] = tr;
+            }
         }
     }
     if (bid == 0xffffffffu) return 0;
@@ -487,7 +574,7 @@ static int tangent_basis(const rt_oracle_scene* s, const OTri* t, V3* tangent, V
 typedef struct {
     const rt_oracle_scene* s;
     rt_oracle_frame* f;
-    int row_lo, row_step_total, nthreads, tid;
+    int* next_row;         /* shared: index of the next row of the subset to render */
     uint64_t closest, shadow, paths;
 } Job;
 
@@ -803,10 +890,21 @@ static void render_pixel(const rt_oracle_scene* s, rt_oracle_frame* f, int px, i
 
 static void* worker(void* arg) {
     Job* j = (Job*)arg;
-    const Uniforms* U = j->f->uniforms;
-    int step = j->row_step_total;
-    for (int y = j->row_lo + j->tid * step; y < U->height; y += step * j->nthreads)
-        for (int x = 0; x < U->width; ++x) render_pixel(j->s, j->f, x, y, &j->closest, &j->shadow, &j->paths);
+    const rt_oracle_frame* f = j->f;
+    const Uniforms* U = f->uniforms;
+    const int step = f->row_step > 0 ? f->row_step : 1;
+    const int T = f->tile_size > 0 ? f->tile_size : 64;
+    const int split = f->nranks > 1;
+    const int tiles_x = (U->width + T - 1) / T;
+    for (;;) {   /* rows handed out one at a time: balanced whatever the per-row cost */
+        int k = __atomic_fetch_add(j->next_row, 1, __ATOMIC_RELAXED);
+        int y = f->row_start + k * step;
+        if (y >= U->height) break;
+        for (int x = 0; x < U->width; ++x) {
+            if (split && ((y / T) * tiles_x + x / T) % f->nranks != f->rank) continue;
+            render_pixel(j->s, j->f, x, y, &j->closest, &j->shadow, &j->paths);
+        }
+    }
     return NULL;
 }
 
@@ -814,14 +912,14 @@ int rt_oracle_render(const rt_oracle_scene* s, rt_oracle_frame* f) {
     if (!s || !f || !f->uniforms || !f->random || !f->accum_out || !f->depth || !f->motion) return 1;
     const Uniforms* U = f->uniforms;
     if (U->lightCount < 1 || U->lightCount > (int)s->nlight || U->maxBounces > 12) return 2;
+    if (f->nranks > 1 && (f->rank < 0 || f->rank >= f->nranks)) return 3;
     pthread_once(&g_primes_once, init_primes);
     int nt = f->threads > 0 ? f->threads : 1;
-    int step = f->row_step > 0 ? f->row_step : 1;
+    int next_row = 0;
     Job* jobs = (Job*)calloc(nt, sizeof(Job));
     pthread_t* th = (pthread_t*)calloc(nt, sizeof(pthread_t));
     for (int i = 0; i < nt; ++i) {
-        jobs[i].s = s; jobs[i].f = f; jobs[i].row_lo = f->row_start; jobs[i].row_step_total = step;
-        jobs[i].nthreads = nt; jobs[i].tid = i;
+        jobs[i].s = s; jobs[i].f = f; jobs[i].next_row = &next_row;
         if (nt > 1) pthread_create(&th[i], NULL, worker, &jobs[i]);
     }
     if (nt == 1) worker(&jobs[0]);

@@ -41,7 +41,9 @@ typedef struct rt_oracle_frame {
     int32_t row_start;           /* render rows row_start, row_start+row_step, ... */
     int32_t row_step;            /* <= 0 means 1 */
     int32_t threads;             /* worker threads (<= 0: 1) */
-    int32_t _pad;
+    int32_t tile_size;           /* with nranks > 1: render only the pixels of the tiles with */
+    int32_t rank;                /* tile_id % nranks == rank (tile_size x tile_size tiles,     */
+    int32_t nranks;              /* numbered row-major), as a rank of the multi-GPU split does */
     uint64_t closest_rays;       /* out */
     uint64_t shadow_rays;        /* out */
     uint64_t paths;              /* out */

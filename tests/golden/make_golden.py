@@ -25,6 +25,12 @@ CASES = {
     "c2_small_b4": ("c2", 64, 36, dict(samplesPerPixel=1, maxBounces=4), 1),
     # c1 + the train with every texture map kind bound (tests/helpers.py textured_scene)
     "tex_b3": ("tex", 64, 48, dict(samplesPerPixel=1, maxBounces=3), 1),
+    # c1 lit by the light types the AppScene does not use (Raytracing.metal:633-643) and by three
+    # and four lights (the light pick of :588-589 with lightCount > 2), PBR and legacy shading
+    "lights_point_b3": ("lights:point", 64, 48, dict(samplesPerPixel=2, maxBounces=3), 1),
+    "lights_sun_b3": ("lights:sun", 64, 48, dict(samplesPerPixel=2, maxBounces=3), 1),
+    "lights_mix4_b3": ("lights:area,spot,point,sun", 64, 48, dict(samplesPerPixel=2, maxBounces=3), 1),
+    "lights_mix3_legacy_b3": ("lights:point,sun,area2", 64, 48, dict(samplesPerPixel=2, maxBounces=3, shadingMode=1), 1),
 }
 SEED = 11
 
@@ -34,6 +40,10 @@ def make_scene(rt, preset, assets):
         sys.path.insert(0, os.path.join(ROOT, "tests"))
         from helpers import textured_scene
         return textured_scene(rt, assets)
+    if preset.startswith("lights:"):
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        from helpers import lights_scene
+        return lights_scene(rt, assets, preset.split(":", 1)[1].split(","))
     return rt.Scene.preset(preset, assets)
 
 
@@ -52,12 +62,16 @@ def render_case(rt, oracle, preset, W, H, knobs, frames, assets):
     return out
 
 
-def main():
+def main(names=None):
+    """Regenerates the named cases (default: all) and rewrites cases.json for every case."""
     rt = importlib.import_module("metal4-raytracing_amd")
     import oracle
     assets = os.path.join(ROOT, "assets")
-    meta = {}
+    path = os.path.join(ROOT, "tests", "golden", "cases.json")
+    meta = json.load(open(path)) if os.path.exists(path) else {}
     for name, (preset, W, H, knobs, frames) in CASES.items():
+        if names and name not in names:
+            continue
         out = render_case(rt, oracle, preset, W, H, knobs, frames, assets)
         np.savez_compressed(os.path.join(ROOT, "tests", "golden", name + ".npz"), radiance=out["radiance"][..., :3],
                             depth=out["depth"], motion=out["motion"],
@@ -70,4 +84,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    main(sys.argv[1:] or None)

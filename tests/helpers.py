@@ -84,3 +84,36 @@ def textured_scene(rt, assets):
     sc.bind_texture(4, 5, "normal", T["normal"])
     sc.bind_texture(4, 5, "ao", T["rough"])              # AO: bound, never sampled (ENABLE_AO 0)
     return sc
+
+
+# ---- light types (Scene.swift:161-208): the reference's factories, with the values Scene.init uses
+# or has commented out (Scene.swift:82-90): area light1 and light2, spot light3, sunLight, pointLight
+LIGHT_TYPES = {"sun": 1, "spot": 2, "point": 3, "area": 4}
+
+
+def make_light(rt, kind):
+    L = rt.Light()
+    f3 = rt.f3
+    if kind == "area":            # Scene.setupLight (light1)
+        L.type, L.position, L.forward = 4, f3(0.0, 1.98, 0.0), f3(0.0, -1.0, 0.0)
+        L.right, L.up, L.color = f3(0.25, 0.0, 0.0), f3(0.0, 0.0, 0.25), f3(4.0, 4.0, 4.0)
+    elif kind == "area2":         # light2 (built, unused by the reference scene)
+        L.type, L.position, L.forward = 4, f3(2.0, 1.98, 3.0), f3(0.0, -0.5, 0.0)
+        L.right, L.up, L.color = f3(0.1, 0.0, 0.0), f3(0.0, 0.0, 0.1), f3(4.0, 4.0, 4.0)
+    elif kind == "spot":          # light3
+        L.type, L.position, L.direction = 2, f3(2.0, 1.0, 4.0), f3(-1.5, -0.5, -1.5)
+        L.coneAngle, L.color = 25.0 / 180.0 * 3.14159265358979323846, f3(4.0, 4.0, 4.0)
+    elif kind == "sun":           # Light.sunLight(direction: [-1, -2, 0], color: [1, 1, 1])
+        L.type, L.direction, L.color = 1, f3(-1.0, -2.0, 0.0), f3(1.0, 1.0, 1.0)
+    elif kind == "point":         # Light.pointLight(position: [1, 1, 1], color: [1, 1, 1])
+        L.type, L.position, L.color = 3, f3(1.0, 1.0, 1.0), f3(1.0, 1.0, 1.0)
+    else:
+        raise ValueError(kind)
+    return L
+
+
+def lights_scene(rt, assets, kinds):
+    """The c1 scene lit by the given lights (lightCount = len(kinds), Raytracing.metal:588-647)."""
+    sc = rt.Scene.preset("c1", assets)
+    sc.set_lights([make_light(rt, k) for k in kinds])
+    return sc

@@ -102,3 +102,37 @@ def test_pack_unpack_roundtrip_with_oracle_frame(rt, orc, assets):
         p = tiles.pack_host(img, 32, r, 3)
         tiles.unpack_host(p, out, 32, r, 3)
     assert np.array_equal(out, img)
+
+
+@pytest.mark.timeout(240)
+@pytest.mark.parametrize("n", [2, 3])
+def test_bench_launcher_starts_ranks(n):
+    """`python bench.py --gpus N` with no WORLD_SIZE starts N rank processes itself (the parent
+    never touches a GPU), they meet over torch.distributed (gloo in --dry-run, RCCL on GPUs), run
+    the barrier / max-over-ranks timing and the tile gather, and rank 0's single JSON line comes
+    through with n_gpus = world_size = N."""
+    import json
+    import subprocess
+    import sys
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(n), "--dry-run", "--steps", "3",
+                        "--warmup", "1", "--width", "200", "--height", "136"], capture_output=True, text=True,
+                       timeout=200, cwd=ROOT, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [x for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == n and d["world_size"] == n and d["steps"] == 3 and d["value"] > 0
+
+
+@pytest.mark.timeout(120)
+def test_bench_launcher_fails_when_a_rank_fails():
+    """Ranks that fail (an invalid frame size reaches every child) make the launcher exit non-zero
+    instead of hanging."""
+    import subprocess
+    import sys
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dry-run", "--steps", "0",
+                        "--warmup", "0", "--scene", "c1", "--width", "-5"], capture_output=True, text=True, timeout=100,
+                       cwd=ROOT, env=env)
+    assert r.returncode != 0

@@ -207,7 +207,8 @@ def test_pipelines_agree_full_frame(rt, assets, W, H, spp, bounces):
 
 @pytest.mark.parametrize("pipeline", PIPELINES)
 @pytest.mark.parametrize("name", ["c1_pbr_b1", "c1_pbr_b4", "c1_legacy_b3", "c1_ema_f3", "c3g_small_b8", "c2_small_b4",
-                                  "tex_b3"])
+                                  "tex_b3", "lights_point_b3", "lights_sun_b3", "lights_mix4_b3",
+                                  "lights_mix3_legacy_b3"])
 def test_gpu_matches_golden_fixtures(rt, assets, name, pipeline):
     """The HIP path against the committed fixtures (tests/golden, oracle-generated, seed 11)."""
     import json
@@ -259,3 +260,33 @@ def test_emissive_parity(rt, orc, assets, tmp_path, pipeline):
         assert rep["n_bad"] == 0, rep
         assert st.closest_rays == o["closest_rays"] and st.shadow_rays == o["shadow_rays"]
     assert float(np.max(g[..., :3])) > 0.5   # the emitter shows
+
+
+@pytest.mark.parametrize("pipeline", PIPELINES)
+@pytest.mark.parametrize("mode", [0, 1])
+@pytest.mark.parametrize("kinds", [("point",), ("sun",), ("area", "spot", "point"), ("area", "spot", "point", "sun"),
+                                   ("sun", "area2", "point", "spot")])
+def test_light_types_parity(rt, orc, assets, kinds, mode, pipeline):
+    """Point and sun lights (Raytracing.metal:633-643; a sun's shadow ray has tmax = inf - 1e-3 =
+    inf, :716-743) and three or four lights (the light pick of :588-589 with lightCount > 2, the
+    lightCount factor of :647), in PBR and legacy shading, over two EMA frames."""
+    from helpers import lights_scene
+    scene = lights_scene(rt, assets, list(kinds))
+    R = make_renderer(rt, scene, 72, 48, pipeline, seed=13)
+    R.samplesPerPixel, R.maxBounces, R.shadingMode = 2, 4, mode
+    osc = orc.OracleScene(scene.desc())
+    prev = motion = None
+    for _ in range(2):
+        u = R.draw()
+        assert u.lightCount == len(kinds)
+        R.wait()
+        g = R.radiance()
+        gd, gm, _ = R.aux()
+        st = R.stats()
+        o = osc.render(u, R.random, accum_in=prev, motion_in=motion)
+        prev, motion = o["radiance"], o["motion"]
+        rep = parity_report(g, o["radiance"])
+        assert rep["n_bad"] == 0, rep
+        assert np.array_equal(gd, o["depth"]) and np.array_equal(gm, o["motion"])
+        assert st.closest_rays == o["closest_rays"] and st.shadow_rays == o["shadow_rays"]
+    assert float(np.max(g[..., :3])) > 0.0

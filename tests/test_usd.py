@@ -416,3 +416,16 @@ def test_preset_c5_loads_a_real_robot_usdz(rt, assets, files, tmp_path):
     np.testing.assert_allclose(M[3], [-0.5, 0.0, 1.0])
     s2 = rt.Scene.preset("c5_synthetic", str(tmp_path))
     assert s2.synthetic
+
+
+@pytest.mark.timeout(60)
+def test_crate_path_jump_cycle_fails_fast(rt, tmp_path):
+    """A crafted PATHS jump table (every entry 'child and sibling at +1', the last a leaf) reaches
+    each entry along exponentially many routes; the reader visits each entry once and rejects the
+    second visit (RT_ERR_IO) instead of hanging."""
+    prims = [dict(path="/P%d" % k, type="Xform", attrs=[]) for k in range(60)]
+    w = W.CrateWriter(jumps_hook=lambda j: [1] * (len(j) - 1) + [-2])
+    p = tmp_path / "cycle.usdc"
+    p.write_bytes(w.write(prims))
+    with pytest.raises(rt.RTError, match="path tree"):
+        rt.Scene().add_usd(str(p), (0, 0, 0))

@@ -185,9 +185,10 @@ _TYPE_OF = {
 
 
 class CrateWriter:
-    def __init__(self):
+    def __init__(self, jumps_hook=None):
         self.tokens, self.tok_index = [], {}
         self.data = bytearray(b"\0" * 88)   # bootstrap, patched at the end
+        self.jumps_hook = jumps_hook          # tests: rewrites the PATHS sibling-jump table
 
     def tok(self, s):
         if s not in self.tok_index:
@@ -411,6 +412,8 @@ class CrateWriter:
                 jumps.append(0)
             else:
                 jumps.append(-2)
+        if self.jumps_hook is not None:
+            jumps = self.jumps_hook(jumps)
         elems = [0 if i == 0 else (-self.tok(e[1]) if e[2] else self.tok(e[1])) for i, e in enumerate(order)]
         section("PATHS", struct.pack("<QQ", len(order), len(order)) + encode_ints(list(range(len(order)))) +
                 encode_ints(elems) + encode_ints(jumps))
