@@ -48,6 +48,7 @@ struct Tuning {
     int finish_frac;   // RT_FINISH_FRAC: percent of the resident grid the finish launch takes (0 = by frames in flight)
     bool log;          // RT_WF_LOG=1: per-round queue sizes, stage times and finish diagnostics on stderr
     bool host_ctl;     // RT_WF_HOST=1: host-driven rounds (queue sizes read back every round)
+    int ray_sort;      // RT_RAY_SORT: 1 = group the rays wf_shade appends by direction octant
 };
 static const Tuning& tuning() {
     static const Tuning t = [] {
@@ -60,6 +61,7 @@ static const Tuning& tuning() {
         v.finish_frac = std::min(env_int("RT_FINISH_FRAC", 0), 100);
         v.log = env_int("RT_WF_LOG", 0) != 0;
         v.host_ctl = env_int("RT_WF_HOST", 0) != 0;
+        v.ray_sort = env_int("RT_RAY_SORT", 0);
         return v;
     }();
     return t;
@@ -123,6 +125,48 @@ __device__ __forceinline__ uint32_t block_alloc_n(uint32_t v, uint32_t* counter,
     return r;
 }
 
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
+    const uint32_t lane = lane_id();
+    #pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t t = __shfl_up(v, off, 64);
+        if (lane >= (uint32_t)off) v += t;
+    }
+    return v;
+}
+
+// Key-grouped block allocation (extend / shadow ray coherence, Q.ray_sort): the block's entries are
+// allocated with ONE returning atomic as in block_alloc, but laid out grouped by key (key-major;
+// the order inside a key is that of the LDS atomics, which does not matter: each path's arithmetic
+// does not depend on which lane or position traces it).  Every thread of the block calls it.
+constexpr int kRayKeys = 8;   // direction octants
+struct KeyAlloc {
+    uint32_t cnt[kRayKeys];
+};
+__device__ __forceinline__ uint32_t block_alloc_keyed(bool pred, uint32_t key, uint32_t* counter, KeyAlloc& sh) {
+    if (threadIdx.x < kRayKeys) sh.cnt[threadIdx.x] = 0u;
+    __syncthreads();
+    uint32_t rank = 0;
+    if (pred) rank = atomicAdd(&sh.cnt[key], 1u);   // LDS atomic
+    __syncthreads();
+    if (threadIdx.x < 64) {   // wave 0: exclusive scan of the key counts + the block's one global atomic
+        const uint32_t v = threadIdx.x < kRayKeys ? sh.cnt[threadIdx.x] : 0u;
+        const uint32_t incl = wave_incl_scan(v);
+        const uint32_t tot = (uint32_t)__shfl((int)incl, 63, 64);
+        uint32_t b = 0;
+        if (threadIdx.x == 0 && tot) b = atomicAdd(counter, tot);
+        b = (uint32_t)__shfl((int)b, 0, 64);
+        if (threadIdx.x < kRayKeys) sh.cnt[threadIdx.x] = b + incl - v;
+    }
+    __syncthreads();
+    const uint32_t slot = pred ? sh.cnt[key] + rank : 0u;
+    __syncthreads();
+    return slot;
+}
+__device__ __forceinline__ uint32_t octant(f3 d) {
+    return (d.x < 0.0f ? 1u : 0u) | (d.y < 0.0f ? 2u : 0u) | (d.z < 0.0f ? 4u : 0u);
+}
+
 __device__ __forceinline__ uint32_t compact1by1(uint32_t x) {
     x &= 0x55555555u;
     x = (x | (x >> 1)) & 0x33333333u;
@@ -168,6 +212,7 @@ struct WfParams {
     int shade_min;         // wf_finish_step: shade once this many lanes wait (or none traverses)
     int fchunk;            // wf_finish_step: paths per chunk grab
     int finish_frac;       // percent of the resident grid the finish launch takes
+    int ray_sort;          // wf_shade: extend / shadow rays grouped by direction octant inside each block's allocation
     int dev_ctl;           // device-side control (enqueue_wavefront): kernels read their queue sizes from
                            // the counters and skip once the live count fell below `tail`
     int finish_q;          // dev_ctl: the finish queue when every enqueued bulk round ran (written by generate)
@@ -444,6 +489,7 @@ __global__ void __launch_bounds__(kBlock) wf_shade(DevScene S, const FrameParams
     __shared__ HaltonDim lds_halton[kHaltonLds];
     __shared__ MatRec lds_mat[kMatLds];
     __shared__ BlockAlloc ba_ray, ba_sh;
+    __shared__ KeyAlloc ka;
     if (tail_mode(Q)) return;
     const ShadeTabs halton = load_tabs(S, lds_halton, lds_mat);
     const Uniforms& U = P.U;
@@ -524,13 +570,15 @@ __global__ void __launch_bounds__(kBlock) wf_shade(DevScene S, const FrameParams
                 if (r.next) Q.W.p_meta[pid] = make_uint4(meta.x, meta.y, pack_state(p.bounce, p.tpass, p.step), meta.w);
             }
         }
-        uint32_t ns = block_alloc(r.shadow, &Q.W.counts[cslot(kCntShadowQ + shard)], ba_sh);
+        uint32_t ns = Q.ray_sort ? block_alloc_keyed(r.shadow, octant(r.sd), &Q.W.counts[cslot(kCntShadowQ + shard)], ka)
+                                 : block_alloc(r.shadow, &Q.W.counts[cslot(kCntShadowQ + shard)], ba_sh);
         if (r.shadow) {
             sqout[3 * (size_t)ns] = make_float4(r.so.x, r.so.y, r.so.z, __uint_as_float(pid));
             sqout[3 * (size_t)ns + 1] = make_float4(r.sd.x, r.sd.y, r.sd.z, r.stmax);
             sqout[3 * (size_t)ns + 2] = make_float4(r.contrib.x, r.contrib.y, r.contrib.z, 0.0f);
         }
-        uint32_t nr = block_alloc(r.next, &Q.W.counts[cslot(next * kShards + shard)], ba_ray);
+        uint32_t nr = Q.ray_sort ? block_alloc_keyed(r.next, octant(rayD), &Q.W.counts[cslot(next * kShards + shard)], ka)
+                                 : block_alloc(r.next, &Q.W.counts[cslot(next * kShards + shard)], ba_ray);
         if (r.next) {
             qout[2 * (size_t)nr] = make_float4(rayO.x, rayO.y, rayO.z, __uint_as_float(pid));
             qout[2 * (size_t)nr + 1] = make_float4(rayD.x, rayD.y, rayD.z, 0.0f);
@@ -544,16 +592,6 @@ __global__ void __launch_bounds__(kBlock) wf_shade(DevScene S, const FrameParams
 // scatter that writes {o, d, hit} of every hit to its bin's range.  Misses are dropped (their
 // paths end, :321-322).  The order inside a bin is arbitrary; per-path results do not depend on
 // the order paths are shaded in, so the output stays bit-identical.
-__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
-    const uint32_t lane = lane_id();
-    #pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        const uint32_t t = __shfl_up(v, off, 64);
-        if (lane >= (uint32_t)off) v += t;
-    }
-    return v;
-}
-
 // block b's share of the dense queue index range (the same in hist and scatter)
 __device__ __forceinline__ void sort_range(uint32_t n, uint32_t& beg, uint32_t& end) {
     beg = (uint32_t)(((uint64_t)n * blockIdx.x) / kSortBlocks);
@@ -1399,6 +1437,7 @@ bool run_wavefront(const DevScene& S, const FrameParams& P, WavefrontBuffers& W,
     Q.diag = tu.log ? 1 : 0;
     Q.shade_min = tu.shade_min;
     Q.fchunk = tu.fchunk;
+    Q.ray_sort = tu.ray_sort;
     // frames in flight: the finish tail takes part of the resident grid and leaves the rest to the
     // other frames' bulk rounds (C3g sweeps, DESIGN.md §3: two slots 40 %; four slots on a small
     // frame, a multi-GPU rank's share, 20 %; else 1 / in_flight); one frame at a time: all of it
