@@ -19,18 +19,12 @@ namespace rt {
 
 constexpr int kStackSize = 16;   // per-thread traversal stack entries (LDS): node groups of the 8-wide BVH
 constexpr int kBlock = 256;      // threads per block for the traversal kernels
-constexpr int kTopNodes = 32;    // first BFS nodes of the 8-wide BVH staged in LDS by wf_trace
-// per kernel (build-time): extend (7 blocks/CU), connect (8 blocks/CU), finish (4 blocks/CU).
-// Three full levels (73 / 48 / 200 nodes, same occupancy) measured 3 % slower on C3g than 32.
-#ifndef RT_TOP_EXTEND
-#define RT_TOP_EXTEND 32
+// First BFS nodes of the 8-wide BVH staged in LDS by the traversal kernels (RT_TOP_NODES at build
+// time; 0 = every node from global memory)
+#ifndef RT_TOP_NODES
+#define RT_TOP_NODES 32
 #endif
-#ifndef RT_TOP_CONNECT
-#define RT_TOP_CONNECT 32
-#endif
-#ifndef RT_TOP_FINISH
-#define RT_TOP_FINISH 32
-#endif
+constexpr int kTopNodes = RT_TOP_NODES;
 
 struct DevScene {
     const float4* tris;

@@ -49,7 +49,6 @@ struct Tuning {
     bool log;          // RT_WF_LOG=1: per-round queue sizes, stage times and finish diagnostics on stderr
     bool host_ctl;     // RT_WF_HOST=1: host-driven rounds (queue sizes read back every round)
     int ray_sort;      // RT_RAY_SORT: 1 = group the rays wf_shade appends by direction octant
-    int shadow_help;   // RT_SHADOW_HELP: 1 = idle finish lanes trace other lanes' shadow rays
 };
 static const Tuning& tuning() {
     static const Tuning t = [] {
@@ -63,7 +62,6 @@ static const Tuning& tuning() {
         v.log = env_int("RT_WF_LOG", 0) != 0;
         v.host_ctl = env_int("RT_WF_HOST", 0) != 0;
         v.ray_sort = env_int("RT_RAY_SORT", 0);
-        v.shadow_help = env_int("RT_SHADOW_HELP", 0);
         return v;
     }();
     return t;
@@ -215,7 +213,6 @@ struct WfParams {
     int fchunk;            // wf_finish_step: paths per chunk grab
     int finish_frac;       // percent of the resident grid the finish launch takes
     int ray_sort;          // wf_shade: extend / shadow rays grouped by direction octant inside each block's allocation
-    int shadow_help;       // wf_finish_step: once the queue is exhausted, idle lanes trace other lanes' shadow rays
     int dev_ctl;           // device-side control (enqueue_wavefront): kernels read their queue sizes from
                            // the counters and skip once the live count fell below `tail`
     int finish_q;          // dev_ctl: the finish queue when every enqueued bulk round ran (written by generate)
@@ -396,7 +393,7 @@ __device__ __forceinline__ bool trav_step(const DevScene& S, Trav& T, bool any, 
         }
         const uint32_t ni = T.g_base + (uint32_t)r;
         NodeWords w;
-        if (ni < n_top) {
+        if (kTopNodes > 0 && ni < n_top) {
             if (COUNT) tc.lds_nodes++;
             const uint4* l = lds_top + 5 * ni;
             w.h0 = __builtin_bit_cast(float4, l[0]);
@@ -415,9 +412,10 @@ __device__ __forceinline__ bool trav_step(const DevScene& S, Trav& T, bool any, 
 
 // Stages the first n_top BFS nodes of the 8-wide BVH in LDS (every thread of the block calls it;
 // the caller's next block barrier publishes them).
-template <int N>
-__device__ __forceinline__ uint32_t stage_top(const DevScene& S, uint4 (&lds_top)[N * 5]) {
-    const uint32_t n_top = (uint32_t)min(S.num_nodes8, N);
+constexpr int kTopLds = kTopNodes > 0 ? kTopNodes : 1;   // LDS array size (>= 1)
+__device__ __forceinline__ uint32_t stage_top(const DevScene& S, uint4* lds_top) {
+    if (kTopNodes == 0) return 0u;
+    const uint32_t n_top = (uint32_t)min(S.num_nodes8, kTopNodes);
     for (uint32_t i = threadIdx.x; i < n_top * 5; i += kBlock) lds_top[i] = reinterpret_cast<const uint4*>(S.nodes8)[i];
     return n_top;
 }
@@ -698,7 +696,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ANY
 wf_trace(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int cur) {
     const FrameParams& P = *Pp;   // per-frame parameters in device memory
     __shared__ int lds_stack[kStackSize * kBlock];
-    __shared__ uint4 lds_top[kTopNodes * 5];   // BVH top levels (BFS order: root, its children, ...)
+    __shared__ uint4 lds_top[kTopLds * 5];   // BVH top levels (BFS order: root, its children, ...)
     int* stack = &lds_stack[threadIdx.x];
     if (Q.dev_ctl) {
         // device-side round control: extend decides (uniformly, from the counters) whether this
@@ -717,7 +715,7 @@ wf_trace(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int cur) {
             }
         }
     }
-    const uint32_t n_top = stage_top<kTopNodes>(S, lds_top);
+    const uint32_t n_top = stage_top(S, lds_top);
     __syncthreads();
     const ShardPrefix cnt = load_prefix(ANY ? Q.W.counts + cslot(kCntShadowQ) : Q.W.counts + cslot(cur * kShards));
     const uint32_t n = cnt.end[kShards - 1];
@@ -819,26 +817,18 @@ wf_trace(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int cur) {
 // costs the sum of its own lanes' steps, not the sum over segments of its slowest lane's query:
 // the glass paths left at the tail (up to ~23 segments) do not wait for their wave's worst ray
 // every segment.
-// Shadow helpers (Q.shadow_help): once the queue is exhausted a wave's lanes go idle one by one
-// while its last paths (long glass chains) still run.  A path whose shading emits a shadow ray
-// AND a continuation then hands the shadow query to an idle lane of its wave (LDS job slot) and
-// traces its next closest-hit ray at once; the helper writes back occluded / unoccluded, and the
-// owner adds the contribution before its next shading step (or before ending), so the radiance
-// sums are the reference's in the reference's order.  The two queries of a segment run side by
-// side instead of one after the other on the critical path.
 template <bool COUNT, bool FULL>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 4)))
 wf_finish_step(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int cur) {
     const FrameParams& P = *Pp;   // per-frame parameters in device memory
     if (cur < 0) cur = (int)__builtin_amdgcn_readfirstlane(Q.W.counts[cslot(kCntFinishQ)]);   // dev_ctl
     __shared__ int lds_stack[kStackSize * kBlock];
-    __shared__ uint4 lds_top[kTopNodes * 5];
+    __shared__ uint4 lds_top[kTopLds * 5];
     __shared__ HaltonDim lds_halton[kHaltonLds];
     __shared__ MatRec lds_mat[kMatLds];
-    __shared__ float lds_sray[7][kBlock];   // each lane's shadow ray (origin, direction, tmax: helper jobs)
-    __shared__ uint32_t lds_sres[kBlock];   // helper result for the owner lane: 0 pending, 1 unoccluded, 2 occluded
+    __shared__ float lds_sray[6][kBlock];   // each lane's shadow ray (origin, direction)
     int* stack = &lds_stack[threadIdx.x];
-    const uint32_t n_top = stage_top<kTopNodes>(S, lds_top);
+    const uint32_t n_top = stage_top(S, lds_top);
     const ShadeTabs halton = load_tabs(S, lds_halton, lds_mat);   // ends with a block barrier
     const Uniforms& U = P.U;
     const ShardPrefix cnt = load_prefix(Q.W.counts + cslot(cur * kShards));
@@ -848,13 +838,7 @@ wf_finish_step(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int c
     const float4* qin = Q.W.q[cur];
     uint32_t* chunk_ctr = Q.W.counts + cslot(kCntChunkFinish);
     const uint32_t kChunk = (uint32_t)Q.fchunk;   // paths per grab
-    constexpr int kIdle = 0, kClosest = 1, kShadow = 2, kReady = 3, kHelp = 4;
-    const uint32_t lane = lane_id();
-    const uint32_t wave_base = threadIdx.x - lane;   // LDS index of this wave's lane 0
-    volatile uint32_t* sres = lds_sres;
-    unsigned long long posted = 0ull;   // wave-uniform: owners whose shadow job waits for a helper
-    bool pend = false;                  // owner: a helper traces this lane's shadow ray
-    uint32_t helps = 0;                 // helper: the owner lane
+    constexpr int kIdle = 0, kClosest = 1, kShadow = 2, kReady = 3;
     TraceCounters tc{0, 0, 0};
     bool overflow = false;
     uint32_t n_closest = 0, n_shadow = 0;
@@ -926,32 +910,14 @@ wf_finish_step(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int c
             }
             wnext += (uint32_t)__popcll(idle);
         }
-        if (posted != 0ull) {   // idle lanes take the posted shadow jobs (lowest owner first)
-            unsigned long long free_lanes = __ballot(mode == kIdle);
-            while (posted != 0ull && free_lanes != 0ull) {
-                const uint32_t owner = (uint32_t)__builtin_ctzll(posted), helper = (uint32_t)__builtin_ctzll(free_lanes);
-                if (lane == helper) {
-                    const uint32_t j = wave_base + owner;
-                    trav_start(T, mk3(lds_sray[0][j], lds_sray[1][j], lds_sray[2][j]),
-                               mk3(lds_sray[3][j], lds_sray[4][j], lds_sray[5][j]), lds_sray[6][j]);
-                    helps = owner;
-                    mode = kHelp;
-                }
-                posted &= posted - 1ull;
-                free_lanes &= free_lanes - 1ull;
-            }
-        }
         if (__ballot(mode != kIdle) == 0ull) break;   // idle everywhere => refill found nothing
         ++iters;
 
         // ---- one traversal step (closest hit or shadow any-hit)
-        if (mode == kClosest || mode == kShadow || mode == kHelp) {
-            const bool any = mode != kClosest;
+        if (mode == kClosest || mode == kShadow) {
+            const bool any = mode == kShadow;
             if (trav_step<COUNT>(S, T, any, stack, lds_top, n_top, tc, overflow)) {
-                if (mode == kHelp) {   // the owner's shadow query is done: post the result
-                    sres[wave_base + helps] = T.hit_any ? 2u : 1u;
-                    mode = kIdle;
-                } else if (any) {   // shadow ray done: unoccluded -> add its contribution (:741-743)
+                if (any) {   // shadow ray done: unoccluded -> add its contribution (:741-743)
                     if (!T.hit_any) p.accum = p.accum + contrib;
                     if (next) {
                         trav_start(T, rayO, rayD, INFINITY);
@@ -961,37 +927,24 @@ wf_finish_step(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int c
                     } else {
                         end_path();
                     }
-                } else if (T.best_id == 0xffffffffu && !pend) {   // miss -> path ends (:321-322)
+                } else if (T.best_id == 0xffffffffu) {   // miss -> path ends (:321-322)
                     end_path();
                 } else {
-                    mode = kReady;   // (a miss with a pending shadow result ends in the shading pass)
+                    mode = kReady;
                 }
             }
         }
 
         // ---- shade the waiting lanes together (:324-774)
-        // owners whose helper has answered apply the shadow contribution first (:741-743, the
-        // reference's order: before the next segment's emission)
-        if (pend && sres[threadIdx.x] != 0u) {
-            if (sres[threadIdx.x] == 1u) p.accum = p.accum + contrib;
-            pend = false;
-        }
-        const unsigned long long ready = __ballot(mode == kReady && !pend);
+        const unsigned long long ready = __ballot(mode == kReady);
         if (ready != 0ull &&
-            (__popcll(ready) >= Q.shade_min || __ballot(mode == kClosest || mode == kShadow || mode == kHelp) == 0ull)) {
-            // lanes that may hand their shadow query to a helper this pass: the queue is exhausted,
-            // so idle lanes stay idle; at most one job per idle lane not already promised
-            const bool drained = Q.shadow_help && exhausted && wnext >= wend;
-            const int spare = drained ? __popcll(__ballot(mode == kIdle)) - __popcll(posted) : 0;
-            bool fresh_shadow = false;   // this lane's shading just emitted a shadow ray
+            (__popcll(ready) >= Q.shade_min || __ballot(mode == kClosest || mode == kShadow) == 0ull)) {
             const uint64_t ts0 = Q.diag ? __builtin_amdgcn_s_memrealtime() : 0;
             if (Q.diag) {
                 ++n_pass;
                 n_shaded += (uint32_t)__popcll(ready);
             }
-            if (mode == kReady && !pend && T.best_id == 0xffffffffu) {   // a miss that waited for its shadow result
-                end_path();
-            } else if (mode == kReady && !pend) {
+            if (mode == kReady) {
                 Hit h;
                 h.t = T.best;
                 h.id = T.best_id;
@@ -1005,16 +958,15 @@ wf_finish_step(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int c
                 next = r.next;
                 if (r.shadow) {
                     contrib = r.contrib;
+                    trav_start(T, r.so, r.sd, r.stmax);
                     lds_sray[0][threadIdx.x] = r.so.x;
                     lds_sray[1][threadIdx.x] = r.so.y;
                     lds_sray[2][threadIdx.x] = r.so.z;
                     lds_sray[3][threadIdx.x] = r.sd.x;
                     lds_sray[4][threadIdx.x] = r.sd.y;
                     lds_sray[5][threadIdx.x] = r.sd.z;
-                    lds_sray[6][threadIdx.x] = r.stmax;
-                    n_shadow++;
                     mode = kShadow;
-                    fresh_shadow = true;
+                    n_shadow++;
                 } else if (r.next) {
                     trav_start(T, rayO, rayD, INFINITY);
                     mode = kClosest;
@@ -1024,36 +976,10 @@ wf_finish_step(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int c
                     end_path();
                 }
             }
-            // hand shadow queries that have a continuation to idle lanes (the first `spare` of them)
-            if (drained) {
-                const bool want = mode == kShadow && next;
-                const unsigned long long wm = __ballot(want);
-                const bool post = want && (int)mbcnt64(wm) < spare;
-                const unsigned long long pm = __ballot(post);
-                if (post) {
-                    sres[threadIdx.x] = 0u;
-                    pend = true;
-                    mode = kClosest;
-                    n_closest++;
-                    segs++;
-                    fresh_shadow = false;
-                    trav_start(T, rayO, rayD, INFINITY);
-                }
-                posted |= pm;
-            }
-            if (fresh_shadow) {
-                const uint32_t j = threadIdx.x;
-                trav_start(T, mk3(lds_sray[0][j], lds_sray[1][j], lds_sray[2][j]),
-                           mk3(lds_sray[3][j], lds_sray[4][j], lds_sray[5][j]), lds_sray[6][j]);
-            }
             // Every lane's ray setup is rebuilt from its ray (a pure function of it, so bit for bit
             // the one trav_start made): the ~19 registers of the traversing lanes' setups are then
             // dead while the shading code runs, which sets the kernel's register peak.
-            if (mode == kHelp) {
-                const uint32_t j = wave_base + helps;
-                T.R = ray_setup(mk3(lds_sray[0][j], lds_sray[1][j], lds_sray[2][j]),
-                                mk3(lds_sray[3][j], lds_sray[4][j], lds_sray[5][j]));
-            } else if (mode == kShadow) {
+            if (mode == kShadow) {
                 T.R = ray_setup(mk3(lds_sray[0][threadIdx.x], lds_sray[1][threadIdx.x], lds_sray[2][threadIdx.x]),
                                 mk3(lds_sray[3][threadIdx.x], lds_sray[4][threadIdx.x], lds_sray[5][threadIdx.x]));
             } else {
@@ -1513,7 +1439,6 @@ bool run_wavefront(const DevScene& S, const FrameParams& P, WavefrontBuffers& W,
     Q.shade_min = tu.shade_min;
     Q.fchunk = tu.fchunk;
     Q.ray_sort = tu.ray_sort;
-    Q.shadow_help = tu.shadow_help;
     // frames in flight: the finish tail takes part of the resident grid and leaves the rest to the
     // other frames' bulk rounds (C3g sweeps, DESIGN.md §3: two slots 40 %; four slots on a small
     // frame, a multi-GPU rank's share, 20 %; else 1 / in_flight); one frame at a time: all of it
