@@ -46,9 +46,9 @@ HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: 8.0 TB/s spec
 # Algorithmic bytes (DESIGN.md §6 'Roofline'): per traced ray its 48-B queue entry (extend: 32 B ray
 # in + 16 B hit out; connect: 48 B shadow entry in); per 8-wide node fetched from memory 80 B; per
 # triangle tested 48 B; per closest hit shaded inside the finish kernel 16 B triangle record +
-# 3 x 16 B normals + 48 B instance transform.  Node tests served from the LDS copy of the BVH's top
-# levels move no memory per visit: they are charged once per block (the staging read, B_NODE x
-# kTopNodes per block).
+# 3 x 16 B normals + 48 B instance transform.  Node tests served from an LDS copy of the BVH's top
+# levels (a build with RT_TOP_NODES > 0; the rt_stats *_lds counters) move no memory per visit:
+# they are charged once per block (the staging read, B_NODE x kTopNodes per block).
 B_RAY = 48
 B_NODE = 80  # compressed 8-wide node (Bvh8Node)
 B_TRI = 48
@@ -392,7 +392,7 @@ def roofline(a, cst, s0, s1, rays_local, closest_local, kms_local, ms_per_step, 
             launch_ms=trace_ms / trace_launches, rays_per_launch=rpl, nodes_per_ray=q_nodes,
             lds_nodes_per_ray=q_nodes_lds, tris_per_ray=q_tris,
             bytes_per_launch=rpl * (B_QRAY + (q_nodes - q_nodes_lds) * B_NODE + q_tris * B_TRI)
-            + blocks * TOP_NODES * B_NODE,
+            + (blocks * TOP_NODES * B_NODE if q_nodes_lds > 0 else 0),
             bytes_all_nodes=rpl * (B_QRAY + q_nodes * B_NODE + q_tris * B_TRI)))
     if s1.pipeline == 1 and finish_launches > 0:
         # wf_finish_step: its rays (48 B ray + hit) + nodes + triangles as above, + the shading
@@ -405,7 +405,7 @@ def roofline(a, cst, s0, s1, rays_local, closest_local, kms_local, ms_per_step, 
             launch_ms=float(stage_ms[5]) / finish_launches, rays_per_launch=f_rays, nodes_per_ray=f_nodes,
             lds_nodes_per_ray=f_nodes_lds, tris_per_ray=f_tris,
             bytes_per_launch=f_rays * (B_RAY + (f_nodes - f_nodes_lds) * B_NODE + f_tris * B_TRI) + f_closest * B_HIT
-            + blocks * TOP_NODES * B_NODE,
+            + (blocks * TOP_NODES * B_NODE if f_nodes_lds > 0 else 0),
             bytes_all_nodes=f_rays * (B_RAY + f_nodes * B_NODE + f_tris * B_TRI) + f_closest * B_HIT))
     if not kernels:
         # megakernel: the whole frame is one launch; every node comes from memory

@@ -396,43 +396,14 @@ std::vector<Range> subtree_ranges(const BvhResult& b2) {
 }
 }  // namespace
 
-Bvh8Result collapse_bvh8(const BvhResult& b2) {
-    Bvh8Result out;
-    out.pad = b2.pad;
-    std::vector<Job> queue;
-    out.nodes.emplace_back();
-    out.parent.push_back(-1);
-    queue.push_back({0, 0u, 0});
-    for (size_t qi = 0; qi < queue.size(); ++qi) {
-        Job job = queue[qi];
-        std::vector<WItem> items;
-        bvh2_children(b2, job.b2node, items);
-        while (items.size() < 8) {
-            int best = -1;
-            float ba = -1.0f;
-            for (size_t i = 0; i < items.size(); ++i)
-                if (!items[i].leaf && item_area(items[i]) > ba) { ba = item_area(items[i]); best = (int)i; }
-            if (best < 0) break;
-            std::vector<WItem> kids;
-            bvh2_children(b2, items[best].node, kids);
-            if (items.size() - 1 + kids.size() > 8) break;
-            items.erase(items.begin() + best);
-            items.insert(items.end(), kids.begin(), kids.end());
-        }
-        emit_bvh8_node(b2, job, items, queue, out);
-    }
-    out.node_box.resize(6 * out.nodes.size());
-    return out;
-}
-
 // SAH-optimal 8-wide collapse (after Ylitie, Karras, Laine, "Efficient Incoherent Ray Traversal
 // on GPUs Through Compressed Wide BVHs", HPG 2017, §4): dynamic programming over the BVH2 for
 // the cheapest way to represent every subtree with at most i (1..8) slots of its parent, a slot
 // being a leaf (<= 4 triangles, the meta field's limit) or an 8-wide child node:
 //   C(n, 1)  = min(A(n) * c_prim * tris(n)  [tris(n) <= 4],  A(n) * c_node + D(n, 8))
 //   C(n, i)  = min(C(n, i - 1), D(n, i)),   D(n, j) = min_k C(l, k) + C(r, j - k)
-// The greedy collapse (open the largest child until 8) leaves the bottom of the tree in nodes
-// with two used slots (C3g: 47 % of its nodes) whose box tests are mostly spent on empty slots.
+// (Round 1's greedy collapse, opening the largest child until 8, left 47 % of the C3g tree's
+// nodes with two used slots whose box tests were mostly spent on empty slots.)
 Bvh8Result collapse_bvh8_dp(const BvhResult& b2, float c_node, float c_prim) {
     // DP nodes: BVH2 internal nodes keep their index; leaf slots are appended
     struct DN { float area; uint32_t start, count; int kid[2]; bool leaf; WItem item; };

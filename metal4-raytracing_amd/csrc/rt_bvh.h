@@ -70,10 +70,6 @@ struct Bvh8Result {
     float pad = 0.0f;
 };
 
-// Collapse a BVH2 into the compressed 8-wide layout (greedy: repeatedly open the internal child
-// with the largest surface area until a node has 8 children).
-Bvh8Result collapse_bvh8(const BvhResult& b2);
-
 // SAH-optimal collapse by dynamic programming over the BVH2 (Ylitie et al. 2017): every node
 // slot is a leaf of <= 4 triangles or a child node, chosen to minimise
 // sum(A(node) * c_node) + sum(A(leaf) * c_prim * triangles).  Best on a BVH2 with 1-triangle leaves.

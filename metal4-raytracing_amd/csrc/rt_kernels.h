@@ -24,6 +24,7 @@ struct FrameParams {
     float4* accum_out;         // new accumulation (TextureIndexPreviousAccumulation, write)
     float* depth;
     float2* motion;            // read (previous frame) + write, in place
+    const float2* motion_prev; // wavefront: the previous frame's motion target (it writes a new one)
     float4* gbuffer;           // 4 planes or null
     uint4* prim_hit;           // wavefront: sample 0's last bounce-0 hit per pixel (wf_motion input)
     unsigned long long* counters;
@@ -103,7 +104,6 @@ struct WavefrontBuffers {
     float4* sq = nullptr;
     uint32_t* counts = nullptr;   // device counter slots (see cslot)
     uint32_t* h_counts = nullptr; // pinned host mirror
-    float2* motion_prev = nullptr;   // the previous frame's motion target (set per frame)
     uint2* px_extra = nullptr;    // per own pixel: (first extra path - base_paths, count)
     // per-bounce hit sort (wf_sort_*): the hits reordered by key as {o, d, hit} float4 triples,
     // per-(bin, block) counts, per-bin totals
@@ -152,6 +152,12 @@ struct WfTimeline {
     Span spans[kMaxEv];
     int n_ev = 0, n_spans = 0;
     bool pending = false;
+    // RT_GRAPH: the slot's frame captured as a HIP graph (events recorded as external event nodes,
+    // so the spans above keep timing it) and replayed while `key` (every launch argument and
+    // enqueue decision of the frame) is unchanged
+    hipGraphExec_t exec = nullptr;
+    std::vector<uint8_t> key;
+    bool graph_failed = false;   // capture was refused once: this slot stays eager
 };
 // Runs (host-driven: queue sizes read back every round; with RT_WF_LOG / RT_WF_HOST=1) or enqueues (device-driven, the default: `tl` receives the timeline, stats come
 // from wavefront_collect after the stream finished) one frame; false on a HIP error (*err).
@@ -186,8 +192,7 @@ struct LbvhInput {
     const uint4* tri_info;
     const float* inst;
     uint32_t n;
-    int ploc = 1;          // BVH2 topology: 1 = PLOC clustering, 0 = LBVH radix tree
-    int dp = 1;            // 8-wide collapse: 1 = SAH dynamic programming, 0 = greedy
+    int ploc = 1;          // BVH2 topology: 1 = PLOC clustering, 0 = LBVH radix tree (8-wide: SAH-DP collapse)
     float c_node = 1.0f;   // DP costs (as the host builder's)
     float c_prim = 0.5f;
 };
@@ -226,6 +231,7 @@ void launch_skin(const float4* rest_pos, const float4* rest_nrm, const ushort4* 
 // flatten also reduces max |world coordinate| into *maxabs_bits (float bits; zero it first)
 void launch_flatten(const uint4* tri_info, const uint32_t* slot_to_tri, const float4* pos, const float* inst,
                     float4* tris, uint32_t n, unsigned* maxabs_bits, hipStream_t s);
+void launch_permute_tris(const float4* tris, float4* tris_p, uint32_t n, hipStream_t s);
 // pad = max(pad_min, 4e-6 * max |coordinate|) as the builder pads (rt_bvh.cpp)
 void launch_refit8_level(Bvh8Node* nodes, float* node_box, const float4* tris, const uint32_t* level_nodes,
                          uint32_t count, float pad_min, const unsigned* maxabs_bits, hipStream_t s);

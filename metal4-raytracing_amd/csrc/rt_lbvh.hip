@@ -571,7 +571,7 @@ struct CollapseArgs {
     const int2* jobs_in;              // (BVH2 reference, 8-wide node)
     uint32_t n_jobs;
     int2* jobs_out;
-    const uint8_t* choice;            // DP choices (lbvh_dp_up_k), null: greedy collapse
+    const uint8_t* choice;            // DP choices (lbvh_dp_up_k)
     uint32_t* counters;               // [0] 8-wide nodes allocated, [1] triangle slots, [2] next jobs,
                                       // [4] error flag (a capacity guard tripped)
     uint32_t n;                       // triangles = capacity of nodes8, tri_order, the job queues
@@ -655,51 +655,33 @@ __global__ void __launch_bounds__(kThreads) lbvh_collapse_k(CollapseArgs A) {
     }
     Item items[8];
     int n_items = 0;
-    if (A.choice) {
-        // DP: the node's eight slots split between its children as chosen bottom-up; a subtree
-        // with budget j either splits again (choice k) or becomes one slot (leaf or node)
-        int2 st[16];
-        int sp = 0;
-        const int k8 = A.choice[10 * (size_t)job.x + 9];
-        st[sp++] = make_int2(A.child[2 * job.x + 1], 8 - k8);
-        st[sp++] = make_int2(A.child[2 * job.x], k8);
-        while (sp > 0) {
-            const int2 e = st[--sp];
-            const int r = e.x;
-            int b = e.y;
-            if (r >= 0 && (uint32_t)r + 1 < A.n) {
-                while (b >= 2 && A.choice[10 * (size_t)r + b] == 0) --b;
-                if (b >= 2 && sp + 2 <= 16) {
-                    const int k = A.choice[10 * (size_t)r + b];
-                    st[sp++] = make_int2(A.child[2 * r + 1], b - k);
-                    st[sp++] = make_int2(A.child[2 * r], k);
-                    continue;
-                }
+    // DP: the node's eight slots split between its children as chosen bottom-up; a subtree
+    // with budget j either splits again (choice k) or becomes one slot (leaf or node)
+    int2 st[16];
+    int sp = 0;
+    const int k8 = A.choice[10 * (size_t)job.x + 9];
+    st[sp++] = make_int2(A.child[2 * job.x + 1], 8 - k8);
+    st[sp++] = make_int2(A.child[2 * job.x], k8);
+    while (sp > 0) {
+        const int2 e = st[--sp];
+        const int r = e.x;
+        int b = e.y;
+        if (r >= 0 && (uint32_t)r + 1 < A.n) {
+            while (b >= 2 && A.choice[10 * (size_t)r + b] == 0) --b;
+            if (b >= 2 && sp + 2 <= 16) {
+                const int k = A.choice[10 * (size_t)r + b];
+                st[sp++] = make_int2(A.child[2 * r + 1], b - k);
+                st[sp++] = make_int2(A.child[2 * r], k);
+                continue;
             }
-            if (n_items >= 8) {   // guard: the budgets add up to 8
-                atomicOr(&A.counters[4], 32u);
-                return;
-            }
-            Item it = make_item(A, r, pad);
-            if (r >= 0) it.leaf = A.choice[10 * (size_t)r + 1] == 1 && it.count <= kLeafMax;
-            items[n_items++] = it;
         }
-    } else {
-        items[n_items++] = make_item(A, A.child[2 * job.x], pad);
-        items[n_items++] = make_item(A, A.child[2 * job.x + 1], pad);
-        while (n_items < 8) {   // open the inner child with the largest surface area
-            int best = -1;
-            float ba = -1.0f;
-            for (int i = 0; i < n_items; ++i)
-                if (!items[i].leaf && item_area(items[i]) > ba) {
-                    ba = item_area(items[i]);
-                    best = i;
-                }
-            if (best < 0) break;
-            const int r = items[best].ref;
-            items[best] = make_item(A, A.child[2 * r], pad);
-            items[n_items++] = make_item(A, A.child[2 * r + 1], pad);
+        if (n_items >= 8) {   // guard: the budgets add up to 8
+            atomicOr(&A.counters[4], 32u);
+            return;
         }
+        Item it = make_item(A, r, pad);
+        if (r >= 0) it.leaf = A.choice[10 * (size_t)r + 1] == 1 && it.count <= kLeafMax;
+        items[n_items++] = it;
     }
     float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
     for (int i = 0; i < n_items; ++i)
@@ -943,7 +925,7 @@ bool lbvh_build(const LbvhInput& in, const LbvhOutput& out, void* scratch, hipSt
         lbvh_boxes_up_k<<<blocks(n), kThreads, 0, s>>>(src, n, child, parent, leaf_parent, tri_box, node_box, flag);
     }
     LB_CHECK(hipGetLastError());
-    if (in.dp) {
+    {   // SAH-DP choices of every inner node, bottom-up
         LB_CHECK(hipMemsetAsync(flag, 0, 4 * (size_t)n, s));
         DpArgs D;
         D.keys = src;
@@ -976,7 +958,7 @@ bool lbvh_build(const LbvhInput& in, const LbvhOutput& out, void* scratch, hipSt
     A.nodes8 = out.nodes8;
     A.node8_box = out.node_box;
     A.tri_order = out.tri_order;
-    A.choice = in.dp ? choice : nullptr;
+    A.choice = choice;
     res->level_off.assign(1, 0u);
     uint32_t n_jobs = 1, total = 1;
     while (n_jobs > 0) {

@@ -340,13 +340,20 @@ __device__ __forceinline__ bool trav_step(const DevScene& S, Trav& T, bool any, 
         const bool two = T.t_mask != 0u;
         const int k1 = two ? lowest_bit(T.t_mask) : k0;
         if (two) T.t_mask &= T.t_mask - 1u;
-        const float4* tp0 = S.tris + 3 * (size_t)tri_slot(T.t_base, T.t_valid, k0);
-        const float4* tp1 = S.tris + 3 * (size_t)tri_slot(T.t_base, T.t_valid, k1);
+#if RT_TRI_PERM
+        const float4* tris = S.tris_p + 3 * (size_t)T.R.pre.kz * (uint32_t)S.num_tris;
+#define RT_ISECT(v0, v1, v2) intersect_triangle_p(T.R, v0, v1, v2, 0.0f, T.best, &t, &u, &v, &dt)
+#else
+        const float4* tris = S.tris;
+#define RT_ISECT(v0, v1, v2) intersect_triangle_vw(T.R.pre, T.R.o, v0, v1, v2, 0.0f, T.best, &t, &u, &v, &dt)
+#endif
+        const float4* tp0 = tris + 3 * (size_t)tri_slot(T.t_base, T.t_valid, k0);
+        const float4* tp1 = tris + 3 * (size_t)tri_slot(T.t_base, T.t_valid, k1);
         const float4 a0 = tp0[0], a1 = tp0[1], a2 = tp0[2];
         const float4 b0 = tp1[0], b1 = tp1[1], b2 = tp1[2];   // = a when the lane has one triangle
         if (COUNT) tc.tris += two ? 2u : 1u;
         float t, u, v, dt;
-        if (intersect_triangle_vw(T.R.pre, T.R.o, ld3(a0), ld3(a1), ld3(a2), 0.0f, T.best, &t, &u, &v, &dt)) {
+        if (RT_ISECT(ld3(a0), ld3(a1), ld3(a2))) {
             const uint32_t id = __float_as_uint(a0.w);
             if (any) {
                 T.hit_any = true;
@@ -359,7 +366,7 @@ __device__ __forceinline__ bool trav_step(const DevScene& S, Trav& T, bool any, 
                 T.bv = v;
             }
         }
-        if (two && !tdone && intersect_triangle_vw(T.R.pre, T.R.o, ld3(b0), ld3(b1), ld3(b2), 0.0f, T.best, &t, &u, &v, &dt)) {
+        if (two && !tdone && RT_ISECT(ld3(b0), ld3(b1), ld3(b2))) {
             const uint32_t id = __float_as_uint(b0.w);
             if (any) {
                 T.hit_any = true;
@@ -408,6 +415,7 @@ __device__ __forceinline__ bool trav_step(const DevScene& S, Trav& T, bool any, 
         test_node8_words(w, T.R, 0.0f, T.best, T.g_hits, T.t_mask, T.t_valid, T.g_base, T.t_base, T.g_flip);
     }
     return tdone || (T.t_mask == 0u && T.g_hits == 0u && T.sp == 0);
+#undef RT_ISECT
 }
 
 // Stages the first n_top BFS nodes of the 8-wide BVH in LDS (every thread of the block calls it;
@@ -1025,7 +1033,7 @@ __global__ void __launch_bounds__(kBlock) wf_extra(DevScene S, const FrameParams
         own_pixel(P, i, px, py);
         if (px < U.width && py < U.height) {
             pix = (uint32_t)py * (uint32_t)U.width + (uint32_t)px;
-            float2 mv2 = P.motion[pix], pm2 = Q.W.motion_prev[pix];
+            float2 mv2 = P.motion[pix], pm2 = P.motion_prev[pix];
             f2 mv, pm;
             mv.x = mv2.x;
             mv.y = mv2.y;
@@ -1105,7 +1113,7 @@ __global__ void __launch_bounds__(kBlock) wf_resolve(DevScene S, const FramePara
         }
         nsamp += (int)ex.y;
     }
-    float2 mv2 = P.motion[pix], pm2 = Q.W.motion_prev[pix];
+    float2 mv2 = P.motion[pix], pm2 = P.motion_prev[pix];
     f2 mv, pm;
     mv.x = mv2.x;
     mv.y = mv2.y;
@@ -1286,13 +1294,14 @@ namespace {
 struct Enqueue {
     WfTimeline& T;
     hipStream_t stream;
+    bool capture;   // recording into a HIP graph: events and cross-stream waits are external nodes
     int last = -1;
     bool mark(const char** err) {
         if (T.n_ev >= WfTimeline::kMaxEv) {
             *err = "wavefront timeline: too many events";
             return false;
         }
-        const hipError_t e = hipEventRecord(T.ev[T.n_ev], stream);
+        const hipError_t e = hipEventRecordWithFlags(T.ev[T.n_ev], stream, capture ? hipEventRecordExternal : 0u);
         if (e != hipSuccess) {
             *err = hipGetErrorString(e);
             return false;
@@ -1354,10 +1363,11 @@ static bool enqueue_pass(const DevScene& S, const FrameParams& P, const WfParams
 // Issues one frame on `stream`.  Launch arguments come from S, Q and the buffer pointers in P;
 // the per-frame values of P are read by the kernels from Q.Pd.
 static bool record_frame(const DevScene& S, const FrameParams& P, WfParams& Q, bool count, bool full, int maxExtra,
-                         bool with_extra, hipStream_t stream, hipEvent_t prev_done, WfTimeline& T, const char** err) {
+                         bool with_extra, hipStream_t stream, hipEvent_t prev_done, WfTimeline& T, bool capture,
+                         const char** err) {
     WavefrontBuffers& W = Q.W;
     T.n_ev = T.n_spans = 0;
-    Enqueue E{T, stream};
+    Enqueue E{T, stream, capture};
     if (!E.mark(err)) return false;
     WF_CHECK(hipMemsetAsync(W.counts, 0, kWfCountWords * sizeof(uint32_t), stream));
     const int rounds = rounds_for(Q.base_paths, Q.tail);
@@ -1369,7 +1379,7 @@ static bool record_frame(const DevScene& S, const FrameParams& P, WfParams& Q, b
     hipLaunchKernelGGL(wf_motion, dim3(grid_for(Q.own_pixels, 1u << 30)), dim3(kBlock), 0, stream, S, Q.Pd, Q);
     WF_CHECK(hipGetLastError());
     if (!E.span(4, err)) return false;
-    if (prev_done) WF_CHECK(hipStreamWaitEvent(stream, prev_done, 0));
+    if (prev_done) WF_CHECK(hipStreamWaitEvent(stream, prev_done, capture ? hipEventWaitExternal : 0u));
     if (with_extra) {
         // second pass over the motion-adaptive extra samples (:779-789), appended to queue 0
         const int rounds2 = rounds_for((uint64_t)Q.own_pixels * (uint64_t)maxExtra, Q.tail);
@@ -1391,13 +1401,63 @@ static bool record_frame(const DevScene& S, const FrameParams& P, WfParams& Q, b
     return true;
 }
 
+static bool graphs_on() {   // frames are captured into HIP graphs and replayed (RT_GRAPH=0: eager enqueue)
+    static const bool v = env_int("RT_GRAPH", 1) != 0;
+    return v;
+}
+
 static bool enqueue_wavefront(const DevScene& S, const FrameParams& P, WfParams& Q, bool count, bool full,
                               int maxExtra, bool extra_pass, hipStream_t stream, hipEvent_t prev_done, WfTimeline& T,
                               const char** err) {
     Q.dev_ctl = 1;
     Q.finish_q = 0;   // set by record_frame from the round count
     const bool with_extra = maxExtra > 0 && extra_pass;
-    if (!record_frame(S, P, Q, count, full, maxExtra, with_extra, stream, prev_done, T, err)) return false;
+    if (!graphs_on() || T.graph_failed) {
+        if (!record_frame(S, P, Q, count, full, maxExtra, with_extra, stream, prev_done, T, false, err)) return false;
+        T.pending = true;
+        return true;
+    }
+    // The frame's launches, memsets and copies only take S, Q (by value) and the slot's fixed
+    // buffers and events; everything that changes per frame is in the device FrameParams, uploaded
+    // before the launch.  So the graph is valid while these bytes are.
+    std::vector<uint8_t> key(sizeof(DevScene) + sizeof(WfParams) + 4 * sizeof(int) + sizeof(hipEvent_t));
+    {
+        WfParams Qk = Q;
+        Qk.W.param_slot = 0;   // the upload ring position is host bookkeeping
+        uint8_t* k = key.data();
+        std::memcpy(k, &S, sizeof S);
+        std::memcpy(k + sizeof S, &Qk, sizeof Qk);
+        const int flags[4] = {count ? 1 : 0, full ? 1 : 0, with_extra ? 1 : 0, maxExtra};
+        std::memcpy(k + sizeof S + sizeof Qk, flags, sizeof flags);
+        std::memcpy(k + sizeof S + sizeof Qk + sizeof flags, &prev_done, sizeof prev_done);
+    }
+    if (!T.exec || T.key != key) {
+        // the slot's previous frame has finished (its slot was harvested): its graph can go
+        if (T.exec) {
+            WF_CHECK(hipGraphExecDestroy(T.exec));
+            T.exec = nullptr;
+        }
+        const char* rerr = nullptr;
+        hipGraph_t g = nullptr;
+        const hipError_t be = hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal);
+        const bool ok = be == hipSuccess &&
+                        record_frame(S, P, Q, count, full, maxExtra, with_extra, stream, prev_done, T, true, &rerr);
+        const hipError_t ce = be == hipSuccess ? hipStreamEndCapture(stream, &g) : be;
+        hipError_t ie = hipErrorUnknown;
+        if (ok && ce == hipSuccess && g) ie = hipGraphInstantiateWithFlags(&T.exec, g, 0);
+        if (g) (void)hipGraphDestroy(g);
+        if (!ok || ce != hipSuccess || ie != hipSuccess) {
+            // capture refused (an API the runtime cannot capture): this slot renders eagerly
+            (void)hipGetLastError();
+            T.exec = nullptr;
+            T.graph_failed = true;
+            if (!record_frame(S, P, Q, count, full, maxExtra, with_extra, stream, prev_done, T, false, err)) return false;
+            T.pending = true;
+            return true;
+        }
+        T.key.swap(key);
+    }
+    WF_CHECK(hipGraphLaunch(T.exec, stream));
     T.pending = true;
     return true;
 }
@@ -1426,6 +1486,7 @@ bool run_wavefront(const DevScene& S, const FrameParams& P, WavefrontBuffers& W,
                    hipEvent_t prev_done, WfTimeline* tl, WfFrameStats* fs, const char** err) {
     const Tuning& tu = tuning();
     WfParams Q;
+    std::memset(&Q, 0, sizeof Q);   // no stray padding bytes (frame-graph key)
     Q.W = W;
     Q.spp = max(P.U.samplesPerPixel, 1);
     Q.own_pixels = (uint32_t)own_tiles * (uint32_t)P.tile_size * (uint32_t)P.tile_size;
