@@ -61,8 +61,8 @@ struct FrameSlot {
 // frame (skinning, refit), all frames in flight still overlap, and no more copies exist than
 // frames can read.
 struct Geo {
-    DevBuf pos, prev_pos, nrm, inst, prev_inst, tris, nodes, node_box, tri_bin, tris_p;
-    DevBuf* all[10] = {&pos, &prev_pos, &nrm, &inst, &prev_inst, &tris, &nodes, &node_box, &tri_bin, &tris_p};
+    DevBuf pos, prev_pos, nrm, inst, prev_inst, tris, nodes, node_box, tri_bin;
+    DevBuf* all[9] = {&pos, &prev_pos, &nrm, &inst, &prev_inst, &tris, &nodes, &node_box, &tri_bin};
     uint32_t num_nodes8 = 0;
 };
 constexpr int kMaxSlots = 8;
@@ -356,7 +356,7 @@ static rt_status begin_update(rt_ctx* c) {
         if (f.used && f.gen == w) HIPC(c, hipEventSynchronize(f.done));
     Geo& src = c->geo[c->gcur];
     Geo& dst = c->geo[w];
-    for (int i = 0; i < 10; ++i) {
+    for (int i = 0; i < 9; ++i) {
         if (rt_status st = dev_alloc(c, *dst.all[i], src.all[i]->bytes)) return st;
         if (src.all[i]->bytes)
             HIPC(c, hipMemcpyAsync(dst.all[i]->p, src.all[i]->p, src.all[i]->bytes, hipMemcpyDeviceToDevice, c->ustream));
@@ -463,7 +463,8 @@ rt_status rt_destroy(rt_ctx* c) {
             if (e) (void)hipEventDestroy(e);
         for (auto& e : f.wft.ev)
             if (e) (void)hipEventDestroy(e);
-        if (f.wft.exec) (void)hipGraphExecDestroy(f.wft.exec);
+        for (hipGraphExec_t x : f.wft.exec)
+            if (x) (void)hipGraphExecDestroy(x);
         for (auto& e : f.wf.param_ev)
             if (e) (void)hipEventDestroy(e);
         if (f.wf.h_params) (void)hipHostFree(f.wf.h_params);
@@ -716,9 +717,6 @@ rt_status rt_bvh_build(rt_ctx* c) {
     Geo& g = c->G();
     hipStream_t us = c->ustream;
     if ((st = dev_upload(c, g.tris, tris.data(), tris.size() * 16, us))) return st;
-    if ((st = dev_alloc(c, g.tris_p, tris.size() * 16 * 3))) return st;
-    launch_permute_tris((const float4*)g.tris.p, (float4*)g.tris_p.p, n, us);
-    HIPC(c, hipGetLastError());
     if ((st = dev_upload(c, g.nodes, c->bvh8.nodes.data(), nn * sizeof(Bvh8Node), us))) return st;
     if ((st = dev_upload(c, g.node_box, c->bvh8.node_box.data(), c->bvh8.node_box.size() * 4, us))) return st;
     if ((st = dev_upload(c, c->d_slot_to_tri, c->bvh8.tri_order.data(), (size_t)n * 4, us))) return st;
@@ -771,8 +769,6 @@ rt_status rt_bvh_build_device(rt_ctx* c) {
     HIPC(c, hipMemsetAsync(c->d_maxabs.p, 0, 4, us));
     launch_flatten((const uint4*)c->d_tri_info.p, (const uint32_t*)c->d_slot_to_tri.p, (const float4*)g.pos.p,
                    (const float*)g.inst.p, (float4*)g.tris.p, n, (unsigned*)c->d_maxabs.p, us);
-    if ((st = dev_alloc(c, g.tris_p, (size_t)n * 48 * 3))) return st;
-    launch_permute_tris((const float4*)g.tris.p, (float4*)g.tris_p.p, n, us);
     HIPC(c, hipGetLastError());
     HIPC(c, hipStreamSynchronize(us));
     if (res.num_nodes >= (1u << 23)) FAIL(c, RT_ERR_UNSUPPORTED, "BVH too large (2^23 nodes)");
@@ -797,7 +793,6 @@ rt_status rt_bvh_refit(rt_ctx* c) {
     HIPC(c, hipMemsetAsync(c->d_maxabs.p, 0, 4, c->ustream));
     launch_flatten((const uint4*)c->d_tri_info.p, (const uint32_t*)c->d_slot_to_tri.p, (const float4*)g.pos.p,
                    (const float*)g.inst.p, (float4*)g.tris.p, c->num_tris, (unsigned*)c->d_maxabs.p, c->ustream);
-    launch_permute_tris((const float4*)g.tris.p, (float4*)g.tris_p.p, c->num_tris, c->ustream);
     for (int d = (int)c->level_off.size() - 2; d >= 0; --d) {
         uint32_t off = c->level_off[d], cnt = c->level_off[d + 1] - off;
         launch_refit8_level((Bvh8Node*)g.nodes.p, (float*)g.node_box.p, (const float4*)g.tris.p,
@@ -1031,7 +1026,6 @@ rt_status rt_render_frame(rt_ctx* c, const Uniforms* U, const rt_tile_set* tiles
     DevScene S;
     std::memset(&S, 0, sizeof S);   // no stray padding bytes: the frame-graph key compares S byte for byte
     S.tris = (const float4*)geo.tris.p;
-    S.tris_p = (const float4*)geo.tris_p.p;
     S.nodes8 = (const Bvh8Node*)geo.nodes.p;
     S.tri_info = (const uint4*)c->d_tri_info.p;
     S.pos = (const float4*)geo.pos.p;

@@ -20,22 +20,16 @@ namespace rt {
 constexpr int kStackSize = 16;   // per-thread traversal stack entries (LDS): node groups of the 8-wide BVH
 constexpr int kBlock = 256;      // threads per block for the traversal kernels
 // First BFS nodes of the 8-wide BVH staged in LDS by the traversal kernels (RT_TOP_NODES at build
-// time; 0 = every node from global memory)
+// time).  0 (default): every node comes from global memory.  Staging 32 served half of the node
+// tests of an extend ray from LDS but the kernels ran 2 % slower (the LDS / global branch and its
+// register moves cost more VALU than the L1 / L2 hits it saved).
 #ifndef RT_TOP_NODES
-#define RT_TOP_NODES 32
+#define RT_TOP_NODES 0
 #endif
 constexpr int kTopNodes = RT_TOP_NODES;
 
-// Traversal kernels read triangles from three copies whose vertex components are pre-permuted for
-// the watertight test's axes (RT_TRI_PERM; copy k = dominant ray axis k), see tris_perm.
-#ifndef RT_TRI_PERM
-#define RT_TRI_PERM 1
-#endif
-
 struct DevScene {
     const float4* tris;
-    const float4* tris_p;      // 3 copies of tris: copy k (at 3 * k * num_tris) holds (v[kx], v[ky], v[k], w),
-                               // kx = (k + 1) % 3, ky = (k + 2) % 3 (launch_permute_tris)
     const Bvh8Node* nodes8;
     const uint4* tri_info;
     const float4* pos;
@@ -87,10 +81,6 @@ struct RaySetup {
     float ix, iy, iz;   // 1 / d (safe)
     float ox, oy, oz;   // o * (1 / d)
     uint32_t dneg;      // bit a = (d[a] < 0)
-    // the watertight test in the pre-permuted copy pre.kz of the triangles (tris_p): the origin's
-    // components in that order and the shear constants without the kx / ky swap of ray_precompute
-    f3 op;
-    float qx, qy;
 };
 
 __host__ __device__ __forceinline__ RaySetup ray_setup(f3 o, f3 d) {
@@ -115,39 +105,7 @@ __host__ __device__ __forceinline__ RaySetup ray_setup(f3 o, f3 d) {
     R.oy = o.y * R.iy;
     R.oz = o.z * R.iz;
     R.dneg = (d.x < 0.0f ? 1u : 0u) | (d.y < 0.0f ? 2u : 0u) | (d.z < 0.0f ? 4u : 0u);
-    const int kz = R.pre.kz, kx = kz == 2 ? 0 : kz + 1, ky = kx == 2 ? 0 : kx + 1;
-    const bool swapped = R.pre.kx != kx;   // ray_precompute swaps kx / ky when d[kz] < 0
-    R.op = mk3(comp(o, kx), comp(o, ky), comp(o, kz));
-    R.qx = swapped ? R.pre.Sy : R.pre.Sx;   // = d[kx] / d[kz], the same division
-    R.qy = swapped ? R.pre.Sx : R.pre.Sy;
     return R;
-}
-
-// The watertight test (intersect_triangle_vw, Woop et al. 2013) on pre-permuted vertices
-// a = (v0[kx], v0[ky], v0[kz]), ... of copy kz, without the kx / ky swap.  Swapping x and y negates
-// U, V, W, det and T exactly (IEEE subtraction is sign-symmetric), so t, V / det and W / det are
-// bit for bit those of intersect_triangle_vw; the sign and det tests are symmetric.
-__host__ __device__ __forceinline__ bool intersect_triangle_p(const RaySetup& R, f3 a, f3 b, f3 c, float tmin, float tmax,
-                                                              float* t_out, float* V_out, float* W_out, float* det_out) {
-    const f3 A = a - R.op, B = b - R.op, C = c - R.op;
-    const float Ax = A.x - R.qx * A.z, Ay = A.y - R.qy * A.z;
-    const float Bx = B.x - R.qx * B.z, By = B.y - R.qy * B.z;
-    const float Cx = C.x - R.qx * C.z, Cy = C.y - R.qy * C.z;
-    const float U = Cx * By - Cy * Bx;
-    const float V = Ax * Cy - Ay * Cx;
-    const float W = Bx * Ay - By * Ax;
-    if ((U < 0.0f || V < 0.0f || W < 0.0f) && (U > 0.0f || V > 0.0f || W > 0.0f)) return false;
-    const float det = (U + V) + W;
-    if (det == 0.0f) return false;
-    const float Az = R.pre.Sz * A.z, Bz = R.pre.Sz * B.z, Cz = R.pre.Sz * C.z;
-    const float T = (U * Az + V * Bz) + W * Cz;
-    const float t = T / det;
-    if (!(t >= tmin && t <= tmax)) return false;
-    *t_out = t;
-    *V_out = V;
-    *W_out = W;
-    *det_out = det;
-    return true;
 }
 
 __host__ __device__ __forceinline__ float byte_f(uint32_t w, int b) { return (float)((w >> (8 * b)) & 0xffu); }

@@ -152,10 +152,12 @@ struct WfTimeline {
     Span spans[kMaxEv];
     int n_ev = 0, n_spans = 0;
     bool pending = false;
-    // RT_GRAPH: the slot's frame captured as a HIP graph (events recorded as external event nodes,
-    // so the spans above keep timing it) and replayed while `key` (every launch argument and
-    // enqueue decision of the frame) is unchanged
-    hipGraphExec_t exec = nullptr;
+    // RT_GRAPH: the slot's frame captured as two HIP graphs (events recorded as external event
+    // nodes, so the spans above keep timing it) and replayed while `key` (every launch argument and
+    // enqueue decision of the frame) is unchanged: exec[0] up to the motion vectors, exec[1] the
+    // rest, with the wait for the previous frame enqueued between them (a plain stream wait, not a
+    // captured external-event wait node)
+    hipGraphExec_t exec[2] = {nullptr, nullptr};
     std::vector<uint8_t> key;
     bool graph_failed = false;   // capture was refused once: this slot stays eager
 };
@@ -231,7 +233,6 @@ void launch_skin(const float4* rest_pos, const float4* rest_nrm, const ushort4* 
 // flatten also reduces max |world coordinate| into *maxabs_bits (float bits; zero it first)
 void launch_flatten(const uint4* tri_info, const uint32_t* slot_to_tri, const float4* pos, const float* inst,
                     float4* tris, uint32_t n, unsigned* maxabs_bits, hipStream_t s);
-void launch_permute_tris(const float4* tris, float4* tris_p, uint32_t n, hipStream_t s);
 // pad = max(pad_min, 4e-6 * max |coordinate|) as the builder pads (rt_bvh.cpp)
 void launch_refit8_level(Bvh8Node* nodes, float* node_box, const float4* tris, const uint32_t* level_nodes,
                          uint32_t count, float pad_min, const unsigned* maxabs_bits, hipStream_t s);

@@ -110,22 +110,6 @@ __global__ void flatten_k(const uint4* __restrict__ tri_info, const uint32_t* __
     if (threadIdx.x == 0 && maxabs_bits)
         atomicMax(maxabs_bits, __float_as_uint(fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]))));
 }
-// The three pre-permuted copies of the world-space triangles the traversal kernels read
-// (DevScene::tris_p): copy k holds (v[kx], v[ky], v[k], w) with kx = (k + 1) % 3, ky = (k + 2) % 3.
-__global__ void permute_tris_k(const float4* __restrict__ tris, float4* __restrict__ tris_p, uint32_t n) {
-    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;   // one vertex record
-    if (i >= 3 * (size_t)n) return;
-    const float4 v = tris[i];
-    tris_p[i] = make_float4(v.y, v.z, v.x, v.w);                       // k = 0: (y, z, x)
-    tris_p[3 * (size_t)n + i] = make_float4(v.z, v.x, v.y, v.w);       // k = 1: (z, x, y)
-    tris_p[6 * (size_t)n + i] = v;                                     // k = 2: (x, y, z)
-}
-void launch_permute_tris(const float4* tris, float4* tris_p, uint32_t n, hipStream_t s) {
-    if (!n) return;
-    const size_t m = 3 * (size_t)n;
-    hipLaunchKernelGGL(permute_tris_k, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, s, tris, tris_p, n);
-}
-
 void launch_flatten(const uint4* tri_info, const uint32_t* slot_to_tri, const float4* pos, const float* inst,
                     float4* tris, uint32_t n, unsigned* maxabs_bits, hipStream_t s) {
     if (!n) return;

@@ -340,15 +340,9 @@ __device__ __forceinline__ bool trav_step(const DevScene& S, Trav& T, bool any, 
         const bool two = T.t_mask != 0u;
         const int k1 = two ? lowest_bit(T.t_mask) : k0;
         if (two) T.t_mask &= T.t_mask - 1u;
-#if RT_TRI_PERM
-        const float4* tris = S.tris_p + 3 * (size_t)T.R.pre.kz * (uint32_t)S.num_tris;
-#define RT_ISECT(v0, v1, v2) intersect_triangle_p(T.R, v0, v1, v2, 0.0f, T.best, &t, &u, &v, &dt)
-#else
-        const float4* tris = S.tris;
 #define RT_ISECT(v0, v1, v2) intersect_triangle_vw(T.R.pre, T.R.o, v0, v1, v2, 0.0f, T.best, &t, &u, &v, &dt)
-#endif
-        const float4* tp0 = tris + 3 * (size_t)tri_slot(T.t_base, T.t_valid, k0);
-        const float4* tp1 = tris + 3 * (size_t)tri_slot(T.t_base, T.t_valid, k1);
+        const float4* tp0 = S.tris + 3 * (size_t)tri_slot(T.t_base, T.t_valid, k0);
+        const float4* tp1 = S.tris + 3 * (size_t)tri_slot(T.t_base, T.t_valid, k1);
         const float4 a0 = tp0[0], a1 = tp0[1], a2 = tp0[2];
         const float4 b0 = tp1[0], b1 = tp1[1], b2 = tp1[2];   // = a when the lane has one triangle
         if (COUNT) tc.tris += two ? 2u : 1u;
@@ -428,7 +422,40 @@ __device__ __forceinline__ uint32_t stage_top(const DevScene& S, uint4* lds_top)
     return n_top;
 }
 
+// ---- base paths ----------------------------------------------------------------------------------------
+// Path pid of the base pass (own pixel pid / spp, sample pid % spp): its pixel, sample, Halton index
+// (:263-270) and primary ray (:270-292).  False for a path of a tile pixel outside the image.
+__device__ __forceinline__ bool base_path(const FrameParams& P, const ShadeTabs& halton, int spp, uint32_t pid,
+                                          uint32_t& pix, int& s, uint32_t& hidx, f3& o, f3& d) {
+    const Uniforms& U = P.U;
+    s = (int)(pid % (uint32_t)spp);
+    int px, py;
+    own_pixel(P, pid / (uint32_t)spp, px, py);
+    if (px >= U.width || py >= U.height) return false;
+    pix = (uint32_t)py * (uint32_t)U.width + (uint32_t)px;
+    const int maxExtra = (U.enableMotionAdaptiveSampling != 0) ? max(U.motionSamplingMaxExtraSamples, 0) : 0;
+    const int frameOffset = (int)U.frameIndex * (spp + maxExtra) + s;
+    hidx = (uint32_t)(int)(P.random[pix] + (unsigned)frameOffset);
+    primary_ray(U, halton, px, py, (int)hidx, o, d);
+    return true;
+}
+// Per-pixel defaults, written by the pixel's sample-0 path (:252-261).
+__device__ __forceinline__ void init_pixel(const FrameParams& P, uint32_t pix) {
+    P.depth[pix] = 1.0e8f;
+    P.motion[pix] = make_float2(0.0f, 0.0f);
+    P.prim_hit[pix] = make_uint4(0xffffffffu, 0u, 0u, 0u);
+    if (P.gbuffer) {
+        const size_t plane = (size_t)P.U.width * P.U.height;
+        const float4 z = make_float4(0, 0, 0, 0);
+        P.gbuffer[pix] = z;
+        P.gbuffer[plane + pix] = z;
+        P.gbuffer[2 * plane + pix] = z;
+        P.gbuffer[3 * plane + pix] = z;
+    }
+}
 // ---- generate -------------------------------------------------------------------------------------
+// (A first round fused with generate -- extend making the primary rays at refill, shade starting
+// the path state -- was measured slower)
 __global__ void __launch_bounds__(kBlock) wf_generate(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q) {
     const FrameParams& P = *Pp;   // per-frame parameters in device memory
     __shared__ HaltonDim lds_halton[kHaltonLds];
@@ -436,8 +463,6 @@ __global__ void __launch_bounds__(kBlock) wf_generate(DevScene S, const FramePar
     const ShadeTabs halton = load_tabs(S, lds_halton, nullptr);   // no shading: Halton only
     const Uniforms& U = P.U;
     const int spp = Q.spp;
-    const int maxExtra = (U.enableMotionAdaptiveSampling != 0) ? max(U.motionSamplingMaxExtraSamples, 0) : 0;
-    const int stride = spp + maxExtra;
     const int shard = blockIdx.x & (kShards - 1);
     float4* qout = Q.W.q[0] + 2 * (size_t)shard * Q.seg_cap;
     uint32_t n_paths = 0;
@@ -445,35 +470,13 @@ __global__ void __launch_bounds__(kBlock) wf_generate(DevScene S, const FramePar
     if (Q.dev_ctl && blockIdx.x == 0 && threadIdx.x == 0) Q.W.counts[cslot(kCntFinishQ)] = (uint32_t)Q.finish_q;
     for (uint32_t base = blockIdx.x * kBlock; base < total; base += gridDim.x * kBlock) {
         uint32_t pid = base + threadIdx.x;
-        bool valid = pid < total;
-        int px = 0, py = 0, s = 0;
-        uint32_t pix = 0;
-        if (valid) {
-            s = (int)(pid % (uint32_t)spp);
-            own_pixel(P, pid / (uint32_t)spp, px, py);
-            valid = px < U.width && py < U.height;
-            pix = (uint32_t)py * (uint32_t)U.width + (uint32_t)px;
-        }
+        int s = 0;
+        uint32_t pix = 0, hidx = 0;
         f3 o = mk3(0, 0, 0), d = mk3(0, 0, 0);
+        const bool valid = pid < total && base_path(P, halton, spp, pid, pix, s, hidx, o, d);
         if (valid) {
-            uint32_t offset = P.random[pix];
-            int frameOffset = (int)U.frameIndex * stride + s;
-            int hidx = (int)(offset + (unsigned)frameOffset);
-            init_path(Q, pid, pix, s, (uint32_t)hidx);
-            primary_ray(U, halton, px, py, hidx, o, d);
-            if (s == 0) {  // per-pixel defaults (:252-261)
-                P.depth[pix] = 1.0e8f;
-                P.motion[pix] = make_float2(0.0f, 0.0f);
-                P.prim_hit[pix] = make_uint4(0xffffffffu, 0u, 0u, 0u);
-                if (P.gbuffer) {
-                    size_t plane = (size_t)U.width * U.height;
-                    float4 z = make_float4(0, 0, 0, 0);
-                    P.gbuffer[pix] = z;
-                    P.gbuffer[plane + pix] = z;
-                    P.gbuffer[2 * plane + pix] = z;
-                    P.gbuffer[3 * plane + pix] = z;
-                }
-            }
+            init_path(Q, pid, pix, s, hidx);
+            if (s == 0) init_pixel(P, pix);
             n_paths++;
         }
         bool live = valid && U.maxBounces > 0;
@@ -824,7 +827,8 @@ wf_trace(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int cur) {
 // continues with its shadow ray, its next ray, or the next path of the queue.  A wave therefore
 // costs the sum of its own lanes' steps, not the sum over segments of its slowest lane's query:
 // the glass paths left at the tail (up to ~23 segments) do not wait for their wave's worst ray
-// every segment.
+// every segment.  Four waves per SIMD: the shading code's register peak (112 VGPRs, no scratch);
+// five were measured no faster.
 template <bool COUNT, bool FULL>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 4)))
 wf_finish_step(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int cur) {
@@ -1360,14 +1364,15 @@ static bool enqueue_pass(const DevScene& S, const FrameParams& P, const WfParams
     return E.span(5, err);
 }
 
-// Issues one frame on `stream`.  Launch arguments come from S, Q and the buffer pointers in P;
-// the per-frame values of P are read by the kernels from Q.Pd.
-static bool record_frame(const DevScene& S, const FrameParams& P, WfParams& Q, bool count, bool full, int maxExtra,
-                         bool with_extra, hipStream_t stream, hipEvent_t prev_done, WfTimeline& T, bool capture,
-                         const char** err) {
+// One frame on `stream` in two parts: record_base = the base pass and the motion vectors,
+// record_rest = the extra-sample pass and the resolve, which read the previous frame's outputs
+// (the caller enqueues the wait for it in between).  Launch arguments come from S, Q and the
+// buffer pointers in P; the per-frame values of P are read by the kernels from Q.Pd.
+static bool record_base(const DevScene& S, const FrameParams& P, WfParams& Q, bool count, bool full,
+                        hipStream_t stream, WfTimeline& T, bool capture, const char** err) {
     WavefrontBuffers& W = Q.W;
-    T.n_ev = T.n_spans = 0;
     Enqueue E{T, stream, capture};
+    T.n_ev = T.n_spans = 0;
     if (!E.mark(err)) return false;
     WF_CHECK(hipMemsetAsync(W.counts, 0, kWfCountWords * sizeof(uint32_t), stream));
     const int rounds = rounds_for(Q.base_paths, Q.tail);
@@ -1378,8 +1383,14 @@ static bool record_frame(const DevScene& S, const FrameParams& P, WfParams& Q, b
     if (!enqueue_pass(S, P, Q, rounds, count, full, E, err)) return false;
     hipLaunchKernelGGL(wf_motion, dim3(grid_for(Q.own_pixels, 1u << 30)), dim3(kBlock), 0, stream, S, Q.Pd, Q);
     WF_CHECK(hipGetLastError());
-    if (!E.span(4, err)) return false;
-    if (prev_done) WF_CHECK(hipStreamWaitEvent(stream, prev_done, capture ? hipEventWaitExternal : 0u));
+    return E.span(4, err);
+}
+
+static bool record_rest(const DevScene& S, const FrameParams& P, WfParams& Q, bool count, bool full, int maxExtra,
+                        bool with_extra, hipStream_t stream, WfTimeline& T, bool capture, const char** err) {
+    WavefrontBuffers& W = Q.W;
+    Enqueue E{T, stream, capture};
+    E.last = T.n_ev - 1;   // spans continue from record_base's last event
     if (with_extra) {
         // second pass over the motion-adaptive extra samples (:779-789), appended to queue 0
         const int rounds2 = rounds_for((uint64_t)Q.own_pixels * (uint64_t)maxExtra, Q.tail);
@@ -1401,26 +1412,62 @@ static bool record_frame(const DevScene& S, const FrameParams& P, WfParams& Q, b
     return true;
 }
 
+static bool record_part(const DevScene& S, const FrameParams& P, WfParams& Q, bool count, bool full, int maxExtra,
+                        bool with_extra, int part, hipStream_t stream, WfTimeline& T, bool capture, const char** err) {
+    return part == 0 ? record_base(S, P, Q, count, full, stream, T, capture, err)
+                     : record_rest(S, P, Q, count, full, maxExtra, with_extra, stream, T, capture, err);
+}
+
 static bool graphs_on() {   // frames are captured into HIP graphs and replayed (RT_GRAPH=0: eager enqueue)
     static const bool v = env_int("RT_GRAPH", 1) != 0;
     return v;
+}
+
+// part `part` of the frame (record_part), eagerly or captured into T.exec[part] and launched
+static bool capture_part(const DevScene& S, const FrameParams& P, WfParams& Q, bool count, bool full, int maxExtra,
+                         bool with_extra, int part, hipStream_t stream, WfTimeline& T, bool rebuild, const char** err) {
+    if (rebuild) {
+        const char* rerr = nullptr;
+        hipGraph_t g = nullptr;
+        const int n_ev = T.n_ev, n_spans = T.n_spans;
+        const hipError_t be = hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal);
+        const bool ok = be == hipSuccess &&
+                        record_part(S, P, Q, count, full, maxExtra, with_extra, part, stream, T, true, &rerr);
+        const hipError_t ce = be == hipSuccess ? hipStreamEndCapture(stream, &g) : be;
+        hipError_t ie = hipErrorUnknown;
+        if (ok && ce == hipSuccess && g) ie = hipGraphInstantiateWithFlags(&T.exec[part], g, 0);
+        if (g) (void)hipGraphDestroy(g);
+        if (!ok || ce != hipSuccess || ie != hipSuccess) {
+            // capture refused (an API the runtime cannot capture): this slot renders eagerly from now on
+            (void)hipGetLastError();
+            T.exec[part] = nullptr;
+            T.graph_failed = true;
+            T.n_ev = n_ev;
+            T.n_spans = n_spans;
+            return record_part(S, P, Q, count, full, maxExtra, with_extra, part, stream, T, false, err);
+        }
+    }
+    WF_CHECK(hipGraphLaunch(T.exec[part], stream));
+    return true;
 }
 
 static bool enqueue_wavefront(const DevScene& S, const FrameParams& P, WfParams& Q, bool count, bool full,
                               int maxExtra, bool extra_pass, hipStream_t stream, hipEvent_t prev_done, WfTimeline& T,
                               const char** err) {
     Q.dev_ctl = 1;
-    Q.finish_q = 0;   // set by record_frame from the round count
+    Q.finish_q = 0;   // set by record_base from the round count
     const bool with_extra = maxExtra > 0 && extra_pass;
     if (!graphs_on() || T.graph_failed) {
-        if (!record_frame(S, P, Q, count, full, maxExtra, with_extra, stream, prev_done, T, false, err)) return false;
+        if (!record_base(S, P, Q, count, full, stream, T, false, err)) return false;
+        if (prev_done) WF_CHECK(hipStreamWaitEvent(stream, prev_done, 0));
+        if (!record_rest(S, P, Q, count, full, maxExtra, with_extra, stream, T, false, err)) return false;
         T.pending = true;
         return true;
     }
     // The frame's launches, memsets and copies only take S, Q (by value) and the slot's fixed
     // buffers and events; everything that changes per frame is in the device FrameParams, uploaded
     // before the launch.  So the graph is valid while these bytes are.
-    std::vector<uint8_t> key(sizeof(DevScene) + sizeof(WfParams) + 4 * sizeof(int) + sizeof(hipEvent_t));
+    std::vector<uint8_t> key(sizeof(DevScene) + sizeof(WfParams) + 4 * sizeof(int));
     {
         WfParams Qk = Q;
         Qk.W.param_slot = 0;   // the upload ring position is host bookkeeping
@@ -1429,35 +1476,25 @@ static bool enqueue_wavefront(const DevScene& S, const FrameParams& P, WfParams&
         std::memcpy(k + sizeof S, &Qk, sizeof Qk);
         const int flags[4] = {count ? 1 : 0, full ? 1 : 0, with_extra ? 1 : 0, maxExtra};
         std::memcpy(k + sizeof S + sizeof Qk, flags, sizeof flags);
-        std::memcpy(k + sizeof S + sizeof Qk + sizeof flags, &prev_done, sizeof prev_done);
     }
-    if (!T.exec || T.key != key) {
-        // the slot's previous frame has finished (its slot was harvested): its graph can go
-        if (T.exec) {
-            WF_CHECK(hipGraphExecDestroy(T.exec));
-            T.exec = nullptr;
-        }
-        const char* rerr = nullptr;
-        hipGraph_t g = nullptr;
-        const hipError_t be = hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal);
-        const bool ok = be == hipSuccess &&
-                        record_frame(S, P, Q, count, full, maxExtra, with_extra, stream, prev_done, T, true, &rerr);
-        const hipError_t ce = be == hipSuccess ? hipStreamEndCapture(stream, &g) : be;
-        hipError_t ie = hipErrorUnknown;
-        if (ok && ce == hipSuccess && g) ie = hipGraphInstantiateWithFlags(&T.exec, g, 0);
-        if (g) (void)hipGraphDestroy(g);
-        if (!ok || ce != hipSuccess || ie != hipSuccess) {
-            // capture refused (an API the runtime cannot capture): this slot renders eagerly
-            (void)hipGetLastError();
-            T.exec = nullptr;
-            T.graph_failed = true;
-            if (!record_frame(S, P, Q, count, full, maxExtra, with_extra, stream, prev_done, T, false, err)) return false;
-            T.pending = true;
-            return true;
-        }
-        T.key.swap(key);
+    const bool rebuild = !T.exec[0] || !T.exec[1] || T.key != key;
+    if (rebuild) {
+        // the slot's previous frame has finished (its slot was harvested): its graphs can go
+        for (hipGraphExec_t& x : T.exec)
+            if (x) {
+                WF_CHECK(hipGraphExecDestroy(x));
+                x = nullptr;
+            }
+        T.key.clear();
     }
-    WF_CHECK(hipGraphLaunch(T.exec, stream));
+    if (!capture_part(S, P, Q, count, full, maxExtra, with_extra, 0, stream, T, rebuild, err)) return false;
+    if (prev_done) WF_CHECK(hipStreamWaitEvent(stream, prev_done, 0));
+    if (T.graph_failed) {   // part 0 could not be captured
+        if (!record_rest(S, P, Q, count, full, maxExtra, with_extra, stream, T, false, err)) return false;
+    } else if (!capture_part(S, P, Q, count, full, maxExtra, with_extra, 1, stream, T, rebuild, err)) {
+        return false;
+    }
+    if (rebuild && !T.graph_failed) T.key.swap(key);
     T.pending = true;
     return true;
 }
