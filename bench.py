@@ -65,6 +65,32 @@ TRAFFIC_JSON_REL = "profiles/" + (_TRAFFIC[-1] if _TRAFFIC else "r01_traffic.jso
 TRAFFIC_JSON = os.path.join(ROOT, TRAFFIC_JSON_REL)
 
 
+def _newest_profile(pattern):
+    d = os.path.join(ROOT, "profiles")
+    names = sorted(f for f in os.listdir(d) if re.fullmatch(pattern, f)) if os.path.isdir(d) else []
+    return os.path.join(d, names[-1]) if names else None
+
+
+def sorted_l2_hit():
+    """L2 hit rates of the opt-in sorted runs (north star: the sorted-ray shade kernel's L2 hit rate):
+    the hit-sorted shade (--sort-bins 2048, tools/gpurun_sorted_l2.sh) and the wf_shade ray grouping
+    modes (RT_RAY_SORT, tools/gpurun_raysort.sh), from the newest profiles/rNN_l2_*.json."""
+    out = {}
+    p = _newest_profile(r"r\d+_l2_sorted\.json")
+    if p:
+        hits = json.load(open(p)).get("l2_hit") or {}
+        out["hit_sorted"] = {k: v for k, v in hits.items() if re.search(r"wf_(trace|shade|finish)", k)}
+        out["hit_sorted_source"] = "profiles/" + os.path.basename(p)
+    p = _newest_profile(r"r\d+_l2_raysort\.json")
+    if p:
+        rs = json.load(open(p))
+        for m in ("ray_sort_0", "ray_sort_1", "ray_sort_2"):
+            if m in rs:
+                out[m] = {k: v for k, v in rs[m].items() if re.search(r"wf_(trace|shade)", k)}
+        out["ray_sort_source"] = "profiles/" + os.path.basename(p)
+    return out or None
+
+
 def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
@@ -448,6 +474,7 @@ def roofline(a, cst, s0, s1, rays_local, closest_local, kms_local, ms_per_step, 
         # measured HBM bytes of one launch (PMC) over the launch time: what actually crossed HBM
         "hbm_GBs": round(traffic / (dom["launch_ms"] * 1e-3) / 1e9, 1) if traffic else None,
         "l2_hit": l2_hit,
+        "l2_hit_sorted": sorted_l2_hit(),
         "job_achieved": round(job_achieved, 1), "job_frac": round(job_achieved / HBM_PEAK_GBS, 4),
         "job_bytes_per_frame": int(job_bytes),
         "kernel": dom["kernel"], "launch_ms": round(dom["launch_ms"], 4), "bytes_per_launch": int(dom["bytes_per_launch"]),

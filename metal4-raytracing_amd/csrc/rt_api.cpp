@@ -28,6 +28,7 @@ struct DevBuf {
 
 struct MeshInfo {
     uint32_t vbase = 0, vcount = 0, joint_count = 0;
+    uint32_t tbase = 0, tcount = 0;   // the mesh's triangles (original ids are assigned mesh by mesh)
     bool skinned = false;
 };
 
@@ -61,8 +62,8 @@ struct FrameSlot {
 // frame (skinning, refit), all frames in flight still overlap, and no more copies exist than
 // frames can read.
 struct Geo {
-    DevBuf pos, prev_pos, nrm, inst, prev_inst, tris, nodes, node_box, tri_bin;
-    DevBuf* all[9] = {&pos, &prev_pos, &nrm, &inst, &prev_inst, &tris, &nodes, &node_box, &tri_bin};
+    DevBuf pos, prev_pos, nrm, inst, prev_inst, tris, nodes, node_box, tri_bin, tri_nrm;
+    DevBuf* all[10] = {&pos, &prev_pos, &nrm, &inst, &prev_inst, &tris, &nodes, &node_box, &tri_bin, &tri_nrm};
     uint32_t num_nodes8 = 0;
 };
 constexpr int kMaxSlots = 8;
@@ -356,7 +357,7 @@ static rt_status begin_update(rt_ctx* c) {
         if (f.used && f.gen == w) HIPC(c, hipEventSynchronize(f.done));
     Geo& src = c->geo[c->gcur];
     Geo& dst = c->geo[w];
-    for (int i = 0; i < 9; ++i) {
+    for (int i = 0; i < 10; ++i) {
         if (rt_status st = dev_alloc(c, *dst.all[i], src.all[i]->bytes)) return st;
         if (src.all[i]->bytes)
             HIPC(c, hipMemcpyAsync(dst.all[i]->p, src.all[i]->p, src.all[i]->bytes, hipMemcpyDeviceToDevice, c->ustream));
@@ -601,6 +602,7 @@ rt_status rt_scene_upload(rt_ctx* c, const rt_scene_desc* sd) {
         MeshInfo& mi = c->meshes[m];
         mi.vbase = vbase;
         mi.vcount = md.vertex_count;
+        mi.tbase = tri;
         mi.joint_count = md.joint_count;
         mi.skinned = md.joint_count > 0;
         any_skin |= mi.skinned;
@@ -629,6 +631,7 @@ rt_status rt_scene_upload(rt_ctx* c, const rt_scene_desc* sd) {
             }
         }
         vbase += md.vertex_count;
+        mi.tcount = tri - mi.tbase;
     }
     c->h_lights.assign(sd->lights, sd->lights + sd->light_count);
     rt_status st;
@@ -637,6 +640,10 @@ rt_status rt_scene_upload(rt_ctx* c, const rt_scene_desc* sd) {
     if ((st = dev_upload(c, c->G().prev_pos, c->h_pos.data(), nv * 16))) return st;  // previousPositions = positions (SubMesh.swift:60)
     if ((st = dev_upload(c, c->G().nrm, c->h_nrm.data(), nv * 16))) return st;
     if ((st = dev_upload(c, c->d_tri_info, c->h_tri_info.data(), nt * 16))) return st;
+    if ((st = dev_alloc(c, c->G().tri_nrm, nt * 64))) return st;
+    launch_tri_nrm((const uint4*)c->d_tri_info.p, (const float4*)c->G().nrm.p, (float4*)c->G().tri_nrm.p, 0,
+                   (uint32_t)nt, c->stream);
+    HIPC(c, hipGetLastError());
     if ((st = dev_upload(c, c->G().inst, c->h_inst.data(), c->h_inst.size() * 4))) return st;
     if ((st = dev_upload(c, c->G().prev_inst, c->h_inst.data(), c->h_inst.size() * 4))) return st;
     if ((st = dev_upload(c, c->d_mat, c->h_mat.data(), c->h_mat.size() * sizeof(Material)))) return st;
@@ -835,6 +842,8 @@ rt_status rt_skin(rt_ctx* c, uint32_t mesh_index, const float* joints, uint32_t 
     launch_skin((const float4*)c->d_rest_pos.p + mi.vbase, (const float4*)c->d_rest_nrm.p + mi.vbase,
                 (const ushort4*)c->d_jidx.p + mi.vbase, (const float4*)c->d_jw.p + mi.vbase, (const float*)c->d_joints.p,
                 (float4*)g.pos.p + mi.vbase, (float4*)g.nrm.p + mi.vbase, mi.vcount, c->ustream);
+    launch_tri_nrm((const uint4*)c->d_tri_info.p, (const float4*)g.nrm.p, (float4*)g.tri_nrm.p, mi.tbase, mi.tcount,
+                   c->ustream);
     HIPC(c, hipGetLastError());
     HIPC(c, hipStreamSynchronize(c->ustream));  // joint upload buffer is reused next call
     c->world_dirty = true;
@@ -1031,6 +1040,7 @@ rt_status rt_render_frame(rt_ctx* c, const Uniforms* U, const rt_tile_set* tiles
     S.pos = (const float4*)geo.pos.p;
     S.prev_pos = (const float4*)geo.prev_pos.p;
     S.nrm = (const float4*)geo.nrm.p;
+    S.tri_nrm = (const float4*)geo.tri_nrm.p;
     S.inst = (const float*)geo.inst.p;
     S.prev_inst = (const float*)geo.prev_inst.p;
     S.materials = (const Material*)c->d_mat.p;

@@ -35,6 +35,11 @@ struct DevScene {
     const float4* pos;
     const float4* prev_pos;
     const float4* nrm;
+    // per original triangle, 64 B: the object-space normals of vertices (i1, i2, i0) -- the order
+    // :391 weights them by (u, v, w) -- with tri_info's w word in the first record's w, and the
+    // triangle's tri_info (as bits) in the fourth: one cache line per shaded hit instead of the
+    // tri_info record and three vertex-normal gathers behind it (build_tri_nrm, rt_util.hip)
+    const float4* tri_nrm;
     const float* inst;
     const float* prev_inst;
     const Material* materials;

@@ -175,9 +175,11 @@ __device__ __forceinline__ void shade_step(const DevScene& S, const Uniforms& U,
     r.shadow = false;
     r.primary = false;
     r.gbuf = false;
-    uint4 ti = S.tri_info[h.id];
-    int instanceIndex = (int)(ti.w >> 8);
-    int geometryIndex = (int)(ti.w & 0xffu);
+    const float4* const rec = S.tri_nrm + 4 * (size_t)h.id;   // (n1 | ti.w, n2, n0, ti)
+    const float4 rn1 = rec[0], rn2 = rec[1], rn0 = rec[2];
+    const uint32_t tw = __float_as_uint(rn1.w);
+    int instanceIndex = (int)(tw >> 8);
+    int geometryIndex = (int)(tw & 0xffu);
     const float* M = S.inst + 12 * instanceIndex;                                       // :329-333
     f3 P_ = rayO + rayD * h.t;                                                          // :336
     const MatRec mat = halton.material(instanceIndex * S.max_submeshes + geometryIndex); // :337-339 (LDS)
@@ -190,7 +192,7 @@ __device__ __forceinline__ void shade_step(const DevScene& S, const Uniforms& U,
         r.primary = true;   // deferred: the caller records the hit for wf_motion
     }
 
-    f3 objN = (bu * ld3(S.nrm[ti.y]) + bv * ld3(S.nrm[ti.z])) + bw * ld3(S.nrm[ti.x]); // :391
+    f3 objN = (bu * ld3(rn1) + bv * ld3(rn2)) + bw * ld3(rn0);                     // :391
     f3 Ng = normalize(xform(M, objN, 0.0f));                                          // :392-393
     if (length(objN) < 1e-10f) Ng = -rayD;                                            // :395-397
 
@@ -204,7 +206,9 @@ __device__ __forceinline__ void shade_step(const DevScene& S, const Uniforms& U,
     int tnormal = -1;
     f2 tc = f2{0.0f, 0.0f};
     float4 bsample = make_float4(1.0f, 1.0f, 1.0f, 1.0f);
+    uint4 ti = make_uint4(0u, 0u, 0u, tw);
     if (FULL && S.textured) {
+        ti = __builtin_bit_cast(uint4, rec[3]);   // vertex indices for the UVs and the tangent basis
         const int slot = instanceIndex * S.max_submeshes + geometryIndex;
         const int4 t0 = S.mat_tex[2 * slot], t1 = S.mat_tex[2 * slot + 1];
         tflags = (unsigned)t0.x;

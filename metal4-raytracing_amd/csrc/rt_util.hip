@@ -83,6 +83,25 @@ void launch_skin(const float4* rest_pos, const float4* rest_nrm, const ushort4* 
                        out_nrm, n);
 }
 
+// ---- per-triangle shading records (DevScene::tri_nrm) ------------------------------------------
+__global__ void tri_nrm_k(const uint4* __restrict__ tri_info, const float4* __restrict__ nrm, float4* __restrict__ out,
+                          uint32_t t0, uint32_t n) {
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n) return;
+    const uint32_t t = t0 + k;
+    const uint4 ti = tri_info[t];
+    const float4 n0 = nrm[ti.x], n1 = nrm[ti.y], n2 = nrm[ti.z];
+    float4* r = out + 4 * (size_t)t;
+    r[0] = make_float4(n1.x, n1.y, n1.z, __uint_as_float(ti.w));
+    r[1] = make_float4(n2.x, n2.y, n2.z, 0.0f);
+    r[2] = make_float4(n0.x, n0.y, n0.z, 0.0f);
+    r[3] = __builtin_bit_cast(float4, ti);
+}
+void launch_tri_nrm(const uint4* tri_info, const float4* nrm, float4* tri_nrm, uint32_t t0, uint32_t n, hipStream_t s) {
+    if (!n) return;
+    hipLaunchKernelGGL(tri_nrm_k, dim3((n + 255) / 256), dim3(256), 0, s, tri_info, nrm, tri_nrm, t0, n);
+}
+
 // ---- flatten world-space triangles into BVH slot order ----------------------------------------
 __global__ void flatten_k(const uint4* __restrict__ tri_info, const uint32_t* __restrict__ slot_to_tri,
                           const float4* __restrict__ pos, const float* __restrict__ inst, float4* __restrict__ tris,

@@ -48,7 +48,8 @@ struct Tuning {
     int finish_frac;   // RT_FINISH_FRAC: percent of the resident grid the finish launch takes (0 = by frames in flight)
     bool log;          // RT_WF_LOG=1: per-round queue sizes, stage times and finish diagnostics on stderr
     bool host_ctl;     // RT_WF_HOST=1: host-driven rounds (queue sizes read back every round)
-    int ray_sort;      // RT_RAY_SORT: 1 = group the rays wf_shade appends by direction octant
+    int ray_sort;      // RT_RAY_SORT: group the rays wf_shade appends by 1 = direction octant, 2 = direction
+                       // octant + origin octant around the camera (ray_key)
 };
 static const Tuning& tuning() {
     static const Tuning t = [] {
@@ -139,7 +140,7 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
 // allocated with ONE returning atomic as in block_alloc, but laid out grouped by key (key-major;
 // the order inside a key is that of the LDS atomics, which does not matter: each path's arithmetic
 // does not depend on which lane or position traces it).  Every thread of the block calls it.
-constexpr int kRayKeys = 8;   // direction octants
+constexpr int kRayKeys = 64;   // direction octant x origin octant (ray_key)
 struct KeyAlloc {
     uint32_t cnt[kRayKeys];
 };
@@ -165,6 +166,13 @@ __device__ __forceinline__ uint32_t block_alloc_keyed(bool pred, uint32_t key, u
 }
 __device__ __forceinline__ uint32_t octant(f3 d) {
     return (d.x < 0.0f ? 1u : 0u) | (d.y < 0.0f ? 2u : 0u) | (d.z < 0.0f ? 4u : 0u);
+}
+// Q.ray_sort key of a ray: its direction octant (1), or that plus the octant of its origin around
+// the camera position (2: the first level of a Morton key of the origin, view-centred)
+__device__ __forceinline__ uint32_t ray_key(int mode, f3 o, f3 d, const rt_float3& cam) {
+    const uint32_t k = octant(d);
+    if (mode < 2) return k;
+    return k | (octant(mk3(o.x - cam.x, o.y - cam.y, o.z - cam.z)) << 3);
 }
 
 __device__ __forceinline__ uint32_t compact1by1(uint32_t x) {
@@ -212,7 +220,7 @@ struct WfParams {
     int shade_min;         // wf_finish_step: shade once this many lanes wait (or none traverses)
     int fchunk;            // wf_finish_step: paths per chunk grab
     int finish_frac;       // percent of the resident grid the finish launch takes
-    int ray_sort;          // wf_shade: extend / shadow rays grouped by direction octant inside each block's allocation
+    int ray_sort;          // wf_shade: extend / shadow rays grouped by ray_key inside each block's allocation
     int dev_ctl;           // device-side control (enqueue_wavefront): kernels read their queue sizes from
                            // the counters and skip once the live count fell below `tail`
     int finish_q;          // dev_ctl: the finish queue when every enqueued bulk round ran (written by generate)
@@ -582,14 +590,16 @@ __global__ void __launch_bounds__(kBlock) wf_shade(DevScene S, const FrameParams
                 if (r.next) Q.W.p_meta[pid] = make_uint4(meta.x, meta.y, pack_state(p.bounce, p.tpass, p.step), meta.w);
             }
         }
-        uint32_t ns = Q.ray_sort ? block_alloc_keyed(r.shadow, octant(r.sd), &Q.W.counts[cslot(kCntShadowQ + shard)], ka)
+        uint32_t ns = Q.ray_sort ? block_alloc_keyed(r.shadow, ray_key(Q.ray_sort, r.so, r.sd, U.camera.position),
+                                                     &Q.W.counts[cslot(kCntShadowQ + shard)], ka)
                                  : block_alloc(r.shadow, &Q.W.counts[cslot(kCntShadowQ + shard)], ba_sh);
         if (r.shadow) {
             sqout[3 * (size_t)ns] = make_float4(r.so.x, r.so.y, r.so.z, __uint_as_float(pid));
             sqout[3 * (size_t)ns + 1] = make_float4(r.sd.x, r.sd.y, r.sd.z, r.stmax);
             sqout[3 * (size_t)ns + 2] = make_float4(r.contrib.x, r.contrib.y, r.contrib.z, 0.0f);
         }
-        uint32_t nr = Q.ray_sort ? block_alloc_keyed(r.next, octant(rayD), &Q.W.counts[cslot(next * kShards + shard)], ka)
+        uint32_t nr = Q.ray_sort ? block_alloc_keyed(r.next, ray_key(Q.ray_sort, rayO, rayD, U.camera.position),
+                                                     &Q.W.counts[cslot(next * kShards + shard)], ka)
                                  : block_alloc(r.next, &Q.W.counts[cslot(next * kShards + shard)], ba_ray);
         if (r.next) {
             qout[2 * (size_t)nr] = make_float4(rayO.x, rayO.y, rayO.z, __uint_as_float(pid));

@@ -1,0 +1,28 @@
+"""Runtime variants selected by environment switches (read once per process, so each runs in a
+child process): the extend / shadow ray grouping in wf_shade (RT_RAY_SORT=1 direction octant,
+=2 direction + origin octant) and eager enqueue without frame graphs (RT_GRAPH=0), against the
+committed golden fixtures (bit-identical radiance, depth and ray counts).  The bulk pipelines run
+wf_shade every bounce (the small fixture frames would otherwise go straight to the finish kernel)."""
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CASES = "c3g_small_b8,c1_ema_f3,lights_mix4_b3,c2_small_b4"
+PIPES = "wavefront,wavefront-bulk,wavefront-mixed"
+
+
+@pytest.mark.parametrize("env", [{"RT_RAY_SORT": "1"}, {"RT_RAY_SORT": "2"}, {"RT_GRAPH": "0"}],
+                         ids=["raysort1", "raysort2", "nograph"])
+def test_env_variant_matches_golden(env):
+    e = dict(os.environ)
+    e.update(env)
+    r = subprocess.run([sys.executable, "-u", os.path.join(HERE, "env_variant_child.py"), CASES, PIPES], env=e,
+                       capture_output=True, text=True, timeout=150)
+    print(r.stdout[-3000:])
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    assert r.stdout.count(" ok ") == len(CASES.split(",")) * len(PIPES.split(","))
