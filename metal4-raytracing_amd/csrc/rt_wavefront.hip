@@ -50,6 +50,7 @@ struct Tuning {
     bool host_ctl;     // RT_WF_HOST=1: host-driven rounds (queue sizes read back every round)
     int ray_sort;      // RT_RAY_SORT: group the rays wf_shade appends by 1 = direction octant, 2 = direction
                        // octant + origin octant around the camera (ray_key)
+    unsigned shade_blocks;   // RT_SHADE_BLOCKS: wf_shade grid (grid-stride loop), a multiple of 8
 };
 static const Tuning& tuning() {
     static const Tuning t = [] {
@@ -63,6 +64,7 @@ static const Tuning& tuning() {
         v.log = env_int("RT_WF_LOG", 0) != 0;
         v.host_ctl = env_int("RT_WF_HOST", 0) != 0;
         v.ray_sort = env_int("RT_RAY_SORT", 0);
+        v.shade_blocks = (unsigned)std::max(8, env_int("RT_SHADE_BLOCKS", 8192)) / 8u * 8u;
         return v;
     }();
     return t;
@@ -97,6 +99,36 @@ __device__ __forceinline__ uint32_t block_alloc(bool pred, uint32_t* counter, Bl
     uint32_t r = sh.w[wave] + prefix;
     __syncthreads();
     return r;
+}
+
+// Two block-aggregated allocations at once (wf_shade's shadow-ray and extend-ray appends): one
+// pass of barriers, and the two returning atomics issued by one instruction (one round trip).
+struct BlockAlloc2 {
+    uint32_t w[2][kBlock / 64];
+};
+__device__ __forceinline__ void block_alloc2(bool pa, uint32_t* ca, bool pb, uint32_t* cb, BlockAlloc2& sh,
+                                             uint32_t& ra, uint32_t& rb) {
+    const int wave = threadIdx.x >> 6;
+    const unsigned long long ma = __ballot(pa), mb = __ballot(pb);
+    if (lane_id() == 0) {
+        sh.w[0][wave] = (uint32_t)__popcll(ma);
+        sh.w[1][wave] = (uint32_t)__popcll(mb);
+    }
+    __syncthreads();
+    if (threadIdx.x < 2) {
+        uint32_t* w = sh.w[threadIdx.x];
+        const uint32_t c0 = w[0], c1 = w[1], c2 = w[2], c3 = w[3];
+        const uint32_t tot = c0 + c1 + c2 + c3;
+        const uint32_t b = tot ? atomicAdd(threadIdx.x == 0 ? ca : cb, tot) : 0u;
+        w[0] = b;
+        w[1] = b + c0;
+        w[2] = b + c0 + c1;
+        w[3] = b + c0 + c1 + c2;
+    }
+    __syncthreads();
+    ra = sh.w[0][wave] + mbcnt64(ma);
+    rb = sh.w[1][wave] + mbcnt64(mb);
+    __syncthreads();
 }
 
 // Block-aggregated allocation of v slots per thread (wave scan + LDS prefix, one atomic per block).
@@ -508,7 +540,7 @@ __global__ void __launch_bounds__(kBlock) wf_shade(DevScene S, const FrameParams
     const FrameParams& P = *Pp;   // per-frame parameters in device memory
     __shared__ HaltonDim lds_halton[kHaltonLds];
     __shared__ MatRec lds_mat[kMatLds];
-    __shared__ BlockAlloc ba_ray, ba_sh;
+    __shared__ BlockAlloc2 ba2;
     __shared__ KeyAlloc ka;
     if (tail_mode(Q)) return;
     const ShadeTabs halton = load_tabs(S, lds_halton, lds_mat);
@@ -590,17 +622,21 @@ __global__ void __launch_bounds__(kBlock) wf_shade(DevScene S, const FrameParams
                 if (r.next) Q.W.p_meta[pid] = make_uint4(meta.x, meta.y, pack_state(p.bounce, p.tpass, p.step), meta.w);
             }
         }
-        uint32_t ns = Q.ray_sort ? block_alloc_keyed(r.shadow, ray_key(Q.ray_sort, r.so, r.sd, U.camera.position),
-                                                     &Q.W.counts[cslot(kCntShadowQ + shard)], ka)
-                                 : block_alloc(r.shadow, &Q.W.counts[cslot(kCntShadowQ + shard)], ba_sh);
+        uint32_t ns, nr;
+        if (Q.ray_sort) {
+            ns = block_alloc_keyed(r.shadow, ray_key(Q.ray_sort, r.so, r.sd, U.camera.position),
+                                   &Q.W.counts[cslot(kCntShadowQ + shard)], ka);
+            nr = block_alloc_keyed(r.next, ray_key(Q.ray_sort, rayO, rayD, U.camera.position),
+                                   &Q.W.counts[cslot(next * kShards + shard)], ka);
+        } else {
+            block_alloc2(r.shadow, &Q.W.counts[cslot(kCntShadowQ + shard)], r.next,
+                         &Q.W.counts[cslot(next * kShards + shard)], ba2, ns, nr);
+        }
         if (r.shadow) {
             sqout[3 * (size_t)ns] = make_float4(r.so.x, r.so.y, r.so.z, __uint_as_float(pid));
             sqout[3 * (size_t)ns + 1] = make_float4(r.sd.x, r.sd.y, r.sd.z, r.stmax);
             sqout[3 * (size_t)ns + 2] = make_float4(r.contrib.x, r.contrib.y, r.contrib.z, 0.0f);
         }
-        uint32_t nr = Q.ray_sort ? block_alloc_keyed(r.next, ray_key(Q.ray_sort, rayO, rayD, U.camera.position),
-                                                     &Q.W.counts[cslot(next * kShards + shard)], ka)
-                                 : block_alloc(r.next, &Q.W.counts[cslot(next * kShards + shard)], ba_ray);
         if (r.next) {
             qout[2 * (size_t)nr] = make_float4(rayO.x, rayO.y, rayO.z, __uint_as_float(pid));
             qout[2 * (size_t)nr + 1] = make_float4(rayD.x, rayD.y, rayD.z, 0.0f);
@@ -1236,7 +1272,7 @@ static bool iterate(const DevScene& S, const FrameParams& P, WfParams& Q, int& c
         }
         int next = 1 - cur;
         WF_CHECK(hipEventRecord(W.ev[0], stream));
-        unsigned g = grid_for(n, 8192);
+        unsigned g = grid_for(n, tuning().shade_blocks);
         unsigned gt = grid_for(n, trace_grid_cap());
         if (count) hipLaunchKernelGGL((wf_trace<false, true>), dim3(gt), dim3(kBlock), 0, stream, S, Q.Pd, Q, cur);
         else hipLaunchKernelGGL((wf_trace<false, false>), dim3(gt), dim3(kBlock), 0, stream, S, Q.Pd, Q, cur);
@@ -1343,7 +1379,7 @@ static int rounds_for(uint64_t paths, uint32_t tail) {
 static bool enqueue_pass(const DevScene& S, const FrameParams& P, const WfParams& Q, int rounds, bool count, bool full,
                          Enqueue& E, const char** err) {
     hipStream_t stream = E.stream;
-    const unsigned gt = trace_grid_cap(), g = 8192;
+    const unsigned gt = trace_grid_cap(), g = tuning().shade_blocks;
     for (int k = 0; k < rounds; ++k) {
         const int cur = k & 1;
         if (count) hipLaunchKernelGGL((wf_trace<false, true>), dim3(gt), dim3(kBlock), 0, stream, S, Q.Pd, Q, cur);
