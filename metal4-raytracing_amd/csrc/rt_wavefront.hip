@@ -59,7 +59,7 @@ static const Tuning& tuning() {
         v.refill_min = env_int("RT_REFILL_MIN", 8);
         v.chunk = std::max(1, env_int("RT_CHUNK", 64));
         v.fchunk = std::max(1, env_int("RT_FCHUNK", 32));
-        v.shade_min = env_int("RT_SHADE_MIN", 16);
+        v.shade_min = env_int("RT_SHADE_MIN", 24);
         v.finish_frac = std::min(env_int("RT_FINISH_FRAC", 0), 100);
         v.log = env_int("RT_WF_LOG", 0) != 0;
         v.host_ctl = env_int("RT_WF_HOST", 0) != 0;
