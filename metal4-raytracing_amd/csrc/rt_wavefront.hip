@@ -873,7 +873,7 @@ wf_trace(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int cur) {
 // continues with its shadow ray, its next ray, or the next path of the queue.  A wave therefore
 // costs the sum of its own lanes' steps, not the sum over segments of its slowest lane's query:
 // the glass paths left at the tail (up to ~23 segments) do not wait for their wave's worst ray
-// every segment.  Four waves per SIMD: the shading code's register peak (112 VGPRs, no scratch);
+// every segment.  Four waves per SIMD: the shading code's register peak (119 VGPRs, no scratch);
 // five were measured no faster.
 template <bool COUNT, bool FULL>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 4)))
