@@ -740,7 +740,7 @@ __global__ void __launch_bounds__(kSortThreads) wf_sort_scatter(DevScene S, WfPa
 }
 
 // ---- persistent traversal with per-lane refill (extend: ANY = false, connect: ANY = true) -----------
-// The grid is the resident capacity.  Each XCD (blockIdx % 8) owns one eighth of the queue and hands
+// The grid is the resident capacity.  Each XCD (blockIdx % 8) owns queue shard k (what its own shade blocks appended) and hands
 // it out in chunks of Q.chunk rays, one atomic per chunk.  Every iteration advances each lane of a
 // wave by one traversal step (trav_step); a lane whose query ended takes the next ray of the
 // wave's chunk once at least Q.refill_min lanes are idle.  A wave therefore runs ~(steps of its
@@ -795,10 +795,18 @@ wf_trace(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int cur) {
         Q.W.counts[cslot((ANY ? kCntChunkExtend : kCntChunkConnect) + threadIdx.x)] = 0;
     const float4* qin = ANY ? Q.W.sq : Q.W.q[cur];
     const int qstride = ANY ? 3 : 2;
-    // chunks of this XCD's eighth of the queue, grabbed with one atomic per chunk
+    // chunks of this XCD's part of the queue, grabbed with one atomic per chunk
     const uint32_t xcd = blockIdx.x & 7u;
     uint32_t* const chunk_ctr = Q.W.counts + cslot((ANY ? kCntChunkConnect : kCntChunkExtend) + (int)xcd);
-    const uint32_t xbeg = (uint32_t)(((uint64_t)n * xcd) / 8), xend = (uint32_t)(((uint64_t)n * (xcd + 1)) / 8);
+    // XCD k traverses queue shard k, the segment its own shade blocks (blockIdx % 8 == k) appended:
+    // entry = k * seg_cap + g, no per-lane search of the shard prefix
+    uint32_t xend = 0;
+    #pragma unroll
+    for (int j = 0; j < kShards; ++j)
+        if ((uint32_t)j == xcd) xend = cnt.end[j] - (j ? cnt.end[j - 1] : 0u);
+    // (round 3; before, XCD k took the k-th eighth of the dense queue and every refilling lane
+    // searched the prefix for its entry: 7.49 -> 7.56 Grays/s)
+    const uint32_t xbeg = 0, ebase = xcd * Q.seg_cap;
     uint32_t wnext = 0, wend = 0;
     bool exhausted = false;
 
@@ -830,7 +838,7 @@ wf_trace(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int cur) {
             if (!active) {
                 uint32_t g = wnext + mbcnt64(idle);
                 if (g < wend) {
-                    e = entry_of(cnt, g, Q.seg_cap);
+                    e = ebase + g;
                     float4 o4 = qin[(size_t)qstride * e], d4 = qin[(size_t)qstride * e + 1];
                     trav_start(T, ld3(o4), ld3(d4), ANY ? d4.w : INFINITY);
                     active = true;
