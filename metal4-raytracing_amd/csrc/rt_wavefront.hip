@@ -555,14 +555,19 @@ __global__ void __launch_bounds__(kBlock) wf_shade(DevScene S, const FrameParams
     f2 zero2;
     zero2.x = 0.0f;
     zero2.y = 0.0f;
-    uint32_t beg = blockIdx.x * kBlock, end = n, stride = gridDim.x * kBlock;
-    if (SORTED) n = __builtin_amdgcn_readfirstlane(Q.W.counts[cslot(kCntSorted)]);
-    end = n;
-    if (SORTED) {   // grid is a multiple of 8 (grid_for)
-        beg = (uint32_t)(((uint64_t)n * (uint32_t)shard) / kShards);
+    // the blocks of XCD k (blockIdx % 8, the grid is a multiple of 8: grid_for) take queue shard k,
+    // which XCD k's extend launch traced (unsorted), or the k-th eighth of the sorted array
+    uint32_t beg = (blockIdx.x >> 3) * kBlock, end = 0, ebase = 0;
+    const uint32_t stride = (gridDim.x >> 3) * kBlock;
+    if (SORTED) {
+        n = __builtin_amdgcn_readfirstlane(Q.W.counts[cslot(kCntSorted)]);
+        beg += (uint32_t)(((uint64_t)n * (uint32_t)shard) / kShards);
         end = (uint32_t)(((uint64_t)n * (uint32_t)(shard + 1)) / kShards);
-        beg += (blockIdx.x >> 3) * kBlock;
-        stride = (gridDim.x >> 3) * kBlock;
+    } else {
+        #pragma unroll
+        for (int j = 0; j < kShards; ++j)
+            if (j == shard) end = cnt.end[j] - (j ? cnt.end[j - 1] : 0u);
+        ebase = (uint32_t)shard * Q.seg_cap;
     }
     for (uint32_t base = beg; base < end; base += stride) {
         uint32_t g = base + threadIdx.x;
@@ -578,7 +583,7 @@ __global__ void __launch_bounds__(kBlock) wf_shade(DevScene S, const FrameParams
                 d = Q.W.sorted[3 * (size_t)g + 1];
                 hv = Q.W.sorted[3 * (size_t)g + 2];
             } else {
-                uint32_t e = entry_of(cnt, g, Q.seg_cap);
+                const uint32_t e = ebase + g;
                 o = qin[2 * (size_t)e];
                 d = qin[2 * (size_t)e + 1];
                 hv = Q.W.hits[e];
