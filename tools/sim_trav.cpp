@@ -1,0 +1,319 @@
+// sim_trav.cpp — host-side SIMD-efficiency model of the wf_trace traversal schedule (tool, not product).
+//
+// Builds the C3g scene's 8-wide BVH with the product's host builder, makes extend rays (primary
+// rays of a pixel grid, then one diffuse bounce from their hits), and replays the per-lane
+// traversal of trav_step (rt_wavefront.hip) wave by wave (64 lanes, per-lane refill from a ray
+// stream).  A wave iteration costs the VALU issues of every code block that at least one lane
+// executes (block costs from the gfx950 ISA of wf_trace<false,false>); the model reports
+// issues per ray and iterations per ray for several schedules, to rank them before a GPU A/B.
+//
+//   hipcc --offload-arch=gfx950 -O2 -std=c++17 -ffp-contract=off -Iinclude tools/sim_trav.cpp \
+//     -Lmetal4-raytracing_amd -lrt_hip -Wl,-rpath,$PWD/metal4-raytracing_amd -o /tmp/sim_trav
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <cmath>
+#include <vector>
+#include <random>
+#include <algorithm>
+#include "../metal4-raytracing_amd/csrc/rt_device.h"
+#include "../include/rt_scene.h"
+#include "../include/rt_api.h"
+
+using namespace rt;
+static f3 ldf3(const rt_float3& v) { return mk3(v.x, v.y, v.z); }
+
+// VALU issues per block (ISA of wf_trace<false,false>, round 3)
+static double C_HEAD = 20, C_TRI1 = 95, C_TRI2 = 92, C_NODE = 194, C_STACK = 25, C_REFILL = 110;
+
+struct Lane {
+    bool active = false;
+    RaySetup R;
+    float best;
+    uint32_t best_id, g_base, g_hits, t_base, t_mask, t_valid;
+    bool g_flip;
+    int sp;
+    uint32_t stack[64];
+    // postponed triangle group (policy P)
+    uint32_t p_base = 0, p_mask = 0, p_valid = 0;
+    int ray = -1;
+    int steps = 0;
+};
+
+struct Ray { f3 o, d; };
+
+struct Policy {
+    const char* name;
+    int refill_min = 8;
+    int tris_per_step = 2;
+    int postpone_thr = 0;   // > 0: the triangle block runs only when >= thr lanes want it (or a lane is blocked)
+};
+
+struct Scene8 {
+    std::vector<Bvh8Node> nodes;
+    std::vector<float4> tris;   // 3 per slot
+};
+
+static void start(Lane& L, const Ray& r) {
+    L.R = ray_setup(r.o, r.d);
+    L.best = INFINITY;
+    L.best_id = 0xffffffffu;
+    L.g_base = 0;
+    L.g_hits = 1;
+    L.g_flip = false;
+    L.t_mask = 0;
+    L.p_mask = 0;
+    L.sp = 0;
+    L.active = true;
+    L.steps = 0;
+}
+
+static bool tri_test(const Scene8& S, Lane& L, uint32_t slot) {
+    const float4* tp = &S.tris[3 * (size_t)slot];
+    float t, u, v, dt;
+    if (intersect_triangle_vw(L.R.pre, L.R.o, ld3(tp[0]), ld3(tp[1]), ld3(tp[2]), 0.0f, L.best, &t, &u, &v, &dt)) {
+        const uint32_t id = __builtin_bit_cast(uint32_t, tp[0].w);
+        if (t < L.best || id < L.best_id) {
+            L.best = t;
+            L.best_id = id;
+        }
+    }
+    return false;
+}
+
+static bool node_work(const Lane& L) { return L.g_hits != 0u || L.sp > 0; }
+
+static void node_step(const Scene8& S, Lane& L) {
+    if (!L.g_hits) {
+        --L.sp;
+        const uint32_t ent = L.stack[L.sp];
+        L.g_base = ent >> 9;
+        L.g_flip = (ent >> 8) & 1u;
+        L.g_hits = ent & 0xffu;
+    }
+    const int r = L.g_flip ? highest_bit(L.g_hits) : lowest_bit(L.g_hits);
+    L.g_hits &= ~(1u << r);
+    if (L.g_hits) L.stack[L.sp++] = pack_group(L.g_base, L.g_flip, L.g_hits);
+    const uint32_t ni = L.g_base + (uint32_t)r;
+    test_node8(S.nodes.data(), ni, L.R, 0.0f, L.best, L.g_hits, L.t_mask, L.t_valid, L.g_base, L.t_base, L.g_flip);
+}
+
+struct Result {
+    double issues = 0, iters = 0, rays = 0, lane_valu = 0;
+    double blk_iss[5] = {}, blk_lanes[5] = {};   // head, refill, tri (all k), node, stack
+};
+
+static Result simulate(const Scene8& S, const std::vector<Ray>& rays, const Policy& P) {
+    Result res;
+    const int W = 64;
+    size_t next = 0;
+    const size_t chunk = 64;
+    // waves draw chunks of the ray stream in turn (one wave at a time is enough for SIMD efficiency)
+    const int nwaves = 64;
+    std::vector<std::vector<Lane>> waves(nwaves, std::vector<Lane>(W));
+    std::vector<size_t> wnext(nwaves, 0), wend(nwaves, 0);
+    std::vector<bool> done(nwaves, false);
+    int live = nwaves;
+    while (live > 0) {
+        for (int w = 0; w < nwaves; ++w) {
+            if (done[w]) continue;
+            auto& lanes = waves[w];
+            double cost = C_HEAD;
+            int idle = 0;
+            for (auto& L : lanes) idle += !L.active;
+            const bool refill = idle >= P.refill_min || idle == W;
+            if (refill && wnext[w] >= wend[w] && next < rays.size()) {
+                wnext[w] = next;
+                wend[w] = std::min(next + chunk, rays.size());
+                next = wend[w];
+            }
+            if (refill && idle > 0 && wnext[w] < wend[w]) {
+                int got = 0;
+                for (auto& L : lanes)
+                    if (!L.active && wnext[w] < wend[w]) {
+                        start(L, rays[wnext[w]]);
+                        L.ray = (int)wnext[w];
+                        ++wnext[w];
+                        ++got;
+                    }
+                if (got) { cost += C_REFILL; res.blk_iss[1] += C_REFILL; res.blk_lanes[1] += got * C_REFILL; }
+                res.lane_valu += got * C_REFILL;
+            }
+            int nact = 0;
+            for (auto& L : lanes) nact += L.active;
+            if (nact == 0) {
+                done[w] = true;
+                --live;
+                continue;
+            }
+            // triangle block participation
+            int want_tri = 0, blocked = 0;
+            for (auto& L : lanes)
+                if (L.active && (L.t_mask || L.p_mask)) {
+                    ++want_tri;
+                    // blocked: cannot take a node (no node work, or both triangle groups in use)
+                    if (!node_work(L) || (L.t_mask && L.p_mask) || P.postpone_thr == 0) ++blocked;
+                }
+            const bool tri_phase = want_tri > 0 && (P.postpone_thr == 0 || want_tri >= P.postpone_thr || blocked > 0);
+            bool any_t[8] = {}, any_node = false, any_stack = false;
+            int n_t[8] = {}, n_node = 0;
+            for (auto& L : lanes) {
+                if (!L.active) continue;
+                bool did_tri = false;
+                if (tri_phase && (L.t_mask || L.p_mask)) {
+                    if (!L.t_mask) {   // take the postponed group
+                        L.t_mask = L.p_mask; L.t_base = L.p_base; L.t_valid = L.p_valid; L.p_mask = 0;
+                    }
+                    for (int k = 0; k < P.tris_per_step && L.t_mask; ++k) {
+                        const int b = lowest_bit(L.t_mask);
+                        L.t_mask &= L.t_mask - 1u;
+                        tri_test(S, L, tri_slot(L.t_base, L.t_valid, b));
+                        any_t[k] = true;
+                        ++n_t[k];
+                    }
+                    if (!L.t_mask && L.p_mask) {
+                        L.t_mask = L.p_mask; L.t_base = L.p_base; L.t_valid = L.p_valid; L.p_mask = 0;
+                    }
+                    did_tri = true;
+                }
+                (void)did_tri;
+                // node step: no pending triangles (current) or a free postponed slot (policy P)
+                bool can_node = node_work(L) && (L.t_mask == 0u || (P.postpone_thr > 0 && L.p_mask == 0u));
+                if (can_node) {
+                    if (L.t_mask) {   // postpone the current group
+                        L.p_mask = L.t_mask; L.p_base = L.t_base; L.p_valid = L.t_valid; L.t_mask = 0;
+                    }
+                    const bool pop = !L.g_hits;
+                    node_step(S, L);
+                    any_node = true;
+                    ++n_node;
+                    if (pop || L.sp) any_stack = true;
+                }
+                ++L.steps;
+                if (L.t_mask == 0u && L.p_mask == 0u && !node_work(L)) {
+                    L.active = false;
+                    res.rays += 1;
+                    res.iters += L.steps;
+                }
+            }
+            for (int k = 0; k < 8; ++k) if (any_t[k]) { cost += k ? C_TRI2 : C_TRI1; res.blk_iss[2] += k ? C_TRI2 : C_TRI1; res.blk_lanes[2] += n_t[k] * (k ? C_TRI2 : C_TRI1); }
+            res.blk_iss[0] += C_HEAD; res.blk_lanes[0] += nact * C_HEAD;
+            if (any_node) { res.blk_iss[3] += C_NODE; res.blk_lanes[3] += n_node * C_NODE; }
+            if (any_stack) res.blk_iss[4] += C_STACK;
+            if (any_node) cost += C_NODE;
+            if (any_stack) cost += C_STACK;
+            res.lane_valu += n_node * C_NODE + nact * C_HEAD;
+            for (int k = 0; k < 8; ++k) res.lane_valu += n_t[k] * (k ? C_TRI2 : C_TRI1);
+            res.issues += cost;
+        }
+    }
+    return res;
+}
+
+int main(int argc, char** argv) {
+    const char* assets = argc > 1 ? argv[1] : "assets";
+    const int stride = argc > 2 ? atoi(argv[2]) : 4;   // pixel subsampling
+    rt_scene* sc = nullptr;
+    int32_t synth = 0;
+    if (rt_scene_preset("c3g", assets, &sc, &synth) != RT_OK) { fprintf(stderr, "preset failed\n"); return 1; }
+    rt_scene_desc D;
+    rt_scene_get_desc(sc, &D);
+    std::vector<float> world;
+    for (uint32_t m = 0; m < D.mesh_count; ++m) {
+        const rt_mesh_desc& M = D.meshes[m];
+        const float* T = &M.transform.columns[0][0];
+        for (uint32_t s = 0; s < M.submesh_count; ++s) {
+            const rt_submesh_desc& SM = M.submeshes[s];
+            for (uint32_t i = 0; i < SM.index_count; ++i) {
+                const rt_float3& p = M.positions[SM.indices[i]];
+                for (int r = 0; r < 3; ++r)
+                    world.push_back(((T[0 + r] * p.x + T[3 + r] * p.y) + T[6 + r] * p.z) + T[9 + r] * 1.0f);
+            }
+        }
+    }
+    const uint32_t n = (uint32_t)(world.size() / 9);
+    fprintf(stderr, "%u triangles; building\n", n);
+    BvhResult b2;
+    Bvh8Result b8;
+    for (int limit : {64, 48, 40, 32, 28, 24, 21}) {
+        b2 = build_bvh2(world.data(), n, 1, limit);
+        b8 = collapse_bvh8_dp(b2, 1.0f, 0.5f);
+        if (b8.max_depth <= 16) break;
+    }
+    Scene8 S;
+    S.nodes = b8.nodes;
+    S.tris.resize(3 * (size_t)b8.tri_order.size());
+    for (size_t k = 0; k < b8.tri_order.size(); ++k) {
+        const uint32_t id = b8.tri_order[k];
+        for (int v = 0; v < 3; ++v) {
+            const float* p = &world[9 * (size_t)id + 3 * v];
+            S.tris[3 * k + v] = make_float4(p[0], p[1], p[2], v == 0 ? __builtin_bit_cast(float, id) : 0.0f);
+        }
+    }
+    fprintf(stderr, "%zu nodes, depth %d\n", S.nodes.size(), b8.max_depth);
+    // primary rays: every stride-th pixel of 1920x1080, 4 samples each (jittered), queue order
+    Camera cam;
+    rt_camera_default(1920, 1080, &cam);
+    std::mt19937 rng(7);
+    std::uniform_real_distribution<float> U01(0.0f, 1.0f);
+    std::vector<Ray> prim, sec;
+    for (int py = 0; py < 1080; py += stride)
+        for (int px = 0; px < 1920; px += stride)
+            for (int s = 0; s < 4; ++s) {
+                float uvx = ((px + U01(rng)) / 1920.0f) * 2.0f - 1.0f, uvy = ((py + U01(rng)) / 1080.0f) * 2.0f - 1.0f;
+                f3 d = normalize((uvx * ldf3(cam.right) + uvy * ldf3(cam.up)) + ldf3(cam.forward));
+                prim.push_back(Ray{ldf3(cam.position), d});
+            }
+    // one diffuse bounce from each primary hit (closest hit by a serial trace)
+    TraceCounters tc{0, 0, 0};
+    std::vector<int> stackbuf(16 * kBlock);
+    DevScene DS{};
+    DS.tris = S.tris.data();
+    DS.nodes8 = S.nodes.data();
+    for (const Ray& r : prim) {
+        Hit h;
+        bool ovf = false;
+        if (!trace8<false, false>(DS, r.o, r.d, 0.0f, INFINITY, h, stackbuf.data(), tc, ovf) || h.id == 0xffffffffu) continue;
+        const float* p0 = &world[9 * (size_t)h.id];
+        f3 a = mk3(p0[0], p0[1], p0[2]), b = mk3(p0[3], p0[4], p0[5]), c = mk3(p0[6], p0[7], p0[8]);
+        f3 N = normalize(cross(b - a, c - a));
+        if (dot(N, r.d) > 0) N = -N;
+        f3 P = r.o + r.d * h.t;
+        // cosine hemisphere
+        float r1 = U01(rng), r2 = U01(rng), phi = 6.2831853f * r1, sr = sqrtf(r2);
+        f3 t = fabsf(N.x) > 0.5f ? mk3(0, 1, 0) : mk3(1, 0, 0);
+        f3 X = normalize(cross(t, N)), Y = cross(N, X);
+        f3 d = normalize((X * (cosf(phi) * sr) + Y * (sinf(phi) * sr)) + N * sqrtf(1.0f - r2));
+        sec.push_back(Ray{P + N * 1e-3f, d});
+    }
+    fprintf(stderr, "%zu primary, %zu secondary rays\n", prim.size(), sec.size());
+    std::vector<Policy> pols;
+    pols.push_back(Policy{"current (refill 8, 2 tris)", 8, 2, 0});
+    pols.push_back(Policy{"refill 16", 16, 2, 0});
+    pols.push_back(Policy{"1 tri per step", 8, 1, 0});
+    pols.push_back(Policy{"4 tris per step", 8, 4, 0});
+    pols.push_back(Policy{"3 tris per step", 8, 3, 0});
+    pols.push_back(Policy{"postpone 24 + 3 tris", 8, 3, 24});
+    pols.push_back(Policy{"postpone 24 + 4 tris", 8, 4, 24});
+    for (int thr : {8, 24, 48}) {
+        static char buf[8][64];
+        static int bi = 0;
+        snprintf(buf[bi], 64, "postpone thr %d", thr);
+        pols.push_back(Policy{buf[bi++], 8, 2, thr});
+    }
+    for (int set = 0; set < 2; ++set) {
+        const auto& rays = set ? sec : prim;
+        printf("== %s rays (%zu)\n", set ? "secondary (diffuse bounce)" : "primary", rays.size());
+        for (const Policy& P : pols) {
+            Result r = simulate(S, rays, P);
+            printf("  %-28s issues/ray %7.2f  iters/ray %6.2f  lane util %.3f\n", P.name, r.issues / r.rays,
+                   r.iters / r.rays, r.lane_valu / (r.issues * 64.0));
+            const char* bn[5] = {"head", "refill", "tri", "node", "stack"};
+            printf("     ");
+            for (int b = 0; b < 5; ++b) printf(" %s %.2f/ray (util %.2f)", bn[b], r.blk_iss[b] / r.rays, r.blk_iss[b] > 0 ? r.blk_lanes[b] / (64.0 * r.blk_iss[b]) : 0.0);
+            printf("\n");
+        }
+    }
+    rt_scene_free(sc);
+    return 0;
+}
