@@ -37,7 +37,7 @@ struct MeshInfo {
 // the slots and overlap except where frame f needs frame f-1's results (the history target and
 // the previous motion vectors: the extra-sample pass and the resolve).
 struct FrameSlot {
-    DevBuf color, accum, meta, q0, q1, hits, sq, counts, extra, sorted, sort_table, sort_total, params;
+    DevBuf qc, accum, meta, q0, q1, hits, sq, counts, extra, sorted, sort_table, sort_total, params;
     DevBuf depth, gbuffer, counters;
     DevBuf prim_hit;   // wavefront: per pixel, sample 0's last bounce-0 hit (id, u, v) for wf_motion
     WavefrontBuffers wf;
@@ -50,7 +50,7 @@ struct FrameSlot {
     bool gbuf_written = false;                  // the slot's last frame wrote the G-buffer (enableDenoiseGBuffer)
     uint64_t seq = 0;                           // frame number (harvest order)
     int gen = 0;                                // geometry generation the frame reads
-    DevBuf* bufs[17] = {&color, &accum, &meta, &q0, &q1, &hits, &sq, &counts, &extra, &sorted,
+    DevBuf* bufs[17] = {&qc, &accum, &meta, &q0, &q1, &hits, &sq, &counts, &extra, &sorted,
                         &sort_table, &sort_total, &params, &depth, &gbuffer, &counters, &prim_hit};
 };
 // Per-frame geometry (what skinning, instance transforms and refit rewrite between frames), in
@@ -287,15 +287,15 @@ static rt_status ensure_wavefront(rt_ctx* c, FrameSlot& fs, size_t own_px, int s
     rt_status st;
     if (W.cap_paths < paths || W.queue_entries < wavefront_queue_entries(paths, max_extra)) {
         size_t qe = wavefront_queue_entries(paths, max_extra);
-        if ((st = dev_alloc(c, fs.color, paths * 16))) return st;
+        if ((st = dev_alloc(c, fs.qc, 2 * qe * 16))) return st;   // both queues' colour arrays
         if ((st = dev_alloc(c, fs.accum, paths * 16))) return st;
         if ((st = dev_alloc(c, fs.meta, paths * 16))) return st;
         if ((st = dev_alloc(c, fs.q0, qe * 32))) return st;
         if ((st = dev_alloc(c, fs.q1, qe * 32))) return st;
         if ((st = dev_alloc(c, fs.hits, qe * 16))) return st;
         if ((st = dev_alloc(c, fs.sq, qe * 48))) return st;
-        // hit sort output (3 float4 per hit), only with the sort on
-        if (c->sort_bins && (st = dev_alloc(c, fs.sorted, qe * 48))) return st;
+        // hit sort output (4 float4 per hit), only with the sort on
+        if (c->sort_bins && (st = dev_alloc(c, fs.sorted, qe * 64))) return st;
         W.cap_paths = paths;
         W.queue_entries = qe;
     }
@@ -318,7 +318,8 @@ static rt_status ensure_wavefront(rt_ctx* c, FrameSlot& fs, size_t own_px, int s
         HIPC(c, hipHostMalloc((void**)&W.h_params, sizeof(FrameParams) * WavefrontBuffers::kParamSlots, 0));
         W.d_params = (FrameParams*)fs.params.p;
     }
-    W.p_color = (float4*)fs.color.p;
+    W.qc[0] = (float4*)fs.qc.p;
+    W.qc[1] = (float4*)fs.qc.p + W.queue_entries;
     W.p_accum = (float4*)fs.accum.p;
     W.p_meta = (uint4*)fs.meta.p;
     W.q[0] = (float4*)fs.q0.p;

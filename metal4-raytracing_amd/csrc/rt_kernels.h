@@ -96,16 +96,18 @@ constexpr int kWfCountWords = 50 * kCntStride + 64 + 66 + 9;
 __host__ __device__ constexpr uint32_t cslot(int c) { return (uint32_t)c * kCntStride; }
 struct WavefrontBuffers {
     size_t queue_entries = 0;     // kShards segments of queue_entries / kShards
-    float4* p_color = nullptr;
     float4* p_accum = nullptr;
-    uint4* p_meta = nullptr;      // (pixel, sample, bounce | tpass << 8 | step << 16, halton index)
+    uint4* p_meta = nullptr;      // extra-sample paths only: (pixel, sample, 0, halton index)
+    // ray queues: entry e = {origin, w = path id}, {direction, w = path state bits: bounce | tpass << 8 |
+    // step << 16}; qc[q][e] = the path's throughput colour (absent for state 0, the primary ray: 1)
     float4* q[2] = {nullptr, nullptr};
+    float4* qc[2] = {nullptr, nullptr};
     float4* hits = nullptr;
     float4* sq = nullptr;
     uint32_t* counts = nullptr;   // device counter slots (see cslot)
     uint32_t* h_counts = nullptr; // pinned host mirror
     uint2* px_extra = nullptr;    // per own pixel: (first extra path - base_paths, count)
-    // per-bounce hit sort (wf_sort_*): the hits reordered by key as {o, d, hit} float4 triples,
+    // per-bounce hit sort (wf_sort_*): the hits reordered by key as {o, d, hit, colour} float4 quads,
     // per-(bin, block) counts, per-bin totals
     float4* sorted = nullptr;
     uint32_t* sort_table = nullptr;

@@ -216,26 +216,30 @@ __device__ __forceinline__ uint32_t compact1by1(uint32_t x) {
     return x;
 }
 
-// own pixel index -> image coordinates (tiles tile_id % nranks == rank, Morton order in a tile)
-__device__ __forceinline__ void own_pixel(const FrameParams& P, uint32_t i, int& px, int& py) {
-    const uint32_t T = (uint32_t)P.tile_size, per = T * T;
-    uint32_t k = i / per, r = i % per;
-    int tid = P.rank + (int)k * P.nranks;
-    int tx = tid % P.tiles_x, ty = tid / P.tiles_x;
-    uint32_t lx, ly;
-    if ((T & (T - 1)) == 0) {
-        lx = compact1by1(r);
-        ly = compact1by1(r >> 1);
-    } else {
-        lx = r % T;
-        ly = r / T;
-    }
-    px = tx * (int)T + (int)lx;
-    py = ty * (int)T + (int)ly;
-}
 
 __device__ __forceinline__ uint32_t pack_state(int bounce, int tpass, int step) {
     return (uint32_t)bounce | ((uint32_t)tpass << 8) | ((uint32_t)step << 16);
+}
+
+// n / d for 32-bit n by a multiply-high and two shifts (Granlund, Montgomery, PLDI 1994, fig. 4.1):
+// the path-id -> pixel mappings run per refill / per shaded hit, where an integer division by a
+// run-time divisor costs ~30 VALU instructions
+struct FastDiv {
+    uint32_t d, m, s1, s2;
+};
+static FastDiv make_fastdiv(uint32_t d) {
+    FastDiv f;
+    f.d = d;
+    uint32_t l = 0;
+    while (l < 32 && (1ull << l) < d) ++l;
+    f.m = (uint32_t)(((1ull << 32) * ((1ull << l) - d)) / d + 1);
+    f.s1 = l < 1 ? l : 1;
+    f.s2 = l > 1 ? l - 1 : 0;
+    return f;
+}
+__device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv& f) {
+    const uint32_t t = __umulhi(f.m, n);
+    return (t + ((n - t) >> f.s1)) >> f.s2;
 }
 
 struct WfParams {
@@ -257,7 +261,28 @@ struct WfParams {
                            // the counters and skip once the live count fell below `tail`
     int finish_q;          // dev_ctl: the finish queue when every enqueued bulk round ran (written by generate)
     const FrameParams* Pd; // this frame's FrameParams in device memory (W.d_params)
+    // own pixel index -> image pixel (own_pixel): tiles tile_id % nranks == rank of tile x tile pixels
+    FastDiv spp_div, tile_px_div, tiles_x_div;   // by spp, tile * tile, tiles per row
+    int tile, rank, nranks;
 };
+
+// own pixel index -> image coordinates (tiles tile_id % nranks == rank, Morton order in a tile)
+__device__ __forceinline__ void own_pixel(const WfParams& Q, uint32_t i, int& px, int& py) {
+    const uint32_t T = (uint32_t)Q.tile;
+    const uint32_t k = fdiv(i, Q.tile_px_div), r = i - k * Q.tile_px_div.d;
+    const uint32_t tid = (uint32_t)Q.rank + k * (uint32_t)Q.nranks;
+    const uint32_t ty = fdiv(tid, Q.tiles_x_div), tx = tid - ty * Q.tiles_x_div.d;
+    uint32_t lx, ly;
+    if ((T & (T - 1)) == 0) {
+        lx = compact1by1(r);
+        ly = compact1by1(r >> 1);
+    } else {
+        lx = r % T;
+        ly = r / T;
+    }
+    px = (int)(tx * T + lx);
+    py = (int)(ty * T + ly);
+}
 
 // counter slots (cslot): [q*8 + shard] ray queues q = 0, 1; [16 + shard] shadow queue; [24] extra allocator
 constexpr int kCntShadowQ = 16;
@@ -307,10 +332,13 @@ __device__ __forceinline__ uint32_t entry_of(const ShardPrefix& p, uint32_t g, u
     return k * seg_cap + (g - start);
 }
 
+// A path's state between launches: its accumulator here (indexed by path id), its throughput
+// colour and bounce / step counters in the queue entry of its next ray (qc, d.w), its pixel,
+// sample and Halton index recomputed from the path id (path_meta); only the extra-sample paths,
+// whose ids do not encode their pixel, keep them in p_meta.
 __device__ __forceinline__ void init_path(const WfParams& Q, uint32_t pid, uint32_t pix, int sample, uint32_t hidx) {
-    Q.W.p_color[pid] = make_float4(1.0f, 1.0f, 1.0f, 0.0f);
     Q.W.p_accum[pid] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-    Q.W.p_meta[pid] = make_uint4(pix, (uint32_t)sample, 0u, hidx);
+    if (pid >= Q.base_paths) Q.W.p_meta[pid] = make_uint4(pix, (uint32_t)sample, 0u, hidx);
 }
 
 
@@ -463,21 +491,41 @@ __device__ __forceinline__ uint32_t stage_top(const DevScene& S, uint4* lds_top)
 }
 
 // ---- base paths ----------------------------------------------------------------------------------------
-// Path pid of the base pass (own pixel pid / spp, sample pid % spp): its pixel, sample, Halton index
-// (:263-270) and primary ray (:270-292).  False for a path of a tile pixel outside the image.
-__device__ __forceinline__ bool base_path(const FrameParams& P, const ShadeTabs& halton, int spp, uint32_t pid,
-                                          uint32_t& pix, int& s, uint32_t& hidx, f3& o, f3& d) {
+// Halton index of sample s of pixel pix in this frame (:263-270)
+__device__ __forceinline__ uint32_t base_hidx(const FrameParams& P, int spp, uint32_t pix, int s) {
     const Uniforms& U = P.U;
-    s = (int)(pid % (uint32_t)spp);
-    int px, py;
-    own_pixel(P, pid / (uint32_t)spp, px, py);
-    if (px >= U.width || py >= U.height) return false;
-    pix = (uint32_t)py * (uint32_t)U.width + (uint32_t)px;
     const int maxExtra = (U.enableMotionAdaptiveSampling != 0) ? max(U.motionSamplingMaxExtraSamples, 0) : 0;
     const int frameOffset = (int)U.frameIndex * (spp + maxExtra) + s;
-    hidx = (uint32_t)(int)(P.random[pix] + (unsigned)frameOffset);
+    return (uint32_t)(int)(P.random[pix] + (unsigned)frameOffset);
+}
+// Path pid of the base pass (own pixel pid / spp, sample pid % spp): its pixel, sample, Halton index
+// (:263-270) and primary ray (:270-292).  False for a path of a tile pixel outside the image.
+__device__ __forceinline__ bool base_path(const FrameParams& P, const WfParams& Q, const ShadeTabs& halton, uint32_t pid,
+                                          uint32_t& pix, int& s, uint32_t& hidx, f3& o, f3& d) {
+    const Uniforms& U = P.U;
+    const uint32_t i = fdiv(pid, Q.spp_div);
+    s = (int)(pid - i * Q.spp_div.d);
+    int px, py;
+    own_pixel(Q, i, px, py);
+    if (px >= U.width || py >= U.height) return false;
+    pix = (uint32_t)py * (uint32_t)U.width + (uint32_t)px;
+    hidx = base_hidx(P, Q.spp, pix, s);
     primary_ray(U, halton, px, py, (int)hidx, o, d);
     return true;
+}
+// (pixel, sample, Halton index) of path pid: a base path's from its id, as wf_generate made them;
+// an extra-sample path's from p_meta (wf_extra)
+__device__ __forceinline__ uint3 path_meta(const FrameParams& P, const WfParams& Q, uint32_t pid) {
+    if (pid >= Q.base_paths) {
+        const uint4 m = Q.W.p_meta[pid];
+        return make_uint3(m.x, m.y, m.w);
+    }
+    const uint32_t i = fdiv(pid, Q.spp_div);
+    const int s = (int)(pid - i * Q.spp_div.d);
+    int px, py;
+    own_pixel(Q, i, px, py);
+    const uint32_t pix = (uint32_t)py * (uint32_t)P.U.width + (uint32_t)px;
+    return make_uint3(pix, (uint32_t)s, base_hidx(P, Q.spp, pix, s));
 }
 // Per-pixel defaults, written by the pixel's sample-0 path (:252-261).
 __device__ __forceinline__ void init_pixel(const FrameParams& P, uint32_t pix) {
@@ -513,7 +561,7 @@ __global__ void __launch_bounds__(kBlock) wf_generate(DevScene S, const FramePar
         int s = 0;
         uint32_t pix = 0, hidx = 0;
         f3 o = mk3(0, 0, 0), d = mk3(0, 0, 0);
-        const bool valid = pid < total && base_path(P, halton, spp, pid, pix, s, hidx, o, d);
+        const bool valid = pid < total && base_path(P, Q, halton, pid, pix, s, hidx, o, d);
         if (valid) {
             init_path(Q, pid, pix, s, hidx);
             if (s == 0) init_pixel(P, pix);
@@ -551,6 +599,7 @@ __global__ void __launch_bounds__(kBlock) wf_shade(DevScene S, const FrameParams
     uint32_t n = cnt.end[kShards - 1];
     const float4* qin = Q.W.q[cur];
     float4* qout = Q.W.q[next] + 2 * (size_t)shard * Q.seg_cap;
+    float4* qcout = Q.W.qc[next] + (size_t)shard * Q.seg_cap;
     float4* sqout = Q.W.sq + 3 * (size_t)shard * Q.seg_cap;
     f2 zero2;
     zero2.x = 0.0f;
@@ -574,19 +623,23 @@ __global__ void __launch_bounds__(kBlock) wf_shade(DevScene S, const FrameParams
         StepResult r;
         r.next = false;
         r.shadow = false;
-        uint32_t pid = 0;
+        uint32_t pid = 0, nstate = 0;   // nstate, ncol: the continuation's state bits and colour
         f3 rayO = mk3(0, 0, 0), rayD = mk3(0, 0, 0);
+        float4 ncol = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
         if (g < end) {
             float4 o, d, hv;
+            size_t ce = 0;   // the entry's colour: sorted[4g + 3] / qc[cur][e]
             if (SORTED) {
-                o = Q.W.sorted[3 * (size_t)g];
-                d = Q.W.sorted[3 * (size_t)g + 1];
-                hv = Q.W.sorted[3 * (size_t)g + 2];
+                o = Q.W.sorted[4 * (size_t)g];
+                d = Q.W.sorted[4 * (size_t)g + 1];
+                hv = Q.W.sorted[4 * (size_t)g + 2];
+                ce = 4 * (size_t)g + 3;
             } else {
                 const uint32_t e = ebase + g;
                 o = qin[2 * (size_t)e];
                 d = qin[2 * (size_t)e + 1];
                 hv = Q.W.hits[e];
+                ce = e;
             }
             pid = __float_as_uint(o.w);
             Hit h;
@@ -595,8 +648,11 @@ __global__ void __launch_bounds__(kBlock) wf_shade(DevScene S, const FrameParams
             h.u = hv.z;
             h.v = hv.w;
             if (h.id != 0xffffffffu) {                                           // miss -> path ends (:321-322)
-                uint4 meta = Q.W.p_meta[pid];
-                float4 c = Q.W.p_color[pid];
+                const uint32_t state = __float_as_uint(d.w);
+                const uint3 pm = path_meta(P, Q, pid);
+                const uint4 meta = make_uint4(pm.x, pm.y, state, pm.z);
+                const float4 c = state == 0u ? make_float4(1.0f, 1.0f, 1.0f, 0.0f)
+                                             : (SORTED ? Q.W.sorted[ce] : Q.W.qc[cur][ce]);
                 // FULL=false: shade_step only adds color * emission to accum (:585), so it runs on a
                 // zero accumulator and the stored one is read and updated only when that term is
                 // non-zero (accum is never -0, so a + (0 + x) == a + x bit for bit); FULL (debug
@@ -614,7 +670,8 @@ __global__ void __launch_bounds__(kBlock) wf_shade(DevScene S, const FrameParams
                 shade_step<FULL, false>(S, U, halton, (int)meta.w, sample, rayO, rayD, h, p, sample == 0 && p.step == 0,
                                  zero2, false, zero2, r);
                 write_pixel_outputs(P, meta.x, r, h, FULL);
-                if (r.next) Q.W.p_color[pid] = make_float4(p.color.x, p.color.y, p.color.z, 0.0f);
+                nstate = pack_state(p.bounce, p.tpass, p.step);
+                ncol = make_float4(p.color.x, p.color.y, p.color.z, 0.0f);
                 // radiance only changes on emissive hits (:585-586): skip the store otherwise
                 if (__float_as_uint(p.accum.x) != __float_as_uint(a.x) || __float_as_uint(p.accum.y) != __float_as_uint(a.y) ||
                     __float_as_uint(p.accum.z) != __float_as_uint(a.z)) {
@@ -624,7 +681,6 @@ __global__ void __launch_bounds__(kBlock) wf_shade(DevScene S, const FrameParams
                     }
                     Q.W.p_accum[pid] = make_float4(p.accum.x, p.accum.y, p.accum.z, 0.0f);
                 }
-                if (r.next) Q.W.p_meta[pid] = make_uint4(meta.x, meta.y, pack_state(p.bounce, p.tpass, p.step), meta.w);
             }
         }
         uint32_t ns, nr;
@@ -644,7 +700,8 @@ __global__ void __launch_bounds__(kBlock) wf_shade(DevScene S, const FrameParams
         }
         if (r.next) {
             qout[2 * (size_t)nr] = make_float4(rayO.x, rayO.y, rayO.z, __uint_as_float(pid));
-            qout[2 * (size_t)nr + 1] = make_float4(rayD.x, rayD.y, rayD.z, 0.0f);
+            qout[2 * (size_t)nr + 1] = make_float4(rayD.x, rayD.y, rayD.z, __uint_as_float(nstate));
+            qcout[nr] = ncol;
         }
     }
 }
@@ -738,9 +795,10 @@ __global__ void __launch_bounds__(kSortThreads) wf_sort_scatter(DevScene S, WfPa
         if (id == 0xffffffffu) continue;
         const uint32_t pos = atomicAdd(&off[(uint32_t)S.tri_bin[id] >> shift], 1u);
         const float4 o = qin[2 * (size_t)e], d = qin[2 * (size_t)e + 1];
-        Q.W.sorted[3 * (size_t)pos] = o;
-        Q.W.sorted[3 * (size_t)pos + 1] = d;
-        Q.W.sorted[3 * (size_t)pos + 2] = hv;
+        Q.W.sorted[4 * (size_t)pos] = o;
+        Q.W.sorted[4 * (size_t)pos + 1] = d;
+        Q.W.sorted[4 * (size_t)pos + 2] = hv;
+        if (__float_as_uint(d.w) != 0u) Q.W.sorted[4 * (size_t)pos + 3] = Q.W.qc[cur][e];   // state 0: colour 1
     }
 }
 
@@ -961,11 +1019,15 @@ wf_finish_step(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int c
             if (mode == kIdle) {
                 const uint32_t g = wnext + mbcnt64(idle);
                 if (g < wend) {
-                    const float4* src = qin + 2 * (size_t)entry_of(cnt, g, Q.seg_cap);
+                    const uint32_t e = entry_of(cnt, g, Q.seg_cap);
+                    const float4* src = qin + 2 * (size_t)e;
                     const float4 o = src[0], d = src[1];
                     pid = __float_as_uint(o.w);
-                    meta = Q.W.p_meta[pid];
-                    const float4 c = Q.W.p_color[pid], a = Q.W.p_accum[pid];
+                    const uint32_t state = __float_as_uint(d.w);
+                    const uint3 pm = path_meta(P, Q, pid);
+                    meta = make_uint4(pm.x, pm.y, state, pm.z);
+                    const float4 c = state == 0u ? make_float4(1.0f, 1.0f, 1.0f, 0.0f) : Q.W.qc[cur][e];
+                    const float4 a = Q.W.p_accum[pid];
                     p.color = mk3(c.x, c.y, c.z);
                     p.accum = mk3(a.x, a.y, a.z);
                     p.bounce = (int)(meta.z & 0xffu);
@@ -1093,7 +1155,7 @@ __global__ void __launch_bounds__(kBlock) wf_extra(DevScene S, const FrameParams
     int px = 0, py = 0, e = 0;
     uint32_t pix = 0;
     if (i < Q.own_pixels) {
-        own_pixel(P, i, px, py);
+        own_pixel(Q, i, px, py);
         if (px < U.width && py < U.height) {
             pix = (uint32_t)py * (uint32_t)U.width + (uint32_t)px;
             float2 mv2 = P.motion[pix], pm2 = P.motion_prev[pix];
@@ -1140,7 +1202,7 @@ __global__ void __launch_bounds__(kBlock) wf_motion(DevScene S, const FrameParam
     const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
     if (i >= Q.own_pixels) return;
     int px, py;
-    own_pixel(P, i, px, py);
+    own_pixel(Q, i, px, py);
     if (px >= U.width || py >= U.height) return;
     const size_t pix = (size_t)py * U.width + px;
     const uint4 ph = P.prim_hit[pix];
@@ -1159,7 +1221,7 @@ __global__ void __launch_bounds__(kBlock) wf_resolve(DevScene S, const FramePara
     uint32_t i = blockIdx.x * kBlock + threadIdx.x;
     if (i >= Q.own_pixels) return;
     int px, py;
-    own_pixel(P, i, px, py);
+    own_pixel(Q, i, px, py);
     if (px >= U.width || py >= U.height) return;
     size_t pix = (size_t)py * U.width + px;
     f3 total = mk3(0.0f, 0.0f, 0.0f);
@@ -1596,6 +1658,12 @@ bool run_wavefront(const DevScene& S, const FrameParams& P, WavefrontBuffers& W,
     Q.shade_min = tu.shade_min;
     Q.fchunk = tu.fchunk;
     Q.ray_sort = tu.ray_sort;
+    Q.spp_div = make_fastdiv((uint32_t)Q.spp);
+    Q.tile = P.tile_size;
+    Q.rank = P.rank;
+    Q.nranks = P.nranks;
+    Q.tile_px_div = make_fastdiv((uint32_t)P.tile_size * (uint32_t)P.tile_size);
+    Q.tiles_x_div = make_fastdiv((uint32_t)max(P.tiles_x, 1));
     // frames in flight: the finish tail takes part of the resident grid and leaves the rest to the
     // other frames' bulk rounds (C3g sweeps, DESIGN.md §3: two slots 40 %; four slots on a small
     // frame, a multi-GPU rank's share, 20 %; else 1 / in_flight); one frame at a time: all of it

@@ -36,6 +36,8 @@ struct Lane {
     uint32_t stack[64];
     // postponed triangle group (policy P)
     uint32_t p_base = 0, p_mask = 0, p_valid = 0;
+    uint32_t r_mask = 0;   // deferred root triangles (policy defer_root)
+    float r_tn = 0;
     int ray = -1;
     int steps = 0;
 };
@@ -47,6 +49,9 @@ struct Policy {
     int refill_min = 8;
     int tris_per_step = 2;
     int postpone_thr = 0;   // > 0: the triangle block runs only when >= thr lanes want it (or a lane is blocked)
+    int defer_root = 0;     // root-node triangles tested after the rest of the tree, if their leaf box is still in reach
+    int coop = 0;           // > 0: the wave tests every pending triangle of the tri-phase lanes in batches of 64
+                            // (one per lane, owner's ray via LDS / bpermute); coop = per-batch overhead issues
 };
 
 struct Scene8 {
@@ -63,13 +68,18 @@ static void start(Lane& L, const Ray& r) {
     L.g_flip = false;
     L.t_mask = 0;
     L.p_mask = 0;
+    L.r_mask = 0;
     L.sp = 0;
     L.active = true;
     L.steps = 0;
 }
 
+static std::vector<uint32_t> g_tri_tests;
+static double g_nodes = 0, g_tris = 0;
 static bool tri_test(const Scene8& S, Lane& L, uint32_t slot) {
     const float4* tp = &S.tris[3 * (size_t)slot];
+    if (!g_tri_tests.empty()) g_tri_tests[slot]++;
+    g_tris += 1;
     float t, u, v, dt;
     if (intersect_triangle_vw(L.R.pre, L.R.o, ld3(tp[0]), ld3(tp[1]), ld3(tp[2]), 0.0f, L.best, &t, &u, &v, &dt)) {
         const uint32_t id = __builtin_bit_cast(uint32_t, tp[0].w);
@@ -83,6 +93,28 @@ static bool tri_test(const Scene8& S, Lane& L, uint32_t slot) {
 
 static bool node_work(const Lane& L) { return L.g_hits != 0u || L.sp > 0; }
 
+// min entry distance of the hit leaf children of node ni (the slab math of test_node8_words)
+static float leaf_tn(const Scene8& S, uint32_t ni, const RaySetup& R, float tmax) {
+    const Bvh8Node& n = S.nodes[ni];
+    const int k = n.axis_k >> 4;
+    float best = INFINITY;
+    for (int c = k; c < 8; ++c) {
+        float tn = 0.0f, tf = tmax * 1.0000004f;
+        const float inv[3] = {R.ix, R.iy, R.iz}, o[3] = {R.o.x, R.o.y, R.o.z};
+        for (int a = 0; a < 3; ++a) {
+            const float sc = ldexpf(1.0f, (int)n.e[a] - 127);
+            const float lo = n.p[a] + n.q[16 * a + c] * sc, hi = n.p[a] + n.q[16 * a + 8 + c] * sc;
+            float t0 = (lo - o[a]) * inv[a], t1 = (hi - o[a]) * inv[a];
+            if (t0 > t1) std::swap(t0, t1);
+            tn = std::max(tn, t0);
+            tf = std::min(tf, t1);
+        }
+        if (tn <= tf) best = std::min(best, tn);
+    }
+    return best;
+}
+
+static int g_defer_root = 0;
 static void node_step(const Scene8& S, Lane& L) {
     if (!L.g_hits) {
         --L.sp;
@@ -95,7 +127,13 @@ static void node_step(const Scene8& S, Lane& L) {
     L.g_hits &= ~(1u << r);
     if (L.g_hits) L.stack[L.sp++] = pack_group(L.g_base, L.g_flip, L.g_hits);
     const uint32_t ni = L.g_base + (uint32_t)r;
+    g_nodes += 1;
     test_node8(S.nodes.data(), ni, L.R, 0.0f, L.best, L.g_hits, L.t_mask, L.t_valid, L.g_base, L.t_base, L.g_flip);
+    if (g_defer_root && ni == 0 && L.t_mask) {
+        L.r_mask = L.t_mask;
+        L.r_tn = leaf_tn(S, 0, L.R, L.best);
+        L.t_mask = 0;
+    }
 }
 
 struct Result {
@@ -164,12 +202,13 @@ static Result simulate(const Scene8& S, const std::vector<Ray>& rays, const Poli
                     if (!L.t_mask) {   // take the postponed group
                         L.t_mask = L.p_mask; L.t_base = L.p_base; L.t_valid = L.p_valid; L.p_mask = 0;
                     }
-                    for (int k = 0; k < P.tris_per_step && L.t_mask; ++k) {
+                    const int lim = P.coop ? 64 : P.tris_per_step;
+                    for (int k = 0; k < lim && L.t_mask; ++k) {
                         const int b = lowest_bit(L.t_mask);
                         L.t_mask &= L.t_mask - 1u;
                         tri_test(S, L, tri_slot(L.t_base, L.t_valid, b));
-                        any_t[k] = true;
-                        ++n_t[k];
+                        any_t[P.coop ? 0 : k] = true;
+                        ++n_t[P.coop ? 0 : k];
                     }
                     if (!L.t_mask && L.p_mask) {
                         L.t_mask = L.p_mask; L.t_base = L.p_base; L.t_valid = L.p_valid; L.p_mask = 0;
@@ -190,13 +229,29 @@ static Result simulate(const Scene8& S, const std::vector<Ray>& rays, const Poli
                     if (pop || L.sp) any_stack = true;
                 }
                 ++L.steps;
+                if (L.t_mask == 0u && L.p_mask == 0u && !node_work(L) && L.r_mask) {
+                    if (L.r_tn <= L.best * 1.0000004f) {
+                        L.t_mask = L.r_mask;
+                        L.t_base = S.nodes[0].tri_base;
+                        L.t_valid = S.nodes[0].tri_valid;
+                    }
+                    L.r_mask = 0;
+                }
                 if (L.t_mask == 0u && L.p_mask == 0u && !node_work(L)) {
                     L.active = false;
                     res.rays += 1;
                     res.iters += L.steps;
                 }
             }
-            for (int k = 0; k < 8; ++k) if (any_t[k]) { cost += k ? C_TRI2 : C_TRI1; res.blk_iss[2] += k ? C_TRI2 : C_TRI1; res.blk_lanes[2] += n_t[k] * (k ? C_TRI2 : C_TRI1); }
+            if (P.coop) {
+                const int batches = (n_t[0] + 63) / 64;
+                const double c = batches * (C_TRI1 + P.coop);
+                cost += c;
+                res.blk_iss[2] += c;
+                res.blk_lanes[2] += n_t[0] * C_TRI1;
+                n_t[0] = 0;
+            }
+            for (int k = 0; k < 8; ++k) if (any_t[k] && n_t[k]) { cost += k ? C_TRI2 : C_TRI1; res.blk_iss[2] += k ? C_TRI2 : C_TRI1; res.blk_lanes[2] += n_t[k] * (k ? C_TRI2 : C_TRI1); }
             res.blk_iss[0] += C_HEAD; res.blk_lanes[0] += nact * C_HEAD;
             if (any_node) { res.blk_iss[3] += C_NODE; res.blk_lanes[3] += n_node * C_NODE; }
             if (any_stack) res.blk_iss[4] += C_STACK;
@@ -243,6 +298,7 @@ int main(int argc, char** argv) {
     Scene8 S;
     S.nodes = b8.nodes;
     S.tris.resize(3 * (size_t)b8.tri_order.size());
+    fprintf(stderr, "%zu slots for %u triangles\n", b8.tri_order.size(), n);
     for (size_t k = 0; k < b8.tri_order.size(); ++k) {
         const uint32_t id = b8.tri_order[k];
         for (int v = 0; v < 3; ++v) {
@@ -251,6 +307,10 @@ int main(int argc, char** argv) {
         }
     }
     fprintf(stderr, "%zu nodes, depth %d\n", S.nodes.size(), b8.max_depth);
+    for (int ni = 0; ni < 3; ++ni) {
+        const Bvh8Node& r = S.nodes[ni];
+        fprintf(stderr, "node %d: k_int %d tri_base %u tri_valid %08x\n", ni, r.axis_k >> 4, r.tri_base, r.tri_valid);
+    }
     // primary rays: every stride-th pixel of 1920x1080, 4 samples each (jittered), queue order
     Camera cam;
     rt_camera_default(1920, 1080, &cam);
@@ -295,19 +355,44 @@ int main(int argc, char** argv) {
     pols.push_back(Policy{"3 tris per step", 8, 3, 0});
     pols.push_back(Policy{"postpone 24 + 3 tris", 8, 3, 24});
     pols.push_back(Policy{"postpone 24 + 4 tris", 8, 4, 24});
-    for (int thr : {8, 24, 48}) {
+    pols.push_back(Policy{"defer root tris", 8, 2, 0, 1, 0});
+    pols.push_back(Policy{"defer root + postpone 24", 8, 2, 24, 1, 0});
+    pols.push_back(Policy{"coop ovh 40", 8, 2, 0, 0, 40});
+    pols.push_back(Policy{"coop ovh 60", 8, 2, 0, 0, 60});
+    pols.push_back(Policy{"coop ovh 60 + postpone 24", 8, 2, 24, 0, 60});
+    for (int thr : {24}) {
         static char buf[8][64];
         static int bi = 0;
         snprintf(buf[bi], 64, "postpone thr %d", thr);
         pols.push_back(Policy{buf[bi++], 8, 2, thr});
     }
+    if (getenv("SIM_TRISTATS")) {
+        g_tri_tests.assign(S.tris.size() / 3, 0);
+        Policy P0{"x", 8, 2, 0};
+        simulate(S, sec, P0);
+        std::vector<std::pair<uint32_t, uint32_t>> v;
+        double total = 0;
+        for (size_t k = 0; k < g_tri_tests.size(); ++k) { v.push_back({g_tri_tests[k], (uint32_t)k}); total += g_tri_tests[k]; }
+        std::sort(v.rbegin(), v.rend());
+        double acc = 0;
+        printf("secondary: %.0f triangle tests, %.2f per ray\n", total, total / sec.size());
+        for (int i = 0; i < 40; ++i) {
+            acc += v[i].first;
+            const float4* t = &S.tris[3 * (size_t)v[i].second];
+            f3 a = ld3(t[0]), b = ld3(t[1]), c = ld3(t[2]);
+            printf("  slot %u id %u tests %u (cum %.3f) area %.4g\n", v[i].second, __builtin_bit_cast(uint32_t, t[0].w), v[i].first, acc / total, 0.5f * length(cross(b - a, c - a)));
+        }
+        return 0;
+    }
     for (int set = 0; set < 2; ++set) {
         const auto& rays = set ? sec : prim;
         printf("== %s rays (%zu)\n", set ? "secondary (diffuse bounce)" : "primary", rays.size());
         for (const Policy& P : pols) {
+            g_nodes = g_tris = 0;
+            g_defer_root = P.defer_root;
             Result r = simulate(S, rays, P);
-            printf("  %-28s issues/ray %7.2f  iters/ray %6.2f  lane util %.3f\n", P.name, r.issues / r.rays,
-                   r.iters / r.rays, r.lane_valu / (r.issues * 64.0));
+            printf("  %-28s issues/ray %7.2f  iters/ray %6.2f  lane util %.3f  nodes/ray %.2f tris/ray %.2f\n", P.name, r.issues / r.rays,
+                   r.iters / r.rays, r.lane_valu / (r.issues * 64.0), g_nodes / r.rays, g_tris / r.rays);
             const char* bn[5] = {"head", "refill", "tri", "node", "stack"};
             printf("     ");
             for (int b = 0; b < 5; ++b) printf(" %s %.2f/ray (util %.2f)", bn[b], r.blk_iss[b] / r.rays, r.blk_iss[b] > 0 ? r.blk_lanes[b] / (64.0 * r.blk_iss[b]) : 0.0);
