@@ -190,6 +190,18 @@ typedef struct rt_stats {
        memory traffic); included in node_visits / trace_nodes */
     uint64_t node_visits_lds;
     uint64_t trace_nodes_lds;
+    /* wavefront, device clock: each launch from its first workgroup's start to its last wave's end
+       (s_memrealtime, 100 MHz), what a kernel trace records for a dispatch.  With frames in flight
+       the HIP events of trace_ms / kernel_ms also count the time a launch waits for CUs that other
+       frames' kernels hold. */
+    float trace_dev_ms;            /* extend + connect launches of the last frame */
+    int32_t trace_dev_launches;
+    float finish_dev_ms;           /* finish launches of the last frame */
+    int32_t finish_dev_launches;
+    double total_trace_dev_ms;     /* running sums of the four above */
+    uint64_t total_trace_dev_launches;
+    double total_finish_dev_ms;
+    uint64_t total_finish_dev_launches;
 } rt_stats;
 
 rt_status rt_create(const rt_opts* opts, rt_ctx** out);

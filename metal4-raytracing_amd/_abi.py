@@ -178,6 +178,14 @@ class Stats(C.Structure):
         ("total_finish_launches", C.c_uint64),
         ("node_visits_lds", C.c_uint64),
         ("trace_nodes_lds", C.c_uint64),
+        ("trace_dev_ms", C.c_float),
+        ("trace_dev_launches", C.c_int32),
+        ("finish_dev_ms", C.c_float),
+        ("finish_dev_launches", C.c_int32),
+        ("total_trace_dev_ms", C.c_double),
+        ("total_trace_dev_launches", C.c_uint64),
+        ("total_finish_dev_ms", C.c_double),
+        ("total_finish_dev_launches", C.c_uint64),
     ]
 
 

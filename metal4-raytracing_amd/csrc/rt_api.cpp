@@ -309,8 +309,8 @@ static rt_status ensure_wavefront(rt_ctx* c, FrameSlot& fs, size_t own_px, int s
         if ((st = dev_alloc(c, fs.sort_total, (size_t)kSortMaxBins * 4))) return st;
     }
     if (!fs.counts.p) {
-        if ((st = dev_alloc(c, fs.counts, kWfCountWords * 4))) return st;
-        HIPC(c, hipHostMalloc((void**)&W.h_counts, kWfCountWords * 4, 0));
+        if ((st = dev_alloc(c, fs.counts, kWfCountAllocBytes))) return st;
+        HIPC(c, hipHostMalloc((void**)&W.h_counts, kWfCountAllocBytes, 0));
         for (auto& e : W.ev) HIPC(c, hipEventCreate(&e));
         for (auto& e : fs.wft.ev) HIPC(c, hipEventCreate(&e));
         for (auto& e : W.param_ev) HIPC(c, hipEventCreate(&e));
@@ -327,6 +327,8 @@ static rt_status ensure_wavefront(rt_ctx* c, FrameSlot& fs, size_t own_px, int s
     W.hits = (float4*)fs.hits.p;
     W.sq = (float4*)fs.sq.p;
     W.counts = (uint32_t*)fs.counts.p;
+    W.tstamp = (unsigned long long*)((char*)fs.counts.p + kWfTsOffset);
+    W.h_tstamp = (unsigned long long*)((char*)W.h_counts + kWfTsOffset);
     W.px_extra = (uint2*)fs.extra.p;
     W.sorted = (float4*)fs.sorted.p;
     W.sort_table = (uint32_t*)fs.sort_table.p;
@@ -934,6 +936,10 @@ static rt_status harvest(rt_ctx* c, int k) {
     S.trace_rays = f.wavefront ? f.wfs.trace_rays : 0;
     S.trace_launches = f.wavefront ? f.wfs.trace_launches : 0;
     S.trace_ms = f.wavefront ? f.wfs.trace_ms : 0.0f;
+    S.trace_dev_ms = f.wavefront ? f.wfs.trace_dev_ms : 0.0f;
+    S.trace_dev_launches = f.wavefront ? f.wfs.trace_dev_launches : 0;
+    S.finish_dev_ms = f.wavefront ? f.wfs.finish_dev_ms : 0.0f;
+    S.finish_dev_launches = f.wavefront ? f.wfs.finish_dev_launches : 0;
     S.trace_closest_rays = f.wavefront ? f.wfs.trace_closest_rays : 0;
     S.finish_launches = f.wavefront ? f.wfs.finish_launches : 0;
     auto total = [&f](int w) {
@@ -961,6 +967,10 @@ static rt_status harvest(rt_ctx* c, int k) {
     T.total_trace_closest_rays += S.trace_closest_rays;
     T.total_trace_ms += S.trace_ms;
     T.total_trace_launches += (uint64_t)S.trace_launches;
+    T.total_trace_dev_ms += S.trace_dev_ms;
+    T.total_trace_dev_launches += (uint64_t)S.trace_dev_launches;
+    T.total_finish_dev_ms += S.finish_dev_ms;
+    T.total_finish_dev_launches += (uint64_t)S.finish_dev_launches;
     T.total_finish_launches += (uint64_t)S.finish_launches;
     if (total(kCntOverflow)) FAIL(c, RT_ERR_STATE, "traversal stack overflow");
     return RT_OK;
@@ -1349,6 +1359,10 @@ rt_status rt_get_stats(rt_ctx* c, rt_stats* out) {
     out->total_trace_closest_rays = T.total_trace_closest_rays;
     out->total_trace_ms = T.total_trace_ms;
     out->total_trace_launches = T.total_trace_launches;
+    out->total_trace_dev_ms = T.total_trace_dev_ms;
+    out->total_trace_dev_launches = T.total_trace_dev_launches;
+    out->total_finish_dev_ms = T.total_finish_dev_ms;
+    out->total_finish_dev_launches = T.total_finish_dev_launches;
     out->total_finish_launches = T.total_finish_launches;
     return RT_OK;
 }

@@ -106,6 +106,9 @@ struct WavefrontBuffers {
     float4* sq = nullptr;
     uint32_t* counts = nullptr;   // device counter slots (see cslot)
     uint32_t* h_counts = nullptr; // pinned host mirror
+    // device-clock launch spans (kTsSlots launch slots x {start, end}, s_memrealtime) + pinned mirror
+    unsigned long long* tstamp = nullptr;
+    unsigned long long* h_tstamp = nullptr;
     uint2* px_extra = nullptr;    // per own pixel: (first extra path - base_paths, count)
     // per-bounce hit sort (wf_sort_*): the hits reordered by key as {o, d, hit, colour} float4 quads,
     // per-(bin, block) counts, per-bin totals
@@ -132,7 +135,15 @@ constexpr int kSortMaxBins = 4096;
 constexpr int kSortBinsDefault = 0;   // off: measured slower on C3g (DESIGN.md §3 'Hit sort')
 // Per-frame measurements of the wavefront pipeline. stage_ms: [0] generate, [1] extend,
 // [2] shade, [3] connect, [4] resolve (+extra-sample bookkeeping), [5] finish, [6] hit sort.
+// Launch slots of the device-clock spans: per pass (base, extra samples) two per round (extend
+// 2k, connect 2k + 1; rounds <= 16) and the finish launch (kTsFinish); the extra pass at kTsPass.
+constexpr int kTsPass = 40, kTsFinish = 33, kTsSlots = 2 * kTsPass;
+// the counter words and, 8-byte aligned after them, the launch spans share one allocation
+constexpr size_t kWfTsOffset = ((size_t)kWfCountWords * 4 + 7) / 8 * 8;
+constexpr size_t kWfCountAllocBytes = kWfTsOffset + (size_t)kTsSlots * 16;
 struct WfFrameStats {
+    float trace_dev_ms, finish_dev_ms;   // device-clock spans of the extend + connect / finish launches
+    int trace_dev_launches, finish_dev_launches;
     float stage_ms[7];
     int iterations;
     unsigned long long trace_rays;  // rays traced by wf_trace launches (extend + connect)

@@ -295,6 +295,15 @@ constexpr int kCntDiagSegs = 27, kCntDiagIters = 28, kCntDiagTime = 29;   // wf_
 // paths; later bulk launches of the pass return at once), [31] the queue the finish launch reads
 constexpr int kCntTailMode = 30, kCntFinishQ = 31;
 
+// Device-clock span of a launch (WfFrameStats::trace_dev_ms): block 0 records the start, every wave
+// its end; ts < 0 (host-driven rounds) records nothing.
+__device__ __forceinline__ void ts_start(const WfParams& Q, int ts) {
+    if (ts >= 0 && blockIdx.x == 0 && threadIdx.x == 0) Q.W.tstamp[2 * ts] = __builtin_amdgcn_s_memrealtime();
+}
+__device__ __forceinline__ void ts_end(const WfParams& Q, int ts) {
+    if (ts >= 0 && lane_id() == 0) atomicMax(&Q.W.tstamp[2 * ts + 1], (unsigned long long)__builtin_amdgcn_s_memrealtime());
+}
+
 // dev_ctl statistics: rounds run, wf_trace launches run, rays they traced
 __device__ __forceinline__ void stat_add(const WfParams& Q, int word, uint32_t v) {
     if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&Q.W.counts[kWfStat + word], v);
@@ -813,7 +822,7 @@ __global__ void __launch_bounds__(kSortThreads) wf_sort_scatter(DevScene S, WfPa
 #endif
 template <bool ANY, bool COUNT>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ANY ? 8 : RT_EXTEND_WAVES, ANY ? 8 : RT_EXTEND_WAVES)))
-wf_trace(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int cur) {
+wf_trace(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int cur, int ts) {
     const FrameParams& P = *Pp;   // per-frame parameters in device memory
     __shared__ int lds_stack[kStackSize * kBlock];
     __shared__ uint4 lds_top[kTopLds * 5];   // BVH top levels (BFS order: root, its children, ...)
@@ -835,6 +844,7 @@ wf_trace(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int cur) {
             }
         }
     }
+    ts_start(Q, ts);
     const uint32_t n_top = stage_top(S, lds_top);
     __syncthreads();
     const ShardPrefix cnt = load_prefix(ANY ? Q.W.counts + cslot(kCntShadowQ) : Q.W.counts + cslot(cur * kShards));
@@ -933,6 +943,7 @@ wf_trace(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int cur) {
             }
         }
     }
+    ts_end(Q, ts);
     flush_counters(P, ANY ? 0 : rays, ANY ? rays : 0, 0, tc, COUNT, overflow, true);
 }
 
@@ -948,7 +959,7 @@ wf_trace(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int cur) {
 // five were measured no faster.
 template <bool COUNT, bool FULL>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 4)))
-wf_finish_step(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int cur) {
+wf_finish_step(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int cur, int ts) {
     const FrameParams& P = *Pp;   // per-frame parameters in device memory
     if (cur < 0) cur = (int)__builtin_amdgcn_readfirstlane(Q.W.counts[cslot(kCntFinishQ)]);   // dev_ctl
     __shared__ int lds_stack[kStackSize * kBlock];
@@ -957,6 +968,7 @@ wf_finish_step(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int c
     __shared__ MatRec lds_mat[kMatLds];
     __shared__ float lds_sray[6][kBlock];   // each lane's shadow ray (origin, direction)
     int* stack = &lds_stack[threadIdx.x];
+    ts_start(Q, ts);
     const uint32_t n_top = stage_top(S, lds_top);
     const ShadeTabs halton = load_tabs(S, lds_halton, lds_mat);   // ends with a block barrier
     const Uniforms& U = P.U;
@@ -1137,6 +1149,7 @@ wf_finish_step(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int c
             atomicAdd(&Q.W.counts[kWfDiagHist + min(dt / 5000u, 63u)], 1u);
         }
     }
+    ts_end(Q, ts);
     flush_counters(P, n_closest, n_shadow, 0, tc, COUNT, overflow);
 }
 
@@ -1289,16 +1302,17 @@ static unsigned trace_grid_cap() {
 // the finish launch: Q.finish_frac percent of the resident grid (frames in flight: the rest of the
 // machine stays free for the other frames' kernels)
 template <bool COUNT, bool FULL>
-static void launch_finish(const DevScene& S, const WfParams& Q, int cur, uint32_t n, hipStream_t stream) {
+static void launch_finish(const DevScene& S, const WfParams& Q, int cur, uint32_t n, hipStream_t stream, int ts) {
     static const unsigned full_cap = resident_grid(wf_finish_step<COUNT, FULL>, 2);
     const unsigned cap = std::max(1u, full_cap * (unsigned)Q.finish_frac / 100u);
-    hipLaunchKernelGGL((wf_finish_step<COUNT, FULL>), dim3(grid_for(n, cap)), dim3(kBlock), 0, stream, S, Q.Pd, Q, cur);
+    hipLaunchKernelGGL((wf_finish_step<COUNT, FULL>), dim3(grid_for(n, cap)), dim3(kBlock), 0, stream, S, Q.Pd, Q, cur,
+                       ts);
 }
 
 static void launch_finish_any(const DevScene& S, const WfParams& Q, bool count, bool full, int cur, uint32_t n,
-                              hipStream_t stream) {
-    if (count) full ? launch_finish<true, true>(S, Q, cur, n, stream) : launch_finish<true, false>(S, Q, cur, n, stream);
-    else full ? launch_finish<false, true>(S, Q, cur, n, stream) : launch_finish<false, false>(S, Q, cur, n, stream);
+                              hipStream_t stream, int ts = -1) {
+    if (count) full ? launch_finish<true, true>(S, Q, cur, n, stream, ts) : launch_finish<true, false>(S, Q, cur, n, stream, ts);
+    else full ? launch_finish<false, true>(S, Q, cur, n, stream, ts) : launch_finish<false, false>(S, Q, cur, n, stream, ts);
 }
 
 static uint32_t queue_total(const uint32_t* h, int q) {
@@ -1349,8 +1363,8 @@ static bool iterate(const DevScene& S, const FrameParams& P, WfParams& Q, int& c
         WF_CHECK(hipEventRecord(W.ev[0], stream));
         unsigned g = grid_for(n, tuning().shade_blocks);
         unsigned gt = grid_for(n, trace_grid_cap());
-        if (count) hipLaunchKernelGGL((wf_trace<false, true>), dim3(gt), dim3(kBlock), 0, stream, S, Q.Pd, Q, cur);
-        else hipLaunchKernelGGL((wf_trace<false, false>), dim3(gt), dim3(kBlock), 0, stream, S, Q.Pd, Q, cur);
+        if (count) hipLaunchKernelGGL((wf_trace<false, true>), dim3(gt), dim3(kBlock), 0, stream, S, Q.Pd, Q, cur, -1);
+        else hipLaunchKernelGGL((wf_trace<false, false>), dim3(gt), dim3(kBlock), 0, stream, S, Q.Pd, Q, cur, -1);
         WF_CHECK(hipEventRecord(W.ev[1], stream));
         const bool sort = Q.sort_bins != 0;
         if (sort) {
@@ -1367,8 +1381,8 @@ static bool iterate(const DevScene& S, const FrameParams& P, WfParams& Q, int& c
             else hipLaunchKernelGGL((wf_shade<false, false>), dim3(g), dim3(kBlock), 0, stream, S, Q.Pd, Q, cur);
         }
         WF_CHECK(hipEventRecord(W.ev[2], stream));
-        if (count) hipLaunchKernelGGL((wf_trace<true, true>), dim3(gt), dim3(kBlock), 0, stream, S, Q.Pd, Q, cur);
-        else hipLaunchKernelGGL((wf_trace<true, false>), dim3(gt), dim3(kBlock), 0, stream, S, Q.Pd, Q, cur);
+        if (count) hipLaunchKernelGGL((wf_trace<true, true>), dim3(gt), dim3(kBlock), 0, stream, S, Q.Pd, Q, cur, -1);
+        else hipLaunchKernelGGL((wf_trace<true, false>), dim3(gt), dim3(kBlock), 0, stream, S, Q.Pd, Q, cur, -1);
         WF_CHECK(hipGetLastError());
         WF_CHECK(hipEventRecord(W.ev[3], stream));
         WF_CHECK(hipMemcpyAsync(W.h_counts, W.counts, kWfCountWords * sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
@@ -1452,13 +1466,13 @@ static int rounds_for(uint64_t paths, uint32_t tail) {
 }
 
 static bool enqueue_pass(const DevScene& S, const FrameParams& P, const WfParams& Q, int rounds, bool count, bool full,
-                         Enqueue& E, const char** err) {
+                         int ts, Enqueue& E, const char** err) {
     hipStream_t stream = E.stream;
     const unsigned gt = trace_grid_cap(), g = tuning().shade_blocks;
     for (int k = 0; k < rounds; ++k) {
         const int cur = k & 1;
-        if (count) hipLaunchKernelGGL((wf_trace<false, true>), dim3(gt), dim3(kBlock), 0, stream, S, Q.Pd, Q, cur);
-        else hipLaunchKernelGGL((wf_trace<false, false>), dim3(gt), dim3(kBlock), 0, stream, S, Q.Pd, Q, cur);
+        if (count) hipLaunchKernelGGL((wf_trace<false, true>), dim3(gt), dim3(kBlock), 0, stream, S, Q.Pd, Q, cur, ts + 2 * k);
+        else hipLaunchKernelGGL((wf_trace<false, false>), dim3(gt), dim3(kBlock), 0, stream, S, Q.Pd, Q, cur, ts + 2 * k);
         if (!E.span(1, err)) return false;
         if (Q.sort_bins) {
             hipLaunchKernelGGL(wf_sort_hist, dim3(kSortBlocks), dim3(kSortThreads), 0, stream, S, Q, cur);
@@ -1474,13 +1488,13 @@ static bool enqueue_pass(const DevScene& S, const FrameParams& P, const WfParams
             else hipLaunchKernelGGL((wf_shade<false, false>), dim3(g), dim3(kBlock), 0, stream, S, Q.Pd, Q, cur);
         }
         if (!E.span(2, err)) return false;
-        if (count) hipLaunchKernelGGL((wf_trace<true, true>), dim3(gt), dim3(kBlock), 0, stream, S, Q.Pd, Q, cur);
-        else hipLaunchKernelGGL((wf_trace<true, false>), dim3(gt), dim3(kBlock), 0, stream, S, Q.Pd, Q, cur);
+        if (count) hipLaunchKernelGGL((wf_trace<true, true>), dim3(gt), dim3(kBlock), 0, stream, S, Q.Pd, Q, cur, ts + 2 * k + 1);
+        else hipLaunchKernelGGL((wf_trace<true, false>), dim3(gt), dim3(kBlock), 0, stream, S, Q.Pd, Q, cur, ts + 2 * k + 1);
         if (!E.span(3, err)) return false;
     }
     // the finish chunk counter is zero here: the frame start clears every counter and the
     // extra-sample pass clears it again before its own finish launch
-    launch_finish_any(S, Q, count, full, -1, 1u << 30, stream);   // resident grid; input queue from the counters
+    launch_finish_any(S, Q, count, full, -1, 1u << 30, stream, ts + kTsFinish);   // resident grid; input queue from the counters
     WF_CHECK(hipGetLastError());
     return E.span(5, err);
 }
@@ -1495,13 +1509,13 @@ static bool record_base(const DevScene& S, const FrameParams& P, WfParams& Q, bo
     Enqueue E{T, stream, capture};
     T.n_ev = T.n_spans = 0;
     if (!E.mark(err)) return false;
-    WF_CHECK(hipMemsetAsync(W.counts, 0, kWfCountWords * sizeof(uint32_t), stream));
+    WF_CHECK(hipMemsetAsync(W.counts, 0, kWfCountAllocBytes, stream));   // counters and launch spans
     const int rounds = rounds_for(Q.base_paths, Q.tail);
     Q.finish_q = rounds & 1;
     hipLaunchKernelGGL(wf_generate, dim3(grid_for(Q.base_paths, 16384)), dim3(kBlock), 0, stream, S, Q.Pd, Q);
     WF_CHECK(hipGetLastError());
     if (!E.span(0, err)) return false;
-    if (!enqueue_pass(S, P, Q, rounds, count, full, E, err)) return false;
+    if (!enqueue_pass(S, P, Q, rounds, count, full, 0, E, err)) return false;
     hipLaunchKernelGGL(wf_motion, dim3(grid_for(Q.own_pixels, 1u << 30)), dim3(kBlock), 0, stream, S, Q.Pd, Q);
     WF_CHECK(hipGetLastError());
     return E.span(4, err);
@@ -1523,13 +1537,13 @@ static bool record_rest(const DevScene& S, const FrameParams& P, WfParams& Q, bo
         hipLaunchKernelGGL(wf_extra, dim3(grid_for(Q.own_pixels, 1u << 30)), dim3(kBlock), 0, stream, S, Q.Pd, Q, 0);
         WF_CHECK(hipGetLastError());
         if (!E.span(4, err)) return false;
-        if (!enqueue_pass(S, P, Q, rounds2, count, full, E, err)) return false;
+        if (!enqueue_pass(S, P, Q, rounds2, count, full, kTsPass, E, err)) return false;
     }
     hipLaunchKernelGGL(wf_resolve, dim3(grid_for(Q.own_pixels, 1u << 30)), dim3(kBlock), 0, stream, S, Q.Pd, Q,
                        with_extra ? 1 : 0);
     WF_CHECK(hipGetLastError());
     if (!E.span(4, err)) return false;
-    WF_CHECK(hipMemcpyAsync(W.h_counts, W.counts, kWfCountWords * sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
+    WF_CHECK(hipMemcpyAsync(W.h_counts, W.counts, kWfCountAllocBytes, hipMemcpyDeviceToHost, stream));
     return true;
 }
 
@@ -1636,6 +1650,20 @@ bool wavefront_collect(const WavefrontBuffers& W, WfTimeline& T, WfFrameStats* f
     fs->trace_rays = W.h_counts[kWfStat + kStatTraceRays];
     fs->trace_closest_rays = W.h_counts[kWfStat + kStatExtendRays];
     fs->finish_launches = (int)W.h_counts[kWfStat + kStatFinish];
+    for (int pass = 0; pass < 2; ++pass)   // device-clock spans (10 ns ticks) of the launches that ran
+        for (int k = 0; k <= kTsFinish; ++k) {
+            const int slot = pass * kTsPass + k;
+            const unsigned long long a = W.h_tstamp[2 * slot], b = W.h_tstamp[2 * slot + 1];
+            if (a == 0 || b <= a) continue;
+            const float ms = (float)((double)(b - a) * 1e-5);
+            if (k == kTsFinish) {
+                fs->finish_dev_ms += ms;
+                fs->finish_dev_launches++;
+            } else if (k < 2 * 16) {
+                fs->trace_dev_ms += ms;
+                fs->trace_dev_launches++;
+            }
+        }
     return true;
 }
 

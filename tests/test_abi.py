@@ -42,7 +42,7 @@ int main(void) {
   O(Light, position); O(Light, coneAngle); O(Light, direction); O(Uniforms, camera); O(Uniforms, previousCamera);
   O(Uniforms, debugTextureMode); O(Uniforms, motionSamplingHighThresholdPixels); O(Material, textureFlags);
   O(rt_mesh_desc, transform); O(rt_mesh_desc, joint_count); O(rt_submesh_desc, material); O(rt_stats, kernel_ms);
-  O(rt_stats, iterations); O(rt_stats, total_kernel_ms); O(rt_stats, total_finish_launches); O(rt_stats, trace_nodes_lds);
+  O(rt_stats, iterations); O(rt_stats, total_kernel_ms); O(rt_stats, total_finish_launches); O(rt_stats, trace_nodes_lds); O(rt_stats, total_finish_dev_launches);
   return 0;
 }''')
     exe = tmp_path / "layout"
@@ -69,7 +69,8 @@ int main(void) {
             "rt_stats.iterations": A.Stats.iterations.offset,
             "rt_stats.total_kernel_ms": A.Stats.total_kernel_ms.offset,
             "rt_stats.total_finish_launches": A.Stats.total_finish_launches.offset,
-            "rt_stats.trace_nodes_lds": A.Stats.trace_nodes_lds.offset}
+            "rt_stats.trace_nodes_lds": A.Stats.trace_nodes_lds.offset,
+            "rt_stats.total_finish_dev_launches": A.Stats.total_finish_dev_launches.offset}
     for k, v in offs.items():
         assert int(out[k]) == v, k
     assert offs["Light.position"] == 16 and offs["Light.direction"] == 112 and offs["Uniforms.camera"] == 32

@@ -292,7 +292,7 @@ int main(int argc, char** argv) {
     Bvh8Result b8;
     for (int limit : {64, 48, 40, 32, 28, 24, 21}) {
         b2 = build_bvh2(world.data(), n, 1, limit);
-        b8 = collapse_bvh8_dp(b2, 1.0f, 0.5f);
+        b8 = collapse_bvh8_dp(b2, 1.0f, getenv("SIM_CPRIM") ? (float)atof(getenv("SIM_CPRIM")) : 0.5f);
         if (b8.max_depth <= 16) break;
     }
     Scene8 S;
