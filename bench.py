@@ -392,12 +392,13 @@ def main():
 
 
 def roofline(a, cst, s0, s1, rays_local, closest_local, kms_local, ms_per_step, cus):
-    """The dominant kernel's algorithmic bytes per launch over its average launch time, with node
-    bytes counted for the nodes fetched from memory only.  The launch time is the
-    device-clock span of each launch in the timed region (first workgroup start to last wave end,
-    s_memrealtime, what rocprofv3's kernel trace records for a dispatch); the HIP-event time around
-    the same launches on their render stream is reported beside it (launch_ms_events): with frames
-    in flight it also counts the time a launch waits for CUs that other frames' kernels hold."""
+    """The dominant kernel's algorithmic bytes per launch over its average launch time (HIP events
+    around each launch on its render stream, over the timed region), with node bytes counted for
+    the nodes fetched from memory only.  The device-clock span of the same launches
+    (first workgroup start to last wave end, s_memrealtime) is reported beside it
+    (launch_ms_device).  With frames in flight, launches of different frames share the GPU: a
+    launch's span, as rocprofv3's kernel trace records it too, is then longer than it would be
+    alone, and the per-frame kernel times add up to more than the step."""
     d = lambda f: getattr(s1, f) - getattr(s0, f)
     steps = a.steps
     trace_rays, trace_launches, trace_ms = d("total_trace_rays"), d("total_trace_launches"), d("total_trace_ms")
@@ -420,8 +421,9 @@ def roofline(a, cst, s0, s1, rays_local, closest_local, kms_local, ms_per_step, 
         blocks = cus * TRACE_BLOCKS_PER_CU
         kernels.append(dict(
             kernel="rt::wf_trace<{false,true}, false> (extend + connect)", launches=trace_launches / steps,
-            launch_ms=trace_dev_ms / trace_dev_launches if trace_dev_launches else trace_ms / trace_launches,
-            launch_ms_events=trace_ms / trace_launches, rays_per_launch=rpl, nodes_per_ray=q_nodes,
+            launch_ms=trace_ms / trace_launches,
+            launch_ms_device=trace_dev_ms / trace_dev_launches if trace_dev_launches else None,
+            rays_per_launch=rpl, nodes_per_ray=q_nodes,
             lds_nodes_per_ray=q_nodes_lds, tris_per_ray=q_tris,
             bytes_per_launch=rpl * (B_QRAY + (q_nodes - q_nodes_lds) * B_NODE + q_tris * B_TRI)
             + (blocks * TOP_NODES * B_NODE if q_nodes_lds > 0 else 0),
@@ -434,8 +436,9 @@ def roofline(a, cst, s0, s1, rays_local, closest_local, kms_local, ms_per_step, 
         blocks = cus * FINISH_BLOCKS_PER_CU
         kernels.append(dict(
             kernel="rt::wf_finish_step<false, false>", launches=finish_launches / steps,
-            launch_ms=finish_dev_ms / finish_dev_launches if finish_dev_launches else float(stage_ms[5]) / finish_launches,
-            launch_ms_events=float(stage_ms[5]) / finish_launches, rays_per_launch=f_rays, nodes_per_ray=f_nodes,
+            launch_ms=float(stage_ms[5]) / finish_launches,
+            launch_ms_device=finish_dev_ms / finish_dev_launches if finish_dev_launches else None,
+            rays_per_launch=f_rays, nodes_per_ray=f_nodes,
             lds_nodes_per_ray=f_nodes_lds, tris_per_ray=f_tris,
             bytes_per_launch=f_rays * (B_RAY + (f_nodes - f_nodes_lds) * B_NODE + f_tris * B_TRI) + f_closest * B_HIT
             + (blocks * TOP_NODES * B_NODE if f_nodes_lds > 0 else 0),
@@ -448,7 +451,7 @@ def roofline(a, cst, s0, s1, rays_local, closest_local, kms_local, ms_per_step, 
         b = (rpl * (B_RAY + npr * B_NODE + tpr * B_TRI) + closest_local / steps * B_HIT
              + a.width * a.height / max(1, int(os.environ.get("WORLD_SIZE", "1"))) * B_PIXEL)
         kernels.append(dict(kernel="rt::megakernel<false, false>", launches=1, launch_ms=kms_local,
-                            launch_ms_events=kms_local, rays_per_launch=rpl,
+                            launch_ms_device=None, rays_per_launch=rpl,
                             nodes_per_ray=npr, lds_nodes_per_ray=0.0, tris_per_ray=tpr, bytes_per_launch=b,
                             bytes_all_nodes=b))
     for k in kernels:
@@ -485,25 +488,21 @@ def roofline(a, cst, s0, s1, rays_local, closest_local, kms_local, ms_per_step, 
         "l2_hit_sorted": sorted_l2_hit(),
         "job_achieved": round(job_achieved, 1), "job_frac": round(job_achieved / HBM_PEAK_GBS, 4),
         "job_bytes_per_frame": int(job_bytes),
-        "kernel": dom["kernel"], "launch_ms": round(dom["launch_ms"], 4), "launch_ms_events": round(dom["launch_ms_events"], 4),
-        "timing": "device clock" if trace_dev_launches else "hip events",
+        "kernel": dom["kernel"], "launch_ms": round(dom["launch_ms"], 4),
+        "launch_ms_device": round(dom["launch_ms_device"], 4) if dom["launch_ms_device"] else None,
         "bytes_per_launch": int(dom["bytes_per_launch"]),
         "rays_per_launch": int(dom["rays_per_launch"]), "nodes_per_ray": round(dom["nodes_per_ray"], 3),
         "lds_nodes_per_ray": round(dom["lds_nodes_per_ray"], 3), "tris_per_ray": round(dom["tris_per_ray"], 3),
         # every timed kernel of the frame with its own roofline, for comparison
         "kernels": [{"kernel": k["kernel"], "ms_per_frame": round(k["ms_per_frame"], 3),
-                     "launch_ms": round(k["launch_ms"], 4), "launch_ms_events": round(k["launch_ms_events"], 4),
+                     "launch_ms": round(k["launch_ms"], 4),
+                     "launch_ms_device": round(k["launch_ms_device"], 4) if k["launch_ms_device"] else None,
                      "achieved_GBs": round(k["achieved"], 1),
                      "frac": round(k["achieved"] / HBM_PEAK_GBS, 4), "nodes_per_ray": round(k["nodes_per_ray"], 3),
                      "lds_nodes_per_ray": round(k["lds_nodes_per_ray"], 3),
                      "tris_per_ray": round(k["tris_per_ray"], 3)} for k in kernels],
         "_stage_ms": list(stage_ms[:7] / steps),
     }
-    if not trace_dev_launches and dom["ms_per_frame"] > ms_per_step:
-        # timed by HIP events only: with frames in flight the event pairs of a launch also count the
-        # time it waits for CUs held by the other frames; when the dominant kernel's summed event
-        # time exceeds the step, achieved / frac are not a kernel measurement
-        r["not_a_kernel_measurement"] = True
     return r
 
 

@@ -125,11 +125,11 @@ typedef struct rt_opts {
                            sort), < 0 = no sort.  Never changes the image, only memory locality. */
     int32_t frames_in_flight; /* wavefront on the context's own stream: frames rendered concurrently,
                                  each overlapping the previous one until it needs that frame's
-                                 accumulation / motion output; 0 = default (2, or for frames
-                                 that allocate fewer than 8M paths, pixels x (spp + extra
-                                 samples), e.g. a multi-GPU rank's share, 8 when the process has
-                                 GPU_MAX_HW_QUEUES >= 8 and 4 otherwise), 1 = one at a time, at
-                                 most 8.  Each slot holds ~300 B per allocated path.  Four slots
+                                 accumulation / motion output; 0 = default (one per hardware
+                                 queue: 8 when the process has GPU_MAX_HW_QUEUES >= 8, 4
+                                 otherwise, as many as fit in 96 GB, at least 2), 1 = one at a
+                                 time, at most 8.  Each slot holds ~300 B per allocated path,
+                                 pixels x (spp + extra samples).  Four slots
                                  on a frame of 6M+ base paths give the finish tail 25 % of the
                                  grid (20 % below: the rank-share sweep).
                                  Geometry updates (skinning, transforms, refit, builds) rotate

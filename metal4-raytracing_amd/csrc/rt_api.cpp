@@ -77,14 +77,13 @@ constexpr int kGens = kMaxSlots;   // generations allocated at most (ngens of th
 // Final round-2 kernels, 8-way share with four slots: 256K 4.14 / 4.13, 512K 4.25 / 4.26, 768K
 // 4.32 / 4.30 Grays/s per rank -> 768K for four slots.
 constexpr int kTailInFlight[kMaxSlots + 1] = {0, 0, 1310720, 1048576, 786432, 524288, 524288, 524288, 524288};
-// paths a frame allocates (pixels x (spp + motion-adaptive extra samples), what ensure_wavefront
-// sizes a slot for): below, four or eight frames in flight by default (small_frame_slots).  Every 1080p x 4 spp frame (8.29M
-// base paths) stays at two; a 2-way rank share of it with the default two extra samples (6.2M)
-// and the 720p x 4 frame of configs[1] (5.5M) take four.  A slot costs ~300 B per allocated path
-// (128 B path state and ray slots + 176 B of queues), 3.7 GB for 12.4M paths.
-constexpr uint64_t kSmallFrame = 8000000;
+// Default frames in flight (render_frame): their buffers, ~300 B per allocated path (pixels x (spp +
+// motion-adaptive extra samples)) and slot (128 B path state and ray slots + 176 B of queues), stay
+// within kSlotBudget of the 288 GB (1080p x 4 + 2 extra: 3.7 GB a slot; configs[3]'s 3840x2160x16
+// frame on one GPU: 40 GB a slot, two slots).
+constexpr uint64_t kSlotBudget = 96ull << 30, kSlotBytesPerPath = 300;
 constexpr int kMotionTargets = kMaxSlots + 1;
-// Slots for a small frame: eight when the HIP runtime gives the process at least eight hardware
+// Default slots: eight when the HIP runtime gives the process at least eight hardware
 // queues (GPU_MAX_HW_QUEUES, read once; HIP's default is 4), so every slot's stream has a queue of
 // its own; four otherwise (more streams than queues serialise unrelated frames: eight slots on
 // four queues measured 2.85 against 3.54 Grays/s per rank).  8-way rank share of C3g, eight
@@ -994,17 +993,20 @@ rt_status rt_render_frame(rt_ctx* c, const Uniforms* U, const rt_tile_set* tiles
     bool wavefront = c->pipeline == RT_PIPELINE_WAVEFRONT && U->debugTextureMode != DebugTextureModeMotion;
     // Frames in flight (Renderer.swift:1406-1409): wavefront frames on the context's own stream
     // rotate over the frames-in-flight slots; a caller's stream and the megakernel keep one.
-    //  By default two, four for frames of fewer than kSmallFrame allocated paths (a multi-GPU
-    // rank's share of the 1080p frame, the 720p frame): the finish tail's fixed latency dominates a
-    // small frame, and more overlapping frames fill it (C3g per rank, 2 / 3 / 4 slots: 2-way split
-    // 4.52 / 5.15 / 5.49, 8-way 2.30 / 2.73 / 2.92 Grays/s per GPU; configs[1] 720p on one GPU,
-    // 3 / 4 slots: 5.95 / 7.38; 5 and 6 slots measured slower)
+    //  By default one slot per hardware queue the HIP runtime gives the process (four, eight with
+    // GPU_MAX_HW_QUEUES >= 8), as many as fit in kSlotBudget, at least two: the finish tail's
+    // latency-bound launch and the bulk rounds of the other frames fill each other's gaps (round 3,
+    // C3g 1080p x 4 on one MI355X, 2 / 3 / 4 slots: 7.46-7.49 / 7.91-7.94 / 8.36-8.44 Grays/s;
+    // 5 / 6 slots on four queues 7.23-7.28 / 7.59-7.67, 6 / 8 slots on eight queues 8.15-8.24 /
+    // 8.34-8.37; configs[1] 720p, 3 / 4 slots: 5.95 / 7.38 in round 2)
     const int spp = std::max(U->samplesPerPixel, 1);
     const int max_extra = U->enableMotionAdaptiveSampling ? std::max(U->motionSamplingMaxExtraSamples, 0) : 0;
     int nfl = 1;
     if (wavefront && c->stream == c->own_stream) {
         const uint64_t frame_paths = (uint64_t)own * ts * ts * (uint64_t)(spp + max_extra);
-        nfl = c->max_in_flight > 0 ? c->max_in_flight : (frame_paths < kSmallFrame ? small_frame_slots() : 2);
+        nfl = c->max_in_flight > 0 ? c->max_in_flight
+                                   : (int)std::max<uint64_t>(2, std::min<uint64_t>(small_frame_slots(),
+                                                                              kSlotBudget / (frame_paths * kSlotBytesPerPath + 1)));
     }
     const int k = c->frame_no > 0 ? (c->last_slot + 1) % nfl : 0;
     FrameSlot& F = c->slot[k];

@@ -1693,11 +1693,11 @@ bool run_wavefront(const DevScene& S, const FrameParams& P, WavefrontBuffers& W,
     Q.tile_px_div = make_fastdiv((uint32_t)P.tile_size * (uint32_t)P.tile_size);
     Q.tiles_x_div = make_fastdiv((uint32_t)max(P.tiles_x, 1));
     // frames in flight: the finish tail takes part of the resident grid and leaves the rest to the
-    // other frames' bulk rounds (C3g sweeps, DESIGN.md §3: two slots 40 %; four slots on a small
-    // frame, a multi-GPU rank's share, 20 %; else 1 / in_flight); one frame at a time: all of it
+    // other frames' bulk rounds (C3g sweeps, DESIGN.md §3: two slots 40 %; four or more 20 %: C3g
+    // with four slots 20 / 25 / 33 % 8.49-8.54 / 8.21-8.50 / 8.28-8.36 Grays/s, and a multi-GPU
+    // rank's share; three 33 %); one frame at a time: all of it
     Q.finish_frac = tu.finish_frac > 0 ? tu.finish_frac
-                  : (in_flight >= 4 && Q.base_paths < (6u << 20)) ? 20
-                  : in_flight == 2 ? 40 : (in_flight > 1 ? 100 / in_flight : 100);
+                  : in_flight >= 4 ? 20 : in_flight == 2 ? 40 : (in_flight > 1 ? 100 / in_flight : 100);
     if (sort_bins && (sort_bins < kSortMinBins || sort_bins > kSortMaxBins || (sort_bins & (sort_bins - 1)) ||
                       !S.tri_bin || !W.sorted)) {
         *err = "bad hit-sort configuration";

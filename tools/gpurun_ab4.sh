@@ -19,7 +19,7 @@ for i in $(seq ${REPS:-3}); do
 import json,sys
 d=json.loads([x for x in open(sys.argv[1]) if x.startswith('{')][-1])
 r=d['roofline']
-print(sys.argv[2], d['value'], d['ms_per_step'], 'frac', r['frac'], [(k['kernel'][:12], k['launch_ms'], k.get('launch_ms_events'), k['nodes_per_ray']) for k in r['kernels']], d['config']['stage_ms'])" gpurun_out/lab_$name$i.log "$name $i"
+print(sys.argv[2], d['value'], d['ms_per_step'], 'frac', r['frac'], [(k['kernel'][:12], k['launch_ms'], k.get('launch_ms_device'), k['nodes_per_ray']) for k in r['kernels']], d['config']['stage_ms'])" gpurun_out/lab_$name$i.log "$name $i"
   done
 done
 restore
