@@ -75,7 +75,8 @@ rt_status rt_scene_set_lights(rt_scene* scene, const Light* lights, uint32_t cou
 /* Scene.setLightIntensity (Scene.swift:57-63). */
 rt_status rt_scene_set_light_intensity(rt_scene* scene, float intensity);
 
-/* Benchmark / parity presets: "c1", "c2", "c3", "c3g", "c3d", "c5", "app".
+/* Benchmark / parity presets: "c1", "c2", "c3", "c3g", "c3d", "c5", "app"; "c3r" (the
+ * reference's coatball / teapot meshes in the dragon's place, glass: an irregular-geometry check). 
  * `asset_dir` holds the OBJ/MTL files (plane.obj, sphere.obj, ...); a real dragon.obj /
  * bunny.obj / robot.usdz found there is loaded instead of the procedural stand-in unless the
  * preset name ends in "_synthetic". *is_synthetic reports whether a stand-in was used. */

@@ -1458,6 +1458,21 @@ rt_status rt_scene_preset(const char* name_c, const char* asset_dir_c, rt_scene*
         std::string mtl = dir + "/dragon.mtl";
         if (!(st = rt_scene_add_procedural(s, "knot", file_exists(mtl) ? mtl.c_str() : nullptr, pos, rot, 1.2f, &glass)))
             st = base();
+    } else if (name == "c3r") {
+        // Irregular-geometry cross-check of the headline (not a BASELINE config): the reference's own
+        // modelled / scanned meshes in the dragon's place at about its triangle count, glass like
+        // C3g: a 4 x 4 wall of coatballs (AssetResources/coatball, 46,816 triangles each, ~12 units
+        // across) and a row of 8 teapots (15,704 triangles each) in front of it: 874,688 triangles.
+        for (int j = 0; j < 4 && !st; ++j)
+            for (int i = 0; i < 4 && !st; ++i) {
+                float p[3] = {0.3f + (i - 1.5f) * 0.27f, 0.50f + (j - 1.5f) * 0.2f, 2.5f};
+                st = rt_scene_add_obj(s, (dir + "/coatball/coatball.obj").c_str(), p, zero, 0.016f, &glass);
+            }
+        for (int k = 0; k < 8 && !st; ++k) {
+            float p[3] = {0.3f + (k - 3.5f) * 0.17f, 0.0f, 2.75f};
+            st = rt_scene_add_obj(s, (dir + "/teapot.obj").c_str(), p, zero, 0.001f, &glass);
+        }
+        if (!st) st = base();
     } else if (name == "c5" || name == "app") {
         float rp[3] = {-0.5f, 0.0f, 1.0f};
         const std::string robot = dir + "/robot.usdz";

@@ -36,6 +36,11 @@ def test_bench_line_contract():
     # a small frame (< 8M allocated paths) keeps four frames in flight: bench.py fixes HIP's
     # hardware queues at four (rt_api.cpp small_frame_slots)
     assert d["config"]["frames_in_flight"] == 4
+    # with frames in flight the line carries the traversal launches measured alone (one frame in
+    # flight, after the timed region) and says whether the shared-GPU launch time is a kernel time
+    iso = r["isolated"]
+    assert iso["frames_in_flight"] == 1 and iso["launch_ms"] > 0 and 0 < iso["frac"] < 1
+    assert isinstance(r["not_a_kernel_measurement"], bool)
 
 
 def test_bench_emulated_rank_and_animation():

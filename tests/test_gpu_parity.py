@@ -66,6 +66,20 @@ def test_glass_dragon_parity(rt, orc, assets, pipeline):
 
 
 @pytest.mark.parametrize("pipeline", PIPELINES)
+def test_real_meshes_parity(rt, orc, assets, pipeline):
+    """C3r: the reference's own coatball / teapot meshes (irregular, modelled geometry, 884k
+    triangles, glass) in the dragon's place, 8 bounces (the irregular-geometry cross-check of the
+    headline's procedural stand-in)."""
+    (g, gd, gm, st, o), = _render_pair(rt, orc, "c3r", 128, 72, assets, samplesPerPixel=2, maxBounces=8,
+                                       pipeline=pipeline)
+    rep = parity_report(g, o["radiance"])
+    print(rep, st.closest_rays, st.shadow_rays)
+    assert rep["n_bad"] == 0, rep
+    assert np.array_equal(gd, o["depth"]) and np.array_equal(gm, o["motion"])
+    assert st.closest_rays == o["closest_rays"] and st.shadow_rays == o["shadow_rays"]
+
+
+@pytest.mark.parametrize("pipeline", PIPELINES)
 def test_bunny_parity(rt, orc, assets, pipeline):
     (g, gd, gm, st, o), = _render_pair(rt, orc, "c2", 80, 45, assets, samplesPerPixel=2, maxBounces=4,
                                        pipeline=pipeline)

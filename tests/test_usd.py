@@ -405,7 +405,8 @@ def test_preset_c5_loads_a_real_robot_usdz(rt, assets, files, tmp_path):
     """A robot.usdz in the asset directory replaces the procedural stand-in at AppScene's robot
     slot (AppScene.swift:15, scale 0.01), like dragon.obj / bunny.obj do for theirs."""
     for f in os.listdir(assets):
-        shutil.copy(os.path.join(assets, f), tmp_path / f)
+        if os.path.isfile(os.path.join(assets, f)):
+            shutil.copy(os.path.join(assets, f), tmp_path / f)
     shutil.copy(files["robot_c.usdz"], tmp_path / "robot.usdz")
     s = rt.Scene.preset("c5", str(tmp_path))
     assert not s.synthetic
