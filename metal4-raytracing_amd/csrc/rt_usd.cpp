@@ -1,5 +1,6 @@
 // rt_usd.cpp — USD layer readers (.usda text, .usdc crate, .usdz package); see rt_usd.h.
 #include "rt_usd.h"
+#include <set>
 
 #include <zlib.h>
 
@@ -34,6 +35,19 @@ int Stage::add_prim(int parent, const std::string& name) {
     prims.push_back(p);
     const int id = (int)prims.size() - 1;
     prims[parent].children.push_back(id);
+    by_path[path] = id;
+    return id;
+}
+
+int Stage::add_detached(const std::string& path) {
+    auto it = by_path.find(path);
+    if (it != by_path.end()) return it->second;
+    Prim p;
+    const size_t k = path.find_last_of('/');
+    p.name = k == std::string::npos ? path : path.substr(k + 1);
+    p.path = path;
+    prims.push_back(p);
+    const int id = (int)prims.size() - 1;
     by_path[path] = id;
     return id;
 }
@@ -321,17 +335,78 @@ private:
         }
     }
 
-    bool meta_entries(const std::function<void(const std::string&, const Value&)>& on) {
+    // a reference / payload / sublayer list: None, one item or [items]; an item is @asset@, </path>
+    // or @asset@</path>, optionally followed by a (layer offset / custom data) group
+    bool arc_list(std::vector<Arc>& out) {
+        if (is_ident({"None"})) { lx_.next(); return true; }
+        const bool list = is_punct("[");
+        if (list) lx_.next();
+        while (!(list && is_punct("]"))) {
+            Arc a;
+            if (lx_.peek().t == Tok::kAsset) a.asset = lx_.next().s;
+            if (lx_.peek().t == Tok::kPath) a.path = lx_.next().s;
+            else if (a.asset.empty()) { msg_ = "expected a reference"; return false; }
+            if (is_punct("(") && !skip_group()) return false;
+            out.push_back(a);
+            if (!list) return true;
+            if (is_punct(",")) lx_.next();
+            else if (!is_punct("]")) { msg_ = "expected ',' or ']'"; return false; }
+        }
+        lx_.next();
+        return true;
+    }
+    // variants = { string set = "variant" ... }
+    bool variant_selection(int id) {
+        if (!expect("{")) return false;
+        while (!is_punct("}")) {
+            if (is_punct(";")) { lx_.next(); continue; }
+            if (lx_.peek().t == Tok::kIdent && lx_.peek(1).t != Tok::kPunct) lx_.next();   // value type
+            const Tok set = lx_.next();
+            if (set.t != Tok::kIdent && set.t != Tok::kStr) { msg_ = "expected a variant set name"; return false; }
+            if (!expect("=")) return false;
+            const Tok var = lx_.next();
+            if (var.t != Tok::kStr) { msg_ = "expected a variant name"; return false; }
+            st_.prims[id].variant_sel[set.s] = var.s;
+        }
+        lx_.next();
+        return true;
+    }
+
+    // arcs_for: -2 plain metadata, -1 the layer's (subLayers), >= 0 a prim's (references, payload,
+    // variants)
+    bool meta_entries(const std::function<void(const std::string&, const Value&)>& on, int arcs_for = -2) {
         if (!expect("(")) return false;
         while (!is_punct(")")) {
             const Tok& t = lx_.peek();
             if (t.t == Tok::kStr) { lx_.next(); continue; }   // doc string
             if (t.t == Tok::kPunct && t.s == ";") { lx_.next(); continue; }
             if (t.t != Tok::kIdent) { msg_ = "bad metadata"; return false; }
-            if (is_ident({"prepend", "append", "add", "delete", "reorder"}) && lx_.peek(1).t == Tok::kIdent) lx_.next();
+            std::string op;
+            if (is_ident({"prepend", "append", "add", "delete", "reorder"}) && lx_.peek(1).t == Tok::kIdent) op = lx_.next().s;
             std::string key = lx_.next().s;
             if (lx_.peek().t == Tok::kIdent && !is_punct("=")) key = lx_.next().s;   // typed dictionary entry
             if (!expect("=")) return false;
+            if (arcs_for >= -1 && (key == "references" || key == "payload" || key == "subLayers" || key == "inherits" ||
+                                   key == "specializes")) {
+                std::vector<Arc> arcs;
+                if (!arc_list(arcs)) return false;
+                if (op == "delete" || op == "reorder") continue;
+                if (arcs_for == -1 && key == "subLayers")
+                    for (const Arc& a : arcs) st_.sublayers.push_back(a.asset);
+                if (arcs_for >= 0 && key == "references") {
+                    auto& r = st_.prims[arcs_for].references;
+                    r.insert(op == "prepend" ? r.begin() : r.end(), arcs.begin(), arcs.end());
+                }
+                if (arcs_for >= 0 && key == "payload") {
+                    auto& r = st_.prims[arcs_for].payloads;
+                    r.insert(op == "prepend" ? r.begin() : r.end(), arcs.begin(), arcs.end());
+                }
+                continue;   // inherits / specializes: class arcs, not followed
+            }
+            if (arcs_for >= 0 && key == "variants") {
+                if (!variant_selection(arcs_for)) return false;
+                continue;
+            }
             Value v;
             if (!value(v)) return false;
             on(key, v);
@@ -348,7 +423,7 @@ private:
                 if (k == "timeCodesPerSecond" || !tcps_set_) st_.time_codes_per_second = v.num[0];
                 if (k == "timeCodesPerSecond") tcps_set_ = true;
             }
-        });
+        }, -1);
     }
     bool tcps_set_ = false;
 
@@ -362,25 +437,42 @@ private:
         const std::string name = lx_.next().s;
         const int id = st_.add_prim(parent, name);
         if (!type.empty()) st_.prims[id].type = type;
-        if (is_punct("(")) {
-            if (!meta_entries([this, id](const std::string& k, const Value& v) {
-                    Prim& p = st_.prims[id];
-                    if (k == "apiSchemas")
-                        for (const auto& s : v.str) p.api_schemas.push_back(s);
-                    if (k == "active" && v.kind == Value::kNum && !v.num.empty()) p.active = v.num[0] != 0.0;
-                }))
-                return false;
-        }
+        if (is_punct("(") && !prim_meta(id)) return false;
+        return prim_body(id);
+    }
+    bool prim_meta(int id) {
+        return meta_entries([this, id](const std::string& k, const Value& v) {
+            Prim& p = st_.prims[id];
+            if (k == "apiSchemas")
+                for (const auto& s : v.str) p.api_schemas.push_back(s);
+            if (k == "active" && v.kind == Value::kNum && !v.num.empty()) p.active = v.num[0] != 0.0;
+        }, id);
+    }
+    // { properties, child prims, variant sets } of prim id (or of a variant body)
+    bool prim_body(int id) {
         if (!expect("{")) return false;
         while (!is_punct("}")) {
             if (lx_.peek().t == Tok::kEnd) { msg_ = "unterminated prim"; return false; }
             if (is_ident({"def", "over", "class"})) {
                 if (!prim(id)) return false;
             } else if (is_ident({"variantSet"})) {
+                // variantSet "set" = { "variant" (metadata) { body } ... }: each body is kept as a
+                // detached prim "/Prim{set=variant}"; load_stage applies the selected one
+                Nest nest(depth_);
+                if (depth_ > kMaxDepth) { msg_ = "prims nested too deeply"; return false; }
                 lx_.next();
-                lx_.next();   // name
-                if (!expect("=")) return false;
-                if (!skip_group()) return false;
+                const Tok set = lx_.next();
+                if (set.t != Tok::kStr) { msg_ = "expected a variant set name"; return false; }
+                if (!expect("=") || !expect("{")) return false;
+                while (!is_punct("}")) {
+                    const Tok var = lx_.next();
+                    if (var.t != Tok::kStr) { msg_ = "expected a variant name"; return false; }
+                    const int body = st_.add_detached(st_.prims[id].path + "{" + set.s + "=" + var.s + "}");
+                    st_.prims[id].variant_bodies[set.s][var.s] = body;
+                    if (is_punct("(") && !prim_meta(body)) return false;
+                    if (!prim_body(body)) return false;
+                }
+                lx_.next();
             } else if (is_ident({"reorder"})) {
                 lx_.next();
                 lx_.next();
@@ -1232,6 +1324,203 @@ static bool parse_layer(const uint8_t* data, size_t n, Stage& st, std::string& e
     return false;
 }
 
+// ---- composition ------------------------------------------------------------------------------
+namespace {
+
+constexpr int kMaxArcDepth = 16;              // nested layer loads (sublayer / reference chains)
+constexpr size_t kMaxComposedPrims = 1u << 17;  // prims a composition may create (hostile fan-out)
+
+std::string dir_of(const std::string& id) {
+    const size_t k = id.find_last_of('/');
+    return k == std::string::npos ? std::string() : id.substr(0, k + 1);
+}
+// collapses "." and ".." segments (a leading "/" is kept)
+std::string normalize(const std::string& p) {
+    std::vector<std::string> seg;
+    size_t b = 0;
+    while (b <= p.size()) {
+        size_t e = p.find('/', b);
+        if (e == std::string::npos) e = p.size();
+        const std::string x = p.substr(b, e - b);
+        if (x == "..") { if (!seg.empty() && seg.back() != "..") seg.pop_back(); else seg.push_back(x); }
+        else if (!x.empty() && x != ".") seg.push_back(x);
+        b = e + 1;
+    }
+    std::string out = !p.empty() && p[0] == '/' ? "/" : "";
+    for (size_t k = 0; k < seg.size(); ++k) out += (k ? "/" : "") + seg[k];
+    return out;
+}
+// a path of the source subtree rooted at `from`, moved under `to`
+std::string remap(const std::string& x, const std::string& from, const std::string& to) {
+    if (from.empty() || from == to || x.compare(0, from.size(), from) != 0) return x;
+    if (x.size() > from.size() && x[from.size()] != '/' && x[from.size()] != '.') return x;
+    return to + x.substr(from.size());
+}
+
+class Composer {
+public:
+    explicit Composer(const std::vector<PackageFile>* pkg) : pkg_(pkg) {}
+    std::string err;
+
+    // layer `id` parsed and composed into `out`
+    bool load(const std::string& id, Stage& out, int depth) {
+        if (depth > kMaxArcDepth) return fail("composition nested deeper than " + std::to_string(kMaxArcDepth) + " layers");
+        auto c = cache_.find(id);
+        if (c != cache_.end()) { out = c->second; return true; }
+        if (loading_.count(id)) return fail("composition cycle through " + id);
+        std::vector<uint8_t> data;
+        if (!read(id, data)) return fail("cannot open layer " + id);
+        Stage L;
+        std::string e;
+        if (!parse_layer(data.data(), data.size(), L, e)) return fail(id + ": " + e);
+        loading_.insert(id);
+        const bool ok = compose(id, L, depth);
+        loading_.erase(id);
+        if (!ok) return false;
+        cache_[id] = L;
+        out = std::move(L);
+        return true;
+    }
+
+    // sublayers under the layer's own opinions, then every prim's arcs in namespace order
+    bool compose(const std::string& id, Stage& L, int depth) {
+        const std::vector<std::string> subs = L.sublayers;
+        L.sublayers.clear();
+        for (const std::string& sub : subs) {
+            Stage S;
+            if (!load(resolve(id, sub), S, depth + 1)) return false;
+            if (!merge(L, 0, S, 0, "", "")) return false;
+            if (L.default_prim.empty()) L.default_prim = S.default_prim;
+        }
+        std::vector<int> todo{0};
+        while (!todo.empty()) {
+            const int p = todo.back();
+            todo.pop_back();
+            if (!apply_arcs(id, L, p, depth)) return false;
+            const std::vector<int>& ch = L.prims[p].children;
+            for (auto it = ch.rbegin(); it != ch.rend(); ++it) todo.push_back(*it);
+        }
+        return true;
+    }
+
+private:
+    const std::vector<PackageFile>* pkg_;
+    std::set<std::string> loading_;
+    std::map<std::string, Stage> cache_;
+    size_t budget_ = kMaxComposedPrims;
+
+    bool fail(const std::string& m) {
+        err = m;
+        return false;
+    }
+    // an asset path relative to the layer naming it (inside the package for a .usdz)
+    std::string resolve(const std::string& from, const std::string& asset) const {
+        if (!asset.empty() && asset[0] == '/') return normalize(pkg_ ? asset.substr(1) : asset);
+        return normalize(dir_of(from) + asset);
+    }
+    bool read(const std::string& id, std::vector<uint8_t>& data) const {
+        if (pkg_) {
+            for (const PackageFile& f : *pkg_)
+                if (normalize(f.name) == id) { data = f.data; return true; }
+            return false;
+        }
+        FILE* f = std::fopen(id.c_str(), "rb");
+        if (!f) return false;
+        uint8_t buf[1 << 16];
+        size_t k;
+        while ((k = std::fread(buf, 1, sizeof buf, f)) > 0) data.insert(data.end(), buf, buf + k);
+        std::fclose(f);
+        return true;
+    }
+
+    // Prim s of S (and its subtree) merged into prim d of D as the weaker opinion: only what D does
+    // not author is taken; paths under `from` move under `to`.  S may be D (a variant body).
+    bool merge(Stage& D, int d, const Stage& S, int s, const std::string from, const std::string to) {   // paths by value: D.prims may move
+        std::vector<std::pair<int, int>> work{{d, s}};
+        while (!work.empty()) {
+            const auto [dd, ss] = work.back();
+            work.pop_back();
+            const Prim src = S.prims[ss];   // a copy: D's prims may move below when S is D
+            Prim& dp = D.prims[dd];
+            if (dp.type.empty()) dp.type = src.type;
+            for (const std::string& a : src.api_schemas)
+                if (std::find(dp.api_schemas.begin(), dp.api_schemas.end(), a) == dp.api_schemas.end()) dp.api_schemas.push_back(a);
+            for (const auto& kv : src.attrs) {
+                if (dp.attrs.count(kv.first)) continue;
+                Attr a = kv.second;
+                for (std::string& c : a.connections) c = remap(c, from, to);
+                dp.attrs.emplace(kv.first, std::move(a));
+            }
+            for (const auto& kv : src.rels) {
+                if (dp.rels.count(kv.first)) continue;
+                std::vector<std::string> t = kv.second;
+                for (std::string& x : t) x = remap(x, from, to);
+                dp.rels.emplace(kv.first, std::move(t));
+            }
+            // arcs not yet applied (same-layer sources): carried over, applied when the walk gets here
+            dp.references.insert(dp.references.end(), src.references.begin(), src.references.end());
+            dp.payloads.insert(dp.payloads.end(), src.payloads.begin(), src.payloads.end());
+            for (const auto& kv : src.variant_sel) dp.variant_sel.emplace(kv.first, kv.second);
+            for (const auto& kv : src.variant_bodies)
+                for (const auto& v : kv.second) dp.variant_bodies[kv.first].emplace(v.first, v.second);
+            for (int c : src.children) {
+                if (budget_ == 0) return fail("composed stage larger than " + std::to_string(kMaxComposedPrims) + " prims");
+                --budget_;
+                const std::string name = S.prims[c].name;
+                const bool active = S.prims[c].active;
+                const size_t before = D.prims.size();
+                const int dc = D.add_prim(dd, name);
+                if (D.prims.size() > before) D.prims[dc].active = active;
+                work.push_back({dc, c});
+            }
+        }
+        return true;
+    }
+
+    // the prim an arc targets: its path, else the layer's defaultPrim, else its first root prim
+    static int target(const Stage& S, const Arc& a) {
+        if (!a.path.empty()) return S.find(a.path);
+        if (!S.default_prim.empty()) return S.find("/" + S.default_prim);
+        return S.prims[0].children.empty() ? -1 : S.prims[0].children[0];
+    }
+
+    // LIVRPS below local opinions: the selected variants, then references, then payloads
+    bool apply_arcs(const std::string& id, Stage& L, int p, int depth) {
+        for (int round = 0; round < kMaxArcDepth; ++round) {
+            Prim& P = L.prims[p];
+            if (P.variant_sel.empty() && P.references.empty() && P.payloads.empty()) return true;
+            const auto sel = P.variant_sel;
+            const auto bodies = P.variant_bodies;
+            std::vector<Arc> arcs = P.references;
+            arcs.insert(arcs.end(), P.payloads.begin(), P.payloads.end());
+            P.variant_sel.clear();
+            P.variant_bodies.clear();
+            P.references.clear();
+            P.payloads.clear();
+            for (const auto& kv : sel) {
+                auto set = bodies.find(kv.first);
+                if (set == bodies.end()) continue;
+                auto var = set->second.find(kv.second);
+                if (var == set->second.end()) continue;
+                if (!merge(L, p, L, var->second, L.prims[var->second].path, L.prims[p].path)) return false;
+            }
+            for (const Arc& a : arcs) {
+                Stage S;
+                if (a.asset.empty()) S = L;   // internal: this layer's namespace as it stands
+                else if (!load(resolve(id, a.asset), S, depth + 1)) return false;
+                const int t = target(S, a);
+                if (t <= 0) return fail("reference target " + (a.path.empty() ? "(default prim)" : a.path) + " not found in " +
+                                        (a.asset.empty() ? id : a.asset));
+                if (a.asset.empty() && t == p) continue;
+                if (!merge(L, p, S, t, S.prims[t].path, L.prims[p].path)) return false;
+            }
+        }
+        return fail("composition of " + L.prims[p].path + " does not settle");
+    }
+};
+
+}  // namespace
+
 bool load_stage(const std::string& path, Stage& st, std::vector<PackageFile>& files, std::string& err) {
     FILE* f = std::fopen(path.c_str(), "rb");
     if (!f) { err = "cannot open " + path; return false; }
@@ -1245,13 +1534,20 @@ bool load_stage(const std::string& path, Stage& st, std::vector<PackageFile>& fi
         for (const PackageFile& pf : files) {
             const size_t dot = pf.name.find_last_of('.');
             const std::string ext = dot == std::string::npos ? "" : pf.name.substr(dot);
-            if (ext == ".usd" || ext == ".usda" || ext == ".usdc")
-                return parse_layer(pf.data.data(), pf.data.size(), st, err);
+            if (ext == ".usd" || ext == ".usda" || ext == ".usdc") {
+                if (!parse_layer(pf.data.data(), pf.data.size(), st, err)) return false;
+                Composer comp(&files);
+                if (!comp.compose(normalize(pf.name), st, 0)) { err = comp.err; return false; }
+                return true;
+            }
         }
         err = "usdz package without a USD layer";
         return false;
     }
-    return parse_layer(data.data(), data.size(), st, err);
+    if (!parse_layer(data.data(), data.size(), st, err)) return false;
+    Composer comp(nullptr);
+    if (!comp.compose(path, st, 0)) { err = comp.err; return false; }
+    return true;
 }
 
 }  // namespace usd

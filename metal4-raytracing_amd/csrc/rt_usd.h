@@ -11,10 +11,17 @@
 //   .usdc  crate binary layers (bootstrap + TOC; TOKENS / STRINGS / FIELDS / FIELDSETS / PATHS /
 //          SPECS sections; LZ4 + integer-delta compression; inlined and out-of-line value reps,
 //          compressed numeric arrays, list ops, time samples)
-// into one in-memory Stage.  Composition arcs (references, payloads, variants, sublayers) are
-// not followed.  Parity against Pixar's reader is unpinned (no USD asset or library in the
-// snapshot); tests/test_usd.py pins the readers against files written by an independent Python
-// writer of each encoding.
+// into one in-memory Stage, then composed (load_stage): sublayers (stronger layer first), and per
+// prim in namespace order its selected variants, references and payloads (LIVRPS order: local
+// opinions over variants over references over payloads; a weaker opinion only fills in what is not
+// authored yet), external (`@asset@</Prim>`, default prim when no path) and internal (`</Prim>`)
+// arcs, paths inside the referenced subtree remapped to the referencing prim.  Assets resolve
+// next to the layer that names them (inside the package for a .usdz).  A .usdc layer can be the
+// target of an arc, but the arcs authored inside .usdc layers (and their variant specs) are not
+// read; inherits / specializes (class arcs) are not followed.  Parity against Pixar's reader is
+// unpinned (no USD asset or library in the snapshot); tests/test_usd.py pins the readers against
+// files written by an independent Python writer of each encoding, and the composition against the
+// same scene written flat.
 #pragma once
 #include <cstdint>
 #include <map>
@@ -46,8 +53,17 @@ struct Attr {
     int element_size = 1;                   // primvar elementSize metadata
 };
 
+// a reference or payload: asset path (empty: internal) and target prim path (empty: defaultPrim)
+struct Arc {
+    std::string asset, path;
+};
+
 struct Prim {
     std::string name, type, path;
+    // composition arcs authored on this prim (cleared once applied by load_stage)
+    std::vector<Arc> references, payloads;
+    std::map<std::string, std::string> variant_sel;                // variant set -> selected variant
+    std::map<std::string, std::map<std::string, int>> variant_bodies;  // set -> variant -> detached prim
     int parent = -1;
     bool active = true;
     std::vector<int> children;
@@ -70,7 +86,10 @@ struct Stage {
     double time_codes_per_second = 24.0;
     std::string up_axis = "Y";
     std::string default_prim;
+    std::vector<std::string> sublayers;   // subLayers, strongest first
     Stage();
+    // a prim outside the namespace tree (a variant body: path "/Prim{set=variant}")
+    int add_detached(const std::string& path);
     int find(const std::string& path) const {
         auto it = by_path.find(path);
         return it == by_path.end() ? -1 : it->second;

@@ -1,0 +1,141 @@
+"""USD composition (Model.swift:74-81 hands the asset to ModelIO, which composes the stage before
+the mesh walk): sublayers, references (external, default prim, internal), payloads and variant
+selections, each checked against the same content written flat (tests/usd_writers.py), plus the
+error cases (cycles, missing layers, runaway nesting).  Parity with Pixar's composition engine is
+unpinned (no USD library in the image); the arcs follow the published LIVRPS strength order."""
+import numpy as np
+import pytest
+
+import usd_writers as W
+from test_usd import TEX, _mesh_arrays, _scene, robot_prims
+
+import os
+
+HEAD = '#usda 1.0\n(\n    upAxis = "Y"\n    timeCodesPerSecond = 24\n%s)\n'
+
+
+@pytest.fixture(scope="module")
+def d(tmp_path_factory):
+    d = tmp_path_factory.mktemp("compose")
+    prims, _ = robot_prims()
+    (d / "robot.usda").write_bytes(W.write_usda(prims))
+    (d / "robot.usdc").write_bytes(W.write_usdc(prims))
+    os.makedirs(d / "textures", exist_ok=True)
+    (d / "textures" / "tex.png").write_bytes(TEX)
+    return d
+
+
+def _write(d, name, text):
+    (d / name).write_text(text)
+    return str(d / name)
+
+
+def _same_scene(rt, a, b):
+    d0, d1 = a.desc(), b.desc()
+    assert d0.mesh_count == d1.mesh_count
+    for m in range(d0.mesh_count):
+        x, y = _mesh_arrays(d0, m), _mesh_arrays(d1, m)
+        for k in ("pos", "nrm", "uv", "ji", "jw"):
+            if x.get(k) is None:
+                assert y.get(k) is None
+            else:
+                np.testing.assert_array_equal(x[k], y[k], err_msg=f"mesh {m} {k}")
+        assert x["joints"] == y["joints"]
+        assert [(list(s["idx"]), s["mat"], s["tex"]) for s in x["subs"]] == \
+               [(list(s["idx"]), s["mat"], s["tex"]) for s in y["subs"]]
+    assert d0.texture_count == d1.texture_count
+    for t in (0.0, 0.7, 1.9):
+        np.testing.assert_array_equal(a.joint_matrices(0, t), b.joint_matrices(0, t))
+
+
+@pytest.mark.parametrize("arc", ["@./robot.usda@</Robot>", "@robot.usda@", "@./robot.usdc@</Robot>"])
+def test_reference_builds_the_flat_scene(rt, d, arc):
+    # the asset referenced under /World/Robot: relationship and connection targets inside it
+    # (/Robot/Looks/..., /Robot/Skel) move with it
+    root = _write(d, "ref_root.usda", HEAD % '    defaultPrim = "World"\n' +
+                  'def Xform "World"\n{\n    def SkelRoot "Robot" (\n        prepend references = %s\n    )\n    {\n    }\n}\n' % arc)
+    _same_scene(rt, _scene(rt, str(d / "robot.usda")), _scene(rt, root))
+
+
+def test_payload_builds_the_flat_scene(rt, d):
+    root = _write(d, "pay_root.usda", HEAD % "" +
+                  'def Xform "World"\n{\n    def "Robot" (\n        payload = @./robot.usda@</Robot>\n    )\n    {\n    }\n}\n')
+    _same_scene(rt, _scene(rt, str(d / "robot.usda")), _scene(rt, root))
+
+
+def test_sublayers_stronger_layer_wins(rt, d):
+    flat = _scene(rt, str(d / "robot.usda"))
+    only = _write(d, "sub_only.usda", HEAD % "    subLayers = [\n        @./robot.usda@\n    ]\n")
+    _same_scene(rt, flat, _scene(rt, only))
+    # a stronger layer over the sublayer: one shader input overridden, the rest comes from below
+    over = _write(d, "sub_over.usda", HEAD % "    subLayers = [@./robot.usda@]\n" +
+                  'over "Robot"\n{\n    over "Looks"\n    {\n        over "Red"\n        {\n            over "PBR"\n'
+                  '            {\n                color3f inputs:diffuseColor = (0.25, 0.5, 0.75)\n            }\n'
+                  '        }\n    }\n}\n')
+    got = _scene(rt, over)
+    from importlib import import_module
+    Mt = import_module("metal4-raytracing_amd._abi").Material
+    a, b = _mesh_arrays(flat.desc(), 0), _mesh_arrays(got.desc(), 0)
+    np.testing.assert_array_equal(a["pos"], b["pos"])
+    red0, red1 = Mt.from_buffer_copy(a["subs"][1]["mat"]), Mt.from_buffer_copy(b["subs"][1]["mat"])
+    assert (red1.baseColor.x, red1.baseColor.y, red1.baseColor.z) == (0.25, 0.5, 0.75)
+    assert (red1.specular.x, red1.refractionIndex, red1.opacity) == (red0.specular.x, red0.refractionIndex, red0.opacity)
+    assert a["subs"][0]["mat"] == b["subs"][0]["mat"]   # the textured subset is untouched
+
+
+BOX = ('def Mesh "Box"\n{\n    int[] faceVertexCounts = [4]\n    int[] faceVertexIndices = [0, 1, 2, 3]\n'
+       '    point3f[] points = [(0, 0, 0), (1, 0, 0), (1, 1, 0), (0, 1, 0)]\n}\n')
+
+
+@pytest.mark.parametrize("sel", ["full", "proxy", None])
+def test_variant_selection(rt, d, sel):
+    body = ('def Xform "World" (\n%s    prepend variantSets = "lod"\n)\n{\n    variantSet "lod" = {\n'
+            '        "full" {\n            def SkelRoot "Robot" (\n                references = @./robot.usda@</Robot>\n'
+            '            )\n            {\n            }\n        }\n        "proxy" {\n%s        }\n    }\n}\n') % (
+        '    variants = {\n        string lod = "%s"\n    }\n' % sel if sel else "", BOX)
+    path = _write(d, "var_%s.usda" % sel, HEAD % "" + body)
+    if sel is None:   # no selection: neither variant's content is composed
+        with pytest.raises(rt.RTError, match="no meshes"):
+            _scene(rt, path)
+        return
+    got = _scene(rt, path)
+    if sel == "full":
+        _same_scene(rt, _scene(rt, str(d / "robot.usda")), got)
+    else:
+        assert got.desc().mesh_count == 1 and got.triangle_count == 2
+
+
+def test_internal_reference_copies_the_subtree(rt, d):
+    root = _write(d, "internal.usda", HEAD % "" + 'def Xform "World"\n{\n' + BOX.replace("\n", "\n    ") +
+                  '\n    def "Copy" (\n        references = </World/Box>\n    )\n    {\n    }\n}\n')
+    s = _scene(rt, root)
+    desc = s.desc()
+    assert desc.mesh_count == 2 and s.triangle_count == 4
+    a, b = _mesh_arrays(desc, 0), _mesh_arrays(desc, 1)
+    np.testing.assert_array_equal(a["pos"], b["pos"])
+
+
+def test_composition_errors(rt, d):
+    _write(d, "cyc_a.usda", HEAD % "" + 'def Xform "A" (\n    references = @./cyc_b.usda@\n)\n{\n}\n')
+    _write(d, "cyc_b.usda", HEAD % "" + 'def Xform "B" (\n    references = @./cyc_a.usda@\n)\n{\n}\n')
+    with pytest.raises(rt.RTError, match="cycle"):
+        _scene(rt, str(d / "cyc_a.usda"))
+    missing = _write(d, "missing.usda", HEAD % "" + 'def Xform "A" (\n    references = @./nowhere.usda@\n)\n{\n}\n')
+    with pytest.raises(rt.RTError, match="cannot open layer"):
+        _scene(rt, missing)
+    notarget = _write(d, "notarget.usda", HEAD % "" + 'def Xform "A" (\n    references = @./robot.usda@</Nope>\n)\n{\n}\n')
+    with pytest.raises(rt.RTError, match="not found"):
+        _scene(rt, notarget)
+    # a chain of 24 layers, each referencing the next: refused past 16 nested layers
+    for k in range(24):
+        _write(d, "chain%d.usda" % k, HEAD % "" + 'def Xform "L" (\n    references = @./chain%d.usda@\n)\n{\n}\n' % (k + 1))
+    with pytest.raises(rt.RTError, match="nested deeper"):
+        _scene(rt, str(d / "chain0.usda"))
+    # fan-out: every layer references the next one four times (4^12 boxes if unbounded): cut by
+    # the composition's prim budget, fast
+    for k in range(12):
+        refs = "".join('    def "c%d" (\n        references = @./fan%d.usda@\n    )\n    {\n    }\n' % (j, k + 1) for j in range(4))
+        _write(d, "fan%d.usda" % k, HEAD % "" + 'def Xform "F"\n{\n' + refs + "}\n")
+    _write(d, "fan12.usda", HEAD % "" + 'def Xform "F"\n{\n' + BOX.replace("\n", "\n    ") + "\n}\n")
+    with pytest.raises(rt.RTError, match="larger than"):
+        _scene(rt, str(d / "fan0.usda"))
