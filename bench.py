@@ -110,7 +110,7 @@ def parse(argv=None):
     p.add_argument("--sort-bins", type=int, default=0, help="hit-sort bins (0 = library default, -1 = no sort)")
     p.add_argument("--bvh", default="sah", choices=["sah", "lbvh"], help="host binned-SAH or on-device LBVH build")
     p.add_argument("--frames-in-flight", type=int, default=0,
-                   help="frames the renderer overlaps (0 = library default: 2; below 8M allocated paths per frame 4 with the 4 hardware queues set here, 8 with RT_HW_QUEUES=8; 1 = one at a time)")
+                   help="frames the renderer overlaps (0 = library default: one per hardware queue, 4 with the queues set here, 8 with RT_HW_QUEUES=8, within a 96 GB budget; 1 = one at a time)")
     p.add_argument("--animate", action="store_true",
                    help="configs[4] shape: skin every skinned mesh at t = frame/60 s and refit the BVH before each frame")
     p.add_argument("--rebuild", action="store_true", help="with --animate: rebuild the BVH on the device instead of refitting")
@@ -529,6 +529,7 @@ def isolated(R, tiles, torch, dev, a, cst, cus, kernel, frames):
     timed region) over these launches' own HIP-event and device-clock times."""
     s = torch.cuda.Stream(device=dev)
     R.set_stream(s.cuda_stream)
+    R.set_device_spans(True)   # the stamps cost ~1 % of a frame: on for these frames only
     try:
         R.draw(tiles=tiles)   # capture / warm the single slot
         R.wait()
@@ -540,6 +541,7 @@ def isolated(R, tiles, torch, dev, a, cst, cus, kernel, frames):
         wall = (time.perf_counter() - t0) / frames
         i1 = R.stats()
     finally:
+        R.set_device_spans(False)
         R.set_stream(None)
     d = lambda f: getattr(i1, f) - getattr(i0, f)
     b = argparse.Namespace(**vars(a))

@@ -119,7 +119,7 @@ typedef struct rt_opts {
     int32_t pipeline;   /* RT_PIPELINE_* */
     int32_t tail_paths; /* wavefront: below this many live paths the rest of the frame runs in the
                            persistent finish kernel; 0 = default (4194304 one frame at a time,
-                           1310720 / 1048576 / 524288 with 2 / 3 / 4 frames in flight), 1 = never */
+                           1310720 / 1048576 / 786432 / 524288 with 2 / 3 / 4 / 5+ frames in flight), 1 = never */
     int32_t sort_bins;  /* wavefront: hits are sorted into this many bins of BVH leaf order between
                            extend and shade (a power of two in [1024, 4096]); 0 = default (no
                            sort), < 0 = no sort.  Never changes the image, only memory locality. */
@@ -129,9 +129,9 @@ typedef struct rt_opts {
                                  queue: 8 when the process has GPU_MAX_HW_QUEUES >= 8, 4
                                  otherwise, as many as fit in 96 GB, at least 2), 1 = one at a
                                  time, at most 8.  Each slot holds ~300 B per allocated path,
-                                 pixels x (spp + extra samples).  Four slots
-                                 on a frame of 6M+ base paths give the finish tail 25 % of the
-                                 grid (20 % below: the rank-share sweep).
+                                 pixels x (spp + extra samples).  With four or
+                                 more slots the finish tail takes 20 % of the resident grid,
+                                 with two 40 %.
                                  Geometry updates (skinning, transforms, refit, builds) rotate
                                  over max(2, frames in flight) generations, so per-frame updates
                                  keep every slot's overlap.  Images are identical either way. */
@@ -287,6 +287,11 @@ rt_status rt_unpack_tiles_host(int32_t width, int32_t height, const rt_tile_set*
 /* Device ray/node counters: when enabled, frames also count BVH node visits / triangle tests
  * (a few percent slower). Ray counts are always collected. */
 rt_status rt_set_counting(rt_ctx* ctx, int32_t enabled);
+/* Device-clock launch spans of the wavefront traversal and finish launches (rt_stats
+ * total_*_dev_ms; block 0's start to the last wave's end, s_memrealtime), for frames submitted
+ * while enabled.  Off by default: the stamps cost ~1 % of a C3g frame.  Measurement only (no
+ * reference counterpart). */
+rt_status rt_set_device_spans(rt_ctx* ctx, int32_t enabled);
 rt_status rt_get_stats(rt_ctx* ctx, rt_stats* out);
 
 /* Library build identification (kernel code object arch etc). */

@@ -272,7 +272,7 @@ class Renderer:
         opts.pipeline = {"megakernel": 0, "wavefront": 1}[pipeline]
         opts.tail_paths = int(tail_paths)
         opts.sort_bins = int(sort_bins)   # 0 = default hit sort, < 0 = none
-        opts.frames_in_flight = int(frames_in_flight)   # 0 = default (2; below 8M paths per frame 4, or 8 with GPU_MAX_HW_QUEUES >= 8), 1 = one frame at a time
+        opts.frames_in_flight = int(frames_in_flight)   # 0 = default (one per HIP hardware queue: 4, or 8 with GPU_MAX_HW_QUEUES >= 8; within a 96 GB budget, >= 2), 1 = one frame at a time
         ctx = C.c_void_p()
         _check(lib().rt_create(C.byref(opts), C.byref(ctx)))
         object.__setattr__(self, "_ctx", ctx)
@@ -329,6 +329,10 @@ class Renderer:
 
     def set_counting(self, on):
         _check(lib().rt_set_counting(self._ctx, 1 if on else 0), self._ctx)
+
+    def set_device_spans(self, on):
+        """Device-clock launch spans in the stats (rt_set_device_spans; measurement only)."""
+        _check(lib().rt_set_device_spans(self._ctx, 1 if on else 0), self._ctx)
 
     def stats(self):
         s = Stats()

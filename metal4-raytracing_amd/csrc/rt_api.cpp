@@ -105,6 +105,7 @@ struct rt_ctx {
     hipStream_t own_stream = nullptr, stream = nullptr;
     std::string err;
     bool counting = false;
+    bool spans = false;              // rt_set_device_spans
 
     // host scene copies
     std::vector<float4> h_pos, h_nrm;
@@ -1112,7 +1113,7 @@ rt_status rt_render_frame(rt_ctx* c, const Uniforms* U, const rt_tile_set* tiles
         // flight 1.25M paths against the one-frame-at-a-time optimum of 4M; 3 in flight 1M)
         static const bool tail_env = getenv("RT_TAIL_RAYS") != nullptr;
         const int tail = c->tail_paths ? c->tail_paths : (nfl > 1 && !tail_env ? kTailInFlight[nfl] : 0);
-        if (own > 0 && !run_wavefront(S, P, F.wf, own, c->counting, tail, c->sort_bins, extra_pass, nfl, stream,
+        if (own > 0 && !run_wavefront(S, P, F.wf, own, c->counting, c->spans, tail, c->sort_bins, extra_pass, nfl, stream,
                                       cross ? prev.done : nullptr, &F.wft, &F.wfs, &err))
             FAIL(c, RT_ERR_HIP, std::string("wavefront: ") + (err ? err : "?"));
         if (own == 0 && cross) HIPC(c, hipStreamWaitEvent(stream, prev.done, 0));
@@ -1339,6 +1340,12 @@ rt_status rt_unpack_tiles_host(int32_t w, int32_t h, const rt_tile_set* t, const
 rt_status rt_set_counting(rt_ctx* c, int32_t enabled) {
     if (!c) FAIL(c, RT_ERR_INVALID_ARG, "null ctx");
     c->counting = enabled != 0;
+    return RT_OK;
+}
+
+rt_status rt_set_device_spans(rt_ctx* c, int32_t enabled) {
+    if (!c) FAIL(c, RT_ERR_INVALID_ARG, "null ctx");
+    c->spans = enabled != 0;
     return RT_OK;
 }
 

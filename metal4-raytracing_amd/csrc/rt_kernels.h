@@ -106,7 +106,7 @@ struct WavefrontBuffers {
     float4* sq = nullptr;
     uint32_t* counts = nullptr;   // device counter slots (see cslot)
     uint32_t* h_counts = nullptr; // pinned host mirror
-    // device-clock launch spans (kTsSlots launch slots x {start, end}, s_memrealtime) + pinned mirror
+    // device-clock launch spans (kTsSlots launch slots x kTsStride words, s_memrealtime) + pinned mirror
     unsigned long long* tstamp = nullptr;
     unsigned long long* h_tstamp = nullptr;
     uint2* px_extra = nullptr;    // per own pixel: (first extra path - base_paths, count)
@@ -138,9 +138,12 @@ constexpr int kSortBinsDefault = 0;   // off: measured slower on C3g (DESIGN.md 
 // Launch slots of the device-clock spans: per pass (base, extra samples) two per round (extend
 // 2k, connect 2k + 1; rounds <= 16) and the finish launch (kTsFinish); the extra pass at kTsPass.
 constexpr int kTsPass = 40, kTsFinish = 33, kTsSlots = 2 * kTsPass;
+// a launch slot: its start, then one end word per XCD, each on a 128-B line of its own (the last
+// wave of every block takes the max on its XCD's line; one line for all would serialise them)
+constexpr int kTsLine = 16, kTsStride = 9 * kTsLine;
 // the counter words and, 8-byte aligned after them, the launch spans share one allocation
 constexpr size_t kWfTsOffset = ((size_t)kWfCountWords * 4 + 7) / 8 * 8;
-constexpr size_t kWfCountAllocBytes = kWfTsOffset + (size_t)kTsSlots * 16;
+constexpr size_t kWfCountAllocBytes = kWfTsOffset + (size_t)kTsSlots * kTsStride * 8;
 struct WfFrameStats {
     float trace_dev_ms, finish_dev_ms;   // device-clock spans of the extend + connect / finish launches
     int trace_dev_launches, finish_dev_launches;
@@ -182,7 +185,7 @@ struct WfTimeline {
 // kernel takes 1 / in_flight of the resident grid and leaves the rest to the other frames).  prev_done (may be null): the previous frame, in flight on another
 // stream; the extra-sample pass and the resolve (which read its accumulation and motion outputs)
 // are ordered after it, everything before them overlaps it.
-bool run_wavefront(const DevScene& S, const FrameParams& P, WavefrontBuffers& W, int own_tiles, bool count,
+bool run_wavefront(const DevScene& S, const FrameParams& P, WavefrontBuffers& W, int own_tiles, bool count, bool spans,
                    int tail_paths, int sort_bins, bool extra_pass, int in_flight, hipStream_t stream,
                    hipEvent_t prev_done, WfTimeline* tl, WfFrameStats* fs, const char** err);
 bool wavefront_collect(const WavefrontBuffers& W, WfTimeline& T, WfFrameStats* fs, const char** err);

@@ -257,6 +257,7 @@ struct WfParams {
     int fchunk;            // wf_finish_step: paths per chunk grab
     int finish_frac;       // percent of the resident grid the finish launch takes
     int ray_sort;          // wf_shade: extend / shadow rays grouped by ray_key inside each block's allocation
+    int spans;             // record device-clock launch spans (rt_set_device_spans)
     int dev_ctl;           // device-side control (enqueue_wavefront): kernels read their queue sizes from
                            // the counters and skip once the live count fell below `tail`
     int finish_q;          // dev_ctl: the finish queue when every enqueued bulk round ran (written by generate)
@@ -295,13 +296,20 @@ constexpr int kCntDiagSegs = 27, kCntDiagIters = 28, kCntDiagTime = 29;   // wf_
 // paths; later bulk launches of the pass return at once), [31] the queue the finish launch reads
 constexpr int kCntTailMode = 30, kCntFinishQ = 31;
 
-// Device-clock span of a launch (WfFrameStats::trace_dev_ms): block 0 records the start, every wave
-// its end; ts < 0 (host-driven rounds) records nothing.
+// Device-clock span of a launch (WfFrameStats::trace_dev_ms): block 0 records the start, the last
+// wave of every block its end, as a max on its XCD's line (`done`: an LDS wave counter zeroed
+// before the block's first barrier); ts < 0 (host-driven rounds, or spans off: rt_set_device_spans)
+// records nothing.  C3g, four slots: one 64-bit atomic per wave on one line cost the frame 2.5 %
+// (8.67-8.71 -> 8.47-8.50 Grays/s), per block on per-XCD lines still ~1 % (8.58-8.62), so the
+// spans are off unless asked for.
 __device__ __forceinline__ void ts_start(const WfParams& Q, int ts) {
-    if (ts >= 0 && blockIdx.x == 0 && threadIdx.x == 0) Q.W.tstamp[2 * ts] = __builtin_amdgcn_s_memrealtime();
+    if (ts >= 0 && blockIdx.x == 0 && threadIdx.x == 0) Q.W.tstamp[ts * kTsStride] = __builtin_amdgcn_s_memrealtime();
 }
-__device__ __forceinline__ void ts_end(const WfParams& Q, int ts) {
-    if (ts >= 0 && lane_id() == 0) atomicMax(&Q.W.tstamp[2 * ts + 1], (unsigned long long)__builtin_amdgcn_s_memrealtime());
+__device__ __forceinline__ void ts_end(const WfParams& Q, int ts, uint32_t* done) {
+    if (ts < 0 || lane_id() != 0) return;
+    if (atomicAdd(done, 1u) == (blockDim.x + 63u) / 64u - 1u)
+        atomicMax(&Q.W.tstamp[ts * kTsStride + kTsLine * (1 + (int)(blockIdx.x % 8u))],
+                  (unsigned long long)__builtin_amdgcn_s_memrealtime());
 }
 
 // dev_ctl statistics: rounds run, wf_trace launches run, rays they traced
@@ -844,6 +852,8 @@ wf_trace(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int cur, in
             }
         }
     }
+    __shared__ uint32_t ts_done;
+    if (threadIdx.x == 0) ts_done = 0u;
     ts_start(Q, ts);
     const uint32_t n_top = stage_top(S, lds_top);
     __syncthreads();
@@ -943,7 +953,7 @@ wf_trace(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int cur, in
             }
         }
     }
-    ts_end(Q, ts);
+    ts_end(Q, ts, &ts_done);
     flush_counters(P, ANY ? 0 : rays, ANY ? rays : 0, 0, tc, COUNT, overflow, true);
 }
 
@@ -968,6 +978,8 @@ wf_finish_step(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int c
     __shared__ MatRec lds_mat[kMatLds];
     __shared__ float lds_sray[6][kBlock];   // each lane's shadow ray (origin, direction)
     int* stack = &lds_stack[threadIdx.x];
+    __shared__ uint32_t ts_done;
+    if (threadIdx.x == 0) ts_done = 0u;
     ts_start(Q, ts);
     const uint32_t n_top = stage_top(S, lds_top);
     const ShadeTabs halton = load_tabs(S, lds_halton, lds_mat);   // ends with a block barrier
@@ -1149,7 +1161,7 @@ wf_finish_step(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int c
             atomicAdd(&Q.W.counts[kWfDiagHist + min(dt / 5000u, 63u)], 1u);
         }
     }
-    ts_end(Q, ts);
+    ts_end(Q, ts, &ts_done);
     flush_counters(P, n_closest, n_shadow, 0, tc, COUNT, overflow);
 }
 
@@ -1468,6 +1480,7 @@ static int rounds_for(uint64_t paths, uint32_t tail) {
 static bool enqueue_pass(const DevScene& S, const FrameParams& P, const WfParams& Q, int rounds, bool count, bool full,
                          int ts, Enqueue& E, const char** err) {
     hipStream_t stream = E.stream;
+    if (!Q.spans) ts = -1;   // no device-clock spans: the kernels skip the stamps
     const unsigned gt = trace_grid_cap(), g = tuning().shade_blocks;
     for (int k = 0; k < rounds; ++k) {
         const int cur = k & 1;
@@ -1653,7 +1666,9 @@ bool wavefront_collect(const WavefrontBuffers& W, WfTimeline& T, WfFrameStats* f
     for (int pass = 0; pass < 2; ++pass)   // device-clock spans (10 ns ticks) of the launches that ran
         for (int k = 0; k <= kTsFinish; ++k) {
             const int slot = pass * kTsPass + k;
-            const unsigned long long a = W.h_tstamp[2 * slot], b = W.h_tstamp[2 * slot + 1];
+            const unsigned long long a = W.h_tstamp[slot * kTsStride];
+            unsigned long long b = 0;
+            for (int x = 1; x <= 8; ++x) b = std::max(b, W.h_tstamp[slot * kTsStride + kTsLine * x]);
             if (a == 0 || b <= a) continue;
             const float ms = (float)((double)(b - a) * 1e-5);
             if (k == kTsFinish) {
@@ -1667,7 +1682,7 @@ bool wavefront_collect(const WavefrontBuffers& W, WfTimeline& T, WfFrameStats* f
     return true;
 }
 
-bool run_wavefront(const DevScene& S, const FrameParams& P, WavefrontBuffers& W, int own_tiles, bool count,
+bool run_wavefront(const DevScene& S, const FrameParams& P, WavefrontBuffers& W, int own_tiles, bool count, bool spans,
                    int tail_paths, int sort_bins, bool extra_pass, int in_flight, hipStream_t stream,
                    hipEvent_t prev_done, WfTimeline* tl, WfFrameStats* fs, const char** err) {
     const Tuning& tu = tuning();
@@ -1686,6 +1701,7 @@ bool run_wavefront(const DevScene& S, const FrameParams& P, WavefrontBuffers& W,
     Q.shade_min = tu.shade_min;
     Q.fchunk = tu.fchunk;
     Q.ray_sort = tu.ray_sort;
+    Q.spans = spans ? 1 : 0;
     Q.spp_div = make_fastdiv((uint32_t)Q.spp);
     Q.tile = P.tile_size;
     Q.rank = P.rank;

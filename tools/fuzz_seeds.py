@@ -12,7 +12,33 @@ os.makedirs(out, exist_ok=True)
 prims, _ = robot_prims()
 crate = W.write_usdc(prims)
 files = {
-    "seed.usda": W.write_usda(prims).encode() if isinstance(W.write_usda(prims), str) else W.write_usda(prims),
+    # + composition: an internal reference and a variant set whose selected body references it again
+    "seed.usda": W.write_usda(prims) + b"""
+def Xform "World" (
+    variants = {
+        string lod = "full"
+    }
+    prepend variantSets = "lod"
+)
+{
+    def "Copy" (
+        prepend references = </Robot/Prop>
+    )
+    {
+    }
+    variantSet "lod" = {
+        "full" {
+            def "Again" (
+                references = </Robot>
+            )
+            {
+            }
+        }
+        "proxy" {
+        }
+    }
+}
+""",
     "seed.usdc": crate,
     "seed.usdz": W.write_usdz("robot.usdc", crate, [("textures/tex.png", TEX)]),
     "seed.png": TEX,
