@@ -235,6 +235,10 @@ EXPORTED_SYMBOLS = [
 ]
 
 
+# entry points a library built from an older revision may lack without losing any compute path
+OPTIONAL = {"rt_set_device_spans"}
+
+
 def declare(lib):
     """Attach argtypes/restype to every exported function."""
     P = C.POINTER
@@ -296,6 +300,8 @@ def declare(lib):
         "rt_random_offsets": (None, [C.c_uint64, C.c_int32, C.c_int32, P(C.c_uint32)]),
     }
     for name, (res, args) in sig.items():
+        if name in OPTIONAL and not hasattr(lib, name):
+            continue   # measurement hook absent from an older library (A/B runs); compute entry points are required
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args

@@ -168,6 +168,7 @@ struct WfTimeline {
     Span spans[kMaxEv];
     int n_ev = 0, n_spans = 0;
     bool pending = false;
+    bool dev_spans = false;   // the frame recorded device-clock launch spans (tstamp copied back)
     // RT_GRAPH: the slot's frame captured as two HIP graphs (events recorded as external event
     // nodes, so the spans above keep timing it) and replayed while `key` (every launch argument and
     // enqueue decision of the frame) is unchanged: exec[0] up to the motion vectors, exec[1] the

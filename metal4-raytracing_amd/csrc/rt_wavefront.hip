@@ -1522,7 +1522,9 @@ static bool record_base(const DevScene& S, const FrameParams& P, WfParams& Q, bo
     Enqueue E{T, stream, capture};
     T.n_ev = T.n_spans = 0;
     if (!E.mark(err)) return false;
-    WF_CHECK(hipMemsetAsync(W.counts, 0, kWfCountAllocBytes, stream));   // counters and launch spans
+    // counters, and the launch-span stamps when they are recorded
+    T.dev_spans = Q.spans != 0;
+    WF_CHECK(hipMemsetAsync(W.counts, 0, Q.spans ? kWfCountAllocBytes : kWfTsOffset, stream));
     const int rounds = rounds_for(Q.base_paths, Q.tail);
     Q.finish_q = rounds & 1;
     hipLaunchKernelGGL(wf_generate, dim3(grid_for(Q.base_paths, 16384)), dim3(kBlock), 0, stream, S, Q.Pd, Q);
@@ -1556,7 +1558,8 @@ static bool record_rest(const DevScene& S, const FrameParams& P, WfParams& Q, bo
                        with_extra ? 1 : 0);
     WF_CHECK(hipGetLastError());
     if (!E.span(4, err)) return false;
-    WF_CHECK(hipMemcpyAsync(W.h_counts, W.counts, kWfCountAllocBytes, hipMemcpyDeviceToHost, stream));
+    WF_CHECK(hipMemcpyAsync(W.h_counts, W.counts, Q.spans ? kWfCountAllocBytes : kWfTsOffset, hipMemcpyDeviceToHost,
+                            stream));
     return true;
 }
 
@@ -1663,7 +1666,7 @@ bool wavefront_collect(const WavefrontBuffers& W, WfTimeline& T, WfFrameStats* f
     fs->trace_rays = W.h_counts[kWfStat + kStatTraceRays];
     fs->trace_closest_rays = W.h_counts[kWfStat + kStatExtendRays];
     fs->finish_launches = (int)W.h_counts[kWfStat + kStatFinish];
-    for (int pass = 0; pass < 2; ++pass)   // device-clock spans (10 ns ticks) of the launches that ran
+    for (int pass = 0; pass < (T.dev_spans ? 2 : 0); ++pass)   // device-clock spans (10 ns ticks) of the launches that ran
         for (int k = 0; k <= kTsFinish; ++k) {
             const int slot = pass * kTsPass + k;
             const unsigned long long a = W.h_tstamp[slot * kTsStride];
