@@ -139,3 +139,14 @@ def test_composition_errors(rt, d):
     _write(d, "fan12.usda", HEAD % "" + 'def Xform "F"\n{\n' + BOX.replace("\n", "\n    ") + "\n}\n")
     with pytest.raises(rt.RTError, match="larger than"):
         _scene(rt, str(d / "fan0.usda"))
+
+
+def test_reference_inside_a_usdz_package(rt, d):
+    # the root layer (first entry) references a crate layer stored in the same package; assets
+    # resolve inside the package
+    prims, _ = robot_prims()
+    root = (HEAD % '    defaultPrim = "World"\n' +
+            'def Xform "World"\n{\n    def SkelRoot "Robot" (\n        references = @./robot.usdc@</Robot>\n    )\n    {\n    }\n}\n')
+    pkg = W.write_usdz("scene.usda", root.encode(), [("robot.usdc", W.write_usdc(prims)), ("textures/tex.png", TEX)])
+    (d / "composed.usdz").write_bytes(pkg)
+    _same_scene(rt, _scene(rt, str(d / "robot.usda")), _scene(rt, str(d / "composed.usdz")))

@@ -10,7 +10,7 @@ d=json.loads([x for x in open('gpurun_out/cfg_$tag.log') if x.startswith('{')][-
 r=d['roofline']; c=d['cpu_baseline']
 print('$tag', d['value'], d['ms_per_step'], d['config']['frames_in_flight'], r['kernel'][:22], r['frac'], c and c['value'])"
 }
-run c1 --scene c1 --width 256 --height 256 --spp 1 --bounces 1 --steps 64 --warmup 8
-run c2 --scene c2 --width 1280 --height 720 --spp 4 --bounces 4 --steps 32 --warmup 4
-run c3d --scene c3d --steps 16 --warmup 2
-run c5 --scene c5 --bounces 2 --animate --steps 16 --warmup 2
+run c1 --scene c1 --width 256 --height 256 --spp 1 --bounces 1 --steps 400 --warmup 20
+run c2 --scene c2 --width 1280 --height 720 --spp 4 --bounces 4 --steps 128 --warmup 8
+run c3d --scene c3d --steps 32 --warmup 4
+run c5 --scene c5 --bounces 2 --animate --steps 64 --warmup 4
