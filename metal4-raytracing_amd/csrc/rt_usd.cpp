@@ -1,6 +1,7 @@
 // rt_usd.cpp — USD layer readers (.usda text, .usdc crate, .usdz package); see rt_usd.h.
 #include "rt_usd.h"
 #include <set>
+#include <sys/stat.h>
 
 #include <zlib.h>
 
@@ -1329,6 +1330,7 @@ namespace {
 
 constexpr int kMaxArcDepth = 16;              // nested layer loads (sublayer / reference chains)
 constexpr size_t kMaxComposedPrims = 1u << 17;  // prims a composition may create (hostile fan-out)
+constexpr uint64_t kMaxLayerBytes = 1ull << 31;   // a referenced layer file (regular files only)
 
 std::string dir_of(const std::string& id) {
     const size_t k = id.find_last_of('/');
@@ -1424,13 +1426,17 @@ private:
                 if (normalize(f.name) == id) { data = f.data; return true; }
             return false;
         }
+        // an asset path comes from the file: only a regular file of bounded size is read (a
+        // reference to /dev/zero or a FIFO must not hang the loader)
+        struct stat sb;
+        if (stat(id.c_str(), &sb) != 0 || !S_ISREG(sb.st_mode) || (uint64_t)sb.st_size > kMaxLayerBytes) return false;
         FILE* f = std::fopen(id.c_str(), "rb");
         if (!f) return false;
         uint8_t buf[1 << 16];
         size_t k;
-        while ((k = std::fread(buf, 1, sizeof buf, f)) > 0) data.insert(data.end(), buf, buf + k);
+        while ((k = std::fread(buf, 1, sizeof buf, f)) > 0 && data.size() <= kMaxLayerBytes) data.insert(data.end(), buf, buf + k);
         std::fclose(f);
-        return true;
+        return data.size() <= kMaxLayerBytes;
     }
 
     // Prim s of S (and its subtree) merged into prim d of D as the weaker opinion: only what D does
@@ -1522,6 +1528,11 @@ private:
 }  // namespace
 
 bool load_stage(const std::string& path, Stage& st, std::vector<PackageFile>& files, std::string& err) {
+    struct stat sb;
+    if (stat(path.c_str(), &sb) != 0 || !S_ISREG(sb.st_mode) || (uint64_t)sb.st_size > kMaxLayerBytes) {
+        err = "cannot open " + path + " (not a regular file of at most 2 GiB)";
+        return false;
+    }
     FILE* f = std::fopen(path.c_str(), "rb");
     if (!f) { err = "cannot open " + path; return false; }
     std::vector<uint8_t> data;

@@ -123,6 +123,10 @@ def test_composition_errors(rt, d):
     missing = _write(d, "missing.usda", HEAD % "" + 'def Xform "A" (\n    references = @./nowhere.usda@\n)\n{\n}\n')
     with pytest.raises(rt.RTError, match="cannot open layer"):
         _scene(rt, missing)
+    # an asset path naming a device or a directory is refused, not read
+    dev = _write(d, "dev.usda", HEAD % "" + 'def Xform "A" (\n    references = @/dev/zero@\n)\n{\n}\n')
+    with pytest.raises(rt.RTError, match="cannot open layer"):
+        _scene(rt, dev)
     notarget = _write(d, "notarget.usda", HEAD % "" + 'def Xform "A" (\n    references = @./robot.usda@</Nope>\n)\n{\n}\n')
     with pytest.raises(rt.RTError, match="not found"):
         _scene(rt, notarget)
