@@ -1169,6 +1169,46 @@ public:
             for (uint32_t i : items) v.str.push_back(type == kPathListOp ? (i < paths_.size() ? paths_[i] : "") : type == kStringListOp ? str(i) : token(i));
             return true;
         }
+        case kReferenceListOp:
+        case kPayloadListOp: {
+            // SdfListOp<SdfReference | SdfPayload>: each item is {asset path (string index), prim path
+            // (path index), layer offset (two doubles; payloads from crate 0.8), custom data
+            // (references: a dictionary, read only when empty)}; kept as (asset, path) string pairs
+            uint64_t pos = payload;
+            if (!has(pos, 1)) return fail("list op past the end");
+            const uint8_t h = d_[pos++];
+            const uint8_t order[6] = {1u << 1, 1u << 2, 1u << 5, 1u << 6, 1u << 3, 1u << 4};
+            v.kind = Value::kStr;
+            v.array = true;
+            for (int k = 0; k < 6; ++k) {
+                if (!(h & order[k])) continue;
+                uint64_t cnt;
+                if (!u64(pos, cnt)) return false;
+                pos += 8;
+                if (cnt > (1u << 20)) return fail("list op too long");
+                for (uint64_t i = 0; i < cnt; ++i) {
+                    uint32_t a, pth;
+                    if (!u32(pos, a) || !u32(pos + 4, pth)) return false;
+                    pos += 8;
+                    if (type == kReferenceListOp || at_least(0, 8, 0)) pos += 16;
+                    if (type == kReferenceListOp) {
+                        uint64_t nd;
+                        if (!u64(pos, nd)) return false;
+                        pos += 8;
+                        if (nd != 0) {   // custom data is not read: the arcs of this field are dropped
+                            v.kind = Value::kNone;
+                            v.str.clear();
+                            return true;
+                        }
+                    }
+                    if (k < 4) {   // explicit / added / prepended / appended items (deleted / ordered dropped)
+                        v.str.push_back(str(a));
+                        v.str.push_back(pth < paths_.size() ? paths_[pth] : std::string());
+                    }
+                }
+            }
+            return true;
+        }
         case kDoubleVector: {
             uint64_t count;
             if (!u64(payload, count)) return false;
@@ -1251,6 +1291,7 @@ private:
                     if (kv.first == "defaultPrim" && !v.str.empty()) st.default_prim = v.str[0];
                     if (kv.first == "timeCodesPerSecond" && !v.num.empty()) st.time_codes_per_second = v.num[0];
                     if (kv.first == "primChildren") child_order[0] = v.str;
+                    if (kv.first == "subLayers" && v.kind == Value::kStr) st.sublayers = v.str;
                 }
             } else if (sp.type == kSpecPrim) {
                 const int id = ensure_prim(st, path);
@@ -1262,6 +1303,9 @@ private:
                     else if (kv.first == "apiSchemas") p.api_schemas = v.str;
                     else if (kv.first == "active" && !v.num.empty()) p.active = v.num[0] != 0.0;
                     else if (kv.first == "primChildren") child_order[id] = v.str;
+                    else if ((kv.first == "references" || kv.first == "payload") && v.kind == Value::kStr)
+                        for (size_t i = 0; i + 1 < v.str.size(); i += 2)
+                            (kv.first == "references" ? p.references : p.payloads).push_back(Arc{v.str[i], v.str[i + 1]});
                 }
             } else if (sp.type == kSpecAttribute || sp.type == kSpecRelationship) {
                 const size_t dot = path.find_last_of('.');

@@ -16,9 +16,9 @@
 // opinions over variants over references over payloads; a weaker opinion only fills in what is not
 // authored yet), external (`@asset@</Prim>`, default prim when no path) and internal (`</Prim>`)
 // arcs, paths inside the referenced subtree remapped to the referencing prim.  Assets resolve
-// next to the layer that names them (inside the package for a .usdz).  A .usdc layer can be the
-// target of an arc, but the arcs authored inside .usdc layers (and their variant specs) are not
-// read; inherits / specializes (class arcs) are not followed.  Parity against Pixar's reader is
+// next to the layer that names them (inside the package for a .usdz).  .usdc layers contribute
+// their subLayers and references / payloads (a reference with custom data is dropped); their
+// variant specs are not read.  inherits / specializes (class arcs) are not followed.  Parity against Pixar's reader is
 // unpinned (no USD asset or library in the snapshot); tests/test_usd.py pins the readers against
 // files written by an independent Python writer of each encoding, and the composition against the
 // same scene written flat.

@@ -154,3 +154,13 @@ def test_reference_inside_a_usdz_package(rt, d):
     pkg = W.write_usdz("scene.usda", root.encode(), [("robot.usdc", W.write_usdc(prims)), ("textures/tex.png", TEX)])
     (d / "composed.usdz").write_bytes(pkg)
     _same_scene(rt, _scene(rt, str(d / "robot.usda")), _scene(rt, str(d / "composed.usdz")))
+
+
+def test_crate_layer_arcs(rt, d):
+    # arcs authored in binary layers: subLayers on the pseudo-root, a prepended SdfReference
+    (d / "sub_only.usdc").write_bytes(W.write_usdc([], sublayers=["./robot.usda"]))
+    flat = _scene(rt, str(d / "robot.usda"))
+    _same_scene(rt, flat, _scene(rt, str(d / "sub_only.usdc")))
+    (d / "ref_root.usdc").write_bytes(W.write_usdc([dict(path="/Robot", type="SkelRoot",
+                                                         refs=[("./robot.usdc", "/Robot")])]))
+    _same_scene(rt, flat, _scene(rt, str(d / "ref_root.usdc")))

@@ -175,6 +175,7 @@ T_TOKEN, T_ASSET, T_MATRIX4D, T_QUATF = 11, 12, 15, 17
 T_VEC2F, T_VEC3F, T_VEC3H = 20, 24, 25
 T_TOKENLISTOP, T_PATHLISTOP, T_TOKENVECTOR = 32, 34, 41
 T_SPECIFIER, T_VARIABILITY, T_TIMESAMPLES, T_DOUBLEVECTOR = 42, 44, 46, 48
+T_REFERENCELISTOP, T_STRINGVECTOR = 35, 50
 ARRAY, INLINE, COMPRESSED = 1 << 63, 1 << 62, 1 << 61
 
 _TYPE_OF = {
@@ -187,6 +188,7 @@ _TYPE_OF = {
 class CrateWriter:
     def __init__(self, jumps_hook=None):
         self.tokens, self.tok_index = [], {}
+        self.strings, self.str_index = [], {}   # STRINGS: string index -> token index
         self.data = bytearray(b"\0" * 88)   # bootstrap, patched at the end
         self.jumps_hook = jumps_hook          # tests: rewrites the PATHS sibling-jump table
 
@@ -195,6 +197,27 @@ class CrateWriter:
             self.tok_index[s] = len(self.tokens)
             self.tokens.append(s)
         return self.tok_index[s]
+
+    def string(self, s):
+        if s not in self.str_index:
+            self.str_index[s] = len(self.strings)
+            self.strings.append(self.tok(s))
+        return self.str_index[s]
+
+    def string_vector(self, strs):
+        off = self.here()
+        self.data += struct.pack("<Q", len(strs)) + b"".join(struct.pack("<I", self.string(x)) for x in strs)
+        return self.rep(T_STRINGVECTOR, off)
+
+    def reference_list_op(self, refs, path_idx):
+        """prepended SdfReferences: asset (string index), prim path (path index), layer offset
+        (offset 0, scale 1), empty custom data"""
+        off = self.here()
+        self.data += bytes([1 << 5]) + struct.pack("<Q", len(refs))
+        for asset, path in refs:
+            self.data += struct.pack("<II", self.string(asset), path_idx[path]) + struct.pack("<dd", 0.0, 1.0)
+            self.data += struct.pack("<Q", 0)
+        return self.rep(T_REFERENCELISTOP, off)
 
     def here(self):
         return len(self.data)
@@ -312,7 +335,7 @@ class CrateWriter:
         return self.rep(T_TIMESAMPLES, off)
 
     # ---- layer ----------------------------------------------------------------------------------
-    def write(self, prims, tcps=24.0, up_axis="Y"):
+    def write(self, prims, tcps=24.0, up_axis="Y", sublayers=None):
         paths = ["/"]
         kids = {"/": []}
         props = {}
@@ -355,7 +378,8 @@ class CrateWriter:
         root_kids = [c.rsplit("/", 1)[1] for c in kids["/"]]
         spec("/", [field("primChildren", self.token_vector(root_kids)),
                    field("upAxis", self.rep(T_TOKEN, self.tok(up_axis), INLINE)),
-                   field("timeCodesPerSecond", self.scalar(T_DOUBLE, tcps))], 7)
+                   field("timeCodesPerSecond", self.scalar(T_DOUBLE, tcps))] +
+             ([field("subLayers", self.string_vector(sublayers))] if sublayers else []), 7)
         for p in prims:
             fl = [field("specifier", self.rep(T_SPECIFIER, 0, INLINE))]
             if p.get("type"):
@@ -366,6 +390,8 @@ class CrateWriter:
                 fl.append(field("properties", self.token_vector(props[p["path"]])))
             if p.get("api"):
                 fl.append(field("apiSchemas", self.list_op(T_TOKENLISTOP, [self.tok(a) for a in p["api"]])))
+            if p.get("refs"):   # [(asset, target prim path in this layer's path table)]
+                fl.append(field("references", self.reference_list_op(p["refs"], path_idx)))
             spec(p["path"], fl, 6)
             for a in p.get("attrs", []):
                 fl = [field("typeName", self.rep(T_TOKEN, self.tok(a["type"]), INLINE))]
@@ -396,7 +422,7 @@ class CrateWriter:
         blob = b"".join(t.encode() + b"\0" for t in self.tokens)
         comp = fast_compress(blob)
         section("TOKENS", struct.pack("<QQQ", len(self.tokens), len(blob), len(comp)) + comp)
-        section("STRINGS", struct.pack("<Q", 0))
+        section("STRINGS", struct.pack("<Q", len(self.strings)) + b"".join(struct.pack("<I", t) for t in self.strings))
         reps = b"".join(struct.pack("<Q", r) for _, r in fields)
         rc = fast_compress(reps)
         section("FIELDS", struct.pack("<Q", len(fields)) + encode_ints([t for t, _ in fields]) + struct.pack("<Q", len(rc)) + rc)
@@ -427,8 +453,8 @@ class CrateWriter:
         return bytes(self.data)
 
 
-def write_usdc(prims, tcps=24.0, up_axis="Y"):
-    return CrateWriter().write(prims, tcps, up_axis)
+def write_usdc(prims, tcps=24.0, up_axis="Y", sublayers=None):
+    return CrateWriter().write(prims, tcps, up_axis, sublayers)
 
 
 def write_usdz(layer_name, layer_bytes, extra=(), deflate=False):

@@ -10,7 +10,7 @@ from test_usd import TEX, robot_prims  # noqa: E402
 out = sys.argv[1]
 os.makedirs(out, exist_ok=True)
 prims, _ = robot_prims()
-crate = W.write_usdc(prims)
+crate = W.write_usdc(prims + [dict(path="/Copy", type="Xform", refs=[("", "/Robot/Prop")])])   # + an internal reference
 files = {
     # + composition: an internal reference and a variant set whose selected body references it again
     "seed.usda": W.write_usda(prims) + b"""
