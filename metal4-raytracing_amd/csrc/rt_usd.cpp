@@ -1345,7 +1345,11 @@ private:
             std::vector<int> ordered;
             for (const std::string& name : kv.second) {
                 const int c = st.find(p.path == "/" ? "/" + name : p.path + "/" + name);
-                if (c >= 0) ordered.push_back(c);
+                // only real children, each once (a damaged primChildren list may name the prim
+                // itself, an empty name, or one child twice)
+                if (c > 0 && c != kv.first && st.prims[c].parent == kv.first &&
+                    std::find(ordered.begin(), ordered.end(), c) == ordered.end())
+                    ordered.push_back(c);
             }
             for (int c : p.children)
                 if (std::find(ordered.begin(), ordered.end(), c) == ordered.end()) ordered.push_back(c);
@@ -1439,9 +1443,13 @@ public:
             if (L.default_prim.empty()) L.default_prim = S.default_prim;
         }
         std::vector<int> todo{0};
+        std::vector<uint8_t> seen;   // each prim once, whatever its children lists say
         while (!todo.empty()) {
             const int p = todo.back();
             todo.pop_back();
+            if ((size_t)p >= seen.size()) seen.resize(L.prims.size() + 1, 0);
+            if (seen[p]) continue;
+            seen[p] = 1;
             if (!apply_arcs(id, L, p, depth)) return false;
             const std::vector<int>& ch = L.prims[p].children;
             for (auto it = ch.rbegin(); it != ch.rend(); ++it) todo.push_back(*it);
@@ -1458,6 +1466,13 @@ private:
     bool fail(const std::string& m) {
         err = m;
         return false;
+    }
+    // composition work (prims merged, arcs applied, internal snapshots copied) is bounded: a
+    // hostile list of a million arcs must fail fast, not merge a subtree a million times
+    bool spend(size_t n) {
+        if (n > budget_) return fail("composed stage larger than " + std::to_string(kMaxComposedPrims) + " prims");
+        budget_ -= n;
+        return true;
     }
     // an asset path relative to the layer naming it (inside the package for a .usdz)
     std::string resolve(const std::string& from, const std::string& asset) const {
@@ -1490,6 +1505,7 @@ private:
         while (!work.empty()) {
             const auto [dd, ss] = work.back();
             work.pop_back();
+            if (!spend(1)) return false;
             const Prim src = S.prims[ss];   // a copy: D's prims may move below when S is D
             Prim& dp = D.prims[dd];
             if (dp.type.empty()) dp.type = src.type;
@@ -1514,8 +1530,6 @@ private:
             for (const auto& kv : src.variant_bodies)
                 for (const auto& v : kv.second) dp.variant_bodies[kv.first].emplace(v.first, v.second);
             for (int c : src.children) {
-                if (budget_ == 0) return fail("composed stage larger than " + std::to_string(kMaxComposedPrims) + " prims");
-                --budget_;
                 const std::string name = S.prims[c].name;
                 const bool active = S.prims[c].active;
                 const size_t before = D.prims.size();
@@ -1555,6 +1569,7 @@ private:
                 if (!merge(L, p, L, var->second, L.prims[var->second].path, L.prims[p].path)) return false;
             }
             for (const Arc& a : arcs) {
+                if (!spend(1 + (a.asset.empty() ? L.prims.size() : 0))) return false;
                 Stage S;
                 if (a.asset.empty()) S = L;   // internal: this layer's namespace as it stands
                 else if (!load(resolve(id, a.asset), S, depth + 1)) return false;

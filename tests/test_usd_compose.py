@@ -164,3 +164,19 @@ def test_crate_layer_arcs(rt, d):
     (d / "ref_root.usdc").write_bytes(W.write_usdc([dict(path="/Robot", type="SkelRoot",
                                                          refs=[("./robot.usdc", "/Robot")])]))
     _same_scene(rt, flat, _scene(rt, str(d / "ref_root.usdc")))
+
+
+@pytest.mark.timeout(60)
+def test_damaged_children_list_does_not_hang(rt, d):
+    # fuzz find: the root's primChildren count raised from 1 to 36 names garbage tokens, among them
+    # the empty name, i.e. the root itself; the composition walk visits each prim once
+    data = bytearray(W.write_usdc([dict(path="/Robot", type="SkelRoot", refs=[("./robot.usda", "/Robot")])],
+                                  sublayers=["./robot.usdc"]))
+    assert data[88] == 1   # the root's primChildren token vector: its count
+    data[88] = 36
+    (d / "damaged.usdc").write_bytes(bytes(data))
+    try:
+        s = _scene(rt, str(d / "damaged.usdc"))
+        assert s.triangle_count > 0
+    except rt.RTError:
+        pass
