@@ -46,6 +46,7 @@ struct Tuning {
     int fchunk;        // RT_FCHUNK: paths per chunk grab of the finish kernel
     int shade_min;     // RT_SHADE_MIN: the finish kernel shades once this many lanes wait
     int finish_frac;   // RT_FINISH_FRAC: percent of the resident grid the finish launch takes (0 = by frames in flight)
+    int trace_frac;    // RT_TRACE_FRAC: percent of the resident grid the persistent wf_trace launches take (0 = by frames in flight)
     bool log;          // RT_WF_LOG=1: per-round queue sizes, stage times and finish diagnostics on stderr
     bool host_ctl;     // RT_WF_HOST=1: host-driven rounds (queue sizes read back every round)
     int ray_sort;      // RT_RAY_SORT: group the rays wf_shade appends by 1 = direction octant, 2 = direction
@@ -61,6 +62,7 @@ static const Tuning& tuning() {
         v.fchunk = std::max(1, env_int("RT_FCHUNK", 32));
         v.shade_min = env_int("RT_SHADE_MIN", 24);
         v.finish_frac = std::min(env_int("RT_FINISH_FRAC", 0), 100);
+        v.trace_frac = std::min(env_int("RT_TRACE_FRAC", 0), 100);
         v.log = env_int("RT_WF_LOG", 0) != 0;
         v.host_ctl = env_int("RT_WF_HOST", 0) != 0;
         v.ray_sort = env_int("RT_RAY_SORT", 0);
@@ -256,6 +258,7 @@ struct WfParams {
     int shade_min;         // wf_finish_step: shade once this many lanes wait (or none traverses)
     int fchunk;            // wf_finish_step: paths per chunk grab
     int finish_frac;       // percent of the resident grid the finish launch takes
+    int trace_frac;        // percent of the resident grid the bulk wf_trace launches take
     int ray_sort;          // wf_shade: extend / shadow rays grouped by ray_key inside each block's allocation
     int spans;             // record device-clock launch spans (rt_set_device_spans)
     int dev_ctl;           // device-side control (enqueue_wavefront): kernels read their queue sizes from
@@ -1306,9 +1309,10 @@ static unsigned resident_grid(K kernel, int fallback_per_cu) {
 }
 
 // resident blocks of the persistent traversal kernel, queried once
-static unsigned trace_grid_cap() {
+// the bulk traversal launches: Q.trace_frac percent of the resident grid, a multiple of 8 (XCDs)
+static unsigned trace_grid_cap(const WfParams& Q) {
     static const unsigned cap = resident_grid(wf_trace<false, false>, 4);
-    return cap;
+    return std::max(8u, cap * (unsigned)std::max(Q.trace_frac, 1) / 100u / 8u * 8u);
 }
 
 // the finish launch: Q.finish_frac percent of the resident grid (frames in flight: the rest of the
@@ -1374,7 +1378,7 @@ static bool iterate(const DevScene& S, const FrameParams& P, WfParams& Q, int& c
         int next = 1 - cur;
         WF_CHECK(hipEventRecord(W.ev[0], stream));
         unsigned g = grid_for(n, tuning().shade_blocks);
-        unsigned gt = grid_for(n, trace_grid_cap());
+        unsigned gt = grid_for(n, trace_grid_cap(Q));
         if (count) hipLaunchKernelGGL((wf_trace<false, true>), dim3(gt), dim3(kBlock), 0, stream, S, Q.Pd, Q, cur, -1);
         else hipLaunchKernelGGL((wf_trace<false, false>), dim3(gt), dim3(kBlock), 0, stream, S, Q.Pd, Q, cur, -1);
         WF_CHECK(hipEventRecord(W.ev[1], stream));
@@ -1481,7 +1485,7 @@ static bool enqueue_pass(const DevScene& S, const FrameParams& P, const WfParams
                          int ts, Enqueue& E, const char** err) {
     hipStream_t stream = E.stream;
     if (!Q.spans) ts = -1;   // no device-clock spans: the kernels skip the stamps
-    const unsigned gt = trace_grid_cap(), g = tuning().shade_blocks;
+    const unsigned gt = trace_grid_cap(Q), g = tuning().shade_blocks;
     for (int k = 0; k < rounds; ++k) {
         const int cur = k & 1;
         if (count) hipLaunchKernelGGL((wf_trace<false, true>), dim3(gt), dim3(kBlock), 0, stream, S, Q.Pd, Q, cur, ts + 2 * k);
@@ -1715,6 +1719,10 @@ bool run_wavefront(const DevScene& S, const FrameParams& P, WavefrontBuffers& W,
     // other frames' bulk rounds (C3g sweeps, DESIGN.md §3: two slots 40 %; four or more 20 %: C3g
     // with four slots 20 / 25 / 33 % 8.49-8.54 / 8.21-8.50 / 8.28-8.36 Grays/s, and a multi-GPU
     // rank's share; three 33 %); one frame at a time: all of it
+    // four or more frames in flight: the bulk traversal launches take 60 % of the resident grid,
+    // leaving CUs to the other frames' kernels (C3g 8.51-8.64 -> 8.61-8.72 Grays/s over five
+    // alternating pairs, 75 % +0.5 %; the 8-way rank share at 75 % +0.9 %); fewer frames: all of it
+    Q.trace_frac = tu.trace_frac > 0 ? tu.trace_frac : (in_flight >= 4 ? 60 : 100);
     Q.finish_frac = tu.finish_frac > 0 ? tu.finish_frac
                   : in_flight >= 4 ? 20 : in_flight == 2 ? 40 : (in_flight > 1 ? 100 / in_flight : 100);
     if (sort_bins && (sort_bins < kSortMinBins || sort_bins > kSortMaxBins || (sort_bins & (sort_bins - 1)) ||
