@@ -1280,9 +1280,24 @@ rt_status rt_scene_add_obj(rt_scene* s, const char* obj_path, const float positi
     return RT_OK;
 }
 
+static rt_status add_usd_impl(rt_scene* s, const char* path, const float position[3], const float rotation[3], float scale,
+                              const rt_material_override* ov);
+
+// The asset is untrusted: an allocation failure anywhere in reading or mapping it is an I/O error
+// of this call, never an exception across the C-ABI.
 rt_status rt_scene_add_usd(rt_scene* s, const char* path, const float position[3], const float rotation[3], float scale,
                            const rt_material_override* ov) {
     if (!s || !path || !position) return RT_ERR_INVALID_ARG;
+    try {
+        return add_usd_impl(s, path, position, rotation, scale, ov);
+    } catch (const std::exception& e) {
+        s->err = std::string(path) + ": " + e.what();
+        return RT_ERR_IO;
+    }
+}
+
+static rt_status add_usd_impl(rt_scene* s, const char* path, const float position[3], const float rotation[3], float scale,
+                              const rt_material_override* ov) {
     usd::Stage st;
     std::vector<usd::PackageFile> files;
     std::string err;

@@ -12,6 +12,7 @@
 #include <cstring>
 #include <deque>
 #include <functional>
+#include <memory>
 
 namespace rt {
 namespace usd {
@@ -1180,6 +1181,10 @@ public:
             const uint8_t order[6] = {1u << 1, 1u << 2, 1u << 5, 1u << 6, 1u << 3, 1u << 4};
             v.kind = Value::kStr;
             v.array = true;
+            // kept items by list (file order: explicit, added, prepended, appended), composed below as
+            // prepended + explicit + added + appended: a prepended arc is the strongest, as in the
+            // text reader (`prepend references` goes to the front)
+            std::vector<std::string> lists[4];
             for (int k = 0; k < 6; ++k) {
                 if (!(h & order[k])) continue;
                 uint64_t cnt;
@@ -1202,11 +1207,12 @@ public:
                         }
                     }
                     if (k < 4) {   // explicit / added / prepended / appended items (deleted / ordered dropped)
-                        v.str.push_back(str(a));
-                        v.str.push_back(pth < paths_.size() ? paths_[pth] : std::string());
+                        lists[k].push_back(str(a));
+                        lists[k].push_back(pth < paths_.size() ? paths_[pth] : std::string());
                     }
                 }
             }
+            for (int k : {2, 0, 1, 3}) v.str.insert(v.str.end(), lists[k].begin(), lists[k].end());
             return true;
         }
         case kDoubleVector: {
@@ -1379,6 +1385,7 @@ namespace {
 constexpr int kMaxArcDepth = 16;              // nested layer loads (sublayer / reference chains)
 constexpr size_t kMaxComposedPrims = 1u << 17;  // prims a composition may create (hostile fan-out)
 constexpr uint64_t kMaxLayerBytes = 1ull << 31;   // a referenced layer file (regular files only)
+constexpr uint64_t kMaxComposedBytes = 4ull << 30;   // attribute data merges may copy (hostile fan-out)
 
 std::string dir_of(const std::string& id) {
     const size_t k = id.find_last_of('/');
@@ -1412,35 +1419,51 @@ public:
     explicit Composer(const std::vector<PackageFile>* pkg) : pkg_(pkg) {}
     std::string err;
 
-    // layer `id` parsed and composed into `out`
-    bool load(const std::string& id, Stage& out, int depth) {
-        if (depth > kMaxArcDepth) return fail("composition nested deeper than " + std::to_string(kMaxArcDepth) + " layers");
+    // layer `id` parsed and composed; shared by every arc that names it (no copy per arc)
+    std::shared_ptr<const Stage> load(const std::string& id, int depth) {
+        if (depth > kMaxArcDepth) {
+            fail("composition nested deeper than " + std::to_string(kMaxArcDepth) + " layers");
+            return nullptr;
+        }
         auto c = cache_.find(id);
-        if (c != cache_.end()) { out = c->second; return true; }
-        if (loading_.count(id)) return fail("composition cycle through " + id);
+        if (c != cache_.end()) return c->second;
+        if (loading_.count(id)) {
+            fail("composition cycle through " + id);
+            return nullptr;
+        }
         std::vector<uint8_t> data;
-        if (!read(id, data)) return fail("cannot open layer " + id);
-        Stage L;
+        if (!read(id, data)) {
+            fail("cannot open layer " + id);
+            return nullptr;
+        }
+        auto L = std::make_shared<Stage>();
+        L->layer_id = id;
         std::string e;
-        if (!parse_layer(data.data(), data.size(), L, e)) return fail(id + ": " + e);
+        if (!parse_layer(data.data(), data.size(), *L, e)) {
+            fail(id + ": " + e);
+            return nullptr;
+        }
         loading_.insert(id);
-        const bool ok = compose(id, L, depth);
+        const bool ok = compose(id, *L, depth);
         loading_.erase(id);
-        if (!ok) return false;
+        if (!ok) return nullptr;
         cache_[id] = L;
-        out = std::move(L);
-        return true;
+        return L;
     }
 
-    // sublayers under the layer's own opinions, then every prim's arcs in namespace order
+    // sublayers under the layer's own opinions, then every prim's arcs in namespace order.  Variant
+    // selections are composed in the root layer (depth 0) only: a sublayer or referenced layer keeps
+    // its selections and variant bodies unapplied, so the strongest selection of the whole stack
+    // (the root's own, then its sublayers', then the referenced layers') picks the variant.
     bool compose(const std::string& id, Stage& L, int depth) {
+        L.layer_id = id;
         const std::vector<std::string> subs = L.sublayers;
         L.sublayers.clear();
         for (const std::string& sub : subs) {
-            Stage S;
-            if (!load(resolve(id, sub), S, depth + 1)) return false;
-            if (!merge(L, 0, S, 0, "", "")) return false;
-            if (L.default_prim.empty()) L.default_prim = S.default_prim;
+            const std::shared_ptr<const Stage> S = load(resolve(id, sub), depth + 1);
+            if (!S) return false;
+            if (!merge(L, 0, *S, 0, "", "")) return false;
+            if (L.default_prim.empty()) L.default_prim = S->default_prim;
         }
         std::vector<int> todo{0};
         std::vector<uint8_t> seen;   // each prim once, whatever its children lists say
@@ -1450,7 +1473,7 @@ public:
             if ((size_t)p >= seen.size()) seen.resize(L.prims.size() + 1, 0);
             if (seen[p]) continue;
             seen[p] = 1;
-            if (!apply_arcs(id, L, p, depth)) return false;
+            if (!apply_arcs(id, L, p, depth, depth == 0)) return false;
             const std::vector<int>& ch = L.prims[p].children;
             for (auto it = ch.rbegin(); it != ch.rend(); ++it) todo.push_back(*it);
         }
@@ -1460,8 +1483,9 @@ public:
 private:
     const std::vector<PackageFile>* pkg_;
     std::set<std::string> loading_;
-    std::map<std::string, Stage> cache_;
+    std::map<std::string, std::shared_ptr<const Stage>> cache_;
     size_t budget_ = kMaxComposedPrims;
+    uint64_t bytes_budget_ = kMaxComposedBytes;
 
     bool fail(const std::string& m) {
         err = m;
@@ -1473,6 +1497,24 @@ private:
         if (n > budget_) return fail("composed stage larger than " + std::to_string(kMaxComposedPrims) + " prims");
         budget_ -= n;
         return true;
+    }
+    // and so are the attribute bytes merges copy: a few references to one large mesh layer must
+    // not multiply its arrays into terabytes
+    bool spend_bytes(uint64_t n) {
+        if (n > bytes_budget_) return fail("composed attribute data larger than " + std::to_string(kMaxComposedBytes >> 20) + " MiB");
+        bytes_budget_ -= n;
+        return true;
+    }
+    static uint64_t value_bytes(const Value& v) {
+        uint64_t b = 8 * (uint64_t)v.num.size() + 32;
+        for (const std::string& s : v.str) b += s.size() + 32;
+        return b;
+    }
+    static uint64_t attr_bytes(const Attr& a) {
+        uint64_t b = value_bytes(a.value) + 8 * (uint64_t)a.times.size();
+        for (const Value& v : a.samples) b += value_bytes(v);
+        for (const std::string& s : a.connections) b += s.size() + 32;
+        return b;
     }
     // an asset path relative to the layer naming it (inside the package for a .usdz)
     std::string resolve(const std::string& from, const std::string& asset) const {
@@ -1513,6 +1555,7 @@ private:
                 if (std::find(dp.api_schemas.begin(), dp.api_schemas.end(), a) == dp.api_schemas.end()) dp.api_schemas.push_back(a);
             for (const auto& kv : src.attrs) {
                 if (dp.attrs.count(kv.first)) continue;
+                if (!spend_bytes(attr_bytes(kv.second))) return false;
                 Attr a = kv.second;
                 for (std::string& c : a.connections) c = remap(c, from, to);
                 dp.attrs.emplace(kv.first, std::move(a));
@@ -1523,12 +1566,38 @@ private:
                 for (std::string& x : t) x = remap(x, from, to);
                 dp.rels.emplace(kv.first, std::move(t));
             }
-            // arcs not yet applied (same-layer sources): carried over, applied when the walk gets here
-            dp.references.insert(dp.references.end(), src.references.begin(), src.references.end());
-            dp.payloads.insert(dp.payloads.end(), src.payloads.begin(), src.payloads.end());
+            // arcs not yet applied: carried over, applied when the walk gets here; out of another layer
+            // they keep resolving against that layer (its assets, its namespace for internal arcs)
+            for (int k = 0; k < 2; ++k) {
+                const std::vector<Arc>& from_arcs = k ? src.payloads : src.references;
+                std::vector<Arc>& to_arcs = k ? dp.payloads : dp.references;
+                for (Arc a : from_arcs) {
+                    if (&S != &D && !a.resolved && !S.layer_id.empty()) {
+                        a.asset = a.asset.empty() ? S.layer_id : resolve(S.layer_id, a.asset);
+                        a.resolved = true;
+                    }
+                    to_arcs.push_back(std::move(a));
+                }
+            }
             for (const auto& kv : src.variant_sel) dp.variant_sel.emplace(kv.first, kv.second);
+            // variant bodies: prim indices of S.  Within one stage they stay valid; from another stage
+            // (a sublayer, a referenced layer) each body subtree is merged into a detached prim of D
+            // at "<dest path>{set=variant}" first, and D's index is kept.  A body D already has for
+            // that variant is the stronger opinion and stays.
+            std::vector<std::pair<std::pair<std::string, std::string>, int>> foreign;
             for (const auto& kv : src.variant_bodies)
-                for (const auto& v : kv.second) dp.variant_bodies[kv.first].emplace(v.first, v.second);
+                for (const auto& v : kv.second) {
+                    if (&S == &D) dp.variant_bodies[kv.first].emplace(v.first, v.second);
+                    else if (!dp.variant_bodies.count(kv.first) || !dp.variant_bodies[kv.first].count(v.first))
+                        foreign.push_back({{kv.first, v.first}, v.second});
+                }
+            const std::string dpath = dp.path;
+            for (const auto& f : foreign) {   // (dp may move from here on)
+                if (f.second <= 0 || (size_t)f.second >= S.prims.size()) continue;
+                const int body = D.add_detached(dpath + "{" + f.first.first + "=" + f.first.second + "}");
+                if (!merge(D, body, S, f.second, from, to)) return false;
+                D.prims[dd].variant_bodies[f.first.first].emplace(f.first.second, body);
+            }
             for (int c : src.children) {
                 const std::string name = S.prims[c].name;
                 const bool active = S.prims[c].active;
@@ -1548,36 +1617,50 @@ private:
         return S.prims[0].children.empty() ? -1 : S.prims[0].children[0];
     }
 
-    // LIVRPS below local opinions: the selected variants, then references, then payloads
-    bool apply_arcs(const std::string& id, Stage& L, int p, int depth) {
+    // LIVRPS below local opinions: the selected variants, then references, then payloads.  A
+    // selection whose variant set has no body yet stays: a reference or payload merged later may
+    // bring the set (the common pattern: the referencing prim selects a variant of the asset it
+    // references); its own selection stays the stronger one (merge keeps existing selections).
+    // Each set is composed once.
+    bool apply_arcs(const std::string& id, Stage& L, int p, int depth, bool variants) {
+        std::set<std::string> composed;
         for (int round = 0; round < kMaxArcDepth; ++round) {
             Prim& P = L.prims[p];
-            if (P.variant_sel.empty() && P.references.empty() && P.payloads.empty()) return true;
-            const auto sel = P.variant_sel;
-            const auto bodies = P.variant_bodies;
-            std::vector<Arc> arcs = P.references;
-            arcs.insert(arcs.end(), P.payloads.begin(), P.payloads.end());
-            P.variant_sel.clear();
-            P.variant_bodies.clear();
-            P.references.clear();
-            P.payloads.clear();
-            for (const auto& kv : sel) {
-                auto set = bodies.find(kv.first);
-                if (set == bodies.end()) continue;
+            std::vector<int> bodies;
+            for (const auto& kv : P.variant_sel) {
+                if (!variants) break;
+                if (composed.count(kv.first)) continue;
+                auto set = P.variant_bodies.find(kv.first);
+                if (set == P.variant_bodies.end()) continue;
                 auto var = set->second.find(kv.second);
                 if (var == set->second.end()) continue;
-                if (!merge(L, p, L, var->second, L.prims[var->second].path, L.prims[p].path)) return false;
+                composed.insert(kv.first);
+                bodies.push_back(var->second);
             }
+            std::vector<Arc> arcs = P.references;
+            arcs.insert(arcs.end(), P.payloads.begin(), P.payloads.end());
+            P.references.clear();
+            P.payloads.clear();
+            if (bodies.empty() && arcs.empty()) {   // settled (a non-root layer keeps its variants for the stack)
+                if (variants) {
+                    P.variant_sel.clear();
+                    P.variant_bodies.clear();
+                }
+                return true;
+            }
+            for (int b : bodies)
+                if (!merge(L, p, L, b, L.prims[b].path, L.prims[p].path)) return false;
             for (const Arc& a : arcs) {
                 if (!spend(1 + (a.asset.empty() ? L.prims.size() : 0))) return false;
-                Stage S;
-                if (a.asset.empty()) S = L;   // internal: this layer's namespace as it stands
-                else if (!load(resolve(id, a.asset), S, depth + 1)) return false;
-                const int t = target(S, a);
+                std::shared_ptr<const Stage> S;
+                const bool internal = a.asset.empty() || (a.resolved && a.asset == id);
+                if (internal) S = std::make_shared<const Stage>(L);   // this layer's namespace as it stands
+                else if (!(S = load(a.resolved ? a.asset : resolve(id, a.asset), depth + 1))) return false;
+                const int t = target(*S, a);
                 if (t <= 0) return fail("reference target " + (a.path.empty() ? "(default prim)" : a.path) + " not found in " +
-                                        (a.asset.empty() ? id : a.asset));
-                if (a.asset.empty() && t == p) continue;
-                if (!merge(L, p, S, t, S.prims[t].path, L.prims[p].path)) return false;
+                                        (internal ? id : a.asset));
+                if (internal && t == p) continue;
+                if (!merge(L, p, *S, t, S->prims[t].path, L.prims[p].path)) return false;
             }
         }
         return fail("composition of " + L.prims[p].path + " does not settle");
@@ -1586,7 +1669,7 @@ private:
 
 }  // namespace
 
-bool load_stage(const std::string& path, Stage& st, std::vector<PackageFile>& files, std::string& err) {
+static bool load_stage_impl(const std::string& path, Stage& st, std::vector<PackageFile>& files, std::string& err) {
     struct stat sb;
     if (stat(path.c_str(), &sb) != 0 || !S_ISREG(sb.st_mode) || (uint64_t)sb.st_size > kMaxLayerBytes) {
         err = "cannot open " + path + " (not a regular file of at most 2 GiB)";
@@ -1606,6 +1689,7 @@ bool load_stage(const std::string& path, Stage& st, std::vector<PackageFile>& fi
             const std::string ext = dot == std::string::npos ? "" : pf.name.substr(dot);
             if (ext == ".usd" || ext == ".usda" || ext == ".usdc") {
                 if (!parse_layer(pf.data.data(), pf.data.size(), st, err)) return false;
+                st.layer_id = normalize(pf.name);
                 Composer comp(&files);
                 if (!comp.compose(normalize(pf.name), st, 0)) { err = comp.err; return false; }
                 return true;
@@ -1615,9 +1699,25 @@ bool load_stage(const std::string& path, Stage& st, std::vector<PackageFile>& fi
         return false;
     }
     if (!parse_layer(data.data(), data.size(), st, err)) return false;
+    st.layer_id = path;
     Composer comp(nullptr);
     if (!comp.compose(path, st, 0)) { err = comp.err; return false; }
     return true;
+}
+
+// Asset bytes are untrusted: a file that asks for more memory than the process has fails the load
+// (RT_ERR_IO at rt_scene_add_usd) instead of letting std::bad_alloc cross the C-ABI.
+bool load_stage(const std::string& path, Stage& st, std::vector<PackageFile>& files, std::string& err) {
+    try {
+        return load_stage_impl(path, st, files, err);
+    } catch (const std::bad_alloc&) {
+        err = "out of memory while reading " + path;
+    } catch (const std::exception& e) {
+        err = std::string("error while reading ") + path + ": " + e.what();
+    }
+    st = Stage();
+    files.clear();
+    return false;
 }
 
 }  // namespace usd

@@ -56,6 +56,7 @@ struct Attr {
 // a reference or payload: asset path (empty: internal) and target prim path (empty: defaultPrim)
 struct Arc {
     std::string asset, path;
+    bool resolved = false;   // asset is a layer id already (an arc carried out of the layer that authored it)
 };
 
 struct Prim {
@@ -87,6 +88,7 @@ struct Stage {
     std::string up_axis = "Y";
     std::string default_prim;
     std::vector<std::string> sublayers;   // subLayers, strongest first
+    std::string layer_id;                 // the layer this stage was read from (composition)
     Stage();
     // a prim outside the namespace tree (a variant body: path "/Prim{set=variant}")
     int add_detached(const std::string& path);

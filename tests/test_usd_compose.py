@@ -180,3 +180,77 @@ def test_damaged_children_list_does_not_hang(rt, d):
         assert s.triangle_count > 0
     except rt.RTError:
         pass
+
+
+BOX2 = BOX.replace('"Box"', '"Box2"').replace("[4]", "[3, 3]").replace("[0, 1, 2, 3]", "[0, 1, 2, 0, 2, 3]")
+LOD_SET = ('    variantSet "lod" = {\n        "full" {\n            def SkelRoot "Robot" (\n'
+           '                references = @./robot.usda@</Robot>\n            )\n            {\n            }\n        }\n'
+           '        "proxy" {\n%s        }\n        "pair" {\n%s%s        }\n    }\n') % (BOX, BOX, BOX2)
+
+
+@pytest.mark.parametrize("sel", ["full", "proxy", "pair"])
+def test_variant_set_from_a_sublayer_selected_by_the_root(rt, d, sel):
+    # the set and its bodies live in a weaker layer; the stronger root layer only selects
+    _write(d, "lod_sub.usda", HEAD % "" + 'def Xform "World" (\n    prepend variantSets = "lod"\n)\n{\n' + LOD_SET + "}\n")
+    root = _write(d, "lod_root_%s.usda" % sel, HEAD % "    subLayers = [@./lod_sub.usda@]\n" +
+                  'over "World" (\n    variants = {\n        string lod = "%s"\n    }\n)\n{\n}\n' % sel)
+    got = _scene(rt, root)
+    if sel == "full":
+        _same_scene(rt, _scene(rt, str(d / "robot.usda")), got)
+    else:
+        assert got.desc().mesh_count == (1 if sel == "proxy" else 2)
+        assert got.triangle_count == (2 if sel == "proxy" else 4)
+
+
+@pytest.mark.parametrize("own", [None, "full"])
+def test_referencing_prim_selects_the_assets_variant(rt, d, own):
+    # the referenced asset defines the set (with or without a selection of its own); the selection
+    # on the referencing prim is the stronger opinion
+    asset_sel = '    variants = {\n        string lod = "%s"\n    }\n' % own if own else ""
+    _write(d, "lod_asset_%s.usda" % own, HEAD % '    defaultPrim = "Asset"\n' +
+           'def Xform "Asset" (\n%s    prepend variantSets = "lod"\n)\n{\n' % asset_sel + LOD_SET + "}\n")
+    root = _write(d, "lod_refroot_%s.usda" % own, HEAD % "" +
+                  'def Xform "World"\n{\n    def Xform "Model" (\n        references = @./lod_asset_%s.usda@\n'
+                  '        variants = {\n            string lod = "proxy"\n        }\n    )\n    {\n    }\n}\n' % own)
+    got = _scene(rt, root)
+    assert got.desc().mesh_count == 1 and got.triangle_count == 2
+    # without a selection on the referencing prim the asset's own one applies (none: nothing)
+    plain = _write(d, "lod_plain_%s.usda" % own, HEAD % "" +
+                   'def Xform "World"\n{\n    def SkelRoot "Model" (\n        references = @./lod_asset_%s.usda@\n'
+                   '    )\n    {\n    }\n}\n' % own)
+    if own is None:
+        with pytest.raises(rt.RTError, match="no meshes"):
+            _scene(rt, plain)
+    else:
+        _same_scene(rt, _scene(rt, str(d / "robot.usda")), _scene(rt, plain))
+
+
+def test_prepended_reference_is_stronger_than_appended(rt, d):
+    # the same prim authored by two layers with different points; the prepended arc wins in both
+    # encodings (text: list order; crate: prepended list composed before the appended one)
+    _write(d, "pa_a.usda", HEAD % "" + BOX.replace('"Box"', '"M"'))
+    _write(d, "pa_b.usda", HEAD % "" + BOX.replace('"Box"', '"M"').replace("(1, 1, 0)", "(2, 2, 0)"))
+    txt = _write(d, "pa_root.usda", HEAD % "" + 'def Mesh "M" (\n    append references = @./pa_b.usda@</M>\n'
+                 '    prepend references = @./pa_a.usda@</M>\n)\n{\n}\n')
+    def pos(path):   # the scene must outlive its descriptor's arrays
+        sc = _scene(rt, path)
+        return _mesh_arrays(sc.desc(), 0)["pos"]
+
+    want, other = pos(str(d / "pa_a.usda")), pos(str(d / "pa_b.usda"))
+    assert not np.array_equal(want, other)
+    np.testing.assert_array_equal(pos(txt), want)
+    (d / "pa_root.usdc").write_bytes(W.write_usdc([dict(path="/M", type="Mesh", refs=[("./pa_a.usda", "/M")],
+                                                        refs_appended=[("./pa_b.usda", "/M")])]))
+    np.testing.assert_array_equal(pos(str(d / "pa_root.usdc")), want)
+
+
+def test_reference_fan_out_is_bounded_by_bytes(rt, d):
+    # a layer with a 1M-point mesh referenced by many prims: every merge copies the arrays, so the
+    # composition's byte budget stops it with an error instead of exhausting memory
+    n = 1 << 20
+    pts = ", ".join("(%d, 0, 0)" % (k % 7) for k in range(n))
+    _write(d, "big.usda", HEAD % '    defaultPrim = "Big"\n' + 'def Mesh "Big"\n{\n    point3f[] points = [%s]\n}\n' % pts)
+    refs = "".join('    def "c%d" (\n        references = @./big.usda@\n    )\n    {\n    }\n' % j for j in range(256))
+    root = _write(d, "big_fan.usda", HEAD % "" + 'def Xform "F"\n{\n' + refs + "}\n")
+    with pytest.raises(rt.RTError, match="larger than"):
+        _scene(rt, root)

@@ -209,14 +209,19 @@ class CrateWriter:
         self.data += struct.pack("<Q", len(strs)) + b"".join(struct.pack("<I", self.string(x)) for x in strs)
         return self.rep(T_STRINGVECTOR, off)
 
-    def reference_list_op(self, refs, path_idx):
-        """prepended SdfReferences: asset (string index), prim path (path index), layer offset
-        (offset 0, scale 1), empty custom data"""
+    def reference_list_op(self, refs, path_idx, appended=()):
+        """prepended (and appended) SdfReferences: asset (string index), prim path (path index),
+        layer offset (offset 0, scale 1), empty custom data; the lists in file order (explicit,
+        added, prepended, appended)"""
         off = self.here()
-        self.data += bytes([1 << 5]) + struct.pack("<Q", len(refs))
-        for asset, path in refs:
-            self.data += struct.pack("<II", self.string(asset), path_idx[path]) + struct.pack("<dd", 0.0, 1.0)
-            self.data += struct.pack("<Q", 0)
+        self.data += bytes([(1 << 5 if refs else 0) | (1 << 6 if appended else 0)])
+        for items in (refs, appended):
+            if not items:
+                continue
+            self.data += struct.pack("<Q", len(items))
+            for asset, path in items:
+                self.data += struct.pack("<II", self.string(asset), path_idx[path]) + struct.pack("<dd", 0.0, 1.0)
+                self.data += struct.pack("<Q", 0)
         return self.rep(T_REFERENCELISTOP, off)
 
     def here(self):
@@ -390,8 +395,9 @@ class CrateWriter:
                 fl.append(field("properties", self.token_vector(props[p["path"]])))
             if p.get("api"):
                 fl.append(field("apiSchemas", self.list_op(T_TOKENLISTOP, [self.tok(a) for a in p["api"]])))
-            if p.get("refs"):   # [(asset, target prim path in this layer's path table)]
-                fl.append(field("references", self.reference_list_op(p["refs"], path_idx)))
+            if p.get("refs") or p.get("refs_appended"):   # [(asset, target prim path in this layer's path table)]
+                fl.append(field("references", self.reference_list_op(p.get("refs") or [], path_idx,
+                                                                     p.get("refs_appended") or [])))
             spec(p["path"], fl, 6)
             for a in p.get("attrs", []):
                 fl = [field("typeName", self.rep(T_TOKEN, self.tok(a["type"]), INLINE))]
