@@ -62,42 +62,131 @@ B_RAY = 48
 B_NODE = 80  # compressed 8-wide node (Bvh8Node)
 B_TRI = 48
 B_HIT = 16 + 48 + 48
-B_PIXEL = 4 + 16 + 16 + 4 + 16
 B_QRAY = 48
-TOP_NODES = 32          # rt_device.h kTopNodes
+# wf_shade, per shaded hit: ray + hit + colour of the queue entry (64 B), the triangle's normal
+# record (48 B of its 64) and instance transform (48 B) in; the next ray + colour (48 B) and the
+# shadow entry (48 B) out
+B_SHADE_HIT = 64 + 48 + 48 + 48 + 48
+# wf_generate: per path its ray (32 B) and accumulator (16 B); per pixel depth, motion, hit record (28 B)
+B_GEN_PATH, B_GEN_PIXEL = 48, 28
+# wf_motion + wf_resolve, per pixel: the samples' accumulators (16 B each), motion in / out and
+# history in / out (48 B)
+B_RESOLVE_PIXEL = 48
+TOP_NODES = 32          # rt_device.h kTopNodes of an RT_TOP_NODES build
 TRACE_BLOCKS_PER_CU = 8   # wf_trace: 256-thread blocks at 8 waves / SIMD
 FINISH_BLOCKS_PER_CU = 4  # wf_finish_step: 4 waves / SIMD
-# PMC traffic of the newest round (profiles/rNN_traffic.json, tools/gpurun_profile.sh)
-_TRAFFIC = sorted(f for f in os.listdir(os.path.join(ROOT, "profiles")) if re.fullmatch(r"r\d+_traffic\.json", f)) \
-    if os.path.isdir(os.path.join(ROOT, "profiles")) else []
-TRAFFIC_JSON_REL = "profiles/" + (_TRAFFIC[-1] if _TRAFFIC else "r01_traffic.json")
-TRAFFIC_JSON = os.path.join(ROOT, TRAFFIC_JSON_REL)
+# The frame's kernels, grouped as the roofline prices them: key, name, stage_ms slots (rt_stats
+# kernel_ms: [generate, extend, shade, connect, resolve, finish, hit sort]), and the rocprofv3
+# kernel-name pattern of their timed (non-counting) instantiations
+KERNELS = [
+    ("trace", "rt::wf_trace<{false,true}, false> (extend + connect)", (1, 3), r"wf_trace<(true|false),false>"),
+    ("shade", "rt::wf_shade<false, false>", (2,), r"wf_shade<"),
+    ("finish", "rt::wf_finish_step<false, false>", (5,), r"wf_finish_step<false,"),
+    ("generate", "rt::wf_generate", (0,), r"wf_generate"),
+    ("resolve", "rt::wf_motion + rt::wf_resolve", (4,), r"wf_(motion|resolve|extra)\b"),
+]
+PMC_PASSES = [["FETCH_SIZE"], ["WRITE_SIZE"], ["TCC_HIT_sum", "TCC_MISS_sum"]]
 
 
-def _newest_profile(pattern):
-    d = os.path.join(ROOT, "profiles")
-    names = sorted(f for f in os.listdir(d) if re.fullmatch(pattern, f)) if os.path.isdir(d) else []
-    return os.path.join(d, names[-1]) if names else None
+def kernel_key(name):
+    """the KERNELS key of a rocprofv3 kernel name (None: not one of the frame's timed kernels)"""
+    k = name.split("(")[0].replace("void ", "").replace(" ", "")
+    for key, _, _, pat in KERNELS:
+        if re.search(pat, k):
+            return key
+    return None
 
 
-def sorted_l2_hit():
-    """L2 hit rates of the opt-in sorted runs (north star: the sorted-ray shade kernel's L2 hit rate):
-    the hit-sorted shade (--sort-bins 2048, tools/gpurun_sorted_l2.sh) and the wf_shade ray grouping
-    modes (RT_RAY_SORT, tools/gpurun_raysort.sh), from the newest profiles/rNN_l2_*.json."""
+def read_pmc(paths):
+    """Per kernel group from rocprofv3 --pmc counter_collection CSVs (one pass per file): HBM bytes
+    per dispatch (FETCH_SIZE x 2 + WRITE_SIZE, KB units; gfx950's FETCH_SIZE counts half of wide
+    reads, MI355X_MICROARCH.md 'HBM'), the L2 hit rate TCC_HIT / (TCC_HIT + TCC_MISS) and the
+    dispatches seen."""
+    import csv
+    acc = {}
+    for path in paths:
+        if not path or not os.path.exists(path):
+            continue
+        with open(path) as f:
+            for row in csv.DictReader(f):
+                key = kernel_key(row.get("Kernel_Name", ""))
+                if key is None:
+                    continue
+                name = row.get("Counter_Name", "")
+                g = acc.setdefault(key, {})
+                c = g.setdefault(name, [0.0, set()])
+                c[0] += float(row.get("Counter_Value", 0) or 0)
+                c[1].add(row.get("Dispatch_Id") or row.get("Correlation_Id") or len(c[1]))
     out = {}
-    p = _newest_profile(r"r\d+_l2_sorted\.json")
-    if p:
-        hits = json.load(open(p)).get("l2_hit") or {}
-        out["hit_sorted"] = {k: v for k, v in hits.items() if re.search(r"wf_(trace|shade|finish)", k)}
-        out["hit_sorted_source"] = "profiles/" + os.path.basename(p)
-    p = _newest_profile(r"r\d+_l2_raysort\.json")
-    if p:
-        rs = json.load(open(p))
-        for m in ("ray_sort_0", "ray_sort_1", "ray_sort_2"):
-            if m in rs:
-                out[m] = {k: v for k, v in rs[m].items() if re.search(r"wf_(trace|shade)", k)}
-        out["ray_sort_source"] = "profiles/" + os.path.basename(p)
-    return out or None
+    for key, g in acc.items():
+        r = {}
+        if "FETCH_SIZE" in g and "WRITE_SIZE" in g:
+            f, w = g["FETCH_SIZE"], g["WRITE_SIZE"]
+            r["bytes_per_launch"] = int((2 * f[0] / max(len(f[1]), 1) + w[0] / max(len(w[1]), 1)) * 1024)
+            r["dispatches"] = len(f[1])
+        hit, miss = g.get("TCC_HIT_sum", [0.0, ()])[0], g.get("TCC_MISS_sum", [0.0, ()])[0]
+        if hit + miss > 0:
+            r["l2_hit"] = round(hit / (hit + miss), 4)
+        out[key] = r
+    return out
+
+
+def pmc_child_args(a):
+    """bench.py arguments of a PMC pass: the same workload, one frame in flight, a few frames"""
+    args = ["--pmc-child", "--scene", a.scene, "--width", str(a.width), "--height", str(a.height), "--spp", str(a.spp),
+            "--bounces", str(a.bounces), "--tile", str(a.tile), "--pipeline", a.pipeline, "--sort-bins",
+            str(a.sort_bins), "--bvh", a.bvh]
+    if a.emulate_ranks > 1:
+        args += ["--emulate-ranks", str(a.emulate_ranks), "--emulate-rank", str(a.emulate_rank)]
+    if a.animate:
+        args += ["--animate"] + (["--rebuild"] if a.rebuild else [])
+    return args
+
+
+def run_pmc(a):
+    """The rocprofv3 --pmc passes of PMC_PASSES, each its own process (rocprofv3 -- python3 bench.py
+    --pmc-child ...: the same workload, kernels alone), started before this process touches the GPU.
+    Returns (read_pmc result, {counter: csv path}, error or None)."""
+    import glob
+    import shutil
+    import tempfile
+    prof = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
+    if not os.path.exists(prof):
+        return None, {}, "rocprofv3 not found"
+    base = a.pmc_dir or tempfile.mkdtemp(prefix="rt_pmc_", dir="/tmp")
+    csvs = {}
+    env = dict(os.environ, TMPDIR="/tmp")
+    for counters in PMC_PASSES:
+        d = os.path.join(base, counters[0])
+        os.makedirs(d, exist_ok=True)
+        cmd = [prof, "--pmc", *counters, "--output-format", "csv", "-d", d, "-o", "run", "--",
+               sys.executable, os.path.abspath(__file__), *pmc_child_args(a)]
+        try:
+            r = subprocess.run(cmd, cwd="/tmp", env=env, capture_output=True, text=True, timeout=a.pmc_timeout,
+                               start_new_session=True)
+        except subprocess.TimeoutExpired:
+            return None, csvs, f"pmc pass {counters[0]} timed out"
+        found = sorted(glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True))
+        if r.returncode != 0 or not found:
+            return None, csvs, f"pmc pass {counters[0]} failed (rc {r.returncode}): {r.stderr[-300:]}"
+        csvs[counters[0]] = found[-1]
+    return read_pmc(list(csvs.values())), csvs, None
+
+
+def pmc_child(a):
+    """--pmc-child: the workload with one frame in flight (kernels alone), warm-up frame + 3 frames;
+    prints nothing.  Runs under rocprofv3 --pmc (run_pmc)."""
+    rt = importlib.import_module("metal4-raytracing_amd")
+    scene = rt.Scene.preset(a.scene)
+    R = rt.Renderer(scene, a.width, a.height, device=0, pipeline=a.pipeline, seed=3, sort_bins=a.sort_bins, bvh=a.bvh,
+                    frames_in_flight=1)
+    R.samplesPerPixel = a.spp
+    R.maxBounces = a.bounces
+    tiles = (a.tile, a.emulate_rank, a.emulate_ranks) if a.emulate_ranks > 1 else None
+    for _ in range(4):
+        R.draw(tiles=tiles)
+    R.wait()
+    R.close()
 
 
 def parse(argv=None):
@@ -126,7 +215,16 @@ def parse(argv=None):
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--no-isolated", action="store_true", help="skip the one-frame-in-flight traversal measurement")
     p.add_argument("--isolated-frames", type=int, default=6)
-    p.add_argument("--traffic-csv", default=None, help="rocprofv3 --pmc counter_collection.csv for traffic")
+    p.add_argument("--no-pmc", action="store_true",
+                   help="skip the rocprofv3 --pmc passes (HBM bytes and L2 hit rates per kernel); roofline.frac then falls back to algorithmic bytes")
+    p.add_argument("--pmc-dir", default=None, help="keep the PMC pass outputs here (default: a /tmp directory)")
+    p.add_argument("--pmc-timeout", type=float, default=150.0)
+    p.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
+    p.add_argument("--gather-backend", default="nccl", choices=["nccl", "gloo"],
+                   help="multi-GPU tile gather: nccl (RCCL over xGMI, device buffers) or gloo (the packed tiles staged "
+                        "through host memory; ranks may share a GPU, which RCCL refuses)")
+    p.add_argument("--dump-radiance", default=None,
+                   help="rank 0 writes the newest frame's radiance (H, W, 4) float32 here (.npy) after the timed region")
     p.add_argument("--dry-run", action="store_true",
                    help="launcher / collective test on the CPU: gloo instead of RCCL, a stub frame instead of the renderer")
     return p.parse_args(argv)
@@ -199,8 +297,15 @@ def main():
     argv = sys.argv[1:]
     a = parse(argv)
     world_env = int(os.environ.get("WORLD_SIZE") or 0)
+    if a.pmc_child:
+        return pmc_child(a)
     if a.gpus > 1 and world_env == 0:
         sys.exit(launch(a.gpus, argv))
+    # PMC passes (one GPU, before this process touches the GPU): HBM bytes and L2 hit rates per
+    # kernel, measured on the same workload with the kernels alone
+    pmc, pmc_csvs, pmc_err = None, {}, None
+    if not a.no_pmc and not a.dry_run and max(world_env, 1) == 1 and a.pipeline == "wavefront":
+        pmc, pmc_csvs, pmc_err = run_pmc(a)
     import torch
     import torch.distributed as dist
 
@@ -208,8 +313,15 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     n = world
+    gloo = a.dry_run or a.gather_backend == "gloo"
+    if not a.dry_run:
+        # gloo ranks may outnumber the GPUs (a one-GPU box): rank r renders on GPU r mod count
+        ndev = torch.cuda.device_count()
+        local = local % max(ndev, 1) if gloo else local
     if world > 1:
-        if a.dry_run:
+        if gloo:
+            if not a.dry_run:
+                torch.cuda.set_device(local)
             dist.init_process_group("gloo")
         else:
             torch.cuda.set_device(local)
@@ -266,7 +378,7 @@ def main():
     gather = None
     if n > 1:
         tiles_mod = importlib.import_module("metal4-raytracing_amd.tiles")
-        gather = tiles_mod.TileGather(a.width, a.height, T, rank, n, dev, renderer=R)
+        gather = tiles_mod.TileGather(a.width, a.height, T, rank, n, "cpu" if gloo else dev, renderer=R)
 
     skinned = []
     if a.animate:
@@ -334,7 +446,8 @@ def main():
     rays = closest + d("total_shadow_rays")
     kms_local = d("total_frame_ms") / a.steps
 
-    tot = torch.tensor([dt, float(rays), float(closest), kms_local, gather_ms], dtype=torch.float64, device=dev)
+    tot = torch.tensor([dt, float(rays), float(closest), kms_local, gather_ms], dtype=torch.float64,
+                       device="cpu" if gloo else dev)
     if n > 1:
         mx = tot.clone()
         dist.all_reduce(mx, op=dist.ReduceOp.MAX)
@@ -346,6 +459,8 @@ def main():
     if rank != 0:
         dist.destroy_process_group()
         return
+    if a.dump_radiance:
+        np.save(a.dump_radiance, R.radiance())
 
     value = rays_all / dt / 1e9
     ms_per_step = dt / a.steps * 1e3
@@ -353,11 +468,24 @@ def main():
         cus = torch.cuda.get_device_properties(local).multi_processor_count
     except Exception:
         cus = 256
-    roof = roofline(a, cst, s0, s1, rays, closest, kms_local, ms_per_step, cus)
-    if s1.pipeline == 1 and s1.frames_in_flight > 1 and not a.no_isolated:
-        # after the timed region: the same frame with one frame in flight, so the dominant kernel's
-        # launches have the GPU to themselves (its own roofline, beside the shared-GPU figure above)
-        roof["isolated"] = isolated(R, tiles, torch, dev, a, cst, cus, roof["kernel"], a.isolated_frames)
+    ranks = n if n > 1 else max(a.emulate_ranks, 1)
+    pixels = a.width * a.height / ranks
+    table = kernel_table(a, cst, s0, s1, a.steps, pixels, cus)
+    if s1.frames_in_flight > 1 and not a.no_isolated:
+        # after the timed region: the same frame with one frame in flight, so every kernel has the
+        # GPU to itself; the roofline prices these launches, and their wall time per frame is the
+        # single-frame latency
+        i0, i1, ms_frame = isolated(R, tiles, torch, dev, a.isolated_frames)
+        alone, shared = kernel_table(a, cst, i0, i1, a.isolated_frames, pixels, cus), table
+    elif s1.frames_in_flight == 1:
+        alone, shared, ms_frame = table, None, ms_per_step
+    else:
+        alone, shared, ms_frame = table, None, None   # --no-isolated: the shared-GPU launches, flagged
+    roof = roofline(alone, shared, pmc, pmc_err, ms_frame, ms_per_step, pmc_csvs)
+    if alone is table and s1.frames_in_flight > 1:
+        roof["not_a_kernel_measurement"] = True
+    stage_ms = (np.array(list(s1.total_kernel_ms)) - np.array(list(s0.total_kernel_ms))) / a.steps
+    graphs = {k: int(d("total_graph_" + k)) for k in ("replays", "captures", "fallbacks", "eager")}
 
     cpu = None
     if not a.no_cpu and n == 1:
@@ -372,6 +500,9 @@ def main():
         "steps": a.steps,
         "warmup": a.warmup,
         "ms_per_step": round(ms_per_step, 3),
+        # single-frame latency: one frame in flight, wall time per frame (the metric's ms/frame);
+        # ms_per_step is the throughput interval with frames in flight
+        "ms_per_frame": round(ms_frame, 3) if ms_frame else None,
         "higher_is_better": True,
         "scaling": "strong",
         "vs_baseline": None,
@@ -381,18 +512,21 @@ def main():
                 "reference OBJ assets, seeded random offsets",
         "config": {
             "workload": f"{a.scene}: {SCENES.get(a.scene, a.scene + ' scene')} {a.width}x{a.height}x{a.spp}spp, {a.bounces} bounces, "
-                        f"one frame per step, {'tile-split ' + str(T) + 'px + RCCL gather' if n > 1 else 'single GPU'}"
+                        f"one frame per step, {'tile-split ' + str(T) + 'px + ' + ('gloo (host-staged)' if gloo else 'RCCL') + ' gather' if n > 1 else 'single GPU'}"
                         f", frames submitted back to back (overlapping frames in flight)",
             "scene": a.scene, "triangles": scene.triangle_count, "width": a.width, "height": a.height,
             "spp": a.spp, "max_bounces": a.bounces, "pipeline": a.pipeline, "parallelism": f"tiles{n}",
             "rays_per_frame": int(rays_all / a.steps), "kernel_ms_per_frame": round(kms, 3),
             "setup_s": round(setup_s, 2),
             # [generate, extend, shade, connect, resolve, finish, hit sort]
-            "stage_ms": [round(x, 3) for x in roof.pop("_stage_ms")], "sort_bins": a.sort_bins, "bvh": a.bvh,
+            "stage_ms": [round(x, 3) for x in stage_ms], "sort_bins": a.sort_bins, "bvh": a.bvh,
             "pipeline_used": ["megakernel", "wavefront"][s1.pipeline], "iterations": s1.iterations,
             "frames_in_flight": s1.frames_in_flight, "animate": bool(skinned),
             # host time inside the submit calls per step (includes waiting for a free frame slot)
             "host_submit_ms": round(t_host / a.steps * 1e3, 3),
+            # how the timed frames were submitted (rt_stats total_graph_*): replays of the slots'
+            # captured HIP graphs, fresh captures, refused captures (eager), eager by choice
+            "graphs": graphs,
             # multi-GPU: device time per step from the end of the pack through the unpack on rank 0's
             # side of the RCCL gather (max over ranks), and its share of the step
             "gather_ms_per_step": round(gather_ms, 4) if n > 1 else None,
@@ -406,22 +540,22 @@ def main():
         dist.destroy_process_group()
 
 
-def roofline(a, cst, s0, s1, rays_local, closest_local, kms_local, ms_per_step, cus):
-    """The dominant kernel's algorithmic bytes per launch over its average launch time (HIP events
-    around each launch on its render stream, over the timed region), with node bytes counted for
-    the nodes fetched from memory only.  The device-clock span of the same launches
-    (first workgroup start to last wave end, s_memrealtime) is reported beside it
-    (launch_ms_device).  With frames in flight, launches of different frames share the GPU: a
-    launch's span, as rocprofv3's kernel trace records it too, is then longer than it would be
-    alone, and the per-frame kernel times add up to more than the step."""
+def kernel_table(a, cst, s0, s1, frames, pixels, cus):
+    """Per kernel group (KERNELS) over the frames between stats s0 and s1: launches per frame, the
+    average launch time (HIP events around each launch on its render stream), device time per
+    frame, and algorithmic bytes per launch.  Node / triangle counts per ray come
+    from the untimed counting frame `cst`: wf_trace counts its own visits, the finish kernel's are
+    the rest."""
     d = lambda f: getattr(s1, f) - getattr(s0, f)
-    steps = a.steps
-    trace_rays, trace_launches, trace_ms = d("total_trace_rays"), d("total_trace_launches"), d("total_trace_ms")
-    trace_closest, finish_launches = d("total_trace_closest_rays"), d("total_finish_launches")
-    trace_dev_ms, trace_dev_launches = d("total_trace_dev_ms"), d("total_trace_dev_launches")
-    finish_dev_ms, finish_dev_launches = d("total_finish_dev_ms"), d("total_finish_dev_launches")
     stage_ms = np.array(list(s1.total_kernel_ms)) - np.array(list(s0.total_kernel_ms))
-    # per-ray visits of the counting frame: wf_trace's own, and the finish kernel's (the rest)
+    if s1.pipeline != 1:   # megakernel: the whole frame is one launch; every node comes from memory
+        rays_c = cst.closest_rays + cst.shadow_rays
+        rays = (d("total_closest_rays") + d("total_shadow_rays")) / frames
+        npr, tpr = cst.node_visits / max(rays_c, 1), cst.tri_tests / max(rays_c, 1)
+        b = rays * (B_RAY + npr * B_NODE + tpr * B_TRI) + d("total_closest_rays") / frames * B_HIT + pixels * 56
+        ms = d("total_frame_ms") / frames
+        return [dict(key="megakernel", kernel="rt::megakernel<false, false>", launches=1.0, launch_ms=ms,
+                     ms_per_frame=ms, bytes_per_launch=b, nodes_per_ray=npr, tris_per_ray=tpr)]
     rays_c = cst.closest_rays + cst.shadow_rays
     q_nodes = cst.trace_nodes / max(cst.trace_rays, 1)
     q_nodes_lds = cst.trace_nodes_lds / max(cst.trace_rays, 1)
@@ -430,112 +564,102 @@ def roofline(a, cst, s0, s1, rays_local, closest_local, kms_local, ms_per_step, 
     f_nodes = (cst.node_visits - cst.trace_nodes) / max(f_rays_c, 1)
     f_nodes_lds = (cst.node_visits_lds - cst.trace_nodes_lds) / max(f_rays_c, 1)
     f_tris = (cst.tri_tests - cst.trace_tris) / max(f_rays_c, 1)
+    trace_rays, trace_launches = d("total_trace_rays"), d("total_trace_launches")
+    trace_closest, finish_launches = d("total_trace_closest_rays"), d("total_finish_launches")
+    closest, rays = d("total_closest_rays"), d("total_closest_rays") + d("total_shadow_rays")
+    paths = d("total_paths") / frames
+    out = []
+    for key, name, stages, _ in KERNELS:
+        ms = float(sum(stage_ms[i] for i in stages))
+        if key == "trace":
+            n = trace_launches
+            rpl = trace_rays / max(n, 1)
+            b = rpl * (B_QRAY + (q_nodes - q_nodes_lds) * B_NODE + q_tris * B_TRI) + \
+                (cus * TRACE_BLOCKS_PER_CU * TOP_NODES * B_NODE if q_nodes_lds > 0 else 0)
+            extra = dict(rays_per_launch=rpl, nodes_per_ray=q_nodes, lds_nodes_per_ray=q_nodes_lds, tris_per_ray=q_tris)
+        elif key == "finish":
+            n = finish_launches
+            f_rays = (rays - trace_rays) / max(n, 1)
+            f_closest = (closest - trace_closest) / max(n, 1)
+            b = f_rays * (B_RAY + (f_nodes - f_nodes_lds) * B_NODE + f_tris * B_TRI) + f_closest * B_HIT + \
+                (cus * FINISH_BLOCKS_PER_CU * TOP_NODES * B_NODE if f_nodes_lds > 0 else 0)
+            extra = dict(rays_per_launch=f_rays, nodes_per_ray=f_nodes, lds_nodes_per_ray=f_nodes_lds, tris_per_ray=f_tris)
+        elif key == "shade":
+            n = trace_launches / 2   # one per bulk round (extend + connect are the round's wf_trace pair)
+            b = trace_closest / max(n, 1) * B_SHADE_HIT
+            extra = dict(hits_per_launch=trace_closest / max(n, 1))
+        elif key == "generate":
+            n = frames
+            b = paths * B_GEN_PATH + pixels * B_GEN_PIXEL
+            extra = {}
+        else:   # resolve (+ motion vectors): two launches a frame
+            n = 2 * frames
+            b = pixels * (16 * a.spp + B_RESOLVE_PIXEL) / 2
+            extra = {}
+        if n <= 0:
+            continue
+        out.append(dict(key=key, kernel=name, launches=n / frames, launch_ms=ms / n, ms_per_frame=ms / frames,
+                        bytes_per_launch=b, **extra))
+    return out
+
+
+def roofline(alone, shared, pmc, pmc_err, ms_frame_alone, ms_per_step, pmc_csvs):
+    """The bench line's roofline: the dominant kernel is the one with the most device
+    time per frame with the kernels alone (one frame in flight); `frac` = its HBM bytes per launch
+    (rocprofv3 PMC, FETCH_SIZE x 2 + WRITE_SIZE, same workload, kernels alone) over its average
+    launch time alone, against 8 TB/s.  The algorithmic-byte fraction and the L2-gather figure are
+    secondary fields; the shared-GPU figures of the timed region (frames in flight) are under
+    `in_flight`."""
+    dom = max(alone, key=lambda k: k["ms_per_frame"])
+    pmc = pmc or {}
     kernels = []
-    if s1.pipeline == 1 and trace_launches > 0:
-        rpl = trace_rays / trace_launches
-        blocks = cus * TRACE_BLOCKS_PER_CU
-        kernels.append(dict(
-            kernel="rt::wf_trace<{false,true}, false> (extend + connect)", launches=trace_launches / steps,
-            launch_ms=trace_ms / trace_launches,
-            launch_ms_device=trace_dev_ms / trace_dev_launches if trace_dev_launches else None,
-            rays_per_launch=rpl, nodes_per_ray=q_nodes,
-            lds_nodes_per_ray=q_nodes_lds, tris_per_ray=q_tris,
-            bytes_per_launch=rpl * (B_QRAY + (q_nodes - q_nodes_lds) * B_NODE + q_tris * B_TRI)
-            + (blocks * TOP_NODES * B_NODE if q_nodes_lds > 0 else 0),
-            bytes_all_nodes=rpl * (B_QRAY + q_nodes * B_NODE + q_tris * B_TRI)))
-    if s1.pipeline == 1 and finish_launches > 0:
-        # wf_finish_step: its rays (48 B ray + hit) + nodes + triangles as above, + the shading
-        # gathers per closest hit (B_HIT); the path state in and out once per path is left out
-        f_rays = (rays_local - trace_rays) / finish_launches
-        f_closest = (closest_local - trace_closest) / finish_launches
-        blocks = cus * FINISH_BLOCKS_PER_CU
-        kernels.append(dict(
-            kernel="rt::wf_finish_step<false, false>", launches=finish_launches / steps,
-            launch_ms=float(stage_ms[5]) / finish_launches,
-            launch_ms_device=finish_dev_ms / finish_dev_launches if finish_dev_launches else None,
-            rays_per_launch=f_rays, nodes_per_ray=f_nodes,
-            lds_nodes_per_ray=f_nodes_lds, tris_per_ray=f_tris,
-            bytes_per_launch=f_rays * (B_RAY + (f_nodes - f_nodes_lds) * B_NODE + f_tris * B_TRI) + f_closest * B_HIT
-            + (blocks * TOP_NODES * B_NODE if f_nodes_lds > 0 else 0),
-            bytes_all_nodes=f_rays * (B_RAY + f_nodes * B_NODE + f_tris * B_TRI) + f_closest * B_HIT))
-    if not kernels:
-        # megakernel: the whole frame is one launch; every node comes from memory
-        rpl = rays_local / steps
-        npr = cst.node_visits / max(rays_c, 1)
-        tpr = cst.tri_tests / max(rays_c, 1)
-        b = (rpl * (B_RAY + npr * B_NODE + tpr * B_TRI) + closest_local / steps * B_HIT
-             + a.width * a.height / max(1, int(os.environ.get("WORLD_SIZE", "1"))) * B_PIXEL)
-        kernels.append(dict(kernel="rt::megakernel<false, false>", launches=1, launch_ms=kms_local,
-                            launch_ms_device=None, rays_per_launch=rpl,
-                            nodes_per_ray=npr, lds_nodes_per_ray=0.0, tris_per_ray=tpr, bytes_per_launch=b,
-                            bytes_all_nodes=b))
-    for k in kernels:
-        k["achieved"] = k["bytes_per_launch"] / (k["launch_ms"] * 1e-3) / 1e9
-        k["achieved_all_nodes"] = k["bytes_all_nodes"] / (k["launch_ms"] * 1e-3) / 1e9
-        k["ms_per_frame"] = k["launch_ms"] * k["launches"]
-    dom = max(kernels, key=lambda k: k["ms_per_frame"])
-    # the whole frame: every timed kernel's algorithmic bytes over the wall time per frame
-    job_bytes = sum(k["bytes_per_launch"] * k["launches"] for k in kernels)
-    job_achieved = job_bytes / (ms_per_step * 1e-3) / 1e9
-    traffic, traffic_src, l2_hit = None, None, None
-    if a.traffic_csv:
-        traffic = read_traffic(a.traffic_csv.split(","), traffic_key(dom["kernel"]))
-        traffic_src = "live: " + a.traffic_csv
-    elif os.path.exists(TRAFFIC_JSON):
-        with open(TRAFFIC_JSON) as f:
-            tj = json.load(f)
-        if tj.get("config") == [a.scene, a.width, a.height, a.spp, a.bounces]:
-            by_kernel = tj.get("bytes_per_launch_by_kernel") or {}
-            if by_kernel.get(dom["kernel"]) is not None:
-                traffic, traffic_src = by_kernel[dom["kernel"]], TRAFFIC_JSON_REL + " (" + tj.get("source", "") + ")"
-            # TCC hit rates (rocprofv3 TCC_HIT/TCC_MISS pass) of the traversal, shade and finish kernels
-            hits = tj.get("l2_hit") or {}
-            l2_hit = {k: v for k, v in hits.items() if re.search(r"wf_(trace|shade|finish)", k)} or None
-    # frames in flight: launches of different frames share the GPU, so a launch's time is not the
-    # kernel's alone; when the dominant kernel's time per frame exceeds the step, say so
-    shared = dom["ms_per_frame"] > ms_per_step
+    for k in alone:
+        p = pmc.get(k["key"], {})
+        t = p.get("bytes_per_launch")
+        alg = k["bytes_per_launch"] / (k["launch_ms"] * 1e-3) / 1e9
+        hbm = t / (k["launch_ms"] * 1e-3) / 1e9 if t else None
+        kernels.append({
+            "kernel": k["kernel"], "ms_per_frame": round(k["ms_per_frame"], 4), "launches": round(k["launches"], 2),
+            "launch_ms": round(k["launch_ms"], 4), "traffic": t, "hbm_GBs": round(hbm, 1) if hbm else None,
+            "frac": round(hbm / HBM_PEAK_GBS, 4) if hbm else None, "l2_hit": p.get("l2_hit"),
+            "algorithmic_bytes_per_launch": int(k["bytes_per_launch"]), "achieved_algorithmic_GBs": round(alg, 1),
+            "frac_algorithmic": round(alg / HBM_PEAK_GBS, 4),
+            **{x: round(k[x], 3) for x in ("nodes_per_ray", "tris_per_ray") if x in k}})
+    d = next(k for k in kernels if k["kernel"] == dom["kernel"])
     r = {
-        "bound": "hbm", "achieved": round(dom["achieved"], 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-        "frac": round(dom["achieved"] / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": traffic_src,
-        "frac_of_l2_gather_peak": round(dom["achieved"] / L2_GATHER_PEAK_GBS, 4),
-        # the same launch with every node visit charged 80 B (round-2 accounting: LDS-served top
-        # nodes counted as memory bytes)
-        "frac_all_nodes": round(dom["achieved_all_nodes"] / HBM_PEAK_GBS, 4),
-        # measured HBM bytes of one launch (PMC) over the launch time: what actually crossed HBM
-        "hbm_GBs": round(traffic / (dom["launch_ms"] * 1e-3) / 1e9, 1) if traffic else None,
-        "l2_hit": l2_hit,
-        "l2_hit_sorted": sorted_l2_hit(),
-        "job_achieved": round(job_achieved, 1), "job_frac": round(job_achieved / HBM_PEAK_GBS, 4),
-        "job_bytes_per_frame": int(job_bytes),
-        "not_a_kernel_measurement": shared,
-        "note": ("frames in flight share the GPU: the launch time includes time its workgroups wait for CUs "
-                 "other frames' kernels hold (see 'isolated' for the kernel alone)") if shared else None,
-        "kernel": dom["kernel"], "launch_ms": round(dom["launch_ms"], 4),
-        "launch_ms_device": round(dom["launch_ms_device"], 4) if dom["launch_ms_device"] else None,
-        "bytes_per_launch": int(dom["bytes_per_launch"]),
-        "rays_per_launch": int(dom["rays_per_launch"]), "nodes_per_ray": round(dom["nodes_per_ray"], 3),
-        "lds_nodes_per_ray": round(dom["lds_nodes_per_ray"], 3), "tris_per_ray": round(dom["tris_per_ray"], 3),
-        # every timed kernel of the frame with its own roofline, for comparison
-        "kernels": [{"kernel": k["kernel"], "ms_per_frame": round(k["ms_per_frame"], 3),
-                     "launch_ms": round(k["launch_ms"], 4),
-                     "launch_ms_device": round(k["launch_ms_device"], 4) if k["launch_ms_device"] else None,
-                     "achieved_GBs": round(k["achieved"], 1), "bytes_per_launch": int(k["bytes_per_launch"]),
-                     "frac": round(k["achieved"] / HBM_PEAK_GBS, 4), "nodes_per_ray": round(k["nodes_per_ray"], 3),
-                     "lds_nodes_per_ray": round(k["lds_nodes_per_ray"], 3),
-                     "tris_per_ray": round(k["tris_per_ray"], 3)} for k in kernels],
-        "_stage_ms": list(stage_ms[:7] / steps),
+        "bound": "hbm", "peak": HBM_PEAK_GBS, "unit": "GB/s", "kernel": dom["kernel"],
+        "achieved": d["hbm_GBs"] if d["hbm_GBs"] else d["achieved_algorithmic_GBs"],
+        "frac": d["frac"] if d["frac"] is not None else d["frac_algorithmic"],
+        "frac_source": "pmc: rocprofv3 FETCH_SIZE x 2 + WRITE_SIZE per launch, kernels alone, over the launch time alone"
+        if d["frac"] is not None else "algorithmic bytes (no PMC pass: " + (pmc_err or "--no-pmc") + ")",
+        "traffic": d["traffic"], "launch_ms": d["launch_ms"], "ms_per_frame_alone": d["ms_per_frame"],
+        "frame_ms_alone": round(ms_frame_alone, 4) if ms_frame_alone else None,
+        "algorithmic_bytes_per_launch": d["algorithmic_bytes_per_launch"],
+        "achieved_algorithmic": d["achieved_algorithmic_GBs"], "frac_algorithmic": d["frac_algorithmic"],
+        "frac_of_l2_gather_peak": round(d["achieved_algorithmic_GBs"] / L2_GATHER_PEAK_GBS, 4),
+        "l2_hit": {k["kernel"]: k["l2_hit"] for k in kernels if k["l2_hit"] is not None} or None,
+        # north star: the L2 hit rate of the shade kernel (it shades the hits of the rays as the
+        # extend launch traced them), measured in this run
+        "shade_l2_hit": next((k["l2_hit"] for k in kernels if k["kernel"].startswith("rt::wf_shade")), None),
+        "pmc_files": {c: os.path.relpath(p, ROOT) if p.startswith(ROOT) else p for c, p in pmc_csvs.items()} or None,
+        "kernels": kernels,
     }
+    if shared is not None:
+        r["in_flight"] = {
+            "note": "frames in flight share the GPU: a launch's time includes the time its workgroups wait for CUs "
+                    "other frames' kernels hold, so these are not kernel measurements",
+            "ms_per_step": round(ms_per_step, 4),
+            "kernels": [{"kernel": k["kernel"], "ms_per_frame": round(k["ms_per_frame"], 4),
+                         "launch_ms": round(k["launch_ms"], 4)} for k in shared]}
     return r
 
 
-def isolated(R, tiles, torch, dev, a, cst, cus, kernel, frames):
-    """The bench frame with one frame in flight: the renderer on a caller's stream keeps one slot
-    (rt_set_stream), so every launch has the GPU to itself.  After the timed region, not part of
-    the bench value: the dominant kernel's algorithmic bytes per launch (same accounting as the
-    timed region) over these launches' own HIP-event and device-clock times."""
+def isolated(R, tiles, torch, dev, frames):
+    """The bench frame with one frame in flight, after the timed region: the renderer on a caller's
+    stream keeps one slot (rt_set_stream), so every launch has the GPU to itself.  Returns the stats
+    before / after and the wall time per frame (single-frame latency)."""
     s = torch.cuda.Stream(device=dev)
     R.set_stream(s.cuda_stream)
-    R.set_device_spans(True)   # the stamps cost ~1 % of a frame: on for these frames only
     try:
         R.draw(tiles=tiles)   # capture / warm the single slot
         R.wait()
@@ -547,61 +671,8 @@ def isolated(R, tiles, torch, dev, a, cst, cus, kernel, frames):
         wall = (time.perf_counter() - t0) / frames
         i1 = R.stats()
     finally:
-        R.set_device_spans(False)
         R.set_stream(None)
-    d = lambda f: getattr(i1, f) - getattr(i0, f)
-    b = argparse.Namespace(**vars(a))
-    b.steps = frames
-    closest = d("total_closest_rays")
-    r = roofline(b, cst, i0, i1, closest + d("total_shadow_rays"), closest, d("total_frame_ms") / frames,
-                 wall * 1e3, cus)
-    k = next((k for k in r["kernels"] if k["kernel"] == kernel), None)
-    if k is None:
-        return None
-    return {"frames_in_flight": i1.frames_in_flight, "frames": frames, "kernel": kernel,
-            "launch_ms": k["launch_ms"], "launch_ms_device": k["launch_ms_device"],
-            "achieved": k["achieved_GBs"], "frac": k["frac"],
-            "frac_of_l2_gather_peak": round(k["achieved_GBs"] / L2_GATHER_PEAK_GBS, 4),
-            "frac_device": round(k["bytes_per_launch"] / (k["launch_ms_device"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
-            if k["launch_ms_device"] else None,
-            "ms_per_frame": round(wall * 1e3, 3), "kernel_ms_per_frame": round(d("total_frame_ms") / frames, 3),
-            # [generate, extend, shade, connect, resolve, finish, hit sort] per frame, one frame at a time
-            "stage_ms": [round(x, 3) for x in r["_stage_ms"]]}
-
-
-TRAFFIC_KEYS = {"rt::wf_trace": r"wf_trace<(true|false),false>", "rt::wf_finis": r"wf_finish_step<false,false"}
-
-
-def traffic_key(kernel):
-    """rocprof kernel-name pattern of the bench line's dominant kernel"""
-    return TRAFFIC_KEYS.get(kernel[:12], r"megakernel<false,")
-
-
-def read_traffic(paths, kernel_key):
-    """Per-launch HBM bytes of the dominant kernel from rocprofv3 --pmc counter_collection CSVs
-    (FETCH_SIZE and WRITE_SIZE come from separate passes; KB units; gfx950 FETCH_SIZE reports half
-    of wide reads -> x2, MI355X_MICROARCH.md 'HBM').  COUNT=true instantiations are excluded."""
-    import csv
-    fetch, write, nf, nw = 0.0, 0.0, 0, 0
-    for path in paths:
-        if not os.path.exists(path):
-            continue
-        with open(path) as f:
-            for row in csv.DictReader(f):
-                k = row.get("Kernel_Name", "").split("(")[0].replace(" ", "")
-                if not re.search(kernel_key, k):
-                    continue
-                name = row.get("Counter_Name", "")
-                v = float(row.get("Counter_Value", 0))
-                if name == "FETCH_SIZE":
-                    fetch += v
-                    nf += 1
-                elif name == "WRITE_SIZE":
-                    write += v
-                    nw += 1
-    if nf == 0 or nw == 0:
-        return None
-    return int((2 * fetch / nf + write / nw) * 1024)
+    return i0, i1, wall * 1e3
 
 
 def host_cpu():

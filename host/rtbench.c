@@ -301,9 +301,12 @@ int main(int argc, char** argv) {
     if (rank == 0)
     printf("{\"scene\": \"%s\", \"synthetic\": %d, \"width\": %d, \"height\": %d, \"spp\": %d, \"bounces\": %d, "
            "\"frames\": %d, \"frames_in_flight\": %d, \"grays_per_s\": %.4f, \"ms_per_frame\": %.3f, "
-           "\"rays_per_frame\": %.0f, \"last_frame_device_ms\": %.3f, \"triangles\": %llu, \"ranks\": %d}\n",
+           "\"rays_per_frame\": %.0f, \"last_frame_device_ms\": %.3f, \"triangles\": %llu, \"ranks\": %d, "
+           "\"graph_replays\": %llu, \"graph_captures\": %llu, \"graph_fallbacks\": %llu, \"graph_eager\": %llu}\n",
            scene_name, (int)synthetic, W, H, spp, bounces, frames, (int)s1.frames_in_flight, rays / dt / 1e9,
-           dt / frames * 1e3, rays / frames, s1.last_frame_ms, (unsigned long long)s1.triangles, nranks);
+           dt / frames * 1e3, rays / frames, s1.last_frame_ms, (unsigned long long)s1.triangles, nranks,
+           (unsigned long long)s1.total_graph_replays, (unsigned long long)s1.total_graph_captures,
+           (unsigned long long)s1.total_graph_fallbacks, (unsigned long long)s1.total_graph_eager);
 
     if (png && rank == 0) {   /* FramePresenter.draw + fragmentShader (FramePresenter.swift:103-238, Shaders.metal:39-52) */
         rgba8 = (uint8_t*)malloc((size_t)W * H * 4);

@@ -202,6 +202,16 @@ typedef struct rt_stats {
     uint64_t total_trace_dev_launches;
     double total_finish_dev_ms;
     uint64_t total_finish_dev_launches;
+    /* wavefront frames (device-driven, the default) by how they were submitted (running totals):
+       replayed from the slot's two captured HIP graphs, captured anew and launched (first frame of
+       a slot, or a launch argument changed), enqueued eagerly because the runtime refused a
+       capture (the slot then stays eager), enqueued eagerly by choice (RT_GRAPH=0, host-driven
+       rounds).  The replacement of the reference's per-frame command buffers
+       (Renderer.swift:1405-1490). */
+    uint64_t total_graph_replays;
+    uint64_t total_graph_captures;
+    uint64_t total_graph_fallbacks;
+    uint64_t total_graph_eager;
 } rt_stats;
 
 rt_status rt_create(const rt_opts* opts, rt_ctx** out);

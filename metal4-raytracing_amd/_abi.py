@@ -186,6 +186,10 @@ class Stats(C.Structure):
         ("total_trace_dev_launches", C.c_uint64),
         ("total_finish_dev_ms", C.c_double),
         ("total_finish_dev_launches", C.c_uint64),
+        ("total_graph_replays", C.c_uint64),
+        ("total_graph_captures", C.c_uint64),
+        ("total_graph_fallbacks", C.c_uint64),
+        ("total_graph_eager", C.c_uint64),
     ]
 
 

@@ -972,6 +972,11 @@ static rt_status harvest(rt_ctx* c, int k) {
     T.total_finish_dev_ms += S.finish_dev_ms;
     T.total_finish_dev_launches += (uint64_t)S.finish_dev_launches;
     T.total_finish_launches += (uint64_t)S.finish_launches;
+    if (f.wavefront) {
+        const int gm = f.wfs.graph_mode;   // host-driven frames (run_wavefront without a timeline) count as eager
+        (gm == kGraphReplay ? T.total_graph_replays : gm == kGraphCapture ? T.total_graph_captures
+         : gm == kGraphFallback ? T.total_graph_fallbacks : T.total_graph_eager) += 1;
+    }
     if (total(kCntOverflow)) FAIL(c, RT_ERR_STATE, "traversal stack overflow");
     return RT_OK;
 }
@@ -1373,6 +1378,10 @@ rt_status rt_get_stats(rt_ctx* c, rt_stats* out) {
     out->total_finish_dev_ms = T.total_finish_dev_ms;
     out->total_finish_dev_launches = T.total_finish_dev_launches;
     out->total_finish_launches = T.total_finish_launches;
+    out->total_graph_replays = T.total_graph_replays;
+    out->total_graph_captures = T.total_graph_captures;
+    out->total_graph_fallbacks = T.total_graph_fallbacks;
+    out->total_graph_eager = T.total_graph_eager;
     return RT_OK;
 }
 

@@ -26,7 +26,11 @@ constexpr int kBlock = 256;      // threads per block for the traversal kernels
 #ifndef RT_TOP_NODES
 #define RT_TOP_NODES 0
 #endif
-constexpr int kTopNodes = RT_TOP_NODES;
+#ifndef RT_TOP_NODES_FINISH
+#define RT_TOP_NODES_FINISH RT_TOP_NODES
+#endif
+constexpr int kTopNodes = RT_TOP_NODES;               // wf_trace
+constexpr int kTopNodesFinish = RT_TOP_NODES_FINISH;  // wf_finish_step
 
 struct DevScene {
     const float4* tris;

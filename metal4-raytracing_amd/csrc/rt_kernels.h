@@ -92,7 +92,10 @@ constexpr int kStatRounds = 0, kStatTraceLaunches = 1, kStatTraceRays = 2, kStat
 // wf_finish_step diagnostics (RT_WF_LOG): summed over waves, s_memrealtime ticks (10 ns) spent in
 // shading passes and in total, shading passes and lanes shaded
 constexpr int kStatDiagShadeT = 5, kStatDiagTotalT = 6, kStatDiagPasses = 7, kStatDiagShaded = 8;
-constexpr int kWfCountWords = 50 * kCntStride + 64 + 66 + 9;
+// wf_finish_step diagnostics (RT_WF_LOG): paths by segments run in the finish (32 bins) per entry
+// class (18: bounce 0..8 at entry, x refracting or not)
+constexpr int kWfDiagLen = kWfStat + 9;
+constexpr int kWfCountWords = 50 * kCntStride + 64 + 66 + 9 + 18 * 32;
 __host__ __device__ constexpr uint32_t cslot(int c) { return (uint32_t)c * kCntStride; }
 struct WavefrontBuffers {
     size_t queue_entries = 0;     // kShards segments of queue_entries / kShards
@@ -154,6 +157,7 @@ struct WfFrameStats {
     int trace_launches;
     float trace_ms;                 // their summed device time
     int finish_launches;
+    int graph_mode;                 // kGraph*: how the frame was submitted
 };
 // Runs one frame; returns false on a HIP error (message in *err).
 // tail_paths: finish-kernel threshold (0 = default / RT_TAIL_RAYS).
@@ -177,7 +181,9 @@ struct WfTimeline {
     hipGraphExec_t exec[2] = {nullptr, nullptr};
     std::vector<uint8_t> key;
     bool graph_failed = false;   // capture was refused once: this slot stays eager
+    int graph_mode = 0;          // the pending frame: kGraph* (rt_stats total_graph_*)
 };
+constexpr int kGraphEager = 0, kGraphReplay = 1, kGraphCapture = 2, kGraphFallback = 3;
 // Runs (host-driven: queue sizes read back every round; with RT_WF_LOG / RT_WF_HOST=1) or enqueues (device-driven, the default: `tl` receives the timeline, stats come
 // from wavefront_collect after the stream finished) one frame; false on a HIP error (*err).
 // sort_bins: hit-sort bins (0 = no sort).  extra_pass: the motion-adaptive extra samples can be

@@ -418,7 +418,7 @@ __device__ __forceinline__ void trav_start(Trav& T, f3 o, f3 d, float tmax) {
 // children sorted along its longest axis, reversed for rays going the other way).  The node's five
 // 16-B words come from the LDS copy of the top BFS nodes when the index is below n_top.  Returns
 // true once the query is finished (any-hit: an occluder was found).
-template <bool COUNT>
+template <bool COUNT, int TOP>
 __device__ __forceinline__ bool trav_step(const DevScene& S, Trav& T, bool any, int* stack, const uint4* lds_top,
                                           uint32_t n_top, TraceCounters& tc, bool& overflow) {
     bool tdone = false;
@@ -482,7 +482,7 @@ __device__ __forceinline__ bool trav_step(const DevScene& S, Trav& T, bool any, 
         }
         const uint32_t ni = T.g_base + (uint32_t)r;
         NodeWords w;
-        if (kTopNodes > 0 && ni < n_top) {
+        if (TOP > 0 && ni < n_top) {
             if (COUNT) tc.lds_nodes++;
             const uint4* l = lds_top + 5 * ni;
             w.h0 = __builtin_bit_cast(float4, l[0]);
@@ -502,10 +502,10 @@ __device__ __forceinline__ bool trav_step(const DevScene& S, Trav& T, bool any, 
 
 // Stages the first n_top BFS nodes of the 8-wide BVH in LDS (every thread of the block calls it;
 // the caller's next block barrier publishes them).
-constexpr int kTopLds = kTopNodes > 0 ? kTopNodes : 1;   // LDS array size (>= 1)
+template <int TOP>
 __device__ __forceinline__ uint32_t stage_top(const DevScene& S, uint4* lds_top) {
-    if (kTopNodes == 0) return 0u;
-    const uint32_t n_top = (uint32_t)min(S.num_nodes8, kTopNodes);
+    if (TOP == 0) return 0u;
+    const uint32_t n_top = (uint32_t)min(S.num_nodes8, TOP);
     for (uint32_t i = threadIdx.x; i < n_top * 5; i += kBlock) lds_top[i] = reinterpret_cast<const uint4*>(S.nodes8)[i];
     return n_top;
 }
@@ -836,7 +836,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ANY
 wf_trace(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int cur, int ts) {
     const FrameParams& P = *Pp;   // per-frame parameters in device memory
     __shared__ int lds_stack[kStackSize * kBlock];
-    __shared__ uint4 lds_top[kTopLds * 5];   // BVH top levels (BFS order: root, its children, ...)
+    __shared__ uint4 lds_top[(kTopNodes > 0 ? kTopNodes : 1) * 5];   // BVH top levels (BFS order: root, its children, ...)
     int* stack = &lds_stack[threadIdx.x];
     if (Q.dev_ctl) {
         // device-side round control: extend decides (uniformly, from the counters) whether this
@@ -858,7 +858,7 @@ wf_trace(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int cur, in
     __shared__ uint32_t ts_done;
     if (threadIdx.x == 0) ts_done = 0u;
     ts_start(Q, ts);
-    const uint32_t n_top = stage_top(S, lds_top);
+    const uint32_t n_top = stage_top<kTopNodes>(S, lds_top);
     __syncthreads();
     const ShardPrefix cnt = load_prefix(ANY ? Q.W.counts + cslot(kCntShadowQ) : Q.W.counts + cslot(cur * kShards));
     const uint32_t n = cnt.end[kShards - 1];
@@ -937,7 +937,7 @@ wf_trace(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int cur, in
         if (__ballot(active) == 0ull) break;
         if (!active) continue;
         if (COUNT) ++steps;
-        if (trav_step<COUNT>(S, T, ANY, stack, lds_top, n_top, tc, overflow)) {
+        if (trav_step<COUNT, kTopNodes>(S, T, ANY, stack, lds_top, n_top, tc, overflow)) {
             active = false;
             if (COUNT && Q.diag) {   // steps-per-ray histogram (log2 bins) of the counting frame
                 atomicAdd(&Q.W.counts[kWfDiagSteps + (ANY ? 32 : 0) + (31 - __builtin_clz(steps))], 1u);
@@ -976,7 +976,7 @@ wf_finish_step(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int c
     const FrameParams& P = *Pp;   // per-frame parameters in device memory
     if (cur < 0) cur = (int)__builtin_amdgcn_readfirstlane(Q.W.counts[cslot(kCntFinishQ)]);   // dev_ctl
     __shared__ int lds_stack[kStackSize * kBlock];
-    __shared__ uint4 lds_top[kTopLds * 5];
+    __shared__ uint4 lds_top[(kTopNodesFinish > 0 ? kTopNodesFinish : 1) * 5];
     __shared__ HaltonDim lds_halton[kHaltonLds];
     __shared__ MatRec lds_mat[kMatLds];
     __shared__ float lds_sray[6][kBlock];   // each lane's shadow ray (origin, direction)
@@ -984,7 +984,7 @@ wf_finish_step(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int c
     __shared__ uint32_t ts_done;
     if (threadIdx.x == 0) ts_done = 0u;
     ts_start(Q, ts);
-    const uint32_t n_top = stage_top(S, lds_top);
+    const uint32_t n_top = stage_top<kTopNodesFinish>(S, lds_top);
     const ShadeTabs halton = load_tabs(S, lds_halton, lds_mat);   // ends with a block barrier
     const Uniforms& U = P.U;
     const ShardPrefix cnt = load_prefix(Q.W.counts + cslot(cur * kShards));
@@ -1022,6 +1022,10 @@ wf_finish_step(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int c
     uint32_t n_pass = 0, n_shaded = 0;
     auto end_path = [&]() {
         Q.W.p_accum[pid] = make_float4(p.accum.x, p.accum.y, p.accum.z, 0.0f);
+        if (Q.diag) {   // segments by entry class: bounce at entry, refracting (tpass > 0) or not
+            const uint32_t b0 = min(meta.z & 0xffu, 8u), tp0 = (meta.z >> 8) & 0xffu;
+            atomicAdd(&Q.W.counts[kWfDiagLen + ((tp0 ? 9u : 0u) + b0) * 32u + min(segs, 31u)], 1u);
+        }
         mode = kIdle;
         max_segs = max(max_segs, segs);
         segs = 0;
@@ -1076,7 +1080,7 @@ wf_finish_step(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int c
         // ---- one traversal step (closest hit or shadow any-hit)
         if (mode == kClosest || mode == kShadow) {
             const bool any = mode == kShadow;
-            if (trav_step<COUNT>(S, T, any, stack, lds_top, n_top, tc, overflow)) {
+            if (trav_step<COUNT, kTopNodesFinish>(S, T, any, stack, lds_top, n_top, tc, overflow)) {
                 if (any) {   // shadow ray done: unoccluded -> add its contribution (:741-743)
                     if (!T.hit_any) p.accum = p.accum + contrib;
                     if (next) {
@@ -1368,6 +1372,20 @@ static bool iterate(const DevScene& S, const FrameParams& P, WfParams& Q, int& c
                 const double np = W.h_counts[kWfStat + kStatDiagPasses], ns = W.h_counts[kWfStat + kStatDiagShaded];
                 fprintf(stderr, "[wf] finish: %.1f %% of wave time in shading passes, %.0f passes, %.1f lanes per pass\n",
                         tt > 0 ? 100.0 * st / tt : 0.0, np, np > 0 ? ns / np : 0.0);
+                for (int cl = 0; cl < 18; ++cl) {
+                    uint32_t tot = 0;
+                    double sum = 0;
+                    for (int b = 0; b < 32; ++b) {
+                        tot += W.h_counts[kWfDiagLen + cl * 32 + b];
+                        sum += (double)b * W.h_counts[kWfDiagLen + cl * 32 + b];
+                    }
+                    if (!tot) continue;
+                    fprintf(stderr, "[wf] finish paths entering at bounce %d%s: %u, segments mean %.2f:", cl % 9,
+                            cl >= 9 ? " refracting" : "", tot, sum / tot);
+                    for (int b = 0; b < 32; ++b)
+                        if (W.h_counts[kWfDiagLen + cl * 32 + b]) fprintf(stderr, " %d:%u", b, W.h_counts[kWfDiagLen + cl * 32 + b]);
+                    fprintf(stderr, "\n");
+                }
                 fprintf(stderr, "[wf] finish wave end times (50 us bins):");
                 for (int b = 0; b < 64; ++b)
                     if (W.h_counts[kWfDiagHist + b]) fprintf(stderr, " %d:%u", b, W.h_counts[kWfDiagHist + b]);
@@ -1613,6 +1631,7 @@ static bool enqueue_wavefront(const DevScene& S, const FrameParams& P, WfParams&
     Q.finish_q = 0;   // set by record_base from the round count
     const bool with_extra = maxExtra > 0 && extra_pass;
     if (!graphs_on() || T.graph_failed) {
+        T.graph_mode = graphs_on() ? kGraphFallback : kGraphEager;
         if (!record_base(S, P, Q, count, full, stream, T, false, err)) return false;
         if (prev_done) WF_CHECK(hipStreamWaitEvent(stream, prev_done, 0));
         if (!record_rest(S, P, Q, count, full, maxExtra, with_extra, stream, T, false, err)) return false;
@@ -1650,6 +1669,7 @@ static bool enqueue_wavefront(const DevScene& S, const FrameParams& P, WfParams&
         return false;
     }
     if (rebuild && !T.graph_failed) T.key.swap(key);
+    T.graph_mode = T.graph_failed ? kGraphFallback : rebuild ? kGraphCapture : kGraphReplay;
     T.pending = true;
     return true;
 }
@@ -1670,6 +1690,7 @@ bool wavefront_collect(const WavefrontBuffers& W, WfTimeline& T, WfFrameStats* f
     fs->trace_rays = W.h_counts[kWfStat + kStatTraceRays];
     fs->trace_closest_rays = W.h_counts[kWfStat + kStatExtendRays];
     fs->finish_launches = (int)W.h_counts[kWfStat + kStatFinish];
+    fs->graph_mode = T.graph_mode;
     for (int pass = 0; pass < (T.dev_spans ? 2 : 0); ++pass)   // device-clock spans (10 ns ticks) of the launches that ran
         for (int k = 0; k <= kTsFinish; ++k) {
             const int slot = pass * kTsPass + k;

@@ -60,7 +60,11 @@ class TileGather:
 
     renderer: a Renderer whose latest radiance target holds this rank's tiles (device path), or
     None for the host path (gather(image) with a host image).  device: torch device of the
-    packed buffers (cuda for RCCL, cpu for gloo)."""
+    packed buffers (cuda for RCCL, cpu for gloo).  A renderer with a cpu `device` stages through
+    host memory: the device pack kernel writes a device buffer, the packed tiles cross to the host,
+    gloo gathers them, and the destination unpacks them with the device kernel (the rank flow of
+    the RCCL path with another transport: bench.py --gather-backend gloo, e.g. several ranks on
+    one GPU, which RCCL refuses)."""
 
     def __init__(self, width, height, tile, rank, nranks, device, renderer=None, dst=0):
         import torch
@@ -70,6 +74,10 @@ class TileGather:
         self.max_own = max(tile_count(width, height, tile, r, nranks) for r in range(nranks))
         self.packed = torch.zeros((self.max_own, tile, tile, 4), dtype=torch.float32, device=device)
         self.recv = ([torch.empty_like(self.packed) for _ in range(nranks)] if rank == dst else None)
+        self.staging = renderer is not None and torch.device(device).type == "cpu"
+        if self.staging:   # device-side buffers of the host-staged path
+            self.d_packed = torch.zeros(self.packed.shape, dtype=torch.float32, device="cuda")
+            self.d_recv = [torch.empty_like(self.d_packed) for _ in range(nranks)] if rank == dst else None
 
     def gather(self, image=None, events=None):
         """Gathers this frame's tiles on the dst rank. Device path: enqueued without a host wait;
@@ -82,10 +90,12 @@ class TileGather:
         if self.R is not None:
             # after the newest frame, on the stream the collective is ordered on; the renderer's
             # next frame overlaps the pack and the gather
-            self.R.pack_tiles(self.T, self.rank, self.n, self.packed.data_ptr(),
+            self.R.pack_tiles(self.T, self.rank, self.n, (self.d_packed if self.staging else self.packed).data_ptr(),
                               stream=torch.cuda.current_stream().cuda_stream)
             if events is not None:
                 events[0].record()
+            if self.staging:
+                self.packed.copy_(self.d_packed)   # waits for the pack on the current stream
         else:
             self.packed.copy_(torch.from_numpy(pack_host(image, self.T, self.rank, self.n, self.max_own)))
         dist.gather(self.packed, self.recv, dst=self.dst)
@@ -97,7 +107,11 @@ class TileGather:
             s = torch.cuda.current_stream().cuda_stream
             for r in range(self.n):
                 if r != self.rank:
-                    self.R.unpack_tiles(self.T, r, self.n, self.recv[r].data_ptr(), stream=s)
+                    src = self.recv[r]
+                    if self.staging:
+                        self.d_recv[r].copy_(src)
+                        src = self.d_recv[r]
+                    self.R.unpack_tiles(self.T, r, self.n, src.data_ptr(), stream=s)
             if events is not None:
                 events[1].record()
             return None

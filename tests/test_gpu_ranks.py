@@ -1,0 +1,40 @@
+"""The multi-rank frame flow on one GPU (Renderer.swift:1405-1503 renders on one
+device): `bench.py --gpus 2 --gather-backend gloo` starts two rank processes through its own
+launcher, both render their tiles on the box's GPU with the HIP path, pack them with the device
+kernel, gather the packed tiles over gloo (host-staged: RCCL refuses two ranks on one device) and
+rank 0 unpacks them with the device kernel.  Everything but RCCL's transport runs; the gathered
+frame must equal the one-rank frame bit for bit."""
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ARGS = ["--scene", "c1", "--width", "200", "--height", "136", "--spp", "2", "--bounces", "3", "--steps", "3",
+        "--warmup", "1", "--no-cpu", "--no-pmc", "--no-isolated"]
+
+
+def _bench(*extra):
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *ARGS, *extra], capture_output=True, text=True,
+                       timeout=240, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [x for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    return json.loads(lines[0])
+
+
+@pytest.mark.parametrize("n", [2, 3])
+def test_ranks_share_one_gpu_gloo_gather_bitwise(tmp_path, n):
+    one = _bench("--dump-radiance", str(tmp_path / "one.npy"))
+    many = _bench("--gpus", str(n), "--gather-backend", "gloo", "--dump-radiance", str(tmp_path / "many.npy"))
+    assert one["n_gpus"] == 1 and many["n_gpus"] == n and many["world_size"] == n
+    assert many["config"]["parallelism"] == f"tiles{n}" and "gloo" in many["config"]["workload"]
+    # all ranks' rays: the split frame traces the same rays as the whole one
+    assert many["config"]["rays_per_frame"] == one["config"]["rays_per_frame"]
+    a, b = np.load(tmp_path / "one.npy"), np.load(tmp_path / "many.npy")
+    assert a.shape == b.shape == (136, 200, 4)
+    assert np.array_equal(a, b)
