@@ -45,12 +45,13 @@ struct Tuning {
     int chunk;         // RT_CHUNK: rays per chunk grab of the traversal kernel
     int fchunk;        // RT_FCHUNK: paths per chunk grab of the finish kernel
     int shade_min;     // RT_SHADE_MIN: the finish kernel shades once this many lanes wait
+    int shade_min_x;   // RT_SHADE_MIN_X: the same once the finish queue is exhausted
+    int finish_hops;   // RT_FINISH_HOPS: finish launches per pass (all but the last hand sparse waves' paths on)
+    int dump_below;    // RT_DUMP_BELOW: a wave of an exhausted finish launch with fewer active lanes hands its paths on
     int finish_frac;   // RT_FINISH_FRAC: percent of the resident grid the finish launch takes (0 = by frames in flight)
     int trace_frac;    // RT_TRACE_FRAC: percent of the resident grid the persistent wf_trace launches take (0 = by frames in flight)
     bool log;          // RT_WF_LOG=1: per-round queue sizes, stage times and finish diagnostics on stderr
     bool host_ctl;     // RT_WF_HOST=1: host-driven rounds (queue sizes read back every round)
-    int ray_sort;      // RT_RAY_SORT: group the rays wf_shade appends by 1 = direction octant, 2 = direction
-                       // octant + origin octant around the camera (ray_key)
     unsigned shade_blocks;   // RT_SHADE_BLOCKS: wf_shade grid (grid-stride loop), a multiple of 8
 };
 static const Tuning& tuning() {
@@ -61,11 +62,13 @@ static const Tuning& tuning() {
         v.chunk = std::max(1, env_int("RT_CHUNK", 64));
         v.fchunk = std::max(1, env_int("RT_FCHUNK", 32));
         v.shade_min = env_int("RT_SHADE_MIN", 24);
+        v.shade_min_x = env_int("RT_SHADE_MIN_X", 24);
+        v.finish_hops = std::min(std::max(env_int("RT_FINISH_HOPS", 1), 1), 8);
+        v.dump_below = env_int("RT_DUMP_BELOW", 0);
         v.finish_frac = std::min(env_int("RT_FINISH_FRAC", 0), 100);
         v.trace_frac = std::min(env_int("RT_TRACE_FRAC", 0), 100);
         v.log = env_int("RT_WF_LOG", 0) != 0;
         v.host_ctl = env_int("RT_WF_HOST", 0) != 0;
-        v.ray_sort = env_int("RT_RAY_SORT", 0);
         v.shade_blocks = (unsigned)std::max(8, env_int("RT_SHADE_BLOCKS", 8192)) / 8u * 8u;
         return v;
     }();
@@ -170,45 +173,6 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
     return v;
 }
 
-// Key-grouped block allocation (extend / shadow ray coherence, Q.ray_sort): the block's entries are
-// allocated with ONE returning atomic as in block_alloc, but laid out grouped by key (key-major;
-// the order inside a key is that of the LDS atomics, which does not matter: each path's arithmetic
-// does not depend on which lane or position traces it).  Every thread of the block calls it.
-constexpr int kRayKeys = 64;   // direction octant x origin octant (ray_key)
-struct KeyAlloc {
-    uint32_t cnt[kRayKeys];
-};
-__device__ __forceinline__ uint32_t block_alloc_keyed(bool pred, uint32_t key, uint32_t* counter, KeyAlloc& sh) {
-    if (threadIdx.x < kRayKeys) sh.cnt[threadIdx.x] = 0u;
-    __syncthreads();
-    uint32_t rank = 0;
-    if (pred) rank = atomicAdd(&sh.cnt[key], 1u);   // LDS atomic
-    __syncthreads();
-    if (threadIdx.x < 64) {   // wave 0: exclusive scan of the key counts + the block's one global atomic
-        const uint32_t v = threadIdx.x < kRayKeys ? sh.cnt[threadIdx.x] : 0u;
-        const uint32_t incl = wave_incl_scan(v);
-        const uint32_t tot = (uint32_t)__shfl((int)incl, 63, 64);
-        uint32_t b = 0;
-        if (threadIdx.x == 0 && tot) b = atomicAdd(counter, tot);
-        b = (uint32_t)__shfl((int)b, 0, 64);
-        if (threadIdx.x < kRayKeys) sh.cnt[threadIdx.x] = b + incl - v;
-    }
-    __syncthreads();
-    const uint32_t slot = pred ? sh.cnt[key] + rank : 0u;
-    __syncthreads();
-    return slot;
-}
-__device__ __forceinline__ uint32_t octant(f3 d) {
-    return (d.x < 0.0f ? 1u : 0u) | (d.y < 0.0f ? 2u : 0u) | (d.z < 0.0f ? 4u : 0u);
-}
-// Q.ray_sort key of a ray: its direction octant (1), or that plus the octant of its origin around
-// the camera position (2: the first level of a Morton key of the origin, view-centred)
-__device__ __forceinline__ uint32_t ray_key(int mode, f3 o, f3 d, const rt_float3& cam) {
-    const uint32_t k = octant(d);
-    if (mode < 2) return k;
-    return k | (octant(mk3(o.x - cam.x, o.y - cam.y, o.z - cam.z)) << 3);
-}
-
 __device__ __forceinline__ uint32_t compact1by1(uint32_t x) {
     x &= 0x55555555u;
     x = (x | (x >> 1)) & 0x33333333u;
@@ -256,10 +220,13 @@ struct WfParams {
     uint32_t sort_bins;    // hit-sort bins (0 = shade reads the extend queue unsorted)
     int diag;              // wf_finish_step: record the diagnostics slots (RT_WF_LOG)
     int shade_min;         // wf_finish_step: shade once this many lanes wait (or none traverses)
+    int shade_min_x;       // wf_finish_step: the same once the launch's queue is exhausted
+    int finish_hops;       // finish launches per pass (wf_finish_step `hop` 0 .. finish_hops - 1)
+    int dump_below;        // hops before the last: once the launch's queue is exhausted, a wave with fewer
+                           // active lanes appends its paths that start a closest-hit query to the next hop's queue
     int fchunk;            // wf_finish_step: paths per chunk grab
     int finish_frac;       // percent of the resident grid the finish launch takes
     int trace_frac;        // percent of the resident grid the bulk wf_trace launches take
-    int ray_sort;          // wf_shade: extend / shadow rays grouped by ray_key inside each block's allocation
     int spans;             // record device-clock launch spans (rt_set_device_spans)
     int dev_ctl;           // device-side control (enqueue_wavefront): kernels read their queue sizes from
                            // the counters and skip once the live count fell below `tail`
@@ -324,18 +291,20 @@ __device__ __forceinline__ bool tail_mode(const WfParams& Q) {
 }
 constexpr int kCntChunkExtend = 32;   // 8 per-XCD chunk counters each
 constexpr int kCntChunkConnect = 40;
+// finish hops: the paths hop h hands on are counted in [kCntDump + (h & 1) * 8 + shard] (hop h + 1's input)
+constexpr int kCntDump = 50;
 
 // Inclusive prefix of a sharded queue's segment counts, loaded once per kernel (uniform, so the
 // loads are scalar and the lookups below stay in registers).
 struct ShardPrefix {
     uint32_t end[kShards];
 };
-__device__ __forceinline__ ShardPrefix load_prefix(const uint32_t* cnt) {
+__device__ __forceinline__ ShardPrefix load_prefix(const uint32_t* cnt, uint32_t cap = 0xffffffffu) {
     ShardPrefix p;
     uint32_t acc = 0;
     #pragma unroll
     for (int k = 0; k < kShards; ++k) {
-        acc += __builtin_amdgcn_readfirstlane(cnt[cslot(k)]);
+        acc += min(__builtin_amdgcn_readfirstlane(cnt[cslot(k)]), cap);   // a counter may run past a full segment
         p.end[k] = acc;
     }
     return p;
@@ -609,7 +578,6 @@ __global__ void __launch_bounds__(kBlock) wf_shade(DevScene S, const FrameParams
     __shared__ HaltonDim lds_halton[kHaltonLds];
     __shared__ MatRec lds_mat[kMatLds];
     __shared__ BlockAlloc2 ba2;
-    __shared__ KeyAlloc ka;
     if (tail_mode(Q)) return;
     const ShadeTabs halton = load_tabs(S, lds_halton, lds_mat);
     const Uniforms& U = P.U;
@@ -704,15 +672,8 @@ __global__ void __launch_bounds__(kBlock) wf_shade(DevScene S, const FrameParams
             }
         }
         uint32_t ns, nr;
-        if (Q.ray_sort) {
-            ns = block_alloc_keyed(r.shadow, ray_key(Q.ray_sort, r.so, r.sd, U.camera.position),
-                                   &Q.W.counts[cslot(kCntShadowQ + shard)], ka);
-            nr = block_alloc_keyed(r.next, ray_key(Q.ray_sort, rayO, rayD, U.camera.position),
-                                   &Q.W.counts[cslot(next * kShards + shard)], ka);
-        } else {
-            block_alloc2(r.shadow, &Q.W.counts[cslot(kCntShadowQ + shard)], r.next,
-                         &Q.W.counts[cslot(next * kShards + shard)], ba2, ns, nr);
-        }
+        block_alloc2(r.shadow, &Q.W.counts[cslot(kCntShadowQ + shard)], r.next,
+                     &Q.W.counts[cslot(next * kShards + shard)], ba2, ns, nr);
         if (r.shadow) {
             sqout[3 * (size_t)ns] = make_float4(r.so.x, r.so.y, r.so.z, __uint_as_float(pid));
             sqout[3 * (size_t)ns + 1] = make_float4(r.sd.x, r.sd.y, r.sd.z, r.stmax);
@@ -972,9 +933,14 @@ wf_trace(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int cur, in
 // five were measured no faster.
 template <bool COUNT, bool FULL>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 4)))
-wf_finish_step(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int cur, int ts) {
+wf_finish_step(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int cur, int ts, int hop) {
     const FrameParams& P = *Pp;   // per-frame parameters in device memory
     if (cur < 0) cur = (int)__builtin_amdgcn_readfirstlane(Q.W.counts[cslot(kCntFinishQ)]);   // dev_ctl
+    // hop h reads queue cur ^ (h & 1): the pass's remaining paths (h = 0) or what hop h - 1 handed
+    // on (counted in its kCntDump set), and hands its sparse waves' paths on to the other queue
+    const int qi = cur ^ (hop & 1), dq = qi ^ 1;
+    const bool dump = hop < Q.finish_hops - 1 && Q.dump_below > 0;
+    const int shard = blockIdx.x & (kShards - 1);
     __shared__ int lds_stack[kStackSize * kBlock];
     __shared__ uint4 lds_top[(kTopNodesFinish > 0 ? kTopNodesFinish : 1) * 5];
     __shared__ HaltonDim lds_halton[kHaltonLds];
@@ -987,11 +953,12 @@ wf_finish_step(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int c
     const uint32_t n_top = stage_top<kTopNodesFinish>(S, lds_top);
     const ShadeTabs halton = load_tabs(S, lds_halton, lds_mat);   // ends with a block barrier
     const Uniforms& U = P.U;
-    const ShardPrefix cnt = load_prefix(Q.W.counts + cslot(cur * kShards));
+    const ShardPrefix cnt = hop == 0 ? load_prefix(Q.W.counts + cslot(cur * kShards))
+                                     : load_prefix(Q.W.counts + cslot(kCntDump + ((hop - 1) & 1) * kShards), Q.seg_cap);
     const uint32_t n = cnt.end[kShards - 1];
-    if (Q.dev_ctl) stat_add(Q, kStatFinish, 1u);
+    if (Q.dev_ctl && (hop == 0 || n > 0)) stat_add(Q, kStatFinish, 1u);
     if (Q.dev_ctl && n > 0) stat_add(Q, kStatRounds, 1u);
-    const float4* qin = Q.W.q[cur];
+    const float4* qin = Q.W.q[qi];
     uint32_t* chunk_ctr = Q.W.counts + cslot(kCntChunkFinish);
     const uint32_t kChunk = (uint32_t)Q.fchunk;   // paths per grab
     constexpr int kIdle = 0, kClosest = 1, kShadow = 2, kReady = 3;
@@ -1057,7 +1024,7 @@ wf_finish_step(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int c
                     const uint32_t state = __float_as_uint(d.w);
                     const uint3 pm = path_meta(P, Q, pid);
                     meta = make_uint4(pm.x, pm.y, state, pm.z);
-                    const float4 c = state == 0u ? make_float4(1.0f, 1.0f, 1.0f, 0.0f) : Q.W.qc[cur][e];
+                    const float4 c = state == 0u ? make_float4(1.0f, 1.0f, 1.0f, 0.0f) : Q.W.qc[qi][e];
                     const float4 a = Q.W.p_accum[pid];
                     p.color = mk3(c.x, c.y, c.z);
                     p.accum = mk3(a.x, a.y, a.z);
@@ -1075,6 +1042,38 @@ wf_finish_step(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int c
             wnext += (uint32_t)__popcll(idle);
         }
         if (__ballot(mode != kIdle) == 0ull) break;   // idle everywhere => refill found nothing
+        // a sparse wave of an exhausted launch (not the last hop) hands its paths on as they start a
+        // closest-hit query (a query already under way starts again from the root in the next hop:
+        // its result does not depend on where it ran), so the next hop runs them in dense waves
+        // instead of this wave issuing full-width steps for a few lanes
+        if (dump && exhausted) {
+            if (__popcll(__ballot(mode != kIdle)) < (uint32_t)Q.dump_below) {
+                const bool want = mode == kClosest;
+                const unsigned long long wm = __ballot(want);
+                if (wm != 0ull) {
+                    uint32_t s0 = 0;
+                    if (lane_id() == 0)
+                        s0 = atomicAdd(&Q.W.counts[cslot(kCntDump + (hop & 1) * kShards + shard)], (uint32_t)__popcll(wm));
+                    s0 = __builtin_amdgcn_readfirstlane(s0);
+                    if (want) {
+                        const uint32_t slot = s0 + mbcnt64(wm);
+                        if (slot < Q.seg_cap) {   // past a full segment the lane keeps its path
+                            const size_t e = (size_t)shard * Q.seg_cap + slot;
+                            Q.W.q[dq][2 * e] = make_float4(rayO.x, rayO.y, rayO.z, __uint_as_float(pid));
+                            Q.W.q[dq][2 * e + 1] =
+                                make_float4(rayD.x, rayD.y, rayD.z, __uint_as_float(pack_state(p.bounce, p.tpass, p.step)));
+                            Q.W.qc[dq][e] = make_float4(p.color.x, p.color.y, p.color.z, 0.0f);
+                            Q.W.p_accum[pid] = make_float4(p.accum.x, p.accum.y, p.accum.z, 0.0f);
+                            mode = kIdle;
+                            n_closest--;   // the next hop traces (and counts) this query
+                            max_segs = max(max_segs, segs);
+                            segs = 0;
+                        }
+                    }
+                }
+                if (__ballot(mode != kIdle) == 0ull) break;
+            }
+        }
         ++iters;
 
         // ---- one traversal step (closest hit or shadow any-hit)
@@ -1102,7 +1101,7 @@ wf_finish_step(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int c
         // ---- shade the waiting lanes together (:324-774)
         const unsigned long long ready = __ballot(mode == kReady);
         if (ready != 0ull &&
-            (__popcll(ready) >= Q.shade_min || __ballot(mode == kClosest || mode == kShadow) == 0ull)) {
+            (__popcll(ready) >= (exhausted ? Q.shade_min_x : Q.shade_min) || __ballot(mode == kClosest || mode == kShadow) == 0ull)) {
             const uint64_t ts0 = Q.diag ? __builtin_amdgcn_s_memrealtime() : 0;
             if (Q.diag) {
                 ++n_pass;
@@ -1322,17 +1321,26 @@ static unsigned trace_grid_cap(const WfParams& Q) {
 // the finish launch: Q.finish_frac percent of the resident grid (frames in flight: the rest of the
 // machine stays free for the other frames' kernels)
 template <bool COUNT, bool FULL>
-static void launch_finish(const DevScene& S, const WfParams& Q, int cur, uint32_t n, hipStream_t stream, int ts) {
+static void launch_finish(const DevScene& S, const WfParams& Q, int cur, uint32_t n, hipStream_t stream, int ts, int hop) {
     static const unsigned full_cap = resident_grid(wf_finish_step<COUNT, FULL>, 2);
     const unsigned cap = std::max(1u, full_cap * (unsigned)Q.finish_frac / 100u);
     hipLaunchKernelGGL((wf_finish_step<COUNT, FULL>), dim3(grid_for(n, cap)), dim3(kBlock), 0, stream, S, Q.Pd, Q, cur,
-                       ts);
+                       ts, hop);
 }
 
 static void launch_finish_any(const DevScene& S, const WfParams& Q, bool count, bool full, int cur, uint32_t n,
-                              hipStream_t stream, int ts = -1) {
-    if (count) full ? launch_finish<true, true>(S, Q, cur, n, stream, ts) : launch_finish<true, false>(S, Q, cur, n, stream, ts);
-    else full ? launch_finish<false, true>(S, Q, cur, n, stream, ts) : launch_finish<false, false>(S, Q, cur, n, stream, ts);
+                              hipStream_t stream, int ts = -1, int hop = 0) {
+    if (count) full ? launch_finish<true, true>(S, Q, cur, n, stream, ts, hop) : launch_finish<true, false>(S, Q, cur, n, stream, ts, hop);
+    else full ? launch_finish<false, true>(S, Q, cur, n, stream, ts, hop) : launch_finish<false, false>(S, Q, cur, n, stream, ts, hop);
+}
+
+// Before finish hop h (of Q.finish_hops > 1): its hand-on counters start at zero, and so does the
+// chunk counter of every hop after the first (the frame start / extra pass clear it for hop 0).
+static hipError_t hop_reset(const WfParams& Q, int h, hipStream_t stream) {
+    hipError_t e = hipMemsetAsync(Q.W.counts + cslot(kCntDump + (h & 1) * kShards), 0, cslot(kShards) * sizeof(uint32_t),
+                                  stream);
+    if (e == hipSuccess && h > 0) e = hipMemsetD32Async(Q.W.counts + cslot(kCntChunkFinish), 0u, 1, stream);
+    return e;
 }
 
 static uint32_t queue_total(const uint32_t* h, int q) {
@@ -1353,8 +1361,11 @@ static bool iterate(const DevScene& S, const FrameParams& P, WfParams& Q, int& c
             WF_CHECK(hipEventRecord(W.ev[0], stream));
             WF_CHECK(hipMemsetAsync(W.counts + cslot(kCntChunkFinish), 0, sizeof(uint32_t), stream));
             if (Q.diag) WF_CHECK(hipMemsetAsync(W.counts + kWfDiagHist, 0, 64 * sizeof(uint32_t), stream));
-            launch_finish_any(S, Q, count, full, cur, n, stream);
-            WF_CHECK(hipGetLastError());
+            for (int h = 0; h < Q.finish_hops; ++h) {
+                if (Q.finish_hops > 1) WF_CHECK(hop_reset(Q, h, stream));
+                launch_finish_any(S, Q, count, full, cur, h ? 1u << 30 : n, stream, -1, h);
+                WF_CHECK(hipGetLastError());
+            }
             WF_CHECK(hipEventRecord(W.ev[1], stream));
             WF_CHECK(hipMemcpyAsync(W.h_counts, W.counts, kWfCountWords * sizeof(uint32_t), hipMemcpyDeviceToHost,
                                     stream));
@@ -1529,9 +1540,13 @@ static bool enqueue_pass(const DevScene& S, const FrameParams& P, const WfParams
     }
     // the finish chunk counter is zero here: the frame start clears every counter and the
     // extra-sample pass clears it again before its own finish launch
-    launch_finish_any(S, Q, count, full, -1, 1u << 30, stream, ts + kTsFinish);   // resident grid; input queue from the counters
-    WF_CHECK(hipGetLastError());
-    return E.span(5, err);
+    for (int h = 0; h < Q.finish_hops; ++h) {   // resident grid; input queue from the counters
+        if (Q.finish_hops > 1) WF_CHECK(hop_reset(Q, h, stream));
+        launch_finish_any(S, Q, count, full, -1, 1u << 30, stream, h == 0 ? ts + kTsFinish : -1, h);
+        WF_CHECK(hipGetLastError());
+        if (!E.span(5, err)) return false;
+    }
+    return true;
 }
 
 // One frame on `stream` in two parts: record_base = the base pass and the motion vectors,
@@ -1727,8 +1742,10 @@ bool run_wavefront(const DevScene& S, const FrameParams& P, WavefrontBuffers& W,
     Q.sort_bins = (uint32_t)sort_bins;
     Q.diag = tu.log ? 1 : 0;
     Q.shade_min = tu.shade_min;
+    Q.shade_min_x = tu.shade_min_x;
+    Q.finish_hops = tu.dump_below > 0 ? tu.finish_hops : 1;
+    Q.dump_below = tu.dump_below;
     Q.fchunk = tu.fchunk;
-    Q.ray_sort = tu.ray_sort;
     Q.spans = spans ? 1 : 0;
     Q.spp_div = make_fastdiv((uint32_t)Q.spp);
     Q.tile = P.tile_size;

@@ -63,5 +63,5 @@ def _roofline_consistent(d):
 
 def test_bench_emulated_rank_and_animation():
     d = _run("--scene", "c5", "--width", "128", "--height", "96", "--spp", "1", "--bounces", "2", "--steps", "3",
-             "--warmup", "1", "--no-cpu", "--animate", "--emulate-ranks", "2")
+             "--warmup", "1", "--no-cpu", "--no-pmc", "--animate", "--emulate-ranks", "2")
     assert d["value"] > 0 and d["config"]["animate"] is True and d["cpu_baseline"] is None

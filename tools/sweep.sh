@@ -21,7 +21,7 @@ for rep in $(seq ${REPS:-1}); do
       shift
     done; shift
     if [ -n "$lib" ]; then cp ab_$lib.so metal4-raytracing_amd/librt_hip.so; else cp /tmp/librt_keep.so metal4-raytracing_amd/librt_hip.so; fi
-    env "${envs[@]}" timeout -k 10 ${CASE_TIMEOUT:-200} python -u bench.py --no-cpu "$@" > gpurun_out/sw_$name$rep.log 2>&1 \
+    env "${envs[@]}" timeout -k 10 ${CASE_TIMEOUT:-200} python -u bench.py --no-cpu --no-pmc "$@" > gpurun_out/sw_$name$rep.log 2>&1 \
       || { tail -c 2000 gpurun_out/sw_$name$rep.log; exit 1; }
     python3 tools/line_summary.py gpurun_out/sw_$name$rep.log "$name$rep" || exit 1
   done < "$CASEFILE"
