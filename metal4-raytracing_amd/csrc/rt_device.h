@@ -19,18 +19,6 @@ namespace rt {
 
 constexpr int kStackSize = 16;   // per-thread traversal stack entries (LDS): node groups of the 8-wide BVH
 constexpr int kBlock = 256;      // threads per block for the traversal kernels
-// First BFS nodes of the 8-wide BVH staged in LDS by the traversal kernels (RT_TOP_NODES at build
-// time).  0 (default): every node comes from global memory.  Staging 32 served half of the node
-// tests of an extend ray from LDS but the kernels ran 2 % slower (the LDS / global branch and its
-// register moves cost more VALU than the L1 / L2 hits it saved).
-#ifndef RT_TOP_NODES
-#define RT_TOP_NODES 0
-#endif
-#ifndef RT_TOP_NODES_FINISH
-#define RT_TOP_NODES_FINISH RT_TOP_NODES
-#endif
-constexpr int kTopNodes = RT_TOP_NODES;               // wf_trace
-constexpr int kTopNodesFinish = RT_TOP_NODES_FINISH;  // wf_finish_step
 
 struct DevScene {
     const float4* tris;

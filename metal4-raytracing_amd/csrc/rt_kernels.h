@@ -85,7 +85,7 @@ constexpr int kShards = 8;        // queue segments (one allocation counter each
 // [32..39] / [40..47] per-XCD chunk counters of the extend / connect launches; each slot on a
 // 128-B line of its own (cslot), so the per-XCD shards never contend for one line's atomics.
 constexpr int kCntStride = 32;
-constexpr int kCntSlotsWf = 66;                       // counter slots (cslot) before the diagnostics words
+constexpr int kCntSlotsWf = 50;                       // counter slots (cslot) before the diagnostics words
 constexpr int kWfDiagHist = kCntSlotsWf * kCntStride; // 64 words: wf_finish wave end-time histogram (50 us bins)
 constexpr int kWfDiagSteps = kWfDiagHist + 64;        // 66 words: wf_trace steps-per-ray histograms + max
 constexpr int kWfStat = kWfDiagSteps + 66;              // 3 words: rounds, wf_trace launches, their rays

@@ -46,11 +46,10 @@ struct Tuning {
     int fchunk;        // RT_FCHUNK: paths per chunk grab of the finish kernel
     int shade_min;     // RT_SHADE_MIN: the finish kernel shades once this many lanes wait
     int shade_min_x;   // RT_SHADE_MIN_X: the same once the finish queue is exhausted
-    int finish_hops;   // RT_FINISH_HOPS: finish launches per pass (all but the last hand sparse waves' paths on)
-    int dump_below;    // RT_DUMP_BELOW: a wave of an exhausted finish launch with fewer active lanes hands its paths on
     int finish_frac;   // RT_FINISH_FRAC: percent of the resident grid the finish launch takes (0 = by frames in flight)
     int trace_frac;    // RT_TRACE_FRAC: percent of the resident grid the persistent wf_trace launches take (0 = by frames in flight)
-    bool log;          // RT_WF_LOG=1: per-round queue sizes, stage times and finish diagnostics on stderr
+    int log;           // RT_WF_LOG=1: per-round queue sizes, stage times and finish diagnostics on stderr
+                       // (=2 also the finish paths' segment counts: one atomic per path, slows the launch)
     bool host_ctl;     // RT_WF_HOST=1: host-driven rounds (queue sizes read back every round)
     unsigned shade_blocks;   // RT_SHADE_BLOCKS: wf_shade grid (grid-stride loop), a multiple of 8
 };
@@ -63,11 +62,9 @@ static const Tuning& tuning() {
         v.fchunk = std::max(1, env_int("RT_FCHUNK", 32));
         v.shade_min = env_int("RT_SHADE_MIN", 24);
         v.shade_min_x = env_int("RT_SHADE_MIN_X", 24);
-        v.finish_hops = std::min(std::max(env_int("RT_FINISH_HOPS", 1), 1), 8);
-        v.dump_below = env_int("RT_DUMP_BELOW", 0);
         v.finish_frac = std::min(env_int("RT_FINISH_FRAC", 0), 100);
         v.trace_frac = std::min(env_int("RT_TRACE_FRAC", 0), 100);
-        v.log = env_int("RT_WF_LOG", 0) != 0;
+        v.log = env_int("RT_WF_LOG", 0);
         v.host_ctl = env_int("RT_WF_HOST", 0) != 0;
         v.shade_blocks = (unsigned)std::max(8, env_int("RT_SHADE_BLOCKS", 8192)) / 8u * 8u;
         return v;
@@ -221,9 +218,6 @@ struct WfParams {
     int diag;              // wf_finish_step: record the diagnostics slots (RT_WF_LOG)
     int shade_min;         // wf_finish_step: shade once this many lanes wait (or none traverses)
     int shade_min_x;       // wf_finish_step: the same once the launch's queue is exhausted
-    int finish_hops;       // finish launches per pass (wf_finish_step `hop` 0 .. finish_hops - 1)
-    int dump_below;        // hops before the last: once the launch's queue is exhausted, a wave with fewer
-                           // active lanes appends its paths that start a closest-hit query to the next hop's queue
     int fchunk;            // wf_finish_step: paths per chunk grab
     int finish_frac;       // percent of the resident grid the finish launch takes
     int trace_frac;        // percent of the resident grid the bulk wf_trace launches take
@@ -291,8 +285,6 @@ __device__ __forceinline__ bool tail_mode(const WfParams& Q) {
 }
 constexpr int kCntChunkExtend = 32;   // 8 per-XCD chunk counters each
 constexpr int kCntChunkConnect = 40;
-// finish hops: the paths hop h hands on are counted in [kCntDump + (h & 1) * 8 + shard] (hop h + 1's input)
-constexpr int kCntDump = 50;
 
 // Inclusive prefix of a sharded queue's segment counts, loaded once per kernel (uniform, so the
 // loads are scalar and the lookups below stay in registers).
@@ -384,12 +376,12 @@ __device__ __forceinline__ void trav_start(Trav& T, f3 o, f3 d, float tmax) {
 // is tested: one memory latency; tested in mask order, so closest-hit updates are those of the
 // serial loop), then — for a lane whose triangles ran out in this step, and for every lane without
 // triangles — one 8-wide node: the next hit child of the current group in slot order (the node's
-// children sorted along its longest axis, reversed for rays going the other way).  The node's five
-// 16-B words come from the LDS copy of the top BFS nodes when the index is below n_top.  Returns
-// true once the query is finished (any-hit: an occluder was found).
-template <bool COUNT, int TOP>
-__device__ __forceinline__ bool trav_step(const DevScene& S, Trav& T, bool any, int* stack, const uint4* lds_top,
-                                          uint32_t n_top, TraceCounters& tc, bool& overflow) {
+// children sorted along its longest axis, reversed for rays going the other way), its five 16-B
+// words fetched from global memory (an LDS copy of the top levels measured no faster, DESIGN.md
+// §3.5).  Returns true once the query is finished (any-hit: an occluder was found).
+template <bool COUNT>
+__device__ __forceinline__ bool trav_step(const DevScene& S, Trav& T, bool any, int* stack, TraceCounters& tc,
+                                          bool& overflow) {
     bool tdone = false;
     if (T.t_mask != 0u) {
         const int k0 = lowest_bit(T.t_mask);
@@ -450,33 +442,12 @@ __device__ __forceinline__ bool trav_step(const DevScene& S, Trav& T, bool any, 
             }
         }
         const uint32_t ni = T.g_base + (uint32_t)r;
-        NodeWords w;
-        if (TOP > 0 && ni < n_top) {
-            if (COUNT) tc.lds_nodes++;
-            const uint4* l = lds_top + 5 * ni;
-            w.h0 = __builtin_bit_cast(float4, l[0]);
-            w.h1 = l[1];
-            w.qx = l[2];
-            w.qy = l[3];
-            w.qz = l[4];
-        } else {
-            if (COUNT) tc.nodes++;
-            w = load_node8(S.nodes8, ni);
-        }
+        if (COUNT) tc.nodes++;
+        const NodeWords w = load_node8(S.nodes8, ni);
         test_node8_words(w, T.R, 0.0f, T.best, T.g_hits, T.t_mask, T.t_valid, T.g_base, T.t_base, T.g_flip);
     }
     return tdone || (T.t_mask == 0u && T.g_hits == 0u && T.sp == 0);
 #undef RT_ISECT
-}
-
-// Stages the first n_top BFS nodes of the 8-wide BVH in LDS (every thread of the block calls it;
-// the caller's next block barrier publishes them).
-template <int TOP>
-__device__ __forceinline__ uint32_t stage_top(const DevScene& S, uint4* lds_top) {
-    if (TOP == 0) return 0u;
-    const uint32_t n_top = (uint32_t)min(S.num_nodes8, TOP);
-    for (uint32_t i = threadIdx.x; i < n_top * 5; i += kBlock) lds_top[i] = reinterpret_cast<const uint4*>(S.nodes8)[i];
-    return n_top;
 }
 
 // ---- base paths ----------------------------------------------------------------------------------------
@@ -797,7 +768,6 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ANY
 wf_trace(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int cur, int ts) {
     const FrameParams& P = *Pp;   // per-frame parameters in device memory
     __shared__ int lds_stack[kStackSize * kBlock];
-    __shared__ uint4 lds_top[(kTopNodes > 0 ? kTopNodes : 1) * 5];   // BVH top levels (BFS order: root, its children, ...)
     int* stack = &lds_stack[threadIdx.x];
     if (Q.dev_ctl) {
         // device-side round control: extend decides (uniformly, from the counters) whether this
@@ -819,7 +789,6 @@ wf_trace(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int cur, in
     __shared__ uint32_t ts_done;
     if (threadIdx.x == 0) ts_done = 0u;
     ts_start(Q, ts);
-    const uint32_t n_top = stage_top<kTopNodes>(S, lds_top);
     __syncthreads();
     const ShardPrefix cnt = load_prefix(ANY ? Q.W.counts + cslot(kCntShadowQ) : Q.W.counts + cslot(cur * kShards));
     const uint32_t n = cnt.end[kShards - 1];
@@ -898,7 +867,7 @@ wf_trace(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int cur, in
         if (__ballot(active) == 0ull) break;
         if (!active) continue;
         if (COUNT) ++steps;
-        if (trav_step<COUNT, kTopNodes>(S, T, ANY, stack, lds_top, n_top, tc, overflow)) {
+        if (trav_step<COUNT>(S, T, ANY, stack, tc, overflow)) {
             active = false;
             if (COUNT && Q.diag) {   // steps-per-ray histogram (log2 bins) of the counting frame
                 atomicAdd(&Q.W.counts[kWfDiagSteps + (ANY ? 32 : 0) + (31 - __builtin_clz(steps))], 1u);
@@ -933,16 +902,10 @@ wf_trace(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int cur, in
 // five were measured no faster.
 template <bool COUNT, bool FULL>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 4)))
-wf_finish_step(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int cur, int ts, int hop) {
+wf_finish_step(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int cur, int ts) {
     const FrameParams& P = *Pp;   // per-frame parameters in device memory
     if (cur < 0) cur = (int)__builtin_amdgcn_readfirstlane(Q.W.counts[cslot(kCntFinishQ)]);   // dev_ctl
-    // hop h reads queue cur ^ (h & 1): the pass's remaining paths (h = 0) or what hop h - 1 handed
-    // on (counted in its kCntDump set), and hands its sparse waves' paths on to the other queue
-    const int qi = cur ^ (hop & 1), dq = qi ^ 1;
-    const bool dump = hop < Q.finish_hops - 1 && Q.dump_below > 0;
-    const int shard = blockIdx.x & (kShards - 1);
     __shared__ int lds_stack[kStackSize * kBlock];
-    __shared__ uint4 lds_top[(kTopNodesFinish > 0 ? kTopNodesFinish : 1) * 5];
     __shared__ HaltonDim lds_halton[kHaltonLds];
     __shared__ MatRec lds_mat[kMatLds];
     __shared__ float lds_sray[6][kBlock];   // each lane's shadow ray (origin, direction)
@@ -950,15 +913,13 @@ wf_finish_step(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int c
     __shared__ uint32_t ts_done;
     if (threadIdx.x == 0) ts_done = 0u;
     ts_start(Q, ts);
-    const uint32_t n_top = stage_top<kTopNodesFinish>(S, lds_top);
     const ShadeTabs halton = load_tabs(S, lds_halton, lds_mat);   // ends with a block barrier
     const Uniforms& U = P.U;
-    const ShardPrefix cnt = hop == 0 ? load_prefix(Q.W.counts + cslot(cur * kShards))
-                                     : load_prefix(Q.W.counts + cslot(kCntDump + ((hop - 1) & 1) * kShards), Q.seg_cap);
+    const ShardPrefix cnt = load_prefix(Q.W.counts + cslot(cur * kShards));
     const uint32_t n = cnt.end[kShards - 1];
-    if (Q.dev_ctl && (hop == 0 || n > 0)) stat_add(Q, kStatFinish, 1u);
+    if (Q.dev_ctl) stat_add(Q, kStatFinish, 1u);
     if (Q.dev_ctl && n > 0) stat_add(Q, kStatRounds, 1u);
-    const float4* qin = Q.W.q[qi];
+    const float4* qin = Q.W.q[cur];
     uint32_t* chunk_ctr = Q.W.counts + cslot(kCntChunkFinish);
     const uint32_t kChunk = (uint32_t)Q.fchunk;   // paths per grab
     constexpr int kIdle = 0, kClosest = 1, kShadow = 2, kReady = 3;
@@ -989,7 +950,7 @@ wf_finish_step(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int c
     uint32_t n_pass = 0, n_shaded = 0;
     auto end_path = [&]() {
         Q.W.p_accum[pid] = make_float4(p.accum.x, p.accum.y, p.accum.z, 0.0f);
-        if (Q.diag) {   // segments by entry class: bounce at entry, refracting (tpass > 0) or not
+        if (Q.diag > 1) {   // RT_WF_LOG=2: segments by entry class: bounce at entry, refracting (tpass > 0) or not
             const uint32_t b0 = min(meta.z & 0xffu, 8u), tp0 = (meta.z >> 8) & 0xffu;
             atomicAdd(&Q.W.counts[kWfDiagLen + ((tp0 ? 9u : 0u) + b0) * 32u + min(segs, 31u)], 1u);
         }
@@ -1024,7 +985,7 @@ wf_finish_step(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int c
                     const uint32_t state = __float_as_uint(d.w);
                     const uint3 pm = path_meta(P, Q, pid);
                     meta = make_uint4(pm.x, pm.y, state, pm.z);
-                    const float4 c = state == 0u ? make_float4(1.0f, 1.0f, 1.0f, 0.0f) : Q.W.qc[qi][e];
+                    const float4 c = state == 0u ? make_float4(1.0f, 1.0f, 1.0f, 0.0f) : Q.W.qc[cur][e];
                     const float4 a = Q.W.p_accum[pid];
                     p.color = mk3(c.x, c.y, c.z);
                     p.accum = mk3(a.x, a.y, a.z);
@@ -1042,44 +1003,12 @@ wf_finish_step(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int c
             wnext += (uint32_t)__popcll(idle);
         }
         if (__ballot(mode != kIdle) == 0ull) break;   // idle everywhere => refill found nothing
-        // a sparse wave of an exhausted launch (not the last hop) hands its paths on as they start a
-        // closest-hit query (a query already under way starts again from the root in the next hop:
-        // its result does not depend on where it ran), so the next hop runs them in dense waves
-        // instead of this wave issuing full-width steps for a few lanes
-        if (dump && exhausted) {
-            if (__popcll(__ballot(mode != kIdle)) < (uint32_t)Q.dump_below) {
-                const bool want = mode == kClosest;
-                const unsigned long long wm = __ballot(want);
-                if (wm != 0ull) {
-                    uint32_t s0 = 0;
-                    if (lane_id() == 0)
-                        s0 = atomicAdd(&Q.W.counts[cslot(kCntDump + (hop & 1) * kShards + shard)], (uint32_t)__popcll(wm));
-                    s0 = __builtin_amdgcn_readfirstlane(s0);
-                    if (want) {
-                        const uint32_t slot = s0 + mbcnt64(wm);
-                        if (slot < Q.seg_cap) {   // past a full segment the lane keeps its path
-                            const size_t e = (size_t)shard * Q.seg_cap + slot;
-                            Q.W.q[dq][2 * e] = make_float4(rayO.x, rayO.y, rayO.z, __uint_as_float(pid));
-                            Q.W.q[dq][2 * e + 1] =
-                                make_float4(rayD.x, rayD.y, rayD.z, __uint_as_float(pack_state(p.bounce, p.tpass, p.step)));
-                            Q.W.qc[dq][e] = make_float4(p.color.x, p.color.y, p.color.z, 0.0f);
-                            Q.W.p_accum[pid] = make_float4(p.accum.x, p.accum.y, p.accum.z, 0.0f);
-                            mode = kIdle;
-                            n_closest--;   // the next hop traces (and counts) this query
-                            max_segs = max(max_segs, segs);
-                            segs = 0;
-                        }
-                    }
-                }
-                if (__ballot(mode != kIdle) == 0ull) break;
-            }
-        }
         ++iters;
 
         // ---- one traversal step (closest hit or shadow any-hit)
         if (mode == kClosest || mode == kShadow) {
             const bool any = mode == kShadow;
-            if (trav_step<COUNT, kTopNodesFinish>(S, T, any, stack, lds_top, n_top, tc, overflow)) {
+            if (trav_step<COUNT>(S, T, any, stack, tc, overflow)) {
                 if (any) {   // shadow ray done: unoccluded -> add its contribution (:741-743)
                     if (!T.hit_any) p.accum = p.accum + contrib;
                     if (next) {
@@ -1292,13 +1221,15 @@ static unsigned grid_for(uint32_t n, unsigned cap) {
     return g == 0 ? kShards : g;
 }
 
-#define WF_CHECK(expr)                    \
-    do {                                  \
-        hipError_t e_ = (expr);           \
-        if (e_ != hipSuccess) {           \
-            *err = hipGetErrorString(e_); \
-            return false;                 \
-        }                                 \
+#define WF_CHECK(expr)                                                                  \
+    do {                                                                                \
+        hipError_t e_ = (expr);                                                         \
+        if (e_ != hipSuccess) {                                                         \
+            static thread_local char msg_[192];                                         \
+            snprintf(msg_, sizeof msg_, "%.120s: %s", #expr, hipGetErrorString(e_));  \
+            *err = msg_;                                                                \
+            return false;                                                               \
+        }                                                                               \
     } while (0)
 
 // resident blocks (CUs x blocks per CU) of a persistent kernel
@@ -1321,26 +1252,21 @@ static unsigned trace_grid_cap(const WfParams& Q) {
 // the finish launch: Q.finish_frac percent of the resident grid (frames in flight: the rest of the
 // machine stays free for the other frames' kernels)
 template <bool COUNT, bool FULL>
-static void launch_finish(const DevScene& S, const WfParams& Q, int cur, uint32_t n, hipStream_t stream, int ts, int hop) {
-    static const unsigned full_cap = resident_grid(wf_finish_step<COUNT, FULL>, 2);
-    const unsigned cap = std::max(1u, full_cap * (unsigned)Q.finish_frac / 100u);
+static unsigned finish_full_cap() {   // resident blocks of the finish kernel, queried once
+    static const unsigned c = resident_grid(wf_finish_step<COUNT, FULL>, 2);
+    return c;
+}
+template <bool COUNT, bool FULL>
+static void launch_finish(const DevScene& S, const WfParams& Q, int cur, uint32_t n, hipStream_t stream, int ts) {
+    const unsigned cap = std::max(1u, finish_full_cap<COUNT, FULL>() * (unsigned)Q.finish_frac / 100u);
     hipLaunchKernelGGL((wf_finish_step<COUNT, FULL>), dim3(grid_for(n, cap)), dim3(kBlock), 0, stream, S, Q.Pd, Q, cur,
-                       ts, hop);
+                       ts);
 }
 
 static void launch_finish_any(const DevScene& S, const WfParams& Q, bool count, bool full, int cur, uint32_t n,
-                              hipStream_t stream, int ts = -1, int hop = 0) {
-    if (count) full ? launch_finish<true, true>(S, Q, cur, n, stream, ts, hop) : launch_finish<true, false>(S, Q, cur, n, stream, ts, hop);
-    else full ? launch_finish<false, true>(S, Q, cur, n, stream, ts, hop) : launch_finish<false, false>(S, Q, cur, n, stream, ts, hop);
-}
-
-// Before finish hop h (of Q.finish_hops > 1): its hand-on counters start at zero, and so does the
-// chunk counter of every hop after the first (the frame start / extra pass clear it for hop 0).
-static hipError_t hop_reset(const WfParams& Q, int h, hipStream_t stream) {
-    hipError_t e = hipMemsetAsync(Q.W.counts + cslot(kCntDump + (h & 1) * kShards), 0, cslot(kShards) * sizeof(uint32_t),
-                                  stream);
-    if (e == hipSuccess && h > 0) e = hipMemsetD32Async(Q.W.counts + cslot(kCntChunkFinish), 0u, 1, stream);
-    return e;
+                              hipStream_t stream, int ts = -1) {
+    if (count) full ? launch_finish<true, true>(S, Q, cur, n, stream, ts) : launch_finish<true, false>(S, Q, cur, n, stream, ts);
+    else full ? launch_finish<false, true>(S, Q, cur, n, stream, ts) : launch_finish<false, false>(S, Q, cur, n, stream, ts);
 }
 
 static uint32_t queue_total(const uint32_t* h, int q) {
@@ -1361,11 +1287,8 @@ static bool iterate(const DevScene& S, const FrameParams& P, WfParams& Q, int& c
             WF_CHECK(hipEventRecord(W.ev[0], stream));
             WF_CHECK(hipMemsetAsync(W.counts + cslot(kCntChunkFinish), 0, sizeof(uint32_t), stream));
             if (Q.diag) WF_CHECK(hipMemsetAsync(W.counts + kWfDiagHist, 0, 64 * sizeof(uint32_t), stream));
-            for (int h = 0; h < Q.finish_hops; ++h) {
-                if (Q.finish_hops > 1) WF_CHECK(hop_reset(Q, h, stream));
-                launch_finish_any(S, Q, count, full, cur, h ? 1u << 30 : n, stream, -1, h);
-                WF_CHECK(hipGetLastError());
-            }
+            launch_finish_any(S, Q, count, full, cur, n, stream);
+            WF_CHECK(hipGetLastError());
             WF_CHECK(hipEventRecord(W.ev[1], stream));
             WF_CHECK(hipMemcpyAsync(W.h_counts, W.counts, kWfCountWords * sizeof(uint32_t), hipMemcpyDeviceToHost,
                                     stream));
@@ -1487,7 +1410,9 @@ struct Enqueue {
         }
         const hipError_t e = hipEventRecordWithFlags(T.ev[T.n_ev], stream, capture ? hipEventRecordExternal : 0u);
         if (e != hipSuccess) {
-            *err = hipGetErrorString(e);
+            static thread_local char msg[160];
+            snprintf(msg, sizeof msg, "hipEventRecordWithFlags(%s): %s", capture ? "external" : "0", hipGetErrorString(e));
+            *err = msg;
             return false;
         }
         last = T.n_ev++;
@@ -1540,13 +1465,9 @@ static bool enqueue_pass(const DevScene& S, const FrameParams& P, const WfParams
     }
     // the finish chunk counter is zero here: the frame start clears every counter and the
     // extra-sample pass clears it again before its own finish launch
-    for (int h = 0; h < Q.finish_hops; ++h) {   // resident grid; input queue from the counters
-        if (Q.finish_hops > 1) WF_CHECK(hop_reset(Q, h, stream));
-        launch_finish_any(S, Q, count, full, -1, 1u << 30, stream, h == 0 ? ts + kTsFinish : -1, h);
-        WF_CHECK(hipGetLastError());
-        if (!E.span(5, err)) return false;
-    }
-    return true;
+    launch_finish_any(S, Q, count, full, -1, 1u << 30, stream, ts + kTsFinish);   // resident grid; input queue from the counters
+    WF_CHECK(hipGetLastError());
+    return E.span(5, err);
 }
 
 // One frame on `stream` in two parts: record_base = the base pass and the motion vectors,
@@ -1627,6 +1548,14 @@ static bool capture_part(const DevScene& S, const FrameParams& P, WfParams& Q, b
         if (g) (void)hipGraphDestroy(g);
         if (!ok || ce != hipSuccess || ie != hipSuccess) {
             // capture refused (an API the runtime cannot capture): this slot renders eagerly from now on
+            // (rt_stats total_graph_fallbacks counts its frames; the first refusal is reported here)
+            static bool reported = false;
+            if (!reported) {
+                reported = true;
+                fprintf(stderr, "rt: frame graph capture (part %d) refused: begin %s, record %s, end %s, instantiate %s; "
+                        "the slot renders eagerly\n", part, hipGetErrorString(be), ok ? "ok" : (rerr ? rerr : "?"),
+                        hipGetErrorString(ce), hipGetErrorString(ie));
+            }
             (void)hipGetLastError();
             T.exec[part] = nullptr;
             T.graph_failed = true;
@@ -1740,11 +1669,9 @@ bool run_wavefront(const DevScene& S, const FrameParams& P, WavefrontBuffers& W,
     Q.chunk = tu.chunk;
     Q.tail = tail_paths > 0 ? (uint32_t)tail_paths : tu.tail;
     Q.sort_bins = (uint32_t)sort_bins;
-    Q.diag = tu.log ? 1 : 0;
+    Q.diag = tu.log;
     Q.shade_min = tu.shade_min;
     Q.shade_min_x = tu.shade_min_x;
-    Q.finish_hops = tu.dump_below > 0 ? tu.finish_hops : 1;
-    Q.dump_below = tu.dump_below;
     Q.fchunk = tu.fchunk;
     Q.spans = spans ? 1 : 0;
     Q.spp_div = make_fastdiv((uint32_t)Q.spp);
@@ -1784,8 +1711,16 @@ bool run_wavefront(const DevScene& S, const FrameParams& P, WavefrontBuffers& W,
     }
     const bool full = needs_full(P.U, S);
     const int maxExtra = (P.U.enableMotionAdaptiveSampling != 0) ? max(P.U.motionSamplingMaxExtraSamples, 0) : 0;
-    if (dev)
+    if (dev) {
+        // the device queries behind the grid sizes run before a stream is capturing (a capture
+        // must hold stream work only)
+        (void)trace_grid_cap(Q);
+        (void)finish_full_cap<false, false>();
+        (void)finish_full_cap<false, true>();
+        (void)finish_full_cap<true, false>();
+        (void)finish_full_cap<true, true>();
         return enqueue_wavefront(S, P, Q, count, full, maxExtra, extra_pass, stream, prev_done, *tl, err);
+    }
     Q.dev_ctl = 0;
     Q.finish_q = 0;
 

@@ -1,8 +1,7 @@
 """Runtime variants selected by environment switches (read once per process, so each runs in a
-child process): the finish tail as several launches that hand sparse waves' paths on
-(RT_FINISH_HOPS / RT_DUMP_BELOW; 64 hands every path on as soon as a launch's queue runs out) or
-as one launch, and eager enqueue without frame graphs (RT_GRAPH=0), against the committed golden
-fixtures (bit-identical radiance, depth and ray counts).  The bulk pipelines run
+child process): host-driven rounds (RT_WF_HOST=1: queue sizes read back every round instead of
+the device-side round control) and eager enqueue without frame graphs (RT_GRAPH=0), against the
+committed golden fixtures (bit-identical radiance, depth and ray counts).  The bulk pipelines run
 wf_shade every bounce (the small fixture frames would otherwise go straight to the finish kernel)."""
 import os
 import subprocess
@@ -17,10 +16,7 @@ CASES = "c3g_small_b8,c1_ema_f3,lights_mix4_b3,c2_small_b4"
 PIPES = "wavefront,wavefront-bulk,wavefront-mixed"
 
 
-@pytest.mark.parametrize("env", [{"RT_FINISH_HOPS": "3", "RT_DUMP_BELOW": "24"},
-                                 {"RT_FINISH_HOPS": "2", "RT_DUMP_BELOW": "64"},
-                                 {"RT_FINISH_HOPS": "1"}, {"RT_GRAPH": "0"}],
-                         ids=["hops3", "hops2all", "onehop", "nograph"])
+@pytest.mark.parametrize("env", [{"RT_WF_HOST": "1"}, {"RT_GRAPH": "0"}], ids=["hostrounds", "nograph"])
 def test_env_variant_matches_golden(env):
     e = dict(os.environ)
     e.update(env)
