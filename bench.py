@@ -55,9 +55,7 @@ SCENES = {"c3g": "glass dragon scene (configs[2])", "c3": "glass dragon scene (c
 # Algorithmic bytes (DESIGN.md §6 'Roofline'): per traced ray its 48-B queue entry (extend: 32 B ray
 # in + 16 B hit out; connect: 48 B shadow entry in); per 8-wide node fetched from memory 80 B; per
 # triangle tested 48 B; per closest hit shaded inside the finish kernel 16 B triangle record +
-# 3 x 16 B normals + 48 B instance transform.  Node tests served from an LDS copy of the BVH's top
-# levels (a build with RT_TOP_NODES > 0; the rt_stats *_lds counters) move no memory per visit:
-# they are charged once per block (the staging read, B_NODE x kTopNodes per block).
+# 3 x 16 B normals + 48 B instance transform.
 B_RAY = 48
 B_NODE = 80  # compressed 8-wide node (Bvh8Node)
 B_TRI = 48
@@ -72,9 +70,6 @@ B_GEN_PATH, B_GEN_PIXEL = 48, 28
 # wf_motion + wf_resolve, per pixel: the samples' accumulators (16 B each), motion in / out and
 # history in / out (48 B)
 B_RESOLVE_PIXEL = 48
-TOP_NODES = 32          # rt_device.h kTopNodes of an RT_TOP_NODES build
-TRACE_BLOCKS_PER_CU = 8   # wf_trace: 256-thread blocks at 8 waves / SIMD
-FINISH_BLOCKS_PER_CU = 4  # wf_finish_step: 4 waves / SIMD
 # The frame's kernels, grouped as the roofline prices them: key, name, stage_ms slots (rt_stats
 # kernel_ms: [generate, extend, shade, connect, resolve, finish, hit sort]), and the rocprofv3
 # kernel-name pattern of their timed (non-counting) instantiations
@@ -368,6 +363,10 @@ def main():
     R = rt.Renderer(scene, a.width, a.height, device=local, pipeline=a.pipeline, seed=3, sort_bins=a.sort_bins,
                     bvh=a.bvh, frames_in_flight=a.frames_in_flight)
     setup_s = time.time() - t0
+    if a.frames_in_flight == 1:
+        # one frame at a time is the kernel-alone measurement: enqueue launch by launch, so every
+        # stage's HIP events are recorded (graph replays carry none under torch's HIP runtime)
+        R.set_graphs(False)
     R.samplesPerPixel = a.spp
     R.maxBounces = a.bounces
     tiles = (a.tile, rank, n) if n > 1 else None
@@ -475,12 +474,13 @@ def main():
         # after the timed region: the same frame with one frame in flight, so every kernel has the
         # GPU to itself; the roofline prices these launches, and their wall time per frame is the
         # single-frame latency
-        i0, i1, ms_frame = isolated(R, tiles, torch, dev, a.isolated_frames)
-        alone, shared = kernel_table(a, cst, i0, i1, a.isolated_frames, pixels, cus), table
+        i0, i1, ms_frame, cst_alone = isolated(R, tiles, torch, dev, a.isolated_frames)
+        alone, shared = kernel_table(a, cst_alone, i0, i1, a.isolated_frames, pixels, cus), table
+        stage_alone = (np.array(list(i1.total_kernel_ms)) - np.array(list(i0.total_kernel_ms))) / a.isolated_frames
     elif s1.frames_in_flight == 1:
-        alone, shared, ms_frame = table, None, ms_per_step
-    else:
-        alone, shared, ms_frame = table, None, None   # --no-isolated: the shared-GPU launches, flagged
+        alone, shared, ms_frame, stage_alone = table, None, ms_per_step, None
+    else:   # --no-isolated: the shared-GPU launches, flagged
+        alone, shared, ms_frame, stage_alone = table, None, None, None
     roof = roofline(alone, shared, pmc, pmc_err, ms_frame, ms_per_step, pmc_csvs)
     if alone is table and s1.frames_in_flight > 1:
         roof["not_a_kernel_measurement"] = True
@@ -520,6 +520,7 @@ def main():
             "setup_s": round(setup_s, 2),
             # [generate, extend, shade, connect, resolve, finish, hit sort]
             "stage_ms": [round(x, 3) for x in stage_ms], "sort_bins": a.sort_bins, "bvh": a.bvh,
+            "stage_ms_alone": [round(x, 3) for x in stage_alone] if stage_alone is not None else None,
             "pipeline_used": ["megakernel", "wavefront"][s1.pipeline], "iterations": s1.iterations,
             "frames_in_flight": s1.frames_in_flight, "animate": bool(skinned),
             # host time inside the submit calls per step (includes waiting for a free frame slot)
@@ -558,11 +559,9 @@ def kernel_table(a, cst, s0, s1, frames, pixels, cus):
                      ms_per_frame=ms, bytes_per_launch=b, nodes_per_ray=npr, tris_per_ray=tpr)]
     rays_c = cst.closest_rays + cst.shadow_rays
     q_nodes = cst.trace_nodes / max(cst.trace_rays, 1)
-    q_nodes_lds = cst.trace_nodes_lds / max(cst.trace_rays, 1)
     q_tris = cst.trace_tris / max(cst.trace_rays, 1)
     f_rays_c = rays_c - cst.trace_rays
     f_nodes = (cst.node_visits - cst.trace_nodes) / max(f_rays_c, 1)
-    f_nodes_lds = (cst.node_visits_lds - cst.trace_nodes_lds) / max(f_rays_c, 1)
     f_tris = (cst.tri_tests - cst.trace_tris) / max(f_rays_c, 1)
     trace_rays, trace_launches = d("total_trace_rays"), d("total_trace_launches")
     trace_closest, finish_launches = d("total_trace_closest_rays"), d("total_finish_launches")
@@ -574,16 +573,14 @@ def kernel_table(a, cst, s0, s1, frames, pixels, cus):
         if key == "trace":
             n = trace_launches
             rpl = trace_rays / max(n, 1)
-            b = rpl * (B_QRAY + (q_nodes - q_nodes_lds) * B_NODE + q_tris * B_TRI) + \
-                (cus * TRACE_BLOCKS_PER_CU * TOP_NODES * B_NODE if q_nodes_lds > 0 else 0)
-            extra = dict(rays_per_launch=rpl, nodes_per_ray=q_nodes, lds_nodes_per_ray=q_nodes_lds, tris_per_ray=q_tris)
+            b = rpl * (B_QRAY + q_nodes * B_NODE + q_tris * B_TRI)
+            extra = dict(rays_per_launch=rpl, nodes_per_ray=q_nodes, tris_per_ray=q_tris)
         elif key == "finish":
             n = finish_launches
             f_rays = (rays - trace_rays) / max(n, 1)
             f_closest = (closest - trace_closest) / max(n, 1)
-            b = f_rays * (B_RAY + (f_nodes - f_nodes_lds) * B_NODE + f_tris * B_TRI) + f_closest * B_HIT + \
-                (cus * FINISH_BLOCKS_PER_CU * TOP_NODES * B_NODE if f_nodes_lds > 0 else 0)
-            extra = dict(rays_per_launch=f_rays, nodes_per_ray=f_nodes, lds_nodes_per_ray=f_nodes_lds, tris_per_ray=f_tris)
+            b = f_rays * (B_RAY + f_nodes * B_NODE + f_tris * B_TRI) + f_closest * B_HIT
+            extra = dict(rays_per_launch=f_rays, nodes_per_ray=f_nodes, tris_per_ray=f_tris)
         elif key == "shade":
             n = trace_launches / 2   # one per bulk round (extend + connect are the round's wf_trace pair)
             b = trace_closest / max(n, 1) * B_SHADE_HIT
@@ -610,6 +607,12 @@ def roofline(alone, shared, pmc, pmc_err, ms_frame_alone, ms_per_step, pmc_csvs)
     launch time alone, against 8 TB/s.  The algorithmic-byte fraction and the L2-gather figure are
     secondary fields; the shared-GPU figures of the timed region (frames in flight) are under
     `in_flight`."""
+    if not any(k["ms_per_frame"] > 0 for k in alone):
+        # --no-isolated over graph replays: no launch of the run was timed on its own
+        return {"bound": "hbm", "peak": HBM_PEAK_GBS, "unit": "GB/s", "kernel": None, "achieved": None, "frac": None,
+                "traffic": None, "ms_per_step": round(ms_per_step, 4),
+                "note": "no per-kernel times: the timed frames were graph replays (DESIGN.md §3.4) and --no-isolated "
+                        "skipped the kernels-alone frames"}
     dom = max(alone, key=lambda k: k["ms_per_frame"])
     pmc = pmc or {}
     kernels = []
@@ -644,7 +647,11 @@ def roofline(alone, shared, pmc, pmc_err, ms_frame_alone, ms_per_step, pmc_csvs)
         "pmc_files": {c: os.path.relpath(p, ROOT) if p.startswith(ROOT) else p for c, p in pmc_csvs.items()} or None,
         "kernels": kernels,
     }
-    if shared is not None:
+    if shared is not None and sum(k["ms_per_frame"] for k in shared) == 0:
+        r["in_flight"] = {"ms_per_step": round(ms_per_step, 4),
+                          "note": "the timed frames were graph replays, which record no per-stage times under this HIP "
+                                  "runtime (DESIGN.md §3.4)"}
+    elif shared is not None:
         r["in_flight"] = {
             "note": "frames in flight share the GPU: a launch's time includes the time its workgroups wait for CUs "
                     "other frames' kernels hold, so these are not kernel measurements",
@@ -657,11 +664,19 @@ def roofline(alone, shared, pmc, pmc_err, ms_frame_alone, ms_per_step, pmc_csvs)
 def isolated(R, tiles, torch, dev, frames):
     """The bench frame with one frame in flight, after the timed region: the renderer on a caller's
     stream keeps one slot (rt_set_stream), so every launch has the GPU to itself.  Returns the stats
-    before / after and the wall time per frame (single-frame latency)."""
+    before / after, the wall time per frame (single-frame latency) and the stats of a counting frame
+    of the same configuration (one slot: the single-frame finish threshold, so its launches trace
+    other rays than the timed region's)."""
     s = torch.cuda.Stream(device=dev)
     R.set_stream(s.cuda_stream)
+    R.set_graphs(False)   # enqueued launch by launch: every stage's HIP events are recorded
     try:
-        R.draw(tiles=tiles)   # capture / warm the single slot
+        R.set_counting(True)   # warms the single slot and counts its node / triangle visits
+        R.draw(tiles=tiles)
+        R.wait()
+        cst = R.stats()
+        R.set_counting(False)
+        R.draw(tiles=tiles)
         R.wait()
         i0 = R.stats()
         t0 = time.perf_counter()
@@ -671,8 +686,9 @@ def isolated(R, tiles, torch, dev, frames):
         wall = (time.perf_counter() - t0) / frames
         i1 = R.stats()
     finally:
+        R.set_graphs(True)
         R.set_stream(None)
-    return i0, i1, wall * 1e3
+    return i0, i1, wall * 1e3, cst
 
 
 def host_cpu():

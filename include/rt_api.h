@@ -151,8 +151,7 @@ typedef struct rt_tile_set {
 typedef struct rt_stats {
     uint64_t closest_rays;  /* closest-hit queries traced in the last frame (incl. primary) */
     uint64_t shadow_rays;   /* any-hit shadow queries traced in the last frame */
-    uint64_t node_visits;   /* BVH node tests (counting frames only, see rt_set_counting; the LDS-served
-                               share is node_visits_lds) */
+    uint64_t node_visits;   /* BVH node tests (counting frames only, see rt_set_counting) */
     uint64_t tri_tests;     /* triangles tested (counting frames only) */
     uint64_t paths;         /* pixel samples started */
     uint64_t bvh_nodes;     /* nodes in the current BVH */
@@ -186,8 +185,8 @@ typedef struct rt_stats {
     double total_trace_ms;
     uint64_t total_trace_launches;
     uint64_t total_finish_launches;
-    /* counting frames: the node visits served from the LDS copy of the BVH's top levels (no
-       memory traffic); included in node_visits / trace_nodes */
+    /* reserved, always 0 (node visits served from an LDS copy of the BVH's top levels: that
+       staging was measured and removed) */
     uint64_t node_visits_lds;
     uint64_t trace_nodes_lds;
     /* wavefront, device clock: each launch from its first workgroup's start to its last wave's end
@@ -279,8 +278,8 @@ rt_status rt_present(rt_ctx* ctx, const rt_present_opts* opts, uint8_t* host_rgb
 /* Multi-GPU: pack this rank's tiles of the latest radiance into a device buffer of
  * rt_tile_count(...) * tile_size^2 * 4 floats, and the inverse on the gathering rank
  * (writing into the latest radiance target). Device pointers; enqueued after the newest frame
- * on the ctx stream (the _on forms: on `hip_stream`, e.g. the stream the collective runs on),
- * without a host wait.  The next frames overlap them (see frames_in_flight); rt_wait waits for
+ * on the ctx stream (the _on forms: on `hip_stream` exactly as given, e.g. the stream the
+ * collective runs on; NULL is HIP's null stream, PyTorch's default stream), without a host wait.  The next frames overlap them (see frames_in_flight); rt_wait waits for
  * them too. */
 int32_t rt_tile_count(int32_t width, int32_t height, const rt_tile_set* tiles);
 rt_status rt_pack_tiles(rt_ctx* ctx, const rt_tile_set* tiles, void* device_dst);
@@ -302,6 +301,12 @@ rt_status rt_set_counting(rt_ctx* ctx, int32_t enabled);
  * while enabled.  Off by default: the stamps cost ~1 % of a C3g frame.  Measurement only (no
  * reference counterpart). */
 rt_status rt_set_device_spans(rt_ctx* ctx, int32_t enabled);
+/* Wavefront frames captured once per frame slot as HIP graphs and replayed (default: on; the
+ * environment's RT_GRAPH=0 turns the default off), or enqueued launch by launch (off) — the
+ * replacement of the reference's per-frame command buffers (Renderer.swift:1405-1490).  Under a
+ * HIP runtime that takes no timing events inside a graph, replayed frames record no per-stage
+ * times (rt_stats kernel_ms); frames submitted with graphs off always do. */
+rt_status rt_set_graphs(rt_ctx* ctx, int32_t enabled);
 rt_status rt_get_stats(rt_ctx* ctx, rt_stats* out);
 
 /* Library build identification (kernel code object arch etc). */

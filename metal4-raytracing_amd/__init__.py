@@ -334,6 +334,11 @@ class Renderer:
         """Device-clock launch spans in the stats (rt_set_device_spans; measurement only)."""
         _check(lib().rt_set_device_spans(self._ctx, 1 if on else 0), self._ctx)
 
+    def set_graphs(self, on):
+        """Frames captured as HIP graphs and replayed (default) or enqueued launch by launch
+        (rt_set_graphs); frames enqueued eagerly always record their per-stage times."""
+        _check(lib().rt_set_graphs(self._ctx, 1 if on else 0), self._ctx)
+
     def stats(self):
         s = Stats()
         _check(lib().rt_get_stats(self._ctx, C.byref(s)), self._ctx)
@@ -409,8 +414,8 @@ class Renderer:
         return int(lib().rt_tile_count(self.width, self.height, C.byref(ts)))
 
     def pack_tiles(self, tile_size, rank, nranks, device_ptr, stream=None):
-        """Packs this rank's tiles of the newest frame (after it, on `stream`: a HIP stream handle,
-        None = the renderer's stream); no host wait."""
+        """Packs this rank's tiles of the newest frame (after it, on `stream`: a HIP stream handle, 0 =
+        HIP's null stream, i.e. torch's default stream; None = the renderer's stream); no host wait."""
         ts = TileSet(tile_size, rank, nranks, 0)
         if stream is None:
             _check(lib().rt_pack_tiles(self._ctx, C.byref(ts), C.c_void_p(device_ptr)), self._ctx)

@@ -229,7 +229,7 @@ EXPORTED_SYMBOLS = [
     "rt_read_radiance", "rt_read_aux", "rt_tile_count", "rt_pack_tiles", "rt_unpack_tiles",
     "rt_pack_tiles_on", "rt_unpack_tiles_on", "rt_present", "rt_write_png",
     "rt_pack_tiles_host", "rt_unpack_tiles_host",
-    "rt_set_counting", "rt_set_device_spans", "rt_get_stats", "rt_version", "rt_debug_trace_host",
+    "rt_set_counting", "rt_set_device_spans", "rt_set_graphs", "rt_get_stats", "rt_version", "rt_debug_trace_host",
     # rt_scene.h
     "rt_material_override_glass", "rt_scene_new", "rt_scene_free", "rt_scene_last_error",
     "rt_scene_add_obj", "rt_scene_add_usd", "rt_scene_add_procedural", "rt_scene_set_lights", "rt_scene_set_light_intensity",
@@ -275,6 +275,7 @@ def declare(lib):
         "rt_unpack_tiles_host": (st, [C.c_int32, C.c_int32, P(TileSet), P(C.c_float), P(C.c_float)]),
         "rt_set_counting": (st, [vp, C.c_int32]),
         "rt_set_device_spans": (st, [vp, C.c_int32]),
+        "rt_set_graphs": (st, [vp, C.c_int32]),
         "rt_get_stats": (st, [vp, P(Stats)]),
         "rt_version": (C.c_char_p, []),
         "rt_debug_trace_host": (st, [P(SceneDesc), P(C.c_float), P(C.c_float), C.c_uint32, C.c_int32, P(C.c_float),

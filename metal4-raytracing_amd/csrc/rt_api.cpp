@@ -106,6 +106,7 @@ struct rt_ctx {
     std::string err;
     bool counting = false;
     bool spans = false;              // rt_set_device_spans
+    bool graphs = true;              // rt_set_graphs (and RT_GRAPH, read once)
 
     // host scene copies
     std::vector<float4> h_pos, h_nrm;
@@ -950,12 +951,12 @@ static rt_status harvest(rt_ctx* c, int k) {
     S.closest_rays = total(kCntClosest);
     S.shadow_rays = total(kCntShadow);
     S.node_visits = total(kCntNodes);
-    S.node_visits_lds = total(kCntNodesLds);
+    S.node_visits_lds = 0;
     S.tri_tests = total(kCntTris);
     S.paths = total(kCntPaths);
     S.trace_nodes = f.wavefront ? total(kCntTraceNodes) : 0;
     S.trace_tris = f.wavefront ? total(kCntTraceTris) : 0;
-    S.trace_nodes_lds = f.wavefront ? total(kCntTraceNodesLds) : 0;
+    S.trace_nodes_lds = 0;
     rt_stats& T = c->totals;
     T.frames_total += 1;
     T.total_closest_rays += S.closest_rays;
@@ -1119,7 +1120,7 @@ rt_status rt_render_frame(rt_ctx* c, const Uniforms* U, const rt_tile_set* tiles
         static const bool tail_env = getenv("RT_TAIL_RAYS") != nullptr;
         const int tail = c->tail_paths ? c->tail_paths : (nfl > 1 && !tail_env ? kTailInFlight[nfl] : 0);
         if (own > 0 && !run_wavefront(S, P, F.wf, own, c->counting, c->spans, tail, c->sort_bins, extra_pass, nfl, stream,
-                                      cross ? prev.done : nullptr, &F.wft, &F.wfs, &err))
+                                      cross ? prev.done : nullptr, &F.wft, &F.wfs, &err, c->graphs))
             FAIL(c, RT_ERR_HIP, std::string("wavefront: ") + (err ? err : "?"));
         if (own == 0 && cross) HIPC(c, hipStreamWaitEvent(stream, prev.done, 0));
     } else {
@@ -1194,14 +1195,17 @@ rt_status rt_read_aux(rt_ctx* c, float* depth, float* motion, float* gbuffer) {
 // frame's `done` event over themselves: the frame that next writes the same accumulation target
 // (two frames later) waits for it before its resolve, so the gather of frame f overlaps the
 // rendering of frame f+1.
-static rt_status tiles_op(rt_ctx* c, const rt_tile_set* t, const void* src, void* dst, hipStream_t stream, bool pack) {
+// own_stream: the ctx stream (rt_pack_tiles / rt_unpack_tiles); otherwise `stream` as the caller gave it,
+// the null stream included (a collective ordered on PyTorch's default stream must see the pack)
+static rt_status tiles_op(rt_ctx* c, const rt_tile_set* t, const void* src, void* dst, hipStream_t stream, bool pack,
+                          bool own_stream) {
     if (!c || (pack ? !dst : !src)) FAIL(c, RT_ERR_INVALID_ARG, "null argument");
     if (!c->width) FAIL(c, RT_ERR_STATE, "no targets");
     int ts, rank, nranks, tiles_x, own;
     rt_status st = resolve_tiles(c, t, ts, rank, nranks, tiles_x, own);
     if (st) return st;
     HIPC(c, hipSetDevice(c->device));
-    if (!stream) stream = c->stream;
+    if (own_stream) stream = c->stream;
     FrameSlot& f = c->slot[c->last_slot];
     if (f.used) HIPC(c, hipStreamWaitEvent(stream, f.done, 0));
     float4* accum = (float4*)c->d_accum[c->read_idx].p;
@@ -1290,18 +1294,20 @@ rt_status rt_present(rt_ctx* c, const rt_present_opts* o, uint8_t* host_rgba8) {
     return RT_OK;
 }
 
-rt_status rt_pack_tiles(rt_ctx* c, const rt_tile_set* t, void* dst) { return tiles_op(c, t, nullptr, dst, nullptr, true); }
+rt_status rt_pack_tiles(rt_ctx* c, const rt_tile_set* t, void* dst) {
+    return tiles_op(c, t, nullptr, dst, nullptr, true, true);
+}
 
 rt_status rt_unpack_tiles(rt_ctx* c, const rt_tile_set* t, const void* src) {
-    return tiles_op(c, t, src, nullptr, nullptr, false);
+    return tiles_op(c, t, src, nullptr, nullptr, false, true);
 }
 
 rt_status rt_pack_tiles_on(rt_ctx* c, const rt_tile_set* t, void* dst, void* stream) {
-    return tiles_op(c, t, nullptr, dst, (hipStream_t)stream, true);
+    return tiles_op(c, t, nullptr, dst, (hipStream_t)stream, true, false);
 }
 
 rt_status rt_unpack_tiles_on(rt_ctx* c, const rt_tile_set* t, const void* src, void* stream) {
-    return tiles_op(c, t, src, nullptr, (hipStream_t)stream, false);
+    return tiles_op(c, t, src, nullptr, (hipStream_t)stream, false, false);
 }
 
 static rt_status host_tiles(int32_t w, int32_t h, const rt_tile_set* t, int& ts, int& rank, int& nranks, int& tiles_x,
@@ -1351,6 +1357,12 @@ rt_status rt_set_counting(rt_ctx* c, int32_t enabled) {
 rt_status rt_set_device_spans(rt_ctx* c, int32_t enabled) {
     if (!c) FAIL(c, RT_ERR_INVALID_ARG, "null ctx");
     c->spans = enabled != 0;
+    return RT_OK;
+}
+
+rt_status rt_set_graphs(rt_ctx* c, int32_t enabled) {
+    if (!c) FAIL(c, RT_ERR_INVALID_ARG, "null ctx");
+    c->graphs = enabled != 0;
     return RT_OK;
 }
 

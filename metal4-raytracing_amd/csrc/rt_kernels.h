@@ -10,11 +10,11 @@ namespace rt {
 
 constexpr int kHaltonLds = 64;   // first Halton dimensions staged in LDS per block
 
-// kCntNodes: every node test; kCntNodesLds: those served from the LDS copy of the top levels.
+// kCntNodes: every node test.  Slots 8 and 9 are unused (formerly LDS-served node tests).
 // kCntTrace*: the share of the visits made by wf_trace launches.
 enum CounterSlot {
     kCntClosest = 0, kCntShadow = 1, kCntNodes = 2, kCntTris = 3, kCntPaths = 4, kCntOverflow = 5,
-    kCntTraceNodes = 6, kCntTraceTris = 7, kCntNodesLds = 8, kCntTraceNodesLds = 9, kCntSlots = 10
+    kCntTraceNodes = 6, kCntTraceTris = 7, kCntSlots = 10
 };
 
 struct FrameParams {
@@ -85,7 +85,7 @@ constexpr int kShards = 8;        // queue segments (one allocation counter each
 // [32..39] / [40..47] per-XCD chunk counters of the extend / connect launches; each slot on a
 // 128-B line of its own (cslot), so the per-XCD shards never contend for one line's atomics.
 constexpr int kCntStride = 32;
-constexpr int kCntSlotsWf = 50;                       // counter slots (cslot) before the diagnostics words
+constexpr int kCntSlotsWf = 66;                       // counter slots (cslot) before the diagnostics words
 constexpr int kWfDiagHist = kCntSlotsWf * kCntStride; // 64 words: wf_finish wave end-time histogram (50 us bins)
 constexpr int kWfDiagSteps = kWfDiagHist + 64;        // 66 words: wf_trace steps-per-ray histograms + max
 constexpr int kWfStat = kWfDiagSteps + 66;              // 3 words: rounds, wf_trace launches, their rays
@@ -195,7 +195,7 @@ constexpr int kGraphEager = 0, kGraphReplay = 1, kGraphCapture = 2, kGraphFallba
 // are ordered after it, everything before them overlaps it.
 bool run_wavefront(const DevScene& S, const FrameParams& P, WavefrontBuffers& W, int own_tiles, bool count, bool spans,
                    int tail_paths, int sort_bins, bool extra_pass, int in_flight, hipStream_t stream,
-                   hipEvent_t prev_done, WfTimeline* tl, WfFrameStats* fs, const char** err);
+                   hipEvent_t prev_done, WfTimeline* tl, WfFrameStats* fs, const char** err, bool graphs = true);
 bool wavefront_collect(const WavefrontBuffers& W, WfTimeline& T, WfFrameStats* fs, const char** err);
 size_t wavefront_queue_entries(size_t paths, int max_extra);
 

@@ -103,33 +103,34 @@ __device__ __forceinline__ uint32_t block_alloc(bool pred, uint32_t* counter, Bl
     return r;
 }
 
-// Two block-aggregated allocations at once (wf_shade's shadow-ray and extend-ray appends): one
-// pass of barriers, and the two returning atomics issued by one instruction (one round trip).
-struct BlockAlloc2 {
-    uint32_t w[2][kBlock / 64];
+// Three block-aggregated allocations at once (wf_shade: shadow ray, front / back continuation ray).
+struct BlockAlloc3 {
+    uint32_t w[3][kBlock / 64];
 };
-__device__ __forceinline__ void block_alloc2(bool pa, uint32_t* ca, bool pb, uint32_t* cb, BlockAlloc2& sh,
-                                             uint32_t& ra, uint32_t& rb) {
+__device__ __forceinline__ void block_alloc3(const bool (&pr)[3], uint32_t* const (&ctr)[3], BlockAlloc3& sh,
+                                             uint32_t (&out)[3]) {
     const int wave = threadIdx.x >> 6;
-    const unsigned long long ma = __ballot(pa), mb = __ballot(pb);
+    unsigned long long m[3];
+    #pragma unroll
+    for (int i = 0; i < 3; ++i) m[i] = __ballot(pr[i]);
     if (lane_id() == 0) {
-        sh.w[0][wave] = (uint32_t)__popcll(ma);
-        sh.w[1][wave] = (uint32_t)__popcll(mb);
+        #pragma unroll
+        for (int i = 0; i < 3; ++i) sh.w[i][wave] = (uint32_t)__popcll(m[i]);
     }
     __syncthreads();
-    if (threadIdx.x < 2) {
+    if (threadIdx.x < 3) {
         uint32_t* w = sh.w[threadIdx.x];
         const uint32_t c0 = w[0], c1 = w[1], c2 = w[2], c3 = w[3];
         const uint32_t tot = c0 + c1 + c2 + c3;
-        const uint32_t b = tot ? atomicAdd(threadIdx.x == 0 ? ca : cb, tot) : 0u;
+        const uint32_t b = tot ? atomicAdd(ctr[threadIdx.x], tot) : 0u;
         w[0] = b;
         w[1] = b + c0;
         w[2] = b + c0 + c1;
         w[3] = b + c0 + c1 + c2;
     }
     __syncthreads();
-    ra = sh.w[0][wave] + mbcnt64(ma);
-    rb = sh.w[1][wave] + mbcnt64(mb);
+    #pragma unroll
+    for (int i = 0; i < 3; ++i) out[i] = sh.w[i][wave] + mbcnt64(m[i]);
     __syncthreads();
 }
 
@@ -301,16 +302,59 @@ __device__ __forceinline__ ShardPrefix load_prefix(const uint32_t* cnt, uint32_t
     }
     return p;
 }
-// dense consumer index g (< p.end[kShards - 1]) -> entry index of the sharded queue
-__device__ __forceinline__ uint32_t entry_of(const ShardPrefix& p, uint32_t g, uint32_t seg_cap) {
-    uint32_t k = 0, start = 0;
+// A ray queue's shard k holds L[k] entries at the front of its segment (ascending) and S[k] at the
+// back (descending from seg_cap - 1): wf_shade appends the continuation rays of paths that have
+// refracted (likely_long) at the front and the rest at the back, so the finish kernel, which
+// takes the queue front parts first, starts the long glass paths before the short ones (they
+// would otherwise set the end of its launch).  Primary rays (generate, extra samples) go to the
+// front.  Counters: L in [q * 8 + k], S in [kCntBack + q * 8 + k].
+constexpr int kCntBack = 50;
+struct QueueShards {
+    uint32_t L[kShards], S[kShards];
+};
+__device__ __forceinline__ QueueShards load_queue(const uint32_t* counts, int q, uint32_t seg_cap) {
+    QueueShards r;
+    #pragma unroll
+    for (int k = 0; k < kShards; ++k) {
+        const uint32_t l = min(__builtin_amdgcn_readfirstlane(counts[cslot(q * kShards + k)]), seg_cap);
+        r.L[k] = l;
+        r.S[k] = min(__builtin_amdgcn_readfirstlane(counts[cslot(kCntBack + q * kShards + k)]), seg_cap - l);
+    }
+    return r;
+}
+__device__ __forceinline__ uint32_t queue_len(const QueueShards& qs) {
+    uint32_t n = 0;
+    #pragma unroll
+    for (int k = 0; k < kShards; ++k) n += qs.L[k] + qs.S[k];
+    return n;
+}
+// shard-local index g (< L + S) -> position in the shard's segment
+__device__ __forceinline__ uint32_t seg_pos(uint32_t g, uint32_t l, uint32_t seg_cap) {
+    return g < l ? g : seg_cap - 1u - (g - l);
+}
+// dense consumer index g (< queue_len) -> entry index: the front parts of all shards first, then the back parts
+__device__ __forceinline__ uint32_t dense_entry(const QueueShards& qs, uint32_t g, uint32_t seg_cap) {
+    uint32_t ltot = 0;
+    #pragma unroll
+    for (int k = 0; k < kShards; ++k) ltot += qs.L[k];
+    const bool back = g >= ltot;
+    if (back) g -= ltot;
+    uint32_t k = 0, start = 0, acc = 0;
     #pragma unroll
     for (int j = 0; j < kShards - 1; ++j) {
-        const bool past = g >= p.end[j];
+        acc += back ? qs.S[j] : qs.L[j];
+        const bool past = g >= acc;
         k = past ? (uint32_t)(j + 1) : k;
-        start = past ? p.end[j] : start;
+        start = past ? acc : start;
     }
-    return k * seg_cap + (g - start);
+    const uint32_t i = g - start;
+    return k * seg_cap + (back ? seg_cap - 1u - i : i);
+}
+#ifndef RT_LONG_FIRST
+#define RT_LONG_FIRST 1   // 0: every continuation ray to the front (one-sided queues; A/B builds)
+#endif
+__device__ __forceinline__ bool likely_long(const PathRegs& p) {
+    return !RT_LONG_FIRST || p.tpass > 0 || p.bounce < p.step;
 }
 
 // A path's state between launches: its accumulator here (indexed by path id), its throughput
@@ -548,14 +592,13 @@ __global__ void __launch_bounds__(kBlock) wf_shade(DevScene S, const FrameParams
     const FrameParams& P = *Pp;   // per-frame parameters in device memory
     __shared__ HaltonDim lds_halton[kHaltonLds];
     __shared__ MatRec lds_mat[kMatLds];
-    __shared__ BlockAlloc2 ba2;
+    __shared__ BlockAlloc3 ba3;
     if (tail_mode(Q)) return;
     const ShadeTabs halton = load_tabs(S, lds_halton, lds_mat);
     const Uniforms& U = P.U;
     const int next = 1 - cur;
     const int shard = blockIdx.x & (kShards - 1);
-    const ShardPrefix cnt = load_prefix(Q.W.counts + cslot(cur * kShards));
-    uint32_t n = cnt.end[kShards - 1];
+    const QueueShards qs = load_queue(Q.W.counts, cur, Q.seg_cap);
     const float4* qin = Q.W.q[cur];
     float4* qout = Q.W.q[next] + 2 * (size_t)shard * Q.seg_cap;
     float4* qcout = Q.W.qc[next] + (size_t)shard * Q.seg_cap;
@@ -565,16 +608,19 @@ __global__ void __launch_bounds__(kBlock) wf_shade(DevScene S, const FrameParams
     zero2.y = 0.0f;
     // the blocks of XCD k (blockIdx % 8, the grid is a multiple of 8: grid_for) take queue shard k,
     // which XCD k's extend launch traced (unsorted), or the k-th eighth of the sorted array
-    uint32_t beg = (blockIdx.x >> 3) * kBlock, end = 0, ebase = 0;
+    uint32_t beg = (blockIdx.x >> 3) * kBlock, end = 0, ebase = 0, lk = 0;
     const uint32_t stride = (gridDim.x >> 3) * kBlock;
     if (SORTED) {
-        n = __builtin_amdgcn_readfirstlane(Q.W.counts[cslot(kCntSorted)]);
+        const uint32_t n = __builtin_amdgcn_readfirstlane(Q.W.counts[cslot(kCntSorted)]);
         beg += (uint32_t)(((uint64_t)n * (uint32_t)shard) / kShards);
         end = (uint32_t)(((uint64_t)n * (uint32_t)(shard + 1)) / kShards);
     } else {
         #pragma unroll
         for (int j = 0; j < kShards; ++j)
-            if (j == shard) end = cnt.end[j] - (j ? cnt.end[j - 1] : 0u);
+            if (j == shard) {
+                lk = qs.L[j];
+                end = qs.L[j] + qs.S[j];
+            }
         ebase = (uint32_t)shard * Q.seg_cap;
     }
     for (uint32_t base = beg; base < end; base += stride) {
@@ -583,6 +629,7 @@ __global__ void __launch_bounds__(kBlock) wf_shade(DevScene S, const FrameParams
         r.next = false;
         r.shadow = false;
         uint32_t pid = 0, nstate = 0;   // nstate, ncol: the continuation's state bits and colour
+        bool front = true;              // the continuation goes to the queue front (likely_long)
         f3 rayO = mk3(0, 0, 0), rayD = mk3(0, 0, 0);
         float4 ncol = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
         if (g < end) {
@@ -594,7 +641,7 @@ __global__ void __launch_bounds__(kBlock) wf_shade(DevScene S, const FrameParams
                 hv = Q.W.sorted[4 * (size_t)g + 2];
                 ce = 4 * (size_t)g + 3;
             } else {
-                const uint32_t e = ebase + g;
+                const uint32_t e = ebase + seg_pos(g, lk, Q.seg_cap);
                 o = qin[2 * (size_t)e];
                 d = qin[2 * (size_t)e + 1];
                 hv = Q.W.hits[e];
@@ -630,6 +677,7 @@ __global__ void __launch_bounds__(kBlock) wf_shade(DevScene S, const FrameParams
                                  zero2, false, zero2, r);
                 write_pixel_outputs(P, meta.x, r, h, FULL);
                 nstate = pack_state(p.bounce, p.tpass, p.step);
+                front = likely_long(p);
                 ncol = make_float4(p.color.x, p.color.y, p.color.z, 0.0f);
                 // radiance only changes on emissive hits (:585-586): skip the store otherwise
                 if (__float_as_uint(p.accum.x) != __float_as_uint(a.x) || __float_as_uint(p.accum.y) != __float_as_uint(a.y) ||
@@ -642,9 +690,12 @@ __global__ void __launch_bounds__(kBlock) wf_shade(DevScene S, const FrameParams
                 }
             }
         }
-        uint32_t ns, nr;
-        block_alloc2(r.shadow, &Q.W.counts[cslot(kCntShadowQ + shard)], r.next,
-                     &Q.W.counts[cslot(next * kShards + shard)], ba2, ns, nr);
+        const bool pr[3] = {r.shadow, r.next && front, r.next && !front};
+        uint32_t* const ctr[3] = {&Q.W.counts[cslot(kCntShadowQ + shard)], &Q.W.counts[cslot(next * kShards + shard)],
+                                  &Q.W.counts[cslot(kCntBack + next * kShards + shard)]};
+        uint32_t slots[3];
+        block_alloc3(pr, ctr, ba3, slots);
+        const uint32_t ns = slots[0], nr = front ? slots[1] : Q.seg_cap - 1u - slots[2];
         if (r.shadow) {
             sqout[3 * (size_t)ns] = make_float4(r.so.x, r.so.y, r.so.z, __uint_as_float(pid));
             sqout[3 * (size_t)ns + 1] = make_float4(r.sd.x, r.sd.y, r.sd.z, r.stmax);
@@ -681,13 +732,13 @@ __global__ void __launch_bounds__(kSortThreads) wf_sort_hist(DevScene S, WfParam
     if (tail_mode(Q)) return;
     const uint32_t shift = __builtin_ctz(kSortMaxBins) - __builtin_ctz(Q.sort_bins);
     const uint32_t K = Q.sort_bins;
-    const ShardPrefix cnt = load_prefix(Q.W.counts + cslot(cur * kShards));
+    const QueueShards qs = load_queue(Q.W.counts, cur, Q.seg_cap);
     for (uint32_t k = threadIdx.x; k < K; k += kSortThreads) h[k] = 0;
     __syncthreads();
     uint32_t beg, end;
-    sort_range(cnt.end[kShards - 1], beg, end);
+    sort_range(queue_len(qs), beg, end);
     for (uint32_t g = beg + threadIdx.x; g < end; g += kSortThreads) {
-        const uint32_t k = sort_key(S, Q, entry_of(cnt, g, Q.seg_cap), shift);
+        const uint32_t k = sort_key(S, Q, dense_entry(qs, g, Q.seg_cap), shift);
         if (k != kNoKey) atomicAdd(&h[k], 1u);
     }
     __syncthreads();
@@ -716,7 +767,7 @@ __global__ void __launch_bounds__(kSortThreads) wf_sort_scatter(DevScene S, WfPa
     const uint32_t shift = __builtin_ctz(kSortMaxBins) - __builtin_ctz(Q.sort_bins);
     __shared__ uint32_t w[kSortThreads / 64];
     const uint32_t K = Q.sort_bins, per = K / kSortThreads;   // 1, 2 or 4 bins per thread
-    const ShardPrefix cnt = load_prefix(Q.W.counts + cslot(cur * kShards));
+    const QueueShards qs = load_queue(Q.W.counts, cur, Q.seg_cap);
     // bin starts: exclusive scan of the bin totals, plus this block's offset inside each bin
     uint32_t loc[kSortMaxBins / kSortThreads];
     uint32_t s = 0;
@@ -739,9 +790,9 @@ __global__ void __launch_bounds__(kSortThreads) wf_sort_scatter(DevScene S, WfPa
     __syncthreads();
     const float4* qin = Q.W.q[cur];
     uint32_t beg, end;
-    sort_range(cnt.end[kShards - 1], beg, end);
+    sort_range(queue_len(qs), beg, end);
     for (uint32_t g = beg + threadIdx.x; g < end; g += kSortThreads) {
-        const uint32_t e = entry_of(cnt, g, Q.seg_cap);
+        const uint32_t e = dense_entry(qs, g, Q.seg_cap);
         const float4 hv = Q.W.hits[e];
         const uint32_t id = __float_as_uint(hv.y);
         if (id == 0xffffffffu) continue;
@@ -776,8 +827,7 @@ wf_trace(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int cur, in
         if (ANY) {
             if (tm) return;
         } else {
-            const ShardPrefix c0 = load_prefix(Q.W.counts + cslot(cur * kShards));
-            if (tm || c0.end[kShards - 1] < Q.tail) {
+            if (tm || queue_len(load_queue(Q.W.counts, cur, Q.seg_cap)) < Q.tail) {
                 if (!tm && blockIdx.x == 0 && threadIdx.x == 0) {
                     Q.W.counts[cslot(kCntTailMode)] = 1u;
                     Q.W.counts[cslot(kCntFinishQ)] = (uint32_t)cur;
@@ -790,8 +840,9 @@ wf_trace(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int cur, in
     if (threadIdx.x == 0) ts_done = 0u;
     ts_start(Q, ts);
     __syncthreads();
-    const ShardPrefix cnt = load_prefix(ANY ? Q.W.counts + cslot(kCntShadowQ) : Q.W.counts + cslot(cur * kShards));
-    const uint32_t n = cnt.end[kShards - 1];
+    // the shadow queue is one-sided, a ray queue two-sided (front / back parts)
+    const uint32_t n = ANY ? load_prefix(Q.W.counts + cslot(kCntShadowQ)).end[kShards - 1]
+                           : queue_len(load_queue(Q.W.counts, cur, Q.seg_cap));
     if (Q.dev_ctl) {
         stat_add(Q, kStatTraceRays, n);
         stat_add(Q, kStatTraceLaunches, 1u);
@@ -800,10 +851,10 @@ wf_trace(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int cur, in
             stat_add(Q, kStatExtendRays, n);
         }
     }
-    if (!ANY && blockIdx.x == 0 && threadIdx.x < 2 * kShards) {  // reset the queues shade / connect fill
+    if (!ANY && blockIdx.x == 0 && threadIdx.x < 3 * kShards) {  // reset the queues shade / connect fill
         const int next = 1 - cur;
-        uint32_t k = threadIdx.x & (kShards - 1);
-        Q.W.counts[cslot(threadIdx.x < kShards ? next * kShards + k : kCntShadowQ + k)] = 0;
+        const uint32_t k = threadIdx.x & (kShards - 1), part = threadIdx.x / kShards;
+        Q.W.counts[cslot(part == 0 ? next * kShards + k : part == 1 ? kCntShadowQ + k : kCntBack + next * kShards + k)] = 0;
     }
     // chunk counters of the OTHER traversal kind are reset here for its next launch (extend and
     // connect alternate; the frame start zeroes both)
@@ -816,10 +867,15 @@ wf_trace(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int cur, in
     uint32_t* const chunk_ctr = Q.W.counts + cslot((ANY ? kCntChunkConnect : kCntChunkExtend) + (int)xcd);
     // XCD k traverses queue shard k, the segment its own shade blocks (blockIdx % 8 == k) appended:
     // entry = k * seg_cap + g, no per-lane search of the shard prefix
-    uint32_t xend = 0;
-    #pragma unroll
-    for (int j = 0; j < kShards; ++j)
-        if ((uint32_t)j == xcd) xend = cnt.end[j] - (j ? cnt.end[j - 1] : 0u);
+    // shard xcd's entries and its front part (two scalar loads)
+    uint32_t xl, xend;
+    if (ANY) {
+        xl = xend = min(__builtin_amdgcn_readfirstlane(Q.W.counts[cslot(kCntShadowQ + (int)xcd)]), Q.seg_cap);
+    } else {
+        xl = min(__builtin_amdgcn_readfirstlane(Q.W.counts[cslot(cur * kShards + (int)xcd)]), Q.seg_cap);
+        xend = xl + min(__builtin_amdgcn_readfirstlane(Q.W.counts[cslot(kCntBack + cur * kShards + (int)xcd)]),
+                        Q.seg_cap - xl);
+    }
     // (round 3; before, XCD k took the k-th eighth of the dense queue and every refilling lane
     // searched the prefix for its entry: 7.49 -> 7.56 Grays/s)
     const uint32_t xbeg = 0, ebase = xcd * Q.seg_cap;
@@ -854,7 +910,7 @@ wf_trace(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int cur, in
             if (!active) {
                 uint32_t g = wnext + mbcnt64(idle);
                 if (g < wend) {
-                    e = ebase + g;
+                    e = ebase + (ANY ? g : seg_pos(g, xl, Q.seg_cap));
                     float4 o4 = qin[(size_t)qstride * e], d4 = qin[(size_t)qstride * e + 1];
                     trav_start(T, ld3(o4), ld3(d4), ANY ? d4.w : INFINITY);
                     active = true;
@@ -915,8 +971,8 @@ wf_finish_step(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int c
     ts_start(Q, ts);
     const ShadeTabs halton = load_tabs(S, lds_halton, lds_mat);   // ends with a block barrier
     const Uniforms& U = P.U;
-    const ShardPrefix cnt = load_prefix(Q.W.counts + cslot(cur * kShards));
-    const uint32_t n = cnt.end[kShards - 1];
+    const QueueShards qs = load_queue(Q.W.counts, cur, Q.seg_cap);   // front parts first: the likely-long paths
+    const uint32_t n = queue_len(qs);
     if (Q.dev_ctl) stat_add(Q, kStatFinish, 1u);
     if (Q.dev_ctl && n > 0) stat_add(Q, kStatRounds, 1u);
     const float4* qin = Q.W.q[cur];
@@ -978,7 +1034,7 @@ wf_finish_step(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int c
             if (mode == kIdle) {
                 const uint32_t g = wnext + mbcnt64(idle);
                 if (g < wend) {
-                    const uint32_t e = entry_of(cnt, g, Q.seg_cap);
+                    const uint32_t e = dense_entry(qs, g, Q.seg_cap);
                     const float4* src = qin + 2 * (size_t)e;
                     const float4 o = src[0], d = src[1];
                     pid = __float_as_uint(o.w);
@@ -1269,9 +1325,9 @@ static void launch_finish_any(const DevScene& S, const WfParams& Q, bool count, 
     else full ? launch_finish<false, true>(S, Q, cur, n, stream, ts) : launch_finish<false, false>(S, Q, cur, n, stream, ts);
 }
 
-static uint32_t queue_total(const uint32_t* h, int q) {
+static uint32_t queue_total(const uint32_t* h, int q) {   // q = 0, 1: a ray queue (both ends); 2: the shadow queue
     uint32_t s = 0;
-    for (int k = 0; k < kShards; ++k) s += h[cslot(q * kShards + k)];
+    for (int k = 0; k < kShards; ++k) s += h[cslot(q * kShards + k)] + (q < 2 ? h[cslot(kCntBack + q * kShards + k)] : 0u);
     return s;
 }
 
@@ -1398,18 +1454,29 @@ static bool iterate(const DevScene& S, const FrameParams& P, WfParams& Q, int& c
 // Per-stage times come from events between the launches, ray counts and rounds from device
 // counters; both are collected by wavefront_collect once the frame has finished.
 namespace {
+// Whether the HIP runtime takes timeline events inside a captured frame (external event-record
+// nodes).  The system ROCm 7.2 runtime the C host links does; the HIP runtime PyTorch bundles
+// refuses them (hipEventRecordWithFlags(..., hipEventRecordExternal) during capture: invalid
+// argument), so after the first refusal frames are captured without them: the graphs then hold
+// the frame's launches, memsets and copies only, and the per-stage times of replayed frames are
+// not recorded (rt_stats kernel_ms; the frame's own time, taken outside the graphs, is).
+static bool g_graph_events = true;
+static bool g_ext_refused = false;   // set when a capture's external event record was refused
+
 struct Enqueue {
     WfTimeline& T;
     hipStream_t stream;
     bool capture;   // recording into a HIP graph: events and cross-stream waits are external nodes
     int last = -1;
     bool mark(const char** err) {
+        if (capture && !g_graph_events) return true;   // untimed capture
         if (T.n_ev >= WfTimeline::kMaxEv) {
             *err = "wavefront timeline: too many events";
             return false;
         }
         const hipError_t e = hipEventRecordWithFlags(T.ev[T.n_ev], stream, capture ? hipEventRecordExternal : 0u);
         if (e != hipSuccess) {
+            if (capture) g_ext_refused = true;
             static thread_local char msg[160];
             snprintf(msg, sizeof msg, "hipEventRecordWithFlags(%s): %s", capture ? "external" : "0", hipGetErrorString(e));
             *err = msg;
@@ -1420,6 +1487,7 @@ struct Enqueue {
     }
     // closes the span [previous mark, now) as `stage`
     bool span(int stage, const char** err) {
+        if (capture && !g_graph_events) return true;
         const int a = last;
         if (!mark(err)) return false;
         T.spans[T.n_spans++] = WfTimeline::Span{stage, a, last};
@@ -1503,6 +1571,7 @@ static bool record_rest(const DevScene& S, const FrameParams& P, WfParams& Q, bo
         // second pass over the motion-adaptive extra samples (:779-789), appended to queue 0
         const int rounds2 = rounds_for((uint64_t)Q.own_pixels * (uint64_t)maxExtra, Q.tail);
         WF_CHECK(hipMemsetAsync(W.counts, 0, cslot(kShards) * sizeof(uint32_t), stream));
+        WF_CHECK(hipMemsetAsync(W.counts + cslot(kCntBack), 0, cslot(kShards) * sizeof(uint32_t), stream));
         WF_CHECK(hipMemsetAsync(W.counts + cslot(kCntChunkExtend), 0, cslot(2 * kShards) * sizeof(uint32_t), stream));
         WF_CHECK(hipMemsetD32Async(W.counts + cslot(kCntTailMode), 0u, 1, stream));
         WF_CHECK(hipMemsetD32Async(W.counts + cslot(kCntFinishQ), (uint32_t)(rounds2 & 1), 1, stream));
@@ -1539,13 +1608,27 @@ static bool capture_part(const DevScene& S, const FrameParams& P, WfParams& Q, b
         const char* rerr = nullptr;
         hipGraph_t g = nullptr;
         const int n_ev = T.n_ev, n_spans = T.n_spans;
-        const hipError_t be = hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal);
-        const bool ok = be == hipSuccess &&
-                        record_part(S, P, Q, count, full, maxExtra, with_extra, part, stream, T, true, &rerr);
-        const hipError_t ce = be == hipSuccess ? hipStreamEndCapture(stream, &g) : be;
-        hipError_t ie = hipErrorUnknown;
-        if (ok && ce == hipSuccess && g) ie = hipGraphInstantiateWithFlags(&T.exec[part], g, 0);
-        if (g) (void)hipGraphDestroy(g);
+        hipError_t be, ce, ie;
+        bool ok;
+        for (int attempt = 0;; ++attempt) {
+            g_ext_refused = false;
+            be = hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal);
+            ok = be == hipSuccess && record_part(S, P, Q, count, full, maxExtra, with_extra, part, stream, T, true, &rerr);
+            ce = be == hipSuccess ? hipStreamEndCapture(stream, &g) : be;
+            ie = hipErrorUnknown;
+            if (ok && ce == hipSuccess && g) ie = hipGraphInstantiateWithFlags(&T.exec[part], g, 0);
+            if (g) (void)hipGraphDestroy(g);
+            g = nullptr;
+            if (!ok && g_ext_refused && g_graph_events && attempt == 0) {
+                // this runtime takes no timeline events in a graph: capture untimed from now on
+                (void)hipGetLastError();
+                g_graph_events = false;
+                T.n_ev = n_ev;
+                T.n_spans = n_spans;
+                continue;
+            }
+            break;
+        }
         if (!ok || ce != hipSuccess || ie != hipSuccess) {
             // capture refused (an API the runtime cannot capture): this slot renders eagerly from now on
             // (rt_stats total_graph_fallbacks counts its frames; the first refusal is reported here)
@@ -1570,12 +1653,13 @@ static bool capture_part(const DevScene& S, const FrameParams& P, WfParams& Q, b
 
 static bool enqueue_wavefront(const DevScene& S, const FrameParams& P, WfParams& Q, bool count, bool full,
                               int maxExtra, bool extra_pass, hipStream_t stream, hipEvent_t prev_done, WfTimeline& T,
-                              const char** err) {
+                              const char** err, bool graphs) {
     Q.dev_ctl = 1;
     Q.finish_q = 0;   // set by record_base from the round count
     const bool with_extra = maxExtra > 0 && extra_pass;
-    if (!graphs_on() || T.graph_failed) {
-        T.graph_mode = graphs_on() ? kGraphFallback : kGraphEager;
+    graphs = graphs && graphs_on();
+    if (!graphs || T.graph_failed) {
+        T.graph_mode = graphs ? kGraphFallback : kGraphEager;
         if (!record_base(S, P, Q, count, full, stream, T, false, err)) return false;
         if (prev_done) WF_CHECK(hipStreamWaitEvent(stream, prev_done, 0));
         if (!record_rest(S, P, Q, count, full, maxExtra, with_extra, stream, T, false, err)) return false;
@@ -1656,7 +1740,7 @@ bool wavefront_collect(const WavefrontBuffers& W, WfTimeline& T, WfFrameStats* f
 
 bool run_wavefront(const DevScene& S, const FrameParams& P, WavefrontBuffers& W, int own_tiles, bool count, bool spans,
                    int tail_paths, int sort_bins, bool extra_pass, int in_flight, hipStream_t stream,
-                   hipEvent_t prev_done, WfTimeline* tl, WfFrameStats* fs, const char** err) {
+                   hipEvent_t prev_done, WfTimeline* tl, WfFrameStats* fs, const char** err, bool graphs) {
     const Tuning& tu = tuning();
     WfParams Q;
     std::memset(&Q, 0, sizeof Q);   // no stray padding bytes (frame-graph key)
@@ -1719,7 +1803,7 @@ bool run_wavefront(const DevScene& S, const FrameParams& P, WavefrontBuffers& W,
         (void)finish_full_cap<false, true>();
         (void)finish_full_cap<true, false>();
         (void)finish_full_cap<true, true>();
-        return enqueue_wavefront(S, P, Q, count, full, maxExtra, extra_pass, stream, prev_done, *tl, err);
+        return enqueue_wavefront(S, P, Q, count, full, maxExtra, extra_pass, stream, prev_done, *tl, err, graphs);
     }
     Q.dev_ctl = 0;
     Q.finish_q = 0;
@@ -1744,6 +1828,7 @@ bool run_wavefront(const DevScene& S, const FrameParams& P, WavefrontBuffers& W,
     if (maxExtra > 0) {
         // the extra-sample pass appends primary rays to queue `cur` (reset here)
         WF_CHECK(hipMemsetAsync(W.counts + cslot(cur * kShards), 0, cslot(kShards) * sizeof(uint32_t), stream));
+        WF_CHECK(hipMemsetAsync(W.counts + cslot(kCntBack + cur * kShards), 0, cslot(kShards) * sizeof(uint32_t), stream));
         hipLaunchKernelGGL(wf_extra, dim3(grid_for(Q.own_pixels, 1u << 30)), dim3(kBlock), 0, stream, S, Q.Pd, Q, cur);
         WF_CHECK(hipGetLastError());
         WF_CHECK(hipMemcpyAsync(W.h_counts, W.counts, kWfCountWords * sizeof(uint32_t), hipMemcpyDeviceToHost, stream));

@@ -58,7 +58,8 @@ def _roofline_consistent(d):
     assert abs(frac - r["frac"]) <= 1e-3 + 0.01 * frac
     assert r["l2_hit"] and all(0 < v < 1 for v in r["l2_hit"].values())
     assert r["shade_l2_hit"] is not None and 0 < r["shade_l2_hit"] < 1
-    assert "in_flight" in r and r["in_flight"]["kernels"]
+    # the timed frames are graph replays, which carry no per-stage events under torch's HIP runtime
+    assert "in_flight" in r and r["in_flight"]["ms_per_step"] > 0
 
 
 def test_bench_emulated_rank_and_animation():
