@@ -57,7 +57,8 @@ def _roofline_consistent(d):
     frac = r["traffic"] / (r["launch_ms"] * 1e-3) / 1e9 / r["peak"]
     assert abs(frac - r["frac"]) <= 1e-3 + 0.01 * frac
     assert r["l2_hit"] and all(0 < v < 1 for v in r["l2_hit"].values())
-    assert r["shade_l2_hit"] is not None and 0 < r["shade_l2_hit"] < 1
+    if any(k["kernel"].startswith("rt::wf_shade") for k in ks):   # a small frame may run entirely in the finish
+        assert r["shade_l2_hit"] is not None and 0 < r["shade_l2_hit"] < 1
     # the timed frames are graph replays, which carry no per-stage events under torch's HIP runtime
     assert "in_flight" in r and r["in_flight"]["ms_per_step"] > 0
 
