@@ -21,12 +21,13 @@ def _run(*args):
 
 
 def test_bench_line_contract():
-    d = _run("--scene", "c1", "--width", "128", "--height", "96", "--spp", "2", "--bounces", "3", "--steps", "3",
+    # 8 steps over four frame slots: each slot's first timed frame may capture, the later ones replay
+    d = _run("--scene", "c1", "--width", "128", "--height", "96", "--spp", "2", "--bounces", "3", "--steps", "8",
              "--warmup", "1", "--cpu-seconds", "0.5")
     for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
               "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"):
         assert k in d, k
-    assert d["n_gpus"] == 1 and d["steps"] == 3 and d["value"] > 0 and d["unit"] == "Grays/s"
+    assert d["n_gpus"] == 1 and d["steps"] == 8 and d["value"] > 0 and d["unit"] == "Grays/s"
     r = d["roofline"]
     for k in ("bound", "achieved", "peak", "unit", "frac", "traffic"):
         assert k in r, k
@@ -39,7 +40,7 @@ def test_bench_line_contract():
     _roofline_consistent(d)
     # the timed frames replay captured HIP graphs
     g = d["config"]["graphs"]
-    assert g["fallbacks"] == 0 and g["eager"] == 0 and g["replays"] >= 1
+    assert g["fallbacks"] == 0 and g["eager"] == 0 and g["replays"] >= 4 and g["replays"] + g["captures"] == 8
 
 
 def _roofline_consistent(d):
