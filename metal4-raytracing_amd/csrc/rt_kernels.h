@@ -85,7 +85,7 @@ constexpr int kShards = 8;        // queue segments (one allocation counter each
 // [32..39] / [40..47] per-XCD chunk counters of the extend / connect launches; each slot on a
 // 128-B line of its own (cslot), so the per-XCD shards never contend for one line's atomics.
 constexpr int kCntStride = 32;
-constexpr int kCntSlotsWf = 66;                       // counter slots (cslot) before the diagnostics words
+constexpr int kCntSlotsWf = 74;                       // counter slots (cslot) before the diagnostics words
 constexpr int kWfDiagHist = kCntSlotsWf * kCntStride; // 64 words: wf_finish wave end-time histogram (50 us bins)
 constexpr int kWfDiagSteps = kWfDiagHist + 64;        // 66 words: wf_trace steps-per-ray histograms + max
 constexpr int kWfStat = kWfDiagSteps + 66;              // 3 words: rounds, wf_trace launches, their rays
@@ -93,10 +93,16 @@ constexpr int kStatRounds = 0, kStatTraceLaunches = 1, kStatTraceRays = 2, kStat
 // wf_finish_step diagnostics (RT_WF_LOG): summed over waves, s_memrealtime ticks (10 ns) spent in
 // shading passes and in total, shading passes and lanes shaded
 constexpr int kStatDiagShadeT = 5, kStatDiagTotalT = 6, kStatDiagPasses = 7, kStatDiagShaded = 8;
+// ... and split at the wave's queue exhaustion: iterations and ticks before / after it, and the
+// wave's active lanes summed over its iterations after it
+constexpr int kStatDiagItPre = 9, kStatDiagItPost = 10, kStatDiagTPre = 11, kStatDiagTPost = 12, kStatDiagLanesPost = 13;
+constexpr int kWfStatWords = 14;
 // wf_finish_step diagnostics (RT_WF_LOG): paths by segments run in the finish (32 bins) per entry
-// class (18: bounce 0..8 at entry, x refracting or not)
-constexpr int kWfDiagLen = kWfStat + 9;
-constexpr int kWfCountWords = kCntSlotsWf * kCntStride + 64 + 66 + 9 + 18 * 32;
+// class (18: bounce 0..8 at entry, x refracting or not), then the waves' queue-exhaustion times
+// (64 bins of 50 us)
+constexpr int kWfDiagLen = kWfStat + kWfStatWords;
+constexpr int kWfDiagExh = kWfDiagLen + 18 * 32;
+constexpr int kWfCountWords = kCntSlotsWf * kCntStride + 64 + 66 + kWfStatWords + 18 * 32 + 64;
 __host__ __device__ constexpr uint32_t cslot(int c) { return (uint32_t)c * kCntStride; }
 struct WavefrontBuffers {
     size_t queue_entries = 0;     // kShards segments of queue_entries / kShards

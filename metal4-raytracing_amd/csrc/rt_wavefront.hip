@@ -45,7 +45,7 @@ struct Tuning {
     int chunk;         // RT_CHUNK: rays per chunk grab of the traversal kernel
     int fchunk;        // RT_FCHUNK: paths per chunk grab of the finish kernel
     int shade_min;     // RT_SHADE_MIN: the finish kernel shades once this many lanes wait
-    int shade_min_x;   // RT_SHADE_MIN_X: the same once the finish queue is exhausted
+    int shade_min_x;   // RT_SHADE_MIN_X: the same once the finish queue is exhausted (< 0: that percentage of the wave's busy lanes)
     int finish_frac;   // RT_FINISH_FRAC: percent of the resident grid the finish launch takes (0 = by frames in flight)
     int trace_frac;    // RT_TRACE_FRAC: percent of the resident grid the persistent wf_trace launches take (0 = by frames in flight)
     int log;           // RT_WF_LOG=1: per-round queue sizes, stage times and finish diagnostics on stderr
@@ -59,9 +59,9 @@ static const Tuning& tuning() {
         v.tail = (uint32_t)env_int("RT_TAIL_RAYS", 4194304);
         v.refill_min = env_int("RT_REFILL_MIN", 8);
         v.chunk = std::max(1, env_int("RT_CHUNK", 64));
-        v.fchunk = std::max(1, env_int("RT_FCHUNK", 32));
+        v.fchunk = std::max(1, env_int("RT_FCHUNK", 64));
         v.shade_min = env_int("RT_SHADE_MIN", 24);
-        v.shade_min_x = env_int("RT_SHADE_MIN_X", 24);
+        v.shade_min_x = env_int("RT_SHADE_MIN_X", -50);
         v.finish_frac = std::min(env_int("RT_FINISH_FRAC", 0), 100);
         v.trace_frac = std::min(env_int("RT_TRACE_FRAC", 0), 100);
         v.log = env_int("RT_WF_LOG", 0);
@@ -218,7 +218,7 @@ struct WfParams {
     uint32_t sort_bins;    // hit-sort bins (0 = shade reads the extend queue unsorted)
     int diag;              // wf_finish_step: record the diagnostics slots (RT_WF_LOG)
     int shade_min;         // wf_finish_step: shade once this many lanes wait (or none traverses)
-    int shade_min_x;       // wf_finish_step: the same once the launch's queue is exhausted
+    int shade_min_x;       // wf_finish_step: the same once the launch's queue is exhausted (< 0: percent of busy lanes)
     int fchunk;            // wf_finish_step: paths per chunk grab
     int finish_frac;       // percent of the resident grid the finish launch takes
     int trace_frac;        // percent of the resident grid the bulk wf_trace launches take
@@ -253,7 +253,10 @@ __device__ __forceinline__ void own_pixel(const WfParams& Q, uint32_t i, int& px
 // counter slots (cslot): [q*8 + shard] ray queues q = 0, 1; [16 + shard] shadow queue; [24] extra allocator
 constexpr int kCntShadowQ = 16;
 constexpr int kCntExtra = 24;
-constexpr int kCntChunkFinish = 25;
+// [66..73] per-XCD chunk counters of the finish launch: XCD k takes chunks k, k + 8, k + 16, ...
+// of the finish queue (its long-first order kept chip-wide).  One counter for the whole chip
+// serialised the grabs: 3.4M paths in chunks of 32 were ~105K returning atomics on one line.
+constexpr int kCntChunkFinish = 66;
 constexpr int kCntSorted = 26;                 // hits the sort kept (misses dropped) = shade's input size
 constexpr uint32_t kNoKey = 0xffffffffu;       // sort key of a miss (dropped by the sort)
 constexpr int kCntDiagSegs = 27, kCntDiagIters = 28, kCntDiagTime = 29;   // wf_finish diagnostics
@@ -976,7 +979,6 @@ wf_finish_step(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int c
     if (Q.dev_ctl) stat_add(Q, kStatFinish, 1u);
     if (Q.dev_ctl && n > 0) stat_add(Q, kStatRounds, 1u);
     const float4* qin = Q.W.q[cur];
-    uint32_t* chunk_ctr = Q.W.counts + cslot(kCntChunkFinish);
     const uint32_t kChunk = (uint32_t)Q.fchunk;   // paths per grab
     constexpr int kIdle = 0, kClosest = 1, kShadow = 2, kReady = 3;
     TraceCounters tc{0, 0, 0};
@@ -1002,6 +1004,11 @@ wf_finish_step(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int c
     // time (s_memrealtime, 100 MHz) of the slowest wave, time in shading passes
     uint32_t segs = 0, max_segs = 0, iters = 0;
     const uint64_t t_start = Q.diag ? __builtin_amdgcn_s_memrealtime() : 0;
+    // per wave, in LDS (no registers outside RT_WF_LOG runs): iterations and ticks at its queue's
+    // exhaustion, active lanes summed over the iterations after it
+    __shared__ uint32_t diag_x[kBlock / 64][3];
+#define RT_DX diag_x[__builtin_amdgcn_readfirstlane(threadIdx.x) / 64u]
+    if (Q.diag && lane_id() == 0) RT_DX[0] = RT_DX[1] = RT_DX[2] = 0xffffffffu;
     uint64_t t_shade = 0;
     uint32_t n_pass = 0, n_shaded = 0;
     auto end_path = [&]() {
@@ -1016,15 +1023,21 @@ wf_finish_step(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int c
     };
 
     while (true) {
-        // ---- refill idle lanes with the next remaining paths (chunks of Q.fchunk from one counter)
+        // ---- refill idle lanes with the next remaining paths (chunks of Q.fchunk from the XCD's counter)
         const unsigned long long idle = __ballot(mode == kIdle);
         const bool refill = __popcll(idle) >= Q.refill_min || idle == ~0ull;
         if (wnext >= wend && !exhausted && refill) {
             uint32_t base = 0;
-            if (lane_id() == 0) base = atomicAdd(chunk_ctr, kChunk);
-            base = __builtin_amdgcn_readfirstlane(base);
+            // this XCD's next chunk (the grid has >= 8 blocks: launch_finish)
+            if (lane_id() == 0) base = atomicAdd(Q.W.counts + cslot(kCntChunkFinish + (int)(blockIdx.x & 7u)), 1u);
+            base = ((__builtin_amdgcn_readfirstlane(base) << 3) | (blockIdx.x & 7u)) * kChunk;
             if (base >= n) {
                 exhausted = true;
+                if (Q.diag && lane_id() == 0) {
+                    RT_DX[0] = iters;
+                    RT_DX[1] = (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_start);
+                    RT_DX[2] = 0;
+                }
             } else {
                 wnext = base;
                 wend = min(base + kChunk, n);
@@ -1058,8 +1071,10 @@ wf_finish_step(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int c
             }
             wnext += (uint32_t)__popcll(idle);
         }
-        if (__ballot(mode != kIdle) == 0ull) break;   // idle everywhere => refill found nothing
+        const unsigned long long active = __ballot(mode != kIdle);
+        if (active == 0ull) break;   // idle everywhere => refill found nothing
         ++iters;
+        if (Q.diag && exhausted && lane_id() == 0) RT_DX[2] += (uint32_t)__popcll(active);
 
         // ---- one traversal step (closest hit or shadow any-hit)
         if (mode == kClosest || mode == kShadow) {
@@ -1085,8 +1100,9 @@ wf_finish_step(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int c
 
         // ---- shade the waiting lanes together (:324-774)
         const unsigned long long ready = __ballot(mode == kReady);
-        if (ready != 0ull &&
-            (__popcll(ready) >= (exhausted ? Q.shade_min_x : Q.shade_min) || __ballot(mode == kClosest || mode == kShadow) == 0ull)) {
+        int shade_thr = exhausted ? Q.shade_min_x : Q.shade_min;
+        if (shade_thr < 0) shade_thr = max(1, -shade_thr * __popcll(__ballot(mode != kIdle)) / 100);   // % of the busy lanes
+        if (ready != 0ull && (__popcll(ready) >= shade_thr || __ballot(mode == kClosest || mode == kShadow) == 0ull)) {
             const uint64_t ts0 = Q.diag ? __builtin_amdgcn_s_memrealtime() : 0;
             if (Q.diag) {
                 ++n_pass;
@@ -1139,6 +1155,15 @@ wf_finish_step(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int c
     if (Q.diag) {
         const uint32_t dt = (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_start);
         if (lane_id() == 0) {
+            const uint32_t* dx = RT_DX;
+            const bool x = dx[0] != 0xffffffffu;   // else its last grab was in range: it never saw the end
+            const uint32_t it_x = x ? dx[0] : iters, t_x = x ? dx[1] : dt;
+            atomicAdd(&Q.W.counts[kWfStat + kStatDiagItPre], it_x);
+            atomicAdd(&Q.W.counts[kWfStat + kStatDiagItPost], iters - it_x);
+            atomicAdd(&Q.W.counts[kWfStat + kStatDiagTPre], t_x);
+            atomicAdd(&Q.W.counts[kWfStat + kStatDiagTPost], dt - t_x);
+            atomicAdd(&Q.W.counts[kWfStat + kStatDiagLanesPost], x ? dx[2] : 0u);
+            atomicAdd(&Q.W.counts[kWfDiagExh + min(t_x / 5000u, 63u)], 1u);
             atomicAdd(&Q.W.counts[kWfStat + kStatDiagShadeT], (uint32_t)t_shade);
             atomicAdd(&Q.W.counts[kWfStat + kStatDiagTotalT], dt);
             atomicAdd(&Q.W.counts[kWfStat + kStatDiagPasses], n_pass);
@@ -1152,6 +1177,7 @@ wf_finish_step(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int c
             atomicAdd(&Q.W.counts[kWfDiagHist + min(dt / 5000u, 63u)], 1u);
         }
     }
+#undef RT_DX
     ts_end(Q, ts, &ts_done);
     flush_counters(P, n_closest, n_shadow, 0, tc, COUNT, overflow);
 }
@@ -1314,9 +1340,10 @@ static unsigned finish_full_cap() {   // resident blocks of the finish kernel, q
 }
 template <bool COUNT, bool FULL>
 static void launch_finish(const DevScene& S, const WfParams& Q, int cur, uint32_t n, hipStream_t stream, int ts) {
-    const unsigned cap = std::max(1u, finish_full_cap<COUNT, FULL>() * (unsigned)Q.finish_frac / 100u);
-    hipLaunchKernelGGL((wf_finish_step<COUNT, FULL>), dim3(grid_for(n, cap)), dim3(kBlock), 0, stream, S, Q.Pd, Q, cur,
-                       ts);
+    // at least one block per XCD: each takes the chunks of its XCD's counter (wf_finish_step)
+    const unsigned cap = std::max(8u, finish_full_cap<COUNT, FULL>() * (unsigned)Q.finish_frac / 100u);
+    hipLaunchKernelGGL((wf_finish_step<COUNT, FULL>), dim3(std::max(8u, grid_for(n, cap))), dim3(kBlock), 0, stream, S,
+                       Q.Pd, Q, cur, ts);
 }
 
 static void launch_finish_any(const DevScene& S, const WfParams& Q, bool count, bool full, int cur, uint32_t n,
@@ -1341,8 +1368,13 @@ static bool iterate(const DevScene& S, const FrameParams& P, WfParams& Q, int& c
     for (int it = 0; it < max_it && n > 0; ++it) {
         if (n < Q.tail) {   // the rest of the pass in one persistent finish launch
             WF_CHECK(hipEventRecord(W.ev[0], stream));
-            WF_CHECK(hipMemsetAsync(W.counts + cslot(kCntChunkFinish), 0, sizeof(uint32_t), stream));
-            if (Q.diag) WF_CHECK(hipMemsetAsync(W.counts + kWfDiagHist, 0, 64 * sizeof(uint32_t), stream));
+            WF_CHECK(hipMemsetAsync(W.counts + cslot(kCntChunkFinish), 0, cslot(kShards) * sizeof(uint32_t), stream));
+            if (Q.diag) {
+                WF_CHECK(hipMemsetAsync(W.counts + kWfDiagHist, 0, 64 * sizeof(uint32_t), stream));
+                WF_CHECK(hipMemsetAsync(W.counts + kWfDiagExh, 0, 64 * sizeof(uint32_t), stream));
+                WF_CHECK(hipMemsetAsync(W.counts + kWfStat + kStatDiagShadeT, 0, (kWfStatWords - kStatDiagShadeT) * sizeof(uint32_t),
+                                        stream));
+            }
             launch_finish_any(S, Q, count, full, cur, n, stream);
             WF_CHECK(hipGetLastError());
             WF_CHECK(hipEventRecord(W.ev[1], stream));
@@ -1379,7 +1411,18 @@ static bool iterate(const DevScene& S, const FrameParams& P, WfParams& Q, int& c
                 fprintf(stderr, "[wf] finish wave end times (50 us bins):");
                 for (int b = 0; b < 64; ++b)
                     if (W.h_counts[kWfDiagHist + b]) fprintf(stderr, " %d:%u", b, W.h_counts[kWfDiagHist + b]);
-                fprintf(stderr, "\n");
+                fprintf(stderr, "\n[wf] finish queue exhausted at (50 us bins):");
+                for (int b = 0; b < 64; ++b)
+                    if (W.h_counts[kWfDiagExh + b]) fprintf(stderr, " %d:%u", b, W.h_counts[kWfDiagExh + b]);
+                const double ip = W.h_counts[kWfStat + kStatDiagItPre], ix = W.h_counts[kWfStat + kStatDiagItPost];
+                const double tp = W.h_counts[kWfStat + kStatDiagTPre], tx = W.h_counts[kWfStat + kStatDiagTPost];
+                const double lx = W.h_counts[kWfStat + kStatDiagLanesPost];
+                double waves = 0;
+                for (int b = 0; b < 64; ++b) waves += W.h_counts[kWfDiagHist + b];
+                waves = waves > 0 ? waves : 1;
+                fprintf(stderr, "\n[wf] finish per wave: %.0f iterations at %.2f us before its queue ran out, %.0f at %.2f us "
+                        "after (%.1f active lanes)\n", ip / waves, ip > 0 ? tp * 0.01 / ip : 0.0, ix / waves,
+                        ix > 0 ? tx * 0.01 / ix : 0.0, ix > 0 ? lx / ix : 0.0);
             }
             return true;
         }
@@ -1575,7 +1618,7 @@ static bool record_rest(const DevScene& S, const FrameParams& P, WfParams& Q, bo
         WF_CHECK(hipMemsetAsync(W.counts + cslot(kCntChunkExtend), 0, cslot(2 * kShards) * sizeof(uint32_t), stream));
         WF_CHECK(hipMemsetD32Async(W.counts + cslot(kCntTailMode), 0u, 1, stream));
         WF_CHECK(hipMemsetD32Async(W.counts + cslot(kCntFinishQ), (uint32_t)(rounds2 & 1), 1, stream));
-        WF_CHECK(hipMemsetD32Async(W.counts + cslot(kCntChunkFinish), 0u, 1, stream));
+        WF_CHECK(hipMemsetAsync(W.counts + cslot(kCntChunkFinish), 0, cslot(kShards) * sizeof(uint32_t), stream));
         hipLaunchKernelGGL(wf_extra, dim3(grid_for(Q.own_pixels, 1u << 30)), dim3(kBlock), 0, stream, S, Q.Pd, Q, 0);
         WF_CHECK(hipGetLastError());
         if (!E.span(4, err)) return false;

@@ -57,7 +57,11 @@ static int record_part(Slot* S, int part, hipEvent_t wait_on, int capture) {
         CK(hipMemsetAsync(S->buf, 1, kBytes, S->s));
         CK(hipEventRecordWithFlags(S->t1, S->s, rf));
     } else {
-        if (wait_on) CK(hipStreamWaitEvent(S->s, wait_on, capture ? hipEventWaitExternal : 0u));
+        if (wait_on) {
+            if (capture) STEP("  hipStreamWaitEvent(external) during capture");
+            CK(hipStreamWaitEvent(S->s, wait_on, capture ? hipEventWaitExternal : 0u));
+            if (capture) STEP("  returned");
+        }
         CK(hipMemsetAsync(S->buf, 2, kBytes, S->s));
         CK(hipEventRecordWithFlags(S->t2, S->s, rf));
     }
@@ -111,12 +115,14 @@ int main(int argc, char** argv) {
                 CK(hipStreamBeginCapture(S->s, hipStreamCaptureModeThreadLocal));
                 int r = record_part(S, 0, NULL, 1);
                 if (!r) {
-                    STEP("frame %d: captured hipStreamWaitEvent(external) on the previous frame's done", f);
+                    STEP("frame %d: part 1%s", f, prev ? ", after a captured wait on the previous frame's done" : "");
                     r = record_part(S, 1, prev, 1);
                 }
+                STEP("frame %d: end capture", f);
                 hipError_t ce = hipStreamEndCapture(S->s, &g);
                 if (r) return r;
                 CK(ce);
+                STEP("frame %d: instantiate", f);
                 CK(hipGraphInstantiateWithFlags(&S->exec[0], g, 0));
                 CK(hipGraphDestroy(g));
             }
