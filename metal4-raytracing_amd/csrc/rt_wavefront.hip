@@ -353,12 +353,6 @@ __device__ __forceinline__ uint32_t dense_entry(const QueueShards& qs, uint32_t 
     const uint32_t i = g - start;
     return k * seg_cap + (back ? seg_cap - 1u - i : i);
 }
-#ifndef RT_FINISH_HOIST
-#define RT_FINISH_HOIST 1
-#endif
-#ifndef RT_TRACE_HOIST
-#define RT_TRACE_HOIST 0
-#endif
 #ifndef RT_LONG_FIRST
 #define RT_LONG_FIRST 1   // 0: every continuation ray to the front (one-sided queues; A/B builds)
 #endif
@@ -455,72 +449,9 @@ __device__ __forceinline__ uint32_t next_node(Trav& T, int* stack, bool& overflo
     return T.g_base + (uint32_t)r;
 }
 
-// HOIST: a lane whose last triangles are tested in this step fetches its next node together with
-// them (one memory latency for both instead of two in a row; the node is tested after the
-// triangles, against the updated closest hit, so the traversal is the same node for node).
-template <bool COUNT, bool HOIST = false>
+template <bool COUNT>
 __device__ __forceinline__ bool trav_step(const DevScene& S, Trav& T, bool any, int* stack, TraceCounters& tc,
                                           bool& overflow) {
-    if (HOIST) {
-        const bool has_tris = T.t_mask != 0u;
-        int k0 = 0, k1 = 0;
-        bool two = false;
-        if (has_tris) {
-            k0 = lowest_bit(T.t_mask);
-            T.t_mask &= T.t_mask - 1u;
-            two = T.t_mask != 0u;
-            k1 = two ? lowest_bit(T.t_mask) : k0;
-            if (two) T.t_mask &= T.t_mask - 1u;
-        }
-        const float4* tp0 = S.tris + 3 * (size_t)tri_slot(T.t_base, T.t_valid, k0);
-        const float4* tp1 = S.tris + 3 * (size_t)tri_slot(T.t_base, T.t_valid, k1);
-        float4 a0, a1, a2, b0, b1, b2;
-        if (has_tris) {
-            a0 = tp0[0]; a1 = tp0[1]; a2 = tp0[2];
-            b0 = tp1[0]; b1 = tp1[1]; b2 = tp1[2];
-        }
-        const bool do_node = T.t_mask == 0u && (T.g_hits != 0u || T.sp > 0);
-        NodeWords w;
-        if (do_node) w = load_node8(S.nodes8, next_node(T, stack, overflow));
-        bool tdone = false;
-        if (has_tris) {
-#define RT_ISECT(v0, v1, v2) intersect_triangle_vw(T.R.pre, T.R.o, v0, v1, v2, 0.0f, T.best, &t, &u, &v, &dt)
-            if (COUNT) tc.tris += two ? 2u : 1u;
-            float t, u, v, dt;
-            if (RT_ISECT(ld3(a0), ld3(a1), ld3(a2))) {
-                const uint32_t id = __float_as_uint(a0.w);
-                if (any) {
-                    T.hit_any = true;
-                    tdone = true;
-                } else if (t < T.best || id < T.best_id) {
-                    T.best = t;
-                    T.best_id = id;
-                    T.bu = u;
-                    T.bdet = dt;
-                    T.bv = v;
-                }
-            }
-            if (two && !tdone && RT_ISECT(ld3(b0), ld3(b1), ld3(b2))) {
-                const uint32_t id = __float_as_uint(b0.w);
-                if (any) {
-                    T.hit_any = true;
-                    tdone = true;
-                } else if (t < T.best || id < T.best_id) {
-                    T.best = t;
-                    T.best_id = id;
-                    T.bu = u;
-                    T.bdet = dt;
-                    T.bv = v;
-                }
-            }
-#undef RT_ISECT
-        }
-        if (do_node && !tdone) {
-            if (COUNT) tc.nodes++;
-            test_node8_words(w, T.R, 0.0f, T.best, T.g_hits, T.t_mask, T.t_valid, T.g_base, T.t_base, T.g_flip);
-        }
-        return tdone || (T.t_mask == 0u && T.g_hits == 0u && T.sp == 0);
-    }
     bool tdone = false;
     if (T.t_mask != 0u) {
         const int k0 = lowest_bit(T.t_mask);
@@ -1001,7 +932,7 @@ wf_trace(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int cur, in
         if (__ballot(active) == 0ull) break;
         if (!active) continue;
         if (COUNT) ++steps;
-        if (trav_step<COUNT, !ANY && RT_TRACE_HOIST != 0>(S, T, ANY, stack, tc, overflow)) {   // extend only
+        if (trav_step<COUNT>(S, T, ANY, stack, tc, overflow)) {
             active = false;
             if (COUNT && Q.diag) {   // steps-per-ray histogram (log2 bins) of the counting frame
                 atomicAdd(&Q.W.counts[kWfDiagSteps + (ANY ? 32 : 0) + (31 - __builtin_clz(steps))], 1u);
@@ -1154,7 +1085,7 @@ wf_finish_step(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int c
         // ---- one traversal step (closest hit or shadow any-hit)
         if (mode == kClosest || mode == kShadow) {
             const bool any = mode == kShadow;
-            if (trav_step<COUNT, RT_FINISH_HOIST != 0>(S, T, any, stack, tc, overflow)) {
+            if (trav_step<COUNT>(S, T, any, stack, tc, overflow)) {
                 if (any) {   // shadow ray done: unoccluded -> add its contribution (:741-743)
                     if (!T.hit_any) p.accum = p.accum + contrib;
                     if (next) {
