@@ -814,131 +814,6 @@ __global__ void __launch_bounds__(kSortThreads) wf_sort_scatter(DevScene S, WfPa
     }
 }
 
-// ---- extend-ray sort (experiment: RT_RAY_SORT_EXP=1 builds, with rt_opts.sort_bins > 0) ---------------
-// A counting sort of the extend queue by ray key before the extend launch: direction octant (3 bits)
-// x the Morton cell of the origin in an 8^3 grid over the root node's box (9 bits), at
-// Q.sort_bins resolution; XCD k then traces the k-th eighth of the sorted order.  Skipped when the
-// round goes to the finish launch (the extend launch's own test), so the finish keeps its order.
-#ifndef RT_RAY_SORT_EXP
-#define RT_RAY_SORT_EXP 0
-#endif
-#if RT_RAY_SORT_EXP
-__device__ __forceinline__ bool rsort_skip(const WfParams& Q, const QueueShards& qs) {
-    return !Q.dev_ctl || tail_mode(Q) || queue_len(qs) < Q.tail;
-}
-__device__ __forceinline__ uint32_t ray_key(const DevScene& S, const float4& o, const float4& d, uint32_t shift) {
-    const float4 h0 = *reinterpret_cast<const float4*>(S.nodes8);   // root: origin, exponents
-    const uint32_t ew = __float_as_uint(h0.w);
-    uint32_t m = 0;
-    const float oc[3] = {o.x - h0.x, o.y - h0.y, o.z - h0.z};
-    #pragma unroll
-    for (int a = 0; a < 3; ++a) {
-        const float ext = 255.0f * __uint_as_float(((ew >> (8 * a)) & 0xffu) << 23);
-        const int c = min(max((int)(oc[a] * (8.0f / ext)), 0), 7);
-        #pragma unroll
-        for (int b = 0; b < 3; ++b) m |= (uint32_t)((c >> b) & 1) << (3 * b + a);
-    }
-    const uint32_t oct = (d.x < 0.0f ? 1u : 0u) | (d.y < 0.0f ? 2u : 0u) | (d.z < 0.0f ? 4u : 0u);
-    return ((oct << 9) | m) >> shift;
-}
-__global__ void __launch_bounds__(kSortThreads) wf_rsort_hist(DevScene S, WfParams Q, int cur) {
-    __shared__ uint32_t h[kSortMaxBins];
-    const QueueShards qs = load_queue(Q.W.counts, cur, Q.seg_cap);
-    if (rsort_skip(Q, qs)) return;
-    const uint32_t shift = __builtin_ctz(kSortMaxBins) - __builtin_ctz(Q.sort_bins), K = Q.sort_bins;
-    for (uint32_t k = threadIdx.x; k < K; k += kSortThreads) h[k] = 0;
-    __syncthreads();
-    uint32_t beg, end;
-    sort_range(queue_len(qs), beg, end);
-    const float4* qin = Q.W.q[cur];
-    for (uint32_t g = beg + threadIdx.x; g < end; g += kSortThreads) {
-        const uint32_t e = dense_entry(qs, g, Q.seg_cap);
-        atomicAdd(&h[ray_key(S, qin[2 * (size_t)e], qin[2 * (size_t)e + 1], shift)], 1u);
-    }
-    __syncthreads();
-    for (uint32_t k = threadIdx.x; k < K; k += kSortThreads) Q.W.sort_table[(size_t)k * kSortBlocks + blockIdx.x] = h[k];
-}
-__global__ void __launch_bounds__(kSortBlocks) wf_rsort_rowscan(WfParams Q, int cur) {
-    __shared__ uint32_t w[kSortBlocks / 64];
-    if (rsort_skip(Q, load_queue(Q.W.counts, cur, Q.seg_cap))) return;
-    uint32_t* row = Q.W.sort_table + (size_t)blockIdx.x * kSortBlocks;
-    const uint32_t v = row[threadIdx.x];
-    const uint32_t incl = wave_incl_scan(v);
-    const int wave = threadIdx.x >> 6;
-    if (lane_id() == 63) w[wave] = incl;
-    __syncthreads();
-    uint32_t base = 0;
-    for (int i = 0; i < wave; ++i) base += w[i];
-    row[threadIdx.x] = base + incl - v;
-    if (threadIdx.x == kSortBlocks - 1) Q.W.sort_total[blockIdx.x] = base + incl;
-}
-__global__ void __launch_bounds__(kSortThreads) wf_rsort_scatter(DevScene S, WfParams Q, int cur) {
-    __shared__ uint32_t off[kSortMaxBins];
-    __shared__ uint32_t w[kSortThreads / 64];
-    const QueueShards qs = load_queue(Q.W.counts, cur, Q.seg_cap);
-    if (rsort_skip(Q, qs)) return;
-    const uint32_t shift = __builtin_ctz(kSortMaxBins) - __builtin_ctz(Q.sort_bins);
-    const uint32_t K = Q.sort_bins, per = K / kSortThreads;
-    uint32_t loc[kSortMaxBins / kSortThreads];
-    uint32_t s = 0;
-    for (uint32_t i = 0; i < per; ++i) {
-        loc[i] = s;
-        s += Q.W.sort_total[threadIdx.x * per + i];
-    }
-    const uint32_t incl = wave_incl_scan(s);
-    const int wave = threadIdx.x >> 6;
-    if (lane_id() == 63) w[wave] = incl;
-    __syncthreads();
-    uint32_t base = 0;
-    for (int i = 0; i < wave; ++i) base += w[i];
-    const uint32_t excl = base + incl - s;
-    for (uint32_t i = 0; i < per; ++i) {
-        const uint32_t k = threadIdx.x * per + i;
-        off[k] = excl + loc[i] + Q.W.sort_table[(size_t)k * kSortBlocks + blockIdx.x];
-    }
-    __syncthreads();
-    const float4* qin = Q.W.q[cur];
-    uint32_t beg, end;
-    sort_range(queue_len(qs), beg, end);
-    for (uint32_t g = beg + threadIdx.x; g < end; g += kSortThreads) {
-        const uint32_t e = dense_entry(qs, g, Q.seg_cap);
-        const float4 o = qin[2 * (size_t)e], d = qin[2 * (size_t)e + 1];
-        const uint32_t pos = atomicAdd(&off[ray_key(S, o, d, shift)], 1u);
-        Q.W.sorted[4 * (size_t)pos] = o;
-        Q.W.sorted[4 * (size_t)pos + 1] = d;
-        if (__float_as_uint(d.w) != 0u) Q.W.sorted[4 * (size_t)pos + 2] = Q.W.qc[cur][e];
-    }
-}
-// sorted order back into the queue: shard k (XCD k's) holds the k-th eighth, all at the front
-__global__ void __launch_bounds__(kBlock) wf_rsort_back(WfParams Q, int cur) {
-    const QueueShards qs = load_queue(Q.W.counts, cur, Q.seg_cap);
-    if (rsort_skip(Q, qs)) return;
-    const uint32_t n = queue_len(qs), per = n / kShards, rem = n % kShards;
-    float4* q = Q.W.q[cur];
-    for (uint32_t g = blockIdx.x * kBlock + threadIdx.x; g < n; g += gridDim.x * kBlock) {
-        // shard k takes per + (k < rem) entries
-        const uint32_t big = rem * (per + 1);
-        const uint32_t k = g < big ? g / (per + 1) : rem + (g - big) / max(per, 1u);
-        const uint32_t start = k < rem ? k * (per + 1) : big + (k - rem) * per;
-        const uint32_t e = k * Q.seg_cap + (g - start);
-        const float4 d = Q.W.sorted[4 * (size_t)g + 1];
-        q[2 * (size_t)e] = Q.W.sorted[4 * (size_t)g];
-        q[2 * (size_t)e + 1] = d;
-        if (__float_as_uint(d.w) != 0u) Q.W.qc[cur][e] = Q.W.sorted[4 * (size_t)g + 2];
-    }
-}
-__global__ void wf_rsort_counts(WfParams Q, int cur) {
-    const QueueShards qs = load_queue(Q.W.counts, cur, Q.seg_cap);
-    if (rsort_skip(Q, qs)) return;
-    const uint32_t n = queue_len(qs), per = n / kShards, rem = n % kShards;
-    __syncthreads();   // every lane has read the counters before any is rewritten
-    if (threadIdx.x < kShards) {
-        Q.W.counts[cslot(cur * kShards + threadIdx.x)] = per + (threadIdx.x < rem ? 1u : 0u);
-        Q.W.counts[cslot(kCntBack + cur * kShards + threadIdx.x)] = 0u;
-    }
-}
-#endif
-
 // ---- persistent traversal with per-lane refill (extend: ANY = false, connect: ANY = true) -----------
 // The grid is the resident capacity.  Each XCD (blockIdx % 8) owns queue shard k (what its own shade blocks appended) and hands
 // it out in chunks of Q.chunk rays, one atomic per chunk.  Every iteration advances each lane of a
@@ -1684,19 +1559,7 @@ static bool enqueue_pass(const DevScene& S, const FrameParams& P, const WfParams
     const unsigned gt = trace_grid_cap(Q), g = tuning().shade_blocks;
     for (int k = 0; k < rounds; ++k) {
         const int cur = k & 1;
-#if RT_RAY_SORT_EXP
-        if (Q.sort_bins) {
-            hipLaunchKernelGGL(wf_rsort_hist, dim3(kSortBlocks), dim3(kSortThreads), 0, stream, S, Q, cur);
-            hipLaunchKernelGGL(wf_rsort_rowscan, dim3(Q.sort_bins), dim3(kSortBlocks), 0, stream, Q, cur);
-            hipLaunchKernelGGL(wf_rsort_scatter, dim3(kSortBlocks), dim3(kSortThreads), 0, stream, S, Q, cur);
-            hipLaunchKernelGGL(wf_rsort_back, dim3(2048), dim3(kBlock), 0, stream, Q, cur);
-            hipLaunchKernelGGL(wf_rsort_counts, dim3(1), dim3(64), 0, stream, Q, cur);
-            if (!E.span(6, err)) return false;
-        }
-        constexpr bool kHitSort = false;
-#else
         const bool kHitSort = Q.sort_bins != 0;
-#endif
         if (count) hipLaunchKernelGGL((wf_trace<false, true>), dim3(gt), dim3(kBlock), 0, stream, S, Q.Pd, Q, cur, ts + 2 * k);
         else hipLaunchKernelGGL((wf_trace<false, false>), dim3(gt), dim3(kBlock), 0, stream, S, Q.Pd, Q, cur, ts + 2 * k);
         if (!E.span(1, err)) return false;
