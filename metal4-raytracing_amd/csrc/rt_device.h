@@ -138,9 +138,6 @@ __host__ __device__ __forceinline__ uint32_t tri_slot(uint32_t tri_base, uint32_
     return tri_base + (uint32_t)__builtin_popcount(tri_valid & ((1u << k) - 1u));
 }
 
-#ifndef RT_PK_NODE
-#define RT_PK_NODE 0
-#endif
 // Slab-test the 8 children of a node.  Outputs: the internal children hit (bit r = internal rank r
 // = slot r), the triangles to test (nibble space: bit 4j + i = triangle i of leaf j, see
 // tri_slot), the node's tri_valid word, and the traversal direction of the slot order.
@@ -170,28 +167,6 @@ __host__ __device__ __forceinline__ void test_node8_words(const NodeWords& W, co
     const uint32_t fz0 = R.iz >= 0.0f ? qz.z : qz.x, fz1 = R.iz >= 0.0f ? qz.w : qz.y;
     const float tf_max = tmax * 1.0000004f;
     uint32_t hm = 0;
-#if defined(__HIP_DEVICE_COMPILE__) && RT_PK_NODE
-    // packed fp32 (v_pk_fma_f32): (near x, near y), (far x, far y) and (near z, far z) per child;
-    // each element is the same fma as the scalar form, so the same bits
-    typedef float f2v __attribute__((ext_vector_type(2)));
-    const f2v axy = {ax, ay}, bxy = {bx, by}, azz = {az, az}, bzz = {bz, bz};
-    #pragma unroll
-    for (int c = 0; c < 8; ++c) {
-        const int b = c & 3;
-        const uint32_t wnx = c < 4 ? nx0 : nx1, wfx = c < 4 ? fx0 : fx1;
-        const uint32_t wny = c < 4 ? ny0 : ny1, wfy = c < 4 ? fy0 : fy1;
-        const uint32_t wnz = c < 4 ? nz0 : nz1, wfz = c < 4 ? fz0 : fz1;
-        const f2v qn = {byte_f(wnx, b), byte_f(wny, b)}, qf = {byte_f(wfx, b), byte_f(wfy, b)};
-        const f2v qz = {byte_f(wnz, b), byte_f(wfz, b)};
-        const f2v tn2 = __builtin_elementwise_fma(qn, axy, bxy);
-        const f2v tf2 = __builtin_elementwise_fma(qf, axy, bxy);
-        const f2v tz2 = __builtin_elementwise_fma(qz, azz, bzz);
-        const float tn = fmaxf(fmaxf(tn2.x, tn2.y), fmaxf(tz2.x, tmin));
-        const float tf = fminf(fminf(tf2.x, tf2.y), fminf(tz2.y, tf_max));
-        const bool hit = tn <= tf;
-        hm |= hit ? (1u << c) : 0u;
-    }
-#else
     #pragma unroll
     for (int c = 0; c < 8; ++c) {
         const int b = c & 3;
@@ -206,7 +181,6 @@ __host__ __device__ __forceinline__ void test_node8_words(const NodeWords& W, co
         const bool hit = tn <= tf;
         hm |= hit ? (1u << c) : 0u;
     }
-#endif
     ihits = hm & ((1u << k_int) - 1u);
     tmask = spread_nibbles(hm >> k_int) & h1.z;
     tvalid = h1.z;

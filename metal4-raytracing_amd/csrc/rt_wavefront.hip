@@ -46,6 +46,7 @@ struct Tuning {
     int fchunk;        // RT_FCHUNK: paths per chunk grab of the finish kernel
     int shade_min;     // RT_SHADE_MIN: the finish kernel shades once this many lanes wait
     int shade_min_x;   // RT_SHADE_MIN_X: the same once the finish queue is exhausted (< 0: that percentage of the wave's busy lanes)
+    int team;          // RT_TEAM: finish drain, lanes per query once a wave holds <= 64 / team paths (0 / 1: off)
     int finish_frac;   // RT_FINISH_FRAC: percent of the resident grid the finish launch takes (0 = by frames in flight)
     int trace_frac;    // RT_TRACE_FRAC: percent of the resident grid the persistent wf_trace launches take (0 = by frames in flight)
     int log;           // RT_WF_LOG=1: per-round queue sizes, stage times and finish diagnostics on stderr
@@ -62,6 +63,8 @@ static const Tuning& tuning() {
         v.fchunk = std::max(1, env_int("RT_FCHUNK", 64));
         v.shade_min = env_int("RT_SHADE_MIN", 24);
         v.shade_min_x = env_int("RT_SHADE_MIN_X", -50);
+        v.team = env_int("RT_TEAM", 0);
+        if (v.team != 2 && v.team != 4 && v.team != 8) v.team = 0;
         v.finish_frac = std::min(env_int("RT_FINISH_FRAC", 0), 100);
         v.trace_frac = std::min(env_int("RT_TRACE_FRAC", 0), 100);
         v.log = env_int("RT_WF_LOG", 0);
@@ -219,6 +222,7 @@ struct WfParams {
     int diag;              // wf_finish_step: record the diagnostics slots (RT_WF_LOG)
     int shade_min;         // wf_finish_step: shade once this many lanes wait (or none traverses)
     int shade_min_x;       // wf_finish_step: the same once the launch's queue is exhausted (< 0: percent of busy lanes)
+    int team;              // wf_finish_step: lanes per query in the drain (0: no team drain)
     int fchunk;            // wf_finish_step: paths per chunk grab
     int finish_frac;       // percent of the resident grid the finish launch takes
     int trace_frac;        // percent of the resident grid the bulk wf_trace launches take
@@ -449,9 +453,11 @@ __device__ __forceinline__ uint32_t next_node(Trav& T, int* stack, bool& overflo
     return T.g_base + (uint32_t)r;
 }
 
+// `cull`: the distance bound of the box and triangle tests; T.best, or lower in the finish kernel's
+// team drain (the closest hit any member of the team has found); T.best stays this lane's own hit.
 template <bool COUNT>
 __device__ __forceinline__ bool trav_step(const DevScene& S, Trav& T, bool any, int* stack, TraceCounters& tc,
-                                          bool& overflow) {
+                                          bool& overflow, float cull) {
     bool tdone = false;
     if (T.t_mask != 0u) {
         const int k0 = lowest_bit(T.t_mask);
@@ -459,7 +465,7 @@ __device__ __forceinline__ bool trav_step(const DevScene& S, Trav& T, bool any, 
         const bool two = T.t_mask != 0u;
         const int k1 = two ? lowest_bit(T.t_mask) : k0;
         if (two) T.t_mask &= T.t_mask - 1u;
-#define RT_ISECT(v0, v1, v2) intersect_triangle_vw(T.R.pre, T.R.o, v0, v1, v2, 0.0f, T.best, &t, &u, &v, &dt)
+#define RT_ISECT(v0, v1, v2) intersect_triangle_vw(T.R.pre, T.R.o, v0, v1, v2, 0.0f, cull, &t, &u, &v, &dt)
         const float4* tp0 = S.tris + 3 * (size_t)tri_slot(T.t_base, T.t_valid, k0);
         const float4* tp1 = S.tris + 3 * (size_t)tri_slot(T.t_base, T.t_valid, k1);
         const float4 a0 = tp0[0], a1 = tp0[1], a2 = tp0[2];
@@ -497,7 +503,7 @@ __device__ __forceinline__ bool trav_step(const DevScene& S, Trav& T, bool any, 
         const uint32_t ni = next_node(T, stack, overflow);
         if (COUNT) tc.nodes++;
         const NodeWords w = load_node8(S.nodes8, ni);
-        test_node8_words(w, T.R, 0.0f, T.best, T.g_hits, T.t_mask, T.t_valid, T.g_base, T.t_base, T.g_flip);
+        test_node8_words(w, T.R, 0.0f, cull, T.g_hits, T.t_mask, T.t_valid, T.g_base, T.t_base, T.g_flip);
     }
     return tdone || (T.t_mask == 0u && T.g_hits == 0u && T.sp == 0);
 #undef RT_ISECT
@@ -932,7 +938,7 @@ wf_trace(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int cur, in
         if (__ballot(active) == 0ull) break;
         if (!active) continue;
         if (COUNT) ++steps;
-        if (trav_step<COUNT>(S, T, ANY, stack, tc, overflow)) {
+        if (trav_step<COUNT>(S, T, ANY, stack, tc, overflow, T.best)) {
             active = false;
             if (COUNT && Q.diag) {   // steps-per-ray histogram (log2 bins) of the counting frame
                 atomicAdd(&Q.W.counts[kWfDiagSteps + (ANY ? 32 : 0) + (31 - __builtin_clz(steps))], 1u);
@@ -965,7 +971,7 @@ wf_trace(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int cur, in
 // the glass paths left at the tail (up to ~23 segments) do not wait for their wave's worst ray
 // every segment.  Four waves per SIMD: the shading code's register peak (119 VGPRs, no scratch);
 // five were measured no faster.
-template <bool COUNT, bool FULL>
+template <bool COUNT, bool FULL, bool TEAM>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 4)))
 wf_finish_step(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int cur, int ts) {
     const FrameParams& P = *Pp;   // per-frame parameters in device memory
@@ -1028,6 +1034,20 @@ wf_finish_step(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int c
         segs = 0;
     };
 
+    // shade this lane's closest hit (:324-774); rayO / rayD become the next ray
+    auto shade_hit = [&](StepResult& r) {
+        Hit h;
+        h.t = T.best;
+        h.id = T.best_id;
+        h.u = T.bu / T.bdet;
+        h.v = T.bv / T.bdet;
+        const int sample = (int)meta.y;
+        shade_step<FULL, false>(S, U, halton, (int)meta.w, sample, rayO, rayD, h, p, sample == 0 && p.step == 0, zero2,
+                                false, zero2, r);
+        write_pixel_outputs(P, meta.x, r, h, FULL);
+        next = r.next;
+    };
+
     while (true) {
         // ---- refill idle lanes with the next remaining paths (chunks of Q.fchunk from the XCD's counter)
         const unsigned long long idle = __ballot(mode == kIdle);
@@ -1079,13 +1099,14 @@ wf_finish_step(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int c
         }
         const unsigned long long active = __ballot(mode != kIdle);
         if (active == 0ull) break;   // idle everywhere => refill found nothing
+        if (TEAM && exhausted && __popcll(active) * Q.team <= 64) break;   // the rest: team drain below
         ++iters;
         if (Q.diag && exhausted && lane_id() == 0) RT_DX[2] += (uint32_t)__popcll(active);
 
         // ---- one traversal step (closest hit or shadow any-hit)
         if (mode == kClosest || mode == kShadow) {
             const bool any = mode == kShadow;
-            if (trav_step<COUNT>(S, T, any, stack, tc, overflow)) {
+            if (trav_step<COUNT>(S, T, any, stack, tc, overflow, T.best)) {
                 if (any) {   // shadow ray done: unoccluded -> add its contribution (:741-743)
                     if (!T.hit_any) p.accum = p.accum + contrib;
                     if (next) {
@@ -1115,17 +1136,8 @@ wf_finish_step(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int c
                 n_shaded += (uint32_t)__popcll(ready);
             }
             if (mode == kReady) {
-                Hit h;
-                h.t = T.best;
-                h.id = T.best_id;
-                h.u = T.bu / T.bdet;
-                h.v = T.bv / T.bdet;
-                const int sample = (int)meta.y;
                 StepResult r;
-                shade_step<FULL, false>(S, U, halton, (int)meta.w, sample, rayO, rayD, h, p, sample == 0 && p.step == 0,
-                                        zero2, false, zero2, r);
-                write_pixel_outputs(P, meta.x, r, h, FULL);
-                next = r.next;
+                shade_hit(r);
                 if (r.shadow) {
                     contrib = r.contrib;
                     trav_start(T, r.so, r.sd, r.stmax);
@@ -1158,6 +1170,204 @@ wf_finish_step(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int c
             if (Q.diag) t_shade += __builtin_amdgcn_s_memrealtime() - ts0;
         }
     }
+    // ---- team drain (Q.team lanes per query).  The queue has run out and this wave holds at most
+    // 64 / team paths: each moves to a team leader (lane team * r) and the team's lanes traverse its
+    // query together, splitting the node groups and stack entries among themselves (XOR-paired
+    // hand-offs every iteration) and sharing the closest hit found so far as their cull bound; a
+    // closest-hit query ends with the lexicographic minimum of the members' (t, id), the serial
+    // traversal's result, so the same bits; an any-hit query ends at any member's occluder.  The
+    // leader shades, then the team starts the path's next query.
+    if (TEAM && __ballot(mode != kIdle) != 0ull) {
+        const int TM = Q.team;
+        if (mode == kReady) {   // waiting lanes first: every busy lane then holds a query
+            StepResult r;
+            shade_hit(r);
+            if (r.shadow) {
+                contrib = r.contrib;
+                trav_start(T, r.so, r.sd, r.stmax);
+                lds_sray[0][threadIdx.x] = r.so.x;
+                lds_sray[1][threadIdx.x] = r.so.y;
+                lds_sray[2][threadIdx.x] = r.so.z;
+                lds_sray[3][threadIdx.x] = r.sd.x;
+                lds_sray[4][threadIdx.x] = r.sd.y;
+                lds_sray[5][threadIdx.x] = r.sd.z;
+                mode = kShadow;
+                n_shadow++;
+            } else if (r.next) {
+                mode = kClosest;
+                n_closest++;
+                segs++;
+            } else {
+                end_path();
+            }
+        }
+        const unsigned long long busy = __ballot(mode != kIdle);
+        const int lane = (int)lane_id(), j = lane & (TM - 1), lead = lane - j, rk = lane / TM;
+        const int nb = __popcll(busy);
+        int src = lane;   // team leader rk takes the rk-th busy lane's path
+        {
+            unsigned long long b = busy;
+            for (int k = 0; b; ++k) {
+                const int l = __builtin_ctzll(b);
+                b &= b - 1ull;
+                if (j == 0 && rk == k) src = l;
+            }
+        }
+        const bool leader = j == 0 && rk < nb;
+        auto mvu = [&](uint32_t v) { return (uint32_t)__shfl((int)v, src); };
+        auto mvf = [&](float v) { return __shfl(v, src); };
+        auto mv3 = [&](f3 v) { return mk3(mvf(v.x), mvf(v.y), mvf(v.z)); };
+        const uint32_t sbase = threadIdx.x & ~63u;
+        f3 so = mk3(lds_sray[0][sbase + src], lds_sray[1][sbase + src], lds_sray[2][sbase + src]);
+        f3 sd = mk3(lds_sray[3][sbase + src], lds_sray[4][sbase + src], lds_sray[5][sbase + src]);
+        float stm = mvf(T.best);
+        pid = mvu(pid);
+        meta = make_uint4(mvu(meta.x), mvu(meta.y), mvu(meta.z), mvu(meta.w));
+        p.color = mv3(p.color);
+        p.accum = mv3(p.accum);
+        p.bounce = (int)mvu((uint32_t)p.bounce);
+        p.step = (int)mvu((uint32_t)p.step);
+        p.tpass = (int)mvu((uint32_t)p.tpass);
+        rayO = mv3(rayO);
+        rayD = mv3(rayD);
+        contrib = mv3(contrib);
+        next = mvu(next ? 1u : 0u) != 0u;
+        segs = mvu(segs);
+        mode = leader ? (int)mvu((uint32_t)mode) : kIdle;
+        bool fresh = leader;   // the team starts the leader's query
+        float cull = INFINITY;
+        while (true) {
+            const int lmode = __shfl(mode, lead);
+            if (__ballot(lmode != kIdle) == 0ull) break;
+            const bool team_on = lmode == kClosest || lmode == kShadow, any = lmode == kShadow;
+            if (__shfl((int)fresh, lead) != 0 && team_on) {   // start the team's query on every member
+                f3 o, d;
+                float tmax;
+                if (any) {
+                    o = mk3(__shfl(so.x, lead), __shfl(so.y, lead), __shfl(so.z, lead));
+                    d = mk3(__shfl(sd.x, lead), __shfl(sd.y, lead), __shfl(sd.z, lead));
+                    tmax = __shfl(stm, lead);
+                } else {
+                    o = mk3(__shfl(rayO.x, lead), __shfl(rayO.y, lead), __shfl(rayO.z, lead));
+                    d = mk3(__shfl(rayD.x, lead), __shfl(rayD.y, lead), __shfl(rayD.z, lead));
+                    tmax = INFINITY;
+                }
+                trav_start(T, o, d, tmax);
+                if (j != 0) T.g_hits = 0;   // members start without work; the leader hands it out below
+                cull = tmax;
+            }
+            fresh = false;
+            // one traversal step of every member with work
+            if (team_on && !(T.t_mask == 0u && T.g_hits == 0u && T.sp == 0))
+                (void)trav_step<COUNT>(S, T, any, stack, tc, overflow, cull);
+            // occluder anywhere in the team; the team's closest hit so far (the cull bound)
+            int hit = (any && T.hit_any) ? 1 : 0;
+            float bt = T.best;
+            for (int k = 1; k < TM; k <<= 1) {
+                hit |= __shfl_xor(hit, k);
+                bt = fminf(bt, __shfl_xor(bt, k));
+            }
+            if (team_on && !any) cull = bt;
+            if (hit) {
+                T.t_mask = 0u;
+                T.g_hits = 0u;
+                T.sp = 0;
+            }
+            // hand-offs: in round k lane l pairs with lane l ^ k; an idle member takes the later
+            // half (in visiting order) of its partner's node group, or its partner's top stack entry
+            for (int k = 1; k < TM; ++k) {
+                const bool idle_m = team_on && T.t_mask == 0u && T.g_hits == 0u && T.sp == 0;
+                const bool give = team_on && (__popc(T.g_hits) >= 2 || T.sp > 0);
+                const bool p_idle = __shfl_xor((int)idle_m, k) != 0, p_give = __shfl_xor((int)give, k) != 0;
+                uint32_t pay = 0u;
+                if (give && p_idle) {
+                    if (__popc(T.g_hits) >= 2) {
+                        uint32_t keep = 0u, rest = T.g_hits;
+                        for (int c = __popc(T.g_hits) - __popc(T.g_hits) / 2; c > 0; --c) {
+                            const int b = T.g_flip ? highest_bit(rest) : lowest_bit(rest);
+                            keep |= 1u << b;
+                            rest &= ~(1u << b);
+                        }
+                        pay = pack_group(T.g_base, T.g_flip, rest);
+                        T.g_hits = keep;
+                    } else {
+                        --T.sp;
+                        pay = (uint32_t)stack[T.sp * kBlock];
+                    }
+                }
+                const uint32_t got = (uint32_t)__shfl_xor((int)pay, k);
+                if (idle_m && p_give) {
+                    T.g_base = got >> 9;
+                    T.g_flip = (got >> 8) & 1u;
+                    T.g_hits = got & 0xffu;
+                }
+            }
+            // the team's query has ended once no member holds work
+            int work = (team_on && !(T.t_mask == 0u && T.g_hits == 0u && T.sp == 0)) ? 1 : 0;
+            for (int k = 1; k < TM; k <<= 1) work |= __shfl_xor(work, k);
+            if (team_on && !work) {
+                if (!any) {   // lexicographic minimum of the members' (t, id), with its (V, W, det)
+                    float t = T.best, bu = T.bu, bv = T.bv, bd = T.bdet;
+                    uint32_t id = T.best_id;
+                    for (int k = 1; k < TM; k <<= 1) {
+                        const float t2 = __shfl_xor(t, k), u2 = __shfl_xor(bu, k), v2 = __shfl_xor(bv, k),
+                                    d2 = __shfl_xor(bd, k);
+                        const uint32_t id2 = (uint32_t)__shfl_xor((int)id, k);
+                        if (t2 < t || (t2 == t && id2 < id)) {
+                            t = t2;
+                            id = id2;
+                            bu = u2;
+                            bv = v2;
+                            bd = d2;
+                        }
+                    }
+                    T.best = t;
+                    T.best_id = id;
+                    T.bu = bu;
+                    T.bv = bv;
+                    T.bdet = bd;
+                }
+                if (j == 0) {   // the leader: the path's next step (as in the loop above)
+                    if (any) {
+                        if (!hit) p.accum = p.accum + contrib;
+                        if (next) {
+                            mode = kClosest;
+                            n_closest++;
+                            segs++;
+                            fresh = true;
+                        } else {
+                            end_path();
+                        }
+                    } else if (T.best_id == 0xffffffffu) {
+                        end_path();
+                    } else {
+                        mode = kReady;
+                    }
+                }
+            }
+            if (mode == kReady) {   // leaders: shade at once (the drain is latency-bound)
+                StepResult r;
+                shade_hit(r);
+                if (r.shadow) {
+                    contrib = r.contrib;
+                    so = r.so;
+                    sd = r.sd;
+                    stm = r.stmax;
+                    mode = kShadow;
+                    n_shadow++;
+                    fresh = true;
+                } else if (r.next) {
+                    mode = kClosest;
+                    n_closest++;
+                    segs++;
+                    fresh = true;
+                } else {
+                    end_path();
+                }
+            }
+        }
+    }
+
     if (Q.diag) {
         const uint32_t dt = (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_start);
         if (lane_id() == 0) {
@@ -1341,15 +1551,21 @@ static unsigned trace_grid_cap(const WfParams& Q) {
 // machine stays free for the other frames' kernels)
 template <bool COUNT, bool FULL>
 static unsigned finish_full_cap() {   // resident blocks of the finish kernel, queried once
-    static const unsigned c = resident_grid(wf_finish_step<COUNT, FULL>, 2);
+    static const unsigned c = resident_grid(wf_finish_step<COUNT, FULL, false>, 2);
     return c;
 }
 template <bool COUNT, bool FULL>
 static void launch_finish(const DevScene& S, const WfParams& Q, int cur, uint32_t n, hipStream_t stream, int ts) {
     // at least one block per XCD: each takes the chunks of its XCD's counter (wf_finish_step)
     const unsigned cap = std::max(8u, finish_full_cap<COUNT, FULL>() * (unsigned)Q.finish_frac / 100u);
-    hipLaunchKernelGGL((wf_finish_step<COUNT, FULL>), dim3(std::max(8u, grid_for(n, cap))), dim3(kBlock), 0, stream, S,
-                       Q.Pd, Q, cur, ts);
+    // Q.team: the kernel with the team drain (a separate instance: its code would raise the plain
+    // kernel's register pressure)
+    if (Q.team)
+        hipLaunchKernelGGL((wf_finish_step<COUNT, FULL, true>), dim3(std::max(8u, grid_for(n, cap))), dim3(kBlock), 0,
+                           stream, S, Q.Pd, Q, cur, ts);
+    else
+        hipLaunchKernelGGL((wf_finish_step<COUNT, FULL, false>), dim3(std::max(8u, grid_for(n, cap))), dim3(kBlock), 0,
+                           stream, S, Q.Pd, Q, cur, ts);
 }
 
 static void launch_finish_any(const DevScene& S, const WfParams& Q, bool count, bool full, int cur, uint32_t n,
@@ -1806,6 +2022,7 @@ bool run_wavefront(const DevScene& S, const FrameParams& P, WavefrontBuffers& W,
     Q.diag = tu.log;
     Q.shade_min = tu.shade_min;
     Q.shade_min_x = tu.shade_min_x;
+    Q.team = tu.team;
     Q.fchunk = tu.fchunk;
     Q.spans = spans ? 1 : 0;
     Q.spp_div = make_fastdiv((uint32_t)Q.spp);
