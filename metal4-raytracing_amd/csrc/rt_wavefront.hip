@@ -32,6 +32,9 @@ namespace rt {
 
 namespace {
 
+// frames of at most this many base paths use the finish kernel's team drain by default (RT_TEAM)
+constexpr uint32_t kTeamAutoPaths = 2500000u;
+
 static int env_int(const char* name, int dflt) {
     const char* e = getenv(name);
     return e ? atoi(e) : dflt;
@@ -46,7 +49,8 @@ struct Tuning {
     int fchunk;        // RT_FCHUNK: paths per chunk grab of the finish kernel
     int shade_min;     // RT_SHADE_MIN: the finish kernel shades once this many lanes wait
     int shade_min_x;   // RT_SHADE_MIN_X: the same once the finish queue is exhausted (< 0: that percentage of the wave's busy lanes)
-    int team;          // RT_TEAM: finish drain, lanes per query once a wave holds <= 64 / team paths (0 / 1: off)
+    int team;          // RT_TEAM: finish drain, lanes per query once a wave holds <= 64 / team paths (0 / 1: off;
+                       // unset: 4 for frames of at most kTeamAutoPaths paths, off above)
     int finish_frac;   // RT_FINISH_FRAC: percent of the resident grid the finish launch takes (0 = by frames in flight)
     int trace_frac;    // RT_TRACE_FRAC: percent of the resident grid the persistent wf_trace launches take (0 = by frames in flight)
     int log;           // RT_WF_LOG=1: per-round queue sizes, stage times and finish diagnostics on stderr
@@ -63,8 +67,8 @@ static const Tuning& tuning() {
         v.fchunk = std::max(1, env_int("RT_FCHUNK", 64));
         v.shade_min = env_int("RT_SHADE_MIN", 24);
         v.shade_min_x = env_int("RT_SHADE_MIN_X", -50);
-        v.team = env_int("RT_TEAM", 0);
-        if (v.team != 2 && v.team != 4 && v.team != 8) v.team = 0;
+        v.team = env_int("RT_TEAM", -1);
+        if (v.team != -1 && v.team != 2 && v.team != 4 && v.team != 8) v.team = 0;
         v.finish_frac = std::min(env_int("RT_FINISH_FRAC", 0), 100);
         v.trace_frac = std::min(env_int("RT_TRACE_FRAC", 0), 100);
         v.log = env_int("RT_WF_LOG", 0);
@@ -453,8 +457,9 @@ __device__ __forceinline__ uint32_t next_node(Trav& T, int* stack, bool& overflo
     return T.g_base + (uint32_t)r;
 }
 
-// `cull`: the distance bound of the box and triangle tests; T.best, or lower in the finish kernel's
-// team drain (the closest hit any member of the team has found); T.best stays this lane's own hit.
+// `cull`: the distance bound of the box and triangle tests together with T.best (the lower of the
+// two); lower than T.best in the finish kernel's team drain (the closest hit any member of the team
+// has found), where T.best stays this lane's own hit.
 template <bool COUNT>
 __device__ __forceinline__ bool trav_step(const DevScene& S, Trav& T, bool any, int* stack, TraceCounters& tc,
                                           bool& overflow, float cull) {
@@ -465,7 +470,9 @@ __device__ __forceinline__ bool trav_step(const DevScene& S, Trav& T, bool any, 
         const bool two = T.t_mask != 0u;
         const int k1 = two ? lowest_bit(T.t_mask) : k0;
         if (two) T.t_mask &= T.t_mask - 1u;
-#define RT_ISECT(v0, v1, v2) intersect_triangle_vw(T.R.pre, T.R.o, v0, v1, v2, 0.0f, cull, &t, &u, &v, &dt)
+        // the bound is re-read for every test: a triangle must not be accepted beyond a closer hit
+        // found earlier in this step (the update below assumes t <= T.best)
+#define RT_ISECT(v0, v1, v2) intersect_triangle_vw(T.R.pre, T.R.o, v0, v1, v2, 0.0f, fminf(cull, T.best), &t, &u, &v, &dt)
         const float4* tp0 = S.tris + 3 * (size_t)tri_slot(T.t_base, T.t_valid, k0);
         const float4* tp1 = S.tris + 3 * (size_t)tri_slot(T.t_base, T.t_valid, k1);
         const float4 a0 = tp0[0], a1 = tp0[1], a2 = tp0[2];
@@ -503,7 +510,7 @@ __device__ __forceinline__ bool trav_step(const DevScene& S, Trav& T, bool any, 
         const uint32_t ni = next_node(T, stack, overflow);
         if (COUNT) tc.nodes++;
         const NodeWords w = load_node8(S.nodes8, ni);
-        test_node8_words(w, T.R, 0.0f, cull, T.g_hits, T.t_mask, T.t_valid, T.g_base, T.t_base, T.g_flip);
+        test_node8_words(w, T.R, 0.0f, fminf(cull, T.best), T.g_hits, T.t_mask, T.t_valid, T.g_base, T.t_base, T.g_flip);
     }
     return tdone || (T.t_mask == 0u && T.g_hits == 0u && T.sp == 0);
 #undef RT_ISECT
@@ -1233,7 +1240,10 @@ wf_finish_step(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int c
         contrib = mv3(contrib);
         next = mvu(next ? 1u : 0u) != 0u;
         segs = mvu(segs);
-        mode = leader ? (int)mvu((uint32_t)mode) : kIdle;
+        // every lane takes part in the shuffle: a bpermute inside the leaders' branch would read the
+        // (inactive) non-leader source lanes as zero
+        const int src_mode = (int)mvu((uint32_t)mode);
+        mode = leader ? src_mode : kIdle;
         bool fresh = leader;   // the team starts the leader's query
         float cull = INFINITY;
         while (true) {
@@ -2022,7 +2032,10 @@ bool run_wavefront(const DevScene& S, const FrameParams& P, WavefrontBuffers& W,
     Q.diag = tu.log;
     Q.shade_min = tu.shade_min;
     Q.shade_min_x = tu.shade_min_x;
-    Q.team = tu.team;
+    // the team drain pays where the drain is a large part of the finish: small frames (C3g rank
+    // shares, DESIGN.md §3.3: 8-way +1.5-1.8 %, 4-way +1.5-2.9 %, 2-way ±1 %, the whole 1080p frame
+    // four in flight -0.5 %)
+    Q.team = tu.team >= 0 ? tu.team : (Q.base_paths <= kTeamAutoPaths ? 4 : 0);
     Q.fchunk = tu.fchunk;
     Q.spans = spans ? 1 : 0;
     Q.spp_div = make_fastdiv((uint32_t)Q.spp);
