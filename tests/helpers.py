@@ -117,3 +117,22 @@ def lights_scene(rt, assets, kinds):
     sc = rt.Scene.preset("c1", assets)
     sc.set_lights([make_light(rt, k) for k in kinds])
     return sc
+
+
+# ---- a triangle soup: closest-hit order against triangle ids (tests/test_gpu_parity.py) -----------
+def write_triangle_soup(path, n=4000, seed=5):
+    """An OBJ of n random, overlapping, roughly camera-facing triangles in a thin slab: BVH leaves
+    hold several triangles a ray crosses, in slot orders and with ids unrelated to their depth, so
+    a closest-hit search that accepted a triangle beyond a closer hit already found whenever its id
+    is smaller (round 4's second-triangle bound) keeps a farther one."""
+    import os
+    rng = np.random.default_rng(seed)
+    c = rng.uniform([-0.5, -0.5, -0.15], [0.5, 0.5, 0.15], size=(n, 3))
+    off = rng.normal(size=(n, 3, 3)) * np.array([0.08, 0.08, 0.02])
+    v = (c[:, None, :] + off).reshape(-1, 3)
+    with open(path, "w") as fh:
+        fh.write("mtllib soup.mtl\nusemtl None\n")
+        fh.writelines("v %.6f %.6f %.6f\n" % tuple(p) for p in v)
+        fh.writelines("f %d %d %d\n" % (3 * k + 1, 3 * k + 2, 3 * k + 3) for k in range(n))
+    with open(os.path.join(os.path.dirname(path), "soup.mtl"), "w") as fh:
+        fh.write("newmtl None\nKd 0.6 0.7 0.5\nd 1\n")

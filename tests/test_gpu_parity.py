@@ -250,6 +250,29 @@ def test_gpu_matches_golden_fixtures(rt, assets, name, pipeline):
 
 
 @pytest.mark.parametrize("pipeline", PIPELINES)
+def test_triangle_soup_closest_hit(rt, orc, assets, tmp_path, pipeline):
+    """Closest hit in a soup of overlapping triangles whose ids say nothing about their depth
+    (helpers.write_triangle_soup): the nearest triangle must win every primary and secondary hit,
+    as in the oracle's own traversal (t first, the id only on equal t)."""
+    from helpers import write_triangle_soup
+    write_triangle_soup(str(tmp_path / "soup.obj"))
+    scene = rt.Scene.preset("c1", assets)
+    scene.add_model(str(tmp_path / "soup.obj"), (0.0, 1.0, 0.0), scale=3.0)
+    R = make_renderer(rt, scene, 64, 48, pipeline, seed=3)
+    R.samplesPerPixel, R.maxBounces = 2, 3
+    u = R.draw()
+    R.wait()
+    g = R.radiance()
+    depth, _, _ = R.aux()
+    st = R.stats()
+    o = orc.OracleScene(scene.desc()).render(u, R.random)
+    rep = parity_report(g, o["radiance"])
+    assert rep["n_bad"] == 0, rep
+    assert np.array_equal(depth, o["depth"])
+    assert st.closest_rays == o["closest_rays"] and st.shadow_rays == o["shadow_rays"]
+
+
+@pytest.mark.parametrize("pipeline", PIPELINES)
 def test_emissive_parity(rt, orc, assets, tmp_path, pipeline):
     """An emissive untextured material (MTL Ke): the common shading kernels add color * emission
     to the path radiance (:585), the only place shade changes it, over several frames (EMA)."""
