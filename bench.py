@@ -47,6 +47,12 @@ HBM_PEAK_GBS = 8000.0
 # working set (48 MB for C3g) lives in L2 and the Infinity Cache (L2 hit 0.63), so its algorithmic
 # rate is also priced against this cache-gather ceiling.
 L2_GATHER_PEAK_GBS = 16800.0
+# Random 128-B line requests per second (tools/ubench/lane_loads, profiles/r04_gather_ceiling.txt):
+# ~255 G/s for lines that hit the XCD's L2, ~60 G/s for L2 misses (Infinity Cache or HBM); a lane's
+# loads inside one line cost one request.  `frac_of_line_ceiling` prices a kernel's L2 requests
+# (TCC_HIT + TCC_MISS per launch, PMC) against them: hits / 255 G + misses / 60 G per second.
+L2_HIT_LINES_PER_S = 255e9
+L2_MISS_LINES_PER_S = 60e9
 SCENES = {"c3g": "glass dragon scene (configs[2])", "c3": "glass dragon scene (configs[2])",
           "c3d": "opaque dragon scene", "c1": "AppScene base (configs[0])", "c2": "bunny scene (configs[1])",
           "c5": "skinned robot scene (configs[4])",
@@ -122,6 +128,8 @@ def read_pmc(paths):
         hit, miss = g.get("TCC_HIT_sum", [0.0, ()])[0], g.get("TCC_MISS_sum", [0.0, ()])[0]
         if hit + miss > 0:
             r["l2_hit"] = round(hit / (hit + miss), 4)
+            nd = max(len(g.get("TCC_HIT_sum", [0.0, ()])[1]), 1)
+            r["l2_hits_per_launch"], r["l2_misses_per_launch"] = int(hit / nd), int(miss / nd)
         out[key] = r
     return out
 
@@ -627,6 +635,9 @@ def roofline(alone, shared, pmc, pmc_err, ms_frame_alone, ms_per_step, pmc_csvs)
             "frac": round(hbm / HBM_PEAK_GBS, 4) if hbm else None, "l2_hit": p.get("l2_hit"),
             "algorithmic_bytes_per_launch": int(k["bytes_per_launch"]), "achieved_algorithmic_GBs": round(alg, 1),
             "frac_algorithmic": round(alg / HBM_PEAK_GBS, 4),
+            "frac_of_line_ceiling": round((p["l2_hits_per_launch"] / L2_HIT_LINES_PER_S +
+                                           p["l2_misses_per_launch"] / L2_MISS_LINES_PER_S) / (k["launch_ms"] * 1e-3), 4)
+            if "l2_hits_per_launch" in p else None,
             **{x: round(k[x], 3) for x in ("nodes_per_ray", "tris_per_ray") if x in k}})
     d = next(k for k in kernels if k["kernel"] == dom["kernel"])
     r = {
@@ -640,6 +651,7 @@ def roofline(alone, shared, pmc, pmc_err, ms_frame_alone, ms_per_step, pmc_csvs)
         "algorithmic_bytes_per_launch": d["algorithmic_bytes_per_launch"],
         "achieved_algorithmic": d["achieved_algorithmic_GBs"], "frac_algorithmic": d["frac_algorithmic"],
         "frac_of_l2_gather_peak": round(d["achieved_algorithmic_GBs"] / L2_GATHER_PEAK_GBS, 4),
+        "frac_of_line_ceiling": d["frac_of_line_ceiling"],
         "l2_hit": {k["kernel"]: k["l2_hit"] for k in kernels if k["l2_hit"] is not None} or None,
         # north star: the L2 hit rate of the shade kernel (it shades the hits of the rays as the
         # extend launch traced them), measured in this run
