@@ -960,7 +960,13 @@ private:
                     const int32_t ti = elem[me];
                     const uint32_t tok = (uint32_t)(ti < 0 ? -ti : ti);
                     if (tok >= tokens_.size()) return fail("bad path token");
-                    path = ti < 0 ? parent + "." + tokens_[tok] : (parent == "/" ? "/" : parent + "/") + tokens_[tok];
+                    // a variant selection element ("{set=variant}", SdfPath::AppendElementToken) follows
+                    // its prim directly: "/Model{shape=a}", whose children are "/Model{shape=a}/Child"
+                    // here (the .usda reader's detached variant bodies; SdfPath writes "...}Child")
+                    const std::string& e = tokens_[tok];
+                    path = ti < 0 ? parent + "." + e
+                                  : (!e.empty() && e[0] == '{' && parent != "/") ? parent + e
+                                  : (parent == "/" ? "/" : parent + "/") + e;
                 }
                 paths_[idx[me]] = path;
                 child = jump[me] > 0 || jump[me] == -1;
@@ -1224,6 +1230,22 @@ public:
             for (uint64_t i = 0; i < count; ++i) v.num.push_back(read_num(d_ + payload + 8 + 8 * i, 'd'));
             return true;
         }
+        case kVariantSelectionMap: {
+            // SdfVariantSelectionMap: uint64 count, then (set, variant) string indexes; kept as
+            // [set, variant, set, variant, ...]
+            uint64_t count;
+            if (!u64(payload, count)) return false;
+            if (!has_n(payload + 8, count, 8)) return fail("variant selection map past the end");
+            v.kind = Value::kStr;
+            v.array = true;
+            for (uint64_t i = 0; i < count; ++i) {
+                uint32_t a, b;
+                if (!u32(payload + 8 + 8 * i, a) || !u32(payload + 12 + 8 * i, b)) return false;
+                v.str.push_back(str(a));
+                v.str.push_back(str(b));
+            }
+            return true;
+        }
         case kSpecifier:
         case kVariability:
         case kPermission:
@@ -1277,12 +1299,33 @@ private:
     }
 
     bool build(Stage& st) {
-        enum { kSpecAttribute = 1, kSpecPrim = 6, kSpecPseudoRoot = 7, kSpecRelationship = 8 };
+        enum { kSpecAttribute = 1, kSpecPrim = 6, kSpecPseudoRoot = 7, kSpecRelationship = 8, kSpecVariant = 10,
+               kSpecVariantSet = 11 };
         std::map<int, std::vector<std::string>> child_order;
+        // Variant specs first: every "{set=variant}" element of a spec path names a variant body,
+        // kept as the detached prim "<owner>{set=variant}" in the owner's variant_bodies, as the
+        // .usda reader keeps `variantSet` blocks (outer bodies before the bodies nested in them);
+        // the prims, properties and arcs under it then land in the body, and load_stage applies
+        // the selected one.  "{set=}" is the variant set spec itself (nothing to keep).
         for (const Spec& sp : specs_) {
             if (sp.path >= paths_.size()) return fail("spec path index");
             const std::string& path = paths_[sp.path];
-            if (path.find('{') != std::string::npos) continue;   // variant specs
+            for (size_t j = path.find('}'); j != std::string::npos; j = path.find('}', j + 1)) {
+                const size_t i = path.rfind('{', j);
+                if (i == std::string::npos || i == 0) return fail("bad variant selection path");
+                const size_t eq = path.find('=', i);
+                if (eq == std::string::npos || eq > j || eq == i + 1) return fail("bad variant selection path");
+                if (eq + 1 == j) continue;   // "{set=}"
+                const std::string owner = path.substr(0, i);
+                if (owner == "/" || owner.find('.') != std::string::npos) return fail("bad variant selection path");
+                const int o = ensure_prim(st, owner);
+                const int body = st.add_detached(path.substr(0, j + 1));
+                st.prims[o].variant_bodies[path.substr(i + 1, eq - i - 1)].emplace(path.substr(eq + 1, j - eq - 1), body);
+            }
+        }
+        for (const Spec& sp : specs_) {
+            const std::string& path = paths_[sp.path];
+            if (sp.type == kSpecVariantSet) continue;
             std::vector<std::pair<std::string, uint64_t>> f;
             for (uint32_t k = sp.fset; k < fieldsets_.size() && fieldsets_[k] != 0xffffffffu; ++k) {
                 const uint32_t fi = fieldsets_[k];
@@ -1299,7 +1342,8 @@ private:
                     if (kv.first == "primChildren") child_order[0] = v.str;
                     if (kv.first == "subLayers" && v.kind == Value::kStr) st.sublayers = v.str;
                 }
-            } else if (sp.type == kSpecPrim) {
+            } else if (sp.type == kSpecPrim || sp.type == kSpecVariant) {   // a variant spec: its body
+                if (sp.type == kSpecPrim && !path.empty() && path.back() == '}') return fail("prim spec at a variant path");
                 const int id = ensure_prim(st, path);
                 for (auto& kv : f) {
                     Value v;
@@ -1309,6 +1353,8 @@ private:
                     else if (kv.first == "apiSchemas") p.api_schemas = v.str;
                     else if (kv.first == "active" && !v.num.empty()) p.active = v.num[0] != 0.0;
                     else if (kv.first == "primChildren") child_order[id] = v.str;
+                    else if (kv.first == "variantSelection" && v.kind == Value::kStr)
+                        for (size_t i = 0; i + 1 < v.str.size(); i += 2) p.variant_sel[v.str[i]] = v.str[i + 1];
                     else if ((kv.first == "references" || kv.first == "payload") && v.kind == Value::kStr)
                         for (size_t i = 0; i + 1 < v.str.size(); i += 2)
                             (kv.first == "references" ? p.references : p.payloads).push_back(Arc{v.str[i], v.str[i + 1]});

@@ -254,3 +254,70 @@ def test_reference_fan_out_is_bounded_by_bytes(rt, d):
     root = _write(d, "big_fan.usda", HEAD % "" + 'def Xform "F"\n{\n' + refs + "}\n")
     with pytest.raises(rt.RTError, match="larger than"):
         _scene(rt, root)
+
+
+def _box_prims(path, counts=(4,), idx=(0, 1, 2, 3)):
+    return [dict(path=path, type="Mesh", attrs=[
+        dict(name="faceVertexCounts", type="int[]", value=list(counts)),
+        dict(name="faceVertexIndices", type="int[]", value=list(idx)),
+        dict(name="points", type="point3f[]", value=[(0, 0, 0), (1, 0, 0), (1, 1, 0), (0, 1, 0)])])]
+
+
+def _lod_crate(sel=None, robot="./robot.usda"):
+    """/World with variant set "lod" authored in a crate layer: variant specs at
+    /World{lod=full|proxy|pair}, prims under them, the "{lod=}" set spec and a variantSelection"""
+    world = dict(path="/World", type="Xform", variant_sets={"lod": ["full", "proxy", "pair"]})
+    if sel:
+        world["variant_sel"] = {"lod": sel}
+    return ([world,
+             dict(path="/World{lod=full}"), dict(path="/World{lod=full}/Robot", type="SkelRoot",
+                                                 refs=[(robot, "")]),
+             dict(path="/World{lod=proxy}")] + _box_prims("/World{lod=proxy}/Box") +
+            [dict(path="/World{lod=pair}")] + _box_prims("/World{lod=pair}/Box") +
+            _box_prims("/World{lod=pair}/Box2", (3, 3), (0, 1, 2, 0, 2, 3)))
+
+
+@pytest.mark.parametrize("sel", ["full", "proxy", "pair", None])
+def test_crate_variant_specs(rt, d, sel):
+    # variant sets authored in a binary layer (variant specs at "/World{lod=...}" paths, the
+    # variantSelection map) compose like the same sets in text (test_variant_selection)
+    (d / ("lod_%s.usdc" % sel)).write_bytes(W.write_usdc(_lod_crate(sel)))
+    path = str(d / ("lod_%s.usdc" % sel))
+    if sel is None:
+        with pytest.raises(rt.RTError, match="no meshes"):
+            _scene(rt, path)
+        return
+    got = _scene(rt, path)
+    if sel == "full":
+        _same_scene(rt, _scene(rt, str(d / "robot.usda")), got)
+    else:
+        assert got.desc().mesh_count == (1 if sel == "proxy" else 2)
+        assert got.triangle_count == (2 if sel == "proxy" else 4)
+
+
+@pytest.mark.parametrize("sel", ["proxy", "pair"])
+def test_crate_variant_set_selected_by_a_text_layer(rt, d, sel):
+    # the set lives in a crate sublayer; the stronger text root only selects
+    (d / "lod_sub.usdc").write_bytes(W.write_usdc(_lod_crate()))
+    root = _write(d, "lod_croot_%s.usda" % sel, HEAD % "    subLayers = [@./lod_sub.usdc@]\n" +
+                  'over "World" (\n    variants = {\n        string lod = "%s"\n    }\n)\n{\n}\n' % sel)
+    got = _scene(rt, root)
+    assert got.desc().mesh_count == (1 if sel == "proxy" else 2)
+    # and a crate root layer's selection picks a variant set of a referenced text asset
+    _write(d, "lod_tasset.usda", HEAD % '    defaultPrim = "Asset"\n' +
+           'def Xform "Asset" (\n    prepend variantSets = "lod"\n)\n{\n' + LOD_SET + "}\n")
+    (d / ("lod_cref_%s.usdc" % sel)).write_bytes(W.write_usdc([
+        dict(path="/Model", type="Xform", refs=[("./lod_tasset.usda", "")], variant_sel={"lod": sel})]))
+    got = _scene(rt, str(d / ("lod_cref_%s.usdc" % sel)))
+    assert got.desc().mesh_count == (1 if sel == "proxy" else 2)
+    assert got.triangle_count == (2 if sel == "proxy" else 4)
+
+
+def test_crate_bad_variant_paths_fail_cleanly(rt, d):
+    # a variant selection on the pseudo-root, and a prim spec (not a variant spec) at a variant path
+    cases = {"root": _lod_crate("proxy") + [dict(path="/{lod=x}")],
+             "prim": [dict(p, kind=6) if p["path"] == "/World{lod=proxy}" else p for p in _lod_crate("proxy")]}
+    for name, prims in cases.items():
+        (d / ("lod_bad_%s.usdc" % name)).write_bytes(W.write_usdc(prims))
+        with pytest.raises(rt.RTError, match="variant"):
+            _scene(rt, str(d / ("lod_bad_%s.usdc" % name)))

@@ -176,6 +176,7 @@ T_VEC2F, T_VEC3F, T_VEC3H = 20, 24, 25
 T_TOKENLISTOP, T_PATHLISTOP, T_TOKENVECTOR = 32, 34, 41
 T_SPECIFIER, T_VARIABILITY, T_TIMESAMPLES, T_DOUBLEVECTOR = 42, 44, 46, 48
 T_REFERENCELISTOP, T_STRINGVECTOR = 35, 50
+T_STRINGLISTOP, T_VARIANTSELECTIONMAP = 33, 45
 ARRAY, INLINE, COMPRESSED = 1 << 63, 1 << 62, 1 << 61
 
 _TYPE_OF = {
@@ -220,12 +221,22 @@ class CrateWriter:
                 continue
             self.data += struct.pack("<Q", len(items))
             for asset, path in items:
-                self.data += struct.pack("<II", self.string(asset), path_idx[path]) + struct.pack("<dd", 0.0, 1.0)
+                # "" (the asset's default prim): an index past the path table reads as the empty path
+                self.data += struct.pack("<II", self.string(asset), path_idx[path] if path else 0xffffffff)
+                self.data += struct.pack("<dd", 0.0, 1.0)
                 self.data += struct.pack("<Q", 0)
         return self.rep(T_REFERENCELISTOP, off)
 
     def here(self):
         return len(self.data)
+
+    def variant_selection(self, sel):
+        """SdfVariantSelectionMap: count, then (set, variant) string indexes"""
+        off = self.here()
+        self.data += struct.pack("<Q", len(sel))
+        for k, v in sorted(sel.items()):
+            self.data += struct.pack("<II", self.string(k), self.string(v))
+        return self.rep(T_VARIANTSELECTIONMAP, off)
 
     def rep(self, t, payload, flags=0):
         return flags | (t << 48) | payload
@@ -341,11 +352,23 @@ class CrateWriter:
 
     # ---- layer ----------------------------------------------------------------------------------
     def write(self, prims, tcps=24.0, up_axis="Y", sublayers=None):
-        paths = ["/"]
+        """prims: dicts with "path" (a variant body is "<prim>{set=variant}", its children
+        "<prim>{set=variant}/Child"), "type", "attrs", "rels", "api", "refs", "variant_sel"
+        ({set: variant}) and "variant_sets" ({set: [variants]}: the "{set=}" variant set specs and
+        the prim's variantSetNames)"""
+        def split(path):   # (parent path, element token)
+            if path.endswith("}") and path.rfind("{") > path.rfind("/"):
+                return path[:path.rfind("{")], path[path.rfind("{"):]
+            return path.rsplit("/", 1)[0] or "/", path.rsplit("/", 1)[1]
+
+        prims = list(prims)
+        for p in list(prims):   # variant set specs "<prim>{set=}"
+            for vset, names in p.get("variant_sets", {}).items():
+                prims.append({"path": p["path"] + "{" + vset + "=}", "variant_children": names})
         kids = {"/": []}
         props = {}
         for p in prims:
-            parent = p["path"].rsplit("/", 1)[0] or "/"
+            parent = split(p["path"])[0]
             kids.setdefault(parent, []).append(p["path"])
             kids.setdefault(p["path"], [])
             props[p["path"]] = [a["name"] for a in p.get("attrs", [])] + list(p.get("rels", {}))
@@ -354,7 +377,7 @@ class CrateWriter:
         order = []   # (path, element token, is_property, has_child, sibling_path)
 
         def visit(path, sib):
-            name = path.rsplit("/", 1)[1] if path != "/" else ""
+            name = split(path)[1] if path != "/" else ""
             entries = [(path + "." + pr, pr) for pr in props.get(path, [])] + [(c, None) for c in kids.get(path, [])]
             order.append([path, name, False, bool(entries), sib])
             for k, (pp, pr) in enumerate(entries):
@@ -386,11 +409,20 @@ class CrateWriter:
                    field("timeCodesPerSecond", self.scalar(T_DOUBLE, tcps))] +
              ([field("subLayers", self.string_vector(sublayers))] if sublayers else []), 7)
         for p in prims:
+            if "variant_children" in p:   # a variant set spec
+                spec(p["path"], [field("variantChildren", self.token_vector(p["variant_children"]))], 11)
+                continue
             fl = [field("specifier", self.rep(T_SPECIFIER, 0, INLINE))]
             if p.get("type"):
                 fl.append(field("typeName", self.rep(T_TOKEN, self.tok(p["type"]), INLINE)))
-            if kids[p["path"]]:
-                fl.append(field("primChildren", self.token_vector([c.rsplit("/", 1)[1] for c in kids[p["path"]]])))
+            real = [split(c)[1] for c in kids[p["path"]] if not split(c)[1].startswith("{")]
+            if real:
+                fl.append(field("primChildren", self.token_vector(real)))
+            if p.get("variant_sets"):
+                fl.append(field("variantSetNames", self.list_op(T_STRINGLISTOP,
+                                                                [self.string(x) for x in p["variant_sets"]])))
+            if p.get("variant_sel"):
+                fl.append(field("variantSelection", self.variant_selection(p["variant_sel"])))
             if props[p["path"]]:
                 fl.append(field("properties", self.token_vector(props[p["path"]])))
             if p.get("api"):
@@ -398,7 +430,7 @@ class CrateWriter:
             if p.get("refs") or p.get("refs_appended"):   # [(asset, target prim path in this layer's path table)]
                 fl.append(field("references", self.reference_list_op(p.get("refs") or [], path_idx,
                                                                      p.get("refs_appended") or [])))
-            spec(p["path"], fl, 6)
+            spec(p["path"], fl, p.get("kind", 10 if p["path"].endswith("}") else 6))
             for a in p.get("attrs", []):
                 fl = [field("typeName", self.rep(T_TOKEN, self.tok(a["type"]), INLINE))]
                 if a.get("uniform"):

@@ -10,7 +10,11 @@ from test_usd import TEX, robot_prims  # noqa: E402
 out = sys.argv[1]
 os.makedirs(out, exist_ok=True)
 prims, _ = robot_prims()
-crate = W.write_usdc(prims + [dict(path="/Copy", type="Xform", refs=[("", "/Robot/Prop")])])   # + an internal reference
+# + an internal reference, and a variant set whose selected variant spec references it again
+crate = W.write_usdc(prims + [dict(path="/Copy", type="Xform", refs=[("", "/Robot/Prop")]),
+                              dict(path="/Var", type="Xform", variant_sets={"v": ["a", "b"]}, variant_sel={"v": "b"}),
+                              dict(path="/Var{v=a}"), dict(path="/Var{v=b}"),
+                              dict(path="/Var{v=b}/Again", type="Xform", refs=[("", "/Robot/Prop")])])
 files = {
     # + composition: an internal reference and a variant set whose selected body references it again
     "seed.usda": W.write_usda(prims) + b"""
