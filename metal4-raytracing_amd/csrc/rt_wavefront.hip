@@ -1225,9 +1225,25 @@ wf_finish_step(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int c
         auto mvf = [&](float v) { return __shfl(v, src); };
         auto mv3 = [&](f3 v) { return mk3(mvf(v.x), mvf(v.y), mvf(v.z)); };
         const uint32_t sbase = threadIdx.x & ~63u;
-        f3 so = mk3(lds_sray[0][sbase + src], lds_sray[1][sbase + src], lds_sray[2][sbase + src]);
-        f3 sd = mk3(lds_sray[3][sbase + src], lds_sray[4][sbase + src], lds_sray[5][sbase + src]);
-        float stm = mvf(T.best);
+        // the leaders' shadow rays stay in LDS (each leader's slot; the members read it when the
+        // team starts the query): six registers fewer across the shading code
+        {
+            float sr[6];
+            #pragma unroll
+            for (int c = 0; c < 6; ++c) sr[c] = lds_sray[c][sbase + src];
+            #pragma unroll
+            for (int c = 0; c < 6; ++c) lds_sray[c][threadIdx.x] = sr[c];
+        }
+        // the leaders' shadow tmax and contribution stay in LDS as well (lds_tx)
+        __shared__ float lds_tx[4][kBlock];
+        {
+            const float t_src = mvf(T.best);
+            const f3 c_src = mv3(contrib);
+            lds_tx[0][threadIdx.x] = t_src;
+            lds_tx[1][threadIdx.x] = c_src.x;
+            lds_tx[2][threadIdx.x] = c_src.y;
+            lds_tx[3][threadIdx.x] = c_src.z;
+        }
         pid = mvu(pid);
         meta = make_uint4(mvu(meta.x), mvu(meta.y), mvu(meta.z), mvu(meta.w));
         p.color = mv3(p.color);
@@ -1237,7 +1253,6 @@ wf_finish_step(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int c
         p.tpass = (int)mvu((uint32_t)p.tpass);
         rayO = mv3(rayO);
         rayD = mv3(rayD);
-        contrib = mv3(contrib);
         next = mvu(next ? 1u : 0u) != 0u;
         segs = mvu(segs);
         // every lane takes part in the shuffle: a bpermute inside the leaders' branch would read the
@@ -1254,9 +1269,10 @@ wf_finish_step(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int c
                 f3 o, d;
                 float tmax;
                 if (any) {
-                    o = mk3(__shfl(so.x, lead), __shfl(so.y, lead), __shfl(so.z, lead));
-                    d = mk3(__shfl(sd.x, lead), __shfl(sd.y, lead), __shfl(sd.z, lead));
-                    tmax = __shfl(stm, lead);
+                    const uint32_t ls = sbase + (uint32_t)lead;
+                    o = mk3(lds_sray[0][ls], lds_sray[1][ls], lds_sray[2][ls]);
+                    d = mk3(lds_sray[3][ls], lds_sray[4][ls], lds_sray[5][ls]);
+                    tmax = lds_tx[0][ls];
                 } else {
                     o = mk3(__shfl(rayO.x, lead), __shfl(rayO.y, lead), __shfl(rayO.z, lead));
                     d = mk3(__shfl(rayD.x, lead), __shfl(rayD.y, lead), __shfl(rayD.z, lead));
@@ -1339,7 +1355,8 @@ wf_finish_step(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int c
                 }
                 if (j == 0) {   // the leader: the path's next step (as in the loop above)
                     if (any) {
-                        if (!hit) p.accum = p.accum + contrib;
+                        if (!hit)
+                            p.accum = p.accum + mk3(lds_tx[1][threadIdx.x], lds_tx[2][threadIdx.x], lds_tx[3][threadIdx.x]);
                         if (next) {
                             mode = kClosest;
                             n_closest++;
@@ -1359,10 +1376,16 @@ wf_finish_step(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int c
                 StepResult r;
                 shade_hit(r);
                 if (r.shadow) {
-                    contrib = r.contrib;
-                    so = r.so;
-                    sd = r.sd;
-                    stm = r.stmax;
+                    lds_tx[1][threadIdx.x] = r.contrib.x;
+                    lds_tx[2][threadIdx.x] = r.contrib.y;
+                    lds_tx[3][threadIdx.x] = r.contrib.z;
+                    lds_sray[0][threadIdx.x] = r.so.x;
+                    lds_sray[1][threadIdx.x] = r.so.y;
+                    lds_sray[2][threadIdx.x] = r.so.z;
+                    lds_sray[3][threadIdx.x] = r.sd.x;
+                    lds_sray[4][threadIdx.x] = r.sd.y;
+                    lds_sray[5][threadIdx.x] = r.sd.z;
+                    lds_tx[0][threadIdx.x] = r.stmax;
                     mode = kShadow;
                     n_shadow++;
                     fresh = true;
