@@ -609,6 +609,17 @@ __global__ void __launch_bounds__(kBlock) wf_generate(DevScene S, const FramePar
 // blocks of XCD k (blockIdx % 8) shade the k-th eighth of it, so one XCD's L2 serves one scene
 // region and the rays / shadow rays it appends to its queue shard stay grouped by region for
 // the next extend / connect launches (which hand shard k's range to XCD k).
+#ifndef RT_SHADE_NT
+#define RT_SHADE_NT 1   // wf_shade streams its queue entries with nontemporal loads (0: plain loads; A/B builds)
+#endif
+__device__ __forceinline__ float4 ld_stream(const float4* p) {
+    if (RT_SHADE_NT) {
+        typedef float v4f __attribute__((ext_vector_type(4)));
+        const v4f v = __builtin_nontemporal_load(reinterpret_cast<const v4f*>(p));
+        return make_float4(v.x, v.y, v.z, v.w);
+    }
+    return *p;
+}
 template <bool FULL, bool SORTED>
 __global__ void __launch_bounds__(kBlock) wf_shade(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int cur) {
     const FrameParams& P = *Pp;   // per-frame parameters in device memory
@@ -664,9 +675,9 @@ __global__ void __launch_bounds__(kBlock) wf_shade(DevScene S, const FrameParams
                 ce = 4 * (size_t)g + 3;
             } else {
                 const uint32_t e = ebase + seg_pos(g, lk, Q.seg_cap);
-                o = qin[2 * (size_t)e];
-                d = qin[2 * (size_t)e + 1];
-                hv = Q.W.hits[e];
+                o = ld_stream(&qin[2 * (size_t)e]);
+                d = ld_stream(&qin[2 * (size_t)e + 1]);
+                hv = ld_stream(&Q.W.hits[e]);
                 ce = e;
             }
             pid = __float_as_uint(o.w);
@@ -680,7 +691,7 @@ __global__ void __launch_bounds__(kBlock) wf_shade(DevScene S, const FrameParams
                 const uint3 pm = path_meta(P, Q, pid);
                 const uint4 meta = make_uint4(pm.x, pm.y, state, pm.z);
                 const float4 c = state == 0u ? make_float4(1.0f, 1.0f, 1.0f, 0.0f)
-                                             : (SORTED ? Q.W.sorted[ce] : Q.W.qc[cur][ce]);
+                                             : (SORTED ? Q.W.sorted[ce] : ld_stream(&Q.W.qc[cur][ce]));
                 // FULL=false: shade_step only adds color * emission to accum (:585), so it runs on a
                 // zero accumulator and the stored one is read and updated only when that term is
                 // non-zero (accum is never -0, so a + (0 + x) == a + x bit for bit); FULL (debug
