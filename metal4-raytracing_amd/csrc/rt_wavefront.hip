@@ -612,14 +612,17 @@ __global__ void __launch_bounds__(kBlock) wf_generate(DevScene S, const FramePar
 #ifndef RT_SHADE_NT
 #define RT_SHADE_NT 1   // wf_shade streams its queue entries with nontemporal loads (0: plain loads; A/B builds)
 #endif
+#ifndef RT_TRACE_NT
+#define RT_TRACE_NT 2   // bit 0: wf_trace (extend), bit 1: the finish refill read their queue entries nontemporally
+                        // (the extend entries are read again by wf_shade: bit 0 slows it)
+#endif
+// a 16-B load of data read once (nontemporal: it does not displace the lines gathered beside it)
 __device__ __forceinline__ float4 ld_stream(const float4* p) {
-    if (RT_SHADE_NT) {
-        typedef float v4f __attribute__((ext_vector_type(4)));
-        const v4f v = __builtin_nontemporal_load(reinterpret_cast<const v4f*>(p));
-        return make_float4(v.x, v.y, v.z, v.w);
-    }
-    return *p;
+    typedef float v4f __attribute__((ext_vector_type(4)));
+    const v4f v = __builtin_nontemporal_load(reinterpret_cast<const v4f*>(p));
+    return make_float4(v.x, v.y, v.z, v.w);
 }
+__device__ __forceinline__ float4 ld_shade(const float4* p) { return RT_SHADE_NT ? ld_stream(p) : *p; }
 template <bool FULL, bool SORTED>
 __global__ void __launch_bounds__(kBlock) wf_shade(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int cur) {
     const FrameParams& P = *Pp;   // per-frame parameters in device memory
@@ -675,9 +678,9 @@ __global__ void __launch_bounds__(kBlock) wf_shade(DevScene S, const FrameParams
                 ce = 4 * (size_t)g + 3;
             } else {
                 const uint32_t e = ebase + seg_pos(g, lk, Q.seg_cap);
-                o = ld_stream(&qin[2 * (size_t)e]);
-                d = ld_stream(&qin[2 * (size_t)e + 1]);
-                hv = ld_stream(&Q.W.hits[e]);
+                o = ld_shade(&qin[2 * (size_t)e]);
+                d = ld_shade(&qin[2 * (size_t)e + 1]);
+                hv = ld_shade(&Q.W.hits[e]);
                 ce = e;
             }
             pid = __float_as_uint(o.w);
@@ -691,7 +694,7 @@ __global__ void __launch_bounds__(kBlock) wf_shade(DevScene S, const FrameParams
                 const uint3 pm = path_meta(P, Q, pid);
                 const uint4 meta = make_uint4(pm.x, pm.y, state, pm.z);
                 const float4 c = state == 0u ? make_float4(1.0f, 1.0f, 1.0f, 0.0f)
-                                             : (SORTED ? Q.W.sorted[ce] : ld_stream(&Q.W.qc[cur][ce]));
+                                             : (SORTED ? Q.W.sorted[ce] : ld_shade(&Q.W.qc[cur][ce]));
                 // FULL=false: shade_step only adds color * emission to accum (:585), so it runs on a
                 // zero accumulator and the stored one is read and updated only when that term is
                 // non-zero (accum is never -0, so a + (0 + x) == a + x bit for bit); FULL (debug
@@ -944,7 +947,11 @@ wf_trace(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int cur, in
                 uint32_t g = wnext + mbcnt64(idle);
                 if (g < wend) {
                     e = ebase + (ANY ? g : seg_pos(g, xl, Q.seg_cap));
-                    float4 o4 = qin[(size_t)qstride * e], d4 = qin[(size_t)qstride * e + 1];
+                    // an extend entry is read once here (nontemporal: RT_TRACE_NT); a shadow entry
+                    // again when its ray is unoccluded
+                    const bool nt = !ANY && (RT_TRACE_NT & 1);
+                    float4 o4 = nt ? ld_stream(&qin[(size_t)qstride * e]) : qin[(size_t)qstride * e];
+                    float4 d4 = nt ? ld_stream(&qin[(size_t)qstride * e + 1]) : qin[(size_t)qstride * e + 1];
                     trav_start(T, ld3(o4), ld3(d4), ANY ? d4.w : INFINITY);
                     active = true;
                     rays++;
@@ -1093,12 +1100,14 @@ wf_finish_step(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int c
                 if (g < wend) {
                     const uint32_t e = dense_entry(qs, g, Q.seg_cap);
                     const float4* src = qin + 2 * (size_t)e;
-                    const float4 o = src[0], d = src[1];
+                    const float4 o = (RT_TRACE_NT & 2) ? ld_stream(&src[0]) : src[0];
+                    const float4 d = (RT_TRACE_NT & 2) ? ld_stream(&src[1]) : src[1];
                     pid = __float_as_uint(o.w);
                     const uint32_t state = __float_as_uint(d.w);
                     const uint3 pm = path_meta(P, Q, pid);
                     meta = make_uint4(pm.x, pm.y, state, pm.z);
-                    const float4 c = state == 0u ? make_float4(1.0f, 1.0f, 1.0f, 0.0f) : Q.W.qc[cur][e];
+                    const float4 c = state == 0u ? make_float4(1.0f, 1.0f, 1.0f, 0.0f)
+                                     : (RT_TRACE_NT & 2) ? ld_stream(&Q.W.qc[cur][e]) : Q.W.qc[cur][e];
                     const float4 a = Q.W.p_accum[pid];
                     p.color = mk3(c.x, c.y, c.z);
                     p.accum = mk3(a.x, a.y, a.z);
