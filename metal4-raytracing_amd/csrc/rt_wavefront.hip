@@ -32,8 +32,10 @@ namespace rt {
 
 namespace {
 
-// frames of at most this many base paths use the finish kernel's team drain by default (RT_TEAM)
+// frames of kTeamAutoMin .. kTeamAutoPaths base paths use the finish kernel's team drain by default
+// (RT_TEAM): the C3g rank shares gain, the tiny C1 frame (65K paths) loses 7.5 %
 constexpr uint32_t kTeamAutoPaths = 2500000u;
+constexpr uint32_t kTeamAutoMin = 262144u;
 
 static int env_int(const char* name, int dflt) {
     const char* e = getenv(name);
@@ -50,7 +52,7 @@ struct Tuning {
     int shade_min;     // RT_SHADE_MIN: the finish kernel shades once this many lanes wait
     int shade_min_x;   // RT_SHADE_MIN_X: the same once the finish queue is exhausted (< 0: that percentage of the wave's busy lanes)
     int team;          // RT_TEAM: finish drain, lanes per query once a wave holds <= 64 / team paths (0 / 1: off;
-                       // unset: 4 for frames of at most kTeamAutoPaths paths, off above)
+                       // unset: 4 for frames of kTeamAutoMin .. kTeamAutoPaths paths, off otherwise)
     int finish_frac;   // RT_FINISH_FRAC: percent of the resident grid the finish launch takes (0 = by frames in flight)
     int trace_frac;    // RT_TRACE_FRAC: percent of the resident grid the persistent wf_trace launches take (0 = by frames in flight)
     int log;           // RT_WF_LOG=1: per-round queue sizes, stage times and finish diagnostics on stderr
@@ -2076,9 +2078,9 @@ bool run_wavefront(const DevScene& S, const FrameParams& P, WavefrontBuffers& W,
     Q.shade_min = tu.shade_min;
     Q.shade_min_x = tu.shade_min_x;
     // the team drain pays where the drain is a large part of the finish: small frames (C3g rank
-    // shares, DESIGN.md §3.3: 8-way +1.5-1.8 %, 4-way +1.5-2.9 %, 2-way ±1 %, the whole 1080p frame
-    // four in flight -0.5 %)
-    Q.team = tu.team >= 0 ? tu.team : (Q.base_paths <= kTeamAutoPaths ? 4 : 0);
+    // shares, DESIGN.md §3.3: 8-way +2.3 %, 4-way +1.5 %, 2-way ±1 %, the whole 1080p frame four in
+    // flight ±0), but not the smallest (C1 256x256x1: -7.5 %)
+    Q.team = tu.team >= 0 ? tu.team : (Q.base_paths >= kTeamAutoMin && Q.base_paths <= kTeamAutoPaths ? 4 : 0);
     Q.fchunk = tu.fchunk;
     Q.spans = spans ? 1 : 0;
     Q.spp_div = make_fastdiv((uint32_t)Q.spp);

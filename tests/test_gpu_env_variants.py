@@ -3,8 +3,7 @@ child process): host-driven rounds (RT_WF_HOST=1: queue sizes read back every ro
 the device-side round control), eager enqueue without frame graphs (RT_GRAPH=0), and the finish
 kernel's scheduling knobs at other values (odd chunk sizes, an absolute shading threshold after the
 queue runs out, the long-first order's chunks split over few blocks, the finish drain's team
-sizes: 2 and 8 lanes, and off, which these small frames would otherwise
-use with 4 lanes), against the committed golden fixtures (bit-identical radiance, depth and ray counts).  The bulk pipelines run
+sizes: 2, 4 and 8 lanes, and off, which these small frames (< 256K paths) use by default), against the committed golden fixtures (bit-identical radiance, depth and ray counts).  The bulk pipelines run
 wf_shade every bounce (the small fixture frames would otherwise go straight to the finish kernel)."""
 import os
 import subprocess
@@ -22,8 +21,8 @@ PIPES = "wavefront,wavefront-bulk,wavefront-mixed"
 @pytest.mark.parametrize("env", [{"RT_WF_HOST": "1"}, {"RT_GRAPH": "0"},
                                  {"RT_FCHUNK": "7", "RT_SHADE_MIN_X": "24", "RT_FINISH_FRAC": "1"},
                                  {"RT_FCHUNK": "1", "RT_SHADE_MIN_X": "-100", "RT_SHADE_MIN": "1"},
-                                 {"RT_TEAM": "2"}, {"RT_TEAM": "8", "RT_FCHUNK": "3"}, {"RT_TEAM": "0"}],
-                         ids=["hostrounds", "nograph", "finish_chunk7", "finish_chunk1", "team2", "team8", "noteam"])
+                                 {"RT_TEAM": "2"}, {"RT_TEAM": "4"}, {"RT_TEAM": "8", "RT_FCHUNK": "3"}, {"RT_TEAM": "0"}],
+                         ids=["hostrounds", "nograph", "finish_chunk7", "finish_chunk1", "team2", "team4", "team8", "noteam"])
 def test_env_variant_matches_golden(env):
     e = dict(os.environ)
     e.update(env)

@@ -124,6 +124,27 @@ def test_configs3_rank_share(rt, orc, assets, rank):
     assert np.array_equal(canvas[own][:, :3], o["radiance"][own][:, :3])
 
 
+@pytest.mark.parametrize("rank", [0, 5])
+def test_configs2_rank_share_team_drain(rt, orc, assets, rank):
+    """configs[2] split 8 ways (the per-GPU frame of bench.py --gpus 8): rank r's 1.04M paths take
+    the finish kernel's team drain by default (frames of 256K .. 2.5M paths).  Two
+    frames back to back (frame 1 = EMA over frame 0), every pixel of the share and its ray counts."""
+    W, H, T, N = 1920, 1080, 64, 8
+    scene = rt.Scene.preset("c3g", assets)
+    R = make_renderer(rt, scene, W, H, "wavefront", seed=6)
+    R.samplesPerPixel, R.maxBounces = 4, 8
+    us = [R.draw(tiles=(T, rank, N)) for _ in range(2)]
+    key = ("c3g", W, H, 4, 8, T, rank, N)
+    o = _oracle_frames(orc, scene, key, us, R.random, tiles=(T, rank, N))[1]
+    _ORACLE.pop(key)
+    tx = (W + T - 1) // T
+    yy, xx = np.mgrid[0:H, 0:W]
+    own = ((yy // T) * tx + xx // T) % N == rank
+    assert 256 * 1024 <= R.tile_count(T, rank, N) * T * T * 4 <= 2500000   # the team drain's range
+    assert R.stats().frames_total == 2
+    _check(R, o, mask=own)
+
+
 def _f4(ptr, n):
     return np.ctypeslib.as_array(C.cast(ptr, C.POINTER(C.c_float)), shape=(n, 4))
 
