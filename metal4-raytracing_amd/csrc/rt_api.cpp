@@ -39,6 +39,7 @@ struct MeshInfo {
 struct FrameSlot {
     DevBuf qc, accum, meta, q0, q1, hits, sq, counts, extra, sorted, sort_table, sort_total, params;
     DevBuf depth, gbuffer, counters;
+    DevBuf fpool;      // the pooled finish kernel's path records (wavefront_pool_bytes)
     DevBuf prim_hit;   // wavefront: per pixel, sample 0's last bounce-0 hit (id, u, v) for wf_motion
     WavefrontBuffers wf;
     WfTimeline wft;
@@ -50,8 +51,8 @@ struct FrameSlot {
     bool gbuf_written = false;                  // the slot's last frame wrote the G-buffer (enableDenoiseGBuffer)
     uint64_t seq = 0;                           // frame number (harvest order)
     int gen = 0;                                // geometry generation the frame reads
-    DevBuf* bufs[17] = {&qc, &accum, &meta, &q0, &q1, &hits, &sq, &counts, &extra, &sorted,
-                        &sort_table, &sort_total, &params, &depth, &gbuffer, &counters, &prim_hit};
+    DevBuf* bufs[18] = {&qc, &accum, &meta, &q0, &q1, &hits, &sq, &counts, &extra, &sorted,
+                        &sort_table, &sort_total, &params, &depth, &gbuffer, &counters, &prim_hit, &fpool};
 };
 // Per-frame geometry (what skinning, instance transforms and refit rewrite between frames), in
 // generations used round robin: frames read generation `gcur`; the first update after a frame
@@ -305,6 +306,7 @@ static rt_status ensure_wavefront(rt_ctx* c, FrameSlot& fs, size_t own_px, int s
         if ((st = dev_alloc(c, fs.extra, px * 8))) return st;
         W.cap_pixels = px;
     }
+    if (!fs.fpool.p && (st = dev_alloc(c, fs.fpool, wavefront_pool_bytes()))) return st;
     if (c->sort_bins && !fs.sort_table.p) {
         if ((st = dev_alloc(c, fs.sort_table, (size_t)kSortMaxBins * kSortBlocks * 4))) return st;
         if ((st = dev_alloc(c, fs.sort_total, (size_t)kSortMaxBins * 4))) return st;
@@ -334,6 +336,7 @@ static rt_status ensure_wavefront(rt_ctx* c, FrameSlot& fs, size_t own_px, int s
     W.sorted = (float4*)fs.sorted.p;
     W.sort_table = (uint32_t*)fs.sort_table.p;
     W.sort_total = (uint32_t*)fs.sort_total.p;
+    W.fpool = (float4*)fs.fpool.p;
     return RT_OK;
 }
 

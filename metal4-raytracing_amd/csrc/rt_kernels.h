@@ -125,6 +125,9 @@ struct WavefrontBuffers {
     float4* sorted = nullptr;
     uint32_t* sort_table = nullptr;
     uint32_t* sort_total = nullptr;
+    // pooled finish kernel (wf_finish_pool): kPoolRecs path records of 128 B per wave of its
+    // resident grid (wavefront_pool_bytes)
+    float4* fpool = nullptr;
     size_t cap_paths = 0;         // base + extra paths
     size_t cap_pixels = 0;
     hipEvent_t ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
@@ -204,6 +207,8 @@ bool run_wavefront(const DevScene& S, const FrameParams& P, WavefrontBuffers& W,
                    hipEvent_t prev_done, WfTimeline* tl, WfFrameStats* fs, const char** err, bool graphs = true);
 bool wavefront_collect(const WavefrontBuffers& W, WfTimeline& T, WfFrameStats* fs, const char** err);
 size_t wavefront_queue_entries(size_t paths, int max_extra);
+// bytes of WavefrontBuffers::fpool: the pooled finish kernel's path records for its resident grid
+size_t wavefront_pool_bytes();
 
 // Packed-tile layout of the multi-GPU gather: element i of a rank's packed buffer is pixel
 // (i % T, (i / T) % T) of its (i / T^2)-th own tile; own tile k is tile id rank + k * nranks.

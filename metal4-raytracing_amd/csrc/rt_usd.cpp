@@ -1562,6 +1562,15 @@ private:
         for (const std::string& s : a.connections) b += s.size() + 32;
         return b;
     }
+    // what a copy of a whole stage copies (an internal arc's snapshot of its layer)
+    static uint64_t stage_bytes(const Stage& L) {
+        uint64_t b = 0;
+        for (const Prim& pr : L.prims) {
+            b += 256;
+            for (const auto& kv : pr.attrs) b += attr_bytes(kv.second);
+        }
+        return b;
+    }
     // an asset path relative to the layer naming it (inside the package for a .usdz)
     std::string resolve(const std::string& from, const std::string& asset) const {
         if (!asset.empty() && asset[0] == '/') return normalize(pkg_ ? asset.substr(1) : asset);
@@ -1700,8 +1709,13 @@ private:
                 if (!spend(1 + (a.asset.empty() ? L.prims.size() : 0))) return false;
                 std::shared_ptr<const Stage> S;
                 const bool internal = a.asset.empty() || (a.resolved && a.asset == id);
-                if (internal) S = std::make_shared<const Stage>(L);   // this layer's namespace as it stands
-                else if (!(S = load(a.resolved ? a.asset : resolve(id, a.asset), depth + 1))) return false;
+                // an internal arc reads this layer's namespace as it stands: a snapshot, whose copy
+                // is charged against the byte budget like a merge (thousands of internal arcs next to
+                // one large array must fail fast, not copy the layer thousands of times)
+                if (internal) {
+                    if (!spend_bytes(stage_bytes(L))) return false;
+                    S = std::make_shared<const Stage>(L);
+                } else if (!(S = load(a.resolved ? a.asset : resolve(id, a.asset), depth + 1))) return false;
                 const int t = target(*S, a);
                 if (t <= 0) return fail("reference target " + (a.path.empty() ? "(default prim)" : a.path) + " not found in " +
                                         (internal ? id : a.asset));

@@ -24,6 +24,7 @@
 // contribution, then step s+1), and samples are summed per pixel in sample order.
 #include "rt_shade.h"
 
+#include <atomic>
 #include <cstdio>
 #include <cstring>
 #include <vector>
@@ -58,6 +59,7 @@ struct Tuning {
     int log;           // RT_WF_LOG=1: per-round queue sizes, stage times and finish diagnostics on stderr
                        // (=2 also the finish paths' segment counts: one atomic per path, slows the launch)
     bool host_ctl;     // RT_WF_HOST=1: host-driven rounds (queue sizes read back every round)
+    int pool;          // RT_FINISH_POOL: 1 = the pooled finish kernel (wf_finish_pool), 0 = wf_finish_step
     unsigned shade_blocks;   // RT_SHADE_BLOCKS: wf_shade grid (grid-stride loop), a multiple of 8; 2048 (1.6 waves
                              // of the resident grid) leaves CUs to the other frames in flight: C3g four in
                              // flight +1.3-2.2 % against 8192, one frame alone the same
@@ -78,6 +80,7 @@ static const Tuning& tuning() {
         v.log = env_int("RT_WF_LOG", 0);
         v.host_ctl = env_int("RT_WF_HOST", 0) != 0;
         v.shade_blocks = (unsigned)std::max(8, env_int("RT_SHADE_BLOCKS", 2048)) / 8u * 8u;
+        v.pool = env_int("RT_FINISH_POOL", 0);
         return v;
     }();
     return t;
@@ -232,6 +235,7 @@ struct WfParams {
     int shade_min_x;       // wf_finish_step: the same once the launch's queue is exhausted (< 0: percent of busy lanes)
     int team;              // wf_finish_step: lanes per query in the drain (0: no team drain)
     int fchunk;            // wf_finish_step: paths per chunk grab
+    int pool;              // the finish launch runs wf_finish_pool (paths in per-wave record pools)
     int finish_frac;       // percent of the resident grid the finish launch takes
     int trace_frac;        // percent of the resident grid the bulk wf_trace launches take
     int spans;             // record device-clock launch spans (rt_set_device_spans)
@@ -415,7 +419,15 @@ struct Trav {
     uint32_t best_id, g_base, g_hits, t_base, t_mask, t_valid;
     bool g_flip, hit_any;
     int sp;
+#ifdef RT_XP_DUP
+    uint32_t xp;   // cost-attribution experiment: sink of the duplicated tests
+#endif
 };
+#ifdef RT_XP_DUP
+#define RT_XP_SINK(T, dst) do { if ((T).xp == 0x9e3779b9u) (dst) = 1u; } while (0)
+#else
+#define RT_XP_SINK(T, dst) do { } while (0)
+#endif
 
 __device__ __forceinline__ void trav_start(Trav& T, f3 o, f3 d, float tmax) {
     T.R = ray_setup(o, d);
@@ -429,6 +441,9 @@ __device__ __forceinline__ void trav_start(Trav& T, f3 o, f3 d, float tmax) {
     T.t_mask = 0;
     T.sp = 0;
     T.hit_any = false;
+#ifdef RT_XP_DUP
+    T.xp = 0;
+#endif
 }
 
 // One iteration of a query: up to two triangles of the last node test (both fetched before either
@@ -476,13 +491,29 @@ __device__ __forceinline__ bool trav_step(const DevScene& S, Trav& T, bool any, 
         if (two) T.t_mask &= T.t_mask - 1u;
         // the bound is re-read for every test: a triangle must not be accepted beyond a closer hit
         // found earlier in this step (the update below assumes t <= T.best)
+#ifdef RT_XP_STALE_BOUND
+        // round 3's bug, kept as a build-time switch to show the parity tests catch it
+        // (tests/test_gpu_traversal_variants.py): both triangles against the bound from before the step
+        const float stale_bound = fminf(cull, T.best);
+#define RT_ISECT(v0, v1, v2) intersect_triangle_vw(T.R.pre, T.R.o, v0, v1, v2, 0.0f, stale_bound, &t, &u, &v, &dt)
+#else
 #define RT_ISECT(v0, v1, v2) intersect_triangle_vw(T.R.pre, T.R.o, v0, v1, v2, 0.0f, fminf(cull, T.best), &t, &u, &v, &dt)
+#endif
         const float4* tp0 = S.tris + 3 * (size_t)tri_slot(T.t_base, T.t_valid, k0);
         const float4* tp1 = S.tris + 3 * (size_t)tri_slot(T.t_base, T.t_valid, k1);
         const float4 a0 = tp0[0], a1 = tp0[1], a2 = tp0[2];
         const float4 b0 = tp1[0], b1 = tp1[1], b2 = tp1[2];   // = a when the lane has one triangle
         if (COUNT) tc.tris += two ? 2u : 1u;
         float t, u, v, dt;
+#if defined(RT_XP_DUP) && (RT_XP_DUP & 2)
+        {   // the first triangle's test once more on an opaque copy (its cost, not its result)
+            float4 c0 = a0, c1 = a1, c2 = a2;
+            asm volatile("" : "+v"(c0.x), "+v"(c0.y), "+v"(c0.z), "+v"(c1.x), "+v"(c1.y), "+v"(c1.z), "+v"(c2.x), "+v"(c2.y), "+v"(c2.z));
+            float t2 = 0, u2 = 0, v2 = 0, d2 = 0;
+            const bool h2 = intersect_triangle_vw(T.R.pre, T.R.o, ld3(c0), ld3(c1), ld3(c2), 0.0f, fminf(cull, T.best), &t2, &u2, &v2, &d2);
+            T.xp ^= h2 ? __float_as_uint(t2) ^ __float_as_uint(u2) : 1u;
+        }
+#endif
         if (RT_ISECT(ld3(a0), ld3(a1), ld3(a2))) {
             const uint32_t id = __float_as_uint(a0.w);
             if (any) {
@@ -514,6 +545,18 @@ __device__ __forceinline__ bool trav_step(const DevScene& S, Trav& T, bool any, 
         const uint32_t ni = next_node(T, stack, overflow);
         if (COUNT) tc.nodes++;
         const NodeWords w = load_node8(S.nodes8, ni);
+#if defined(RT_XP_DUP) && (RT_XP_DUP & 1)
+        {   // the node test once more on an opaque copy of its words (its cost, not its result)
+            NodeWords c = w;
+            asm volatile("" : "+v"(c.h0.x), "+v"(c.h0.y), "+v"(c.h0.z), "+v"(c.h0.w), "+v"(c.h1.x), "+v"(c.h1.y), "+v"(c.h1.z),
+                         "+v"(c.qx.x), "+v"(c.qx.y), "+v"(c.qx.z), "+v"(c.qx.w), "+v"(c.qy.x), "+v"(c.qy.y), "+v"(c.qy.z),
+                         "+v"(c.qy.w), "+v"(c.qz.x), "+v"(c.qz.y), "+v"(c.qz.z), "+v"(c.qz.w));
+            uint32_t a, b, cc, d, e;
+            bool f;
+            test_node8_words(c, T.R, 0.0f, fminf(cull, T.best), a, b, cc, d, e, f);
+            T.xp ^= a ^ (b << 3) ^ cc ^ d ^ e ^ (f ? 7u : 0u);
+        }
+#endif
         test_node8_words(w, T.R, 0.0f, fminf(cull, T.best), T.g_hits, T.t_mask, T.t_valid, T.g_base, T.t_base, T.g_flip);
     }
     return tdone || (T.t_mask == 0u && T.g_hits == 0u && T.sp == 0);
@@ -986,6 +1029,7 @@ wf_trace(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int cur, in
             }
         }
     }
+    RT_XP_SINK(T, Q.W.counts[cslot(kCntDiagSegs)]);
     ts_end(Q, ts, &ts_done);
     flush_counters(P, ANY ? 0 : rays, ANY ? rays : 0, 0, tc, COUNT, overflow, true);
 }
@@ -1451,6 +1495,301 @@ wf_finish_step(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int c
         }
     }
 #undef RT_DX
+    RT_XP_SINK(T, Q.W.counts[cslot(kCntDiagSegs)]);
+    ts_end(Q, ts, &ts_done);
+    flush_counters(P, n_closest, n_shadow, 0, tc, COUNT, overflow);
+}
+
+// ---- finish, pooled: paths decoupled from lanes (round 5) ------------------------------------------------
+// wf_finish_step binds a path to a lane until the path ends: a lane whose closest hit is found
+// waits (kReady) until its wave shades, and a shading pass runs with the ~22 waiting lanes of 64
+// (profiles/r04_finish_experiments.txt; 28 % VALU lane utilisation over the launch).  Here a wave
+// owns kPoolRecs path records in global memory (128 B each, one cache line) and three rings of
+// record ids in LDS: free records, queries to trace (closest or shadow), and hits to shade.  A lane
+// whose query ends writes the hit into the path's record, pushes the record to the shade ring and
+// takes the next query at once; the wave shades once 64 hits are pending (or, after its queue ran
+// out, a share of what is left), all 64 lanes shading one record each while the traversing lanes
+// keep their queries.  Per path the operations run in the reference's order (shade, shadow ray,
+// next segment), so every path's result is bit for bit wf_finish_step's.  Records are only ever
+// touched by their own wave, in program order: no cross-wave synchronisation.
+//   record: [0] ray origin, w = path id   [1] ray direction, w = bounce | tpass << 8 | step << 16
+//           [2] throughput colour         [3] closest hit (t, id, u, v)
+//           [4] shadow origin, w = tmax   [5] shadow direction, w = path id | next ray << 31
+//           [6] shadow contribution       [7] (pixel, sample, Halton index)
+constexpr int kPoolRecs = 256;   // path records per wave (ring indices are one byte)
+constexpr int kRecF4 = 8;        // float4 words per record
+
+template <bool COUNT, bool FULL>
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 4)))
+wf_finish_pool(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int cur, int ts) {
+    const FrameParams& P = *Pp;   // per-frame parameters in device memory
+    if (cur < 0) cur = (int)__builtin_amdgcn_readfirstlane(Q.W.counts[cslot(kCntFinishQ)]);   // dev_ctl
+    __shared__ int lds_stack[kStackSize * kBlock];
+    __shared__ HaltonDim lds_halton[kHaltonLds];
+    __shared__ MatRec lds_mat[kMatLds];
+    __shared__ uint8_t lds_free[kBlock / 64][kPoolRecs];
+    __shared__ uint8_t lds_shade[kBlock / 64][kPoolRecs];
+    __shared__ uint16_t lds_trace[kBlock / 64][kPoolRecs];   // record id | 0x100 for a shadow query
+    int* stack = &lds_stack[threadIdx.x];
+    __shared__ uint32_t ts_done;
+    if (threadIdx.x == 0) ts_done = 0u;
+    ts_start(Q, ts);
+    const uint32_t wv = threadIdx.x >> 6, lane = lane_id();
+    uint8_t* const rfree = lds_free[wv];
+    uint8_t* const rshade = lds_shade[wv];
+    uint16_t* const rtrace = lds_trace[wv];
+    for (uint32_t i = lane; i < (uint32_t)kPoolRecs; i += 64u) rfree[i] = (uint8_t)i;
+    const ShadeTabs halton = load_tabs(S, lds_halton, lds_mat);   // ends with a block barrier
+    const Uniforms& U = P.U;
+    const QueueShards qs = load_queue(Q.W.counts, cur, Q.seg_cap);   // front parts first: the likely-long paths
+    const uint32_t n = queue_len(qs);
+    if (Q.dev_ctl) stat_add(Q, kStatFinish, 1u);
+    if (Q.dev_ctl && n > 0) stat_add(Q, kStatRounds, 1u);
+    const float4* qin = Q.W.q[cur];
+    const uint32_t kChunk = (uint32_t)Q.fchunk;   // paths per grab
+    float4* const rec = Q.W.fpool + ((size_t)blockIdx.x * (kBlock / 64) + wv) * (size_t)(kPoolRecs * kRecF4);
+    constexpr uint32_t kMask = kPoolRecs - 1;
+    constexpr int kIdle = 0, kClosest = 1, kShadow = 2;
+    // ring positions (wave-uniform): free [fh, ft), queries [th, tt), hits [sh, st)
+    uint32_t fh = 0, ft = kPoolRecs, th = 0, tt = 0, sh = 0, st = 0;
+    TraceCounters tc{0, 0, 0};
+    bool overflow = false;
+    uint32_t n_closest = 0, n_shadow = 0;
+    f2 zero2;
+    zero2.x = 0.0f;
+    zero2.y = 0.0f;
+    uint32_t wnext = 0, wend = 0;
+    bool exhausted = false;
+    int mode = kIdle;
+    uint32_t r = 0;      // the lane's record while it traverses
+    uint32_t spid = 0;   // shadow query: path id | next ray << 31
+    Trav T;
+    trav_start(T, mk3(0, 0, 0), mk3(1, 0, 0), 0.0f);
+    // diagnostics (Q.diag, RT_WF_LOG), as wf_finish_step's: iterations, ticks and busy lanes before /
+    // after the wave's queue ran out, time and lanes in shading passes (wave-uniform registers)
+    uint32_t iters = 0, it_x = 0xffffffffu, t_x = 0, lanes_x = 0, n_pass = 0, n_shaded = 0;
+    uint64_t t_shade = 0;
+    const uint64_t t_start = Q.diag ? __builtin_amdgcn_s_memrealtime() : 0;
+
+    while (true) {
+        ++iters;
+        // ---- shading pass: every lane shades one pending hit (:324-774); traversing lanes keep their query
+        {
+            const uint32_t npend = st - sh;
+            bool pass = npend >= 64u;
+            if (!pass && npend > 0u && exhausted) {
+                const unsigned long long busy = __ballot(mode != kIdle);
+                const int thr = Q.shade_min_x < 0 ? max(1, -Q.shade_min_x * (__popcll(busy) + (int)npend) / 100)
+                                                  : max(1, Q.shade_min_x);
+                pass = (int)npend >= thr || (busy == 0ull && tt == th);
+            }
+            if (pass) {
+                const uint64_t ts0 = Q.diag ? __builtin_amdgcn_s_memrealtime() : 0;
+                const uint32_t m = min(npend, 64u);
+                const bool act = lane < m;
+                uint32_t rid = 0;
+                StepResult sr;
+                sr.next = false;
+                sr.shadow = false;
+                if (act) {
+                    rid = rshade[(sh + lane) & kMask];
+                    float4* R = rec + (size_t)rid * kRecF4;
+                    const float4 o = R[0], d = R[1], c = R[2], hv = R[3], mt = R[7];
+                    const uint32_t pid = __float_as_uint(o.w), state = __float_as_uint(d.w);
+                    Hit h;
+                    h.t = hv.x;
+                    h.id = __float_as_uint(hv.y);
+                    h.u = hv.z;
+                    h.v = hv.w;
+                    const uint32_t pix = __float_as_uint(mt.x);
+                    const int sample = (int)__float_as_uint(mt.y), hidx = (int)__float_as_uint(mt.z);
+                    // FULL=false: shade_step runs on a zero accumulator and the stored one is updated only
+                    // when the emission term is non-zero (as wf_shade: a + (0 + x) == a + x bit for bit)
+                    const float4 a = FULL ? Q.W.p_accum[pid] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+                    PathRegs p;
+                    p.color = ld3(c);
+                    p.accum = ld3(a);
+                    p.bounce = (int)(state & 0xffu);
+                    p.tpass = (int)((state >> 8) & 0xffu);
+                    p.step = (int)(state >> 16);
+                    f3 rayO = ld3(o), rayD = ld3(d);
+                    shade_step<FULL, false>(S, U, halton, hidx, sample, rayO, rayD, h, p, sample == 0 && p.step == 0, zero2,
+                                            false, zero2, sr);
+                    write_pixel_outputs(P, pix, sr, h, FULL);
+                    if (__float_as_uint(p.accum.x) != __float_as_uint(a.x) || __float_as_uint(p.accum.y) != __float_as_uint(a.y) ||
+                        __float_as_uint(p.accum.z) != __float_as_uint(a.z)) {
+                        if (!FULL) {
+                            const float4 s = Q.W.p_accum[pid];
+                            p.accum = mk3(s.x + p.accum.x, s.y + p.accum.y, s.z + p.accum.z);
+                        }
+                        Q.W.p_accum[pid] = make_float4(p.accum.x, p.accum.y, p.accum.z, 0.0f);
+                    }
+                    if (sr.next) {
+                        R[0] = make_float4(rayO.x, rayO.y, rayO.z, o.w);
+                        R[1] = make_float4(rayD.x, rayD.y, rayD.z, __uint_as_float(pack_state(p.bounce, p.tpass, p.step)));
+                        R[2] = make_float4(p.color.x, p.color.y, p.color.z, 0.0f);
+                    }
+                    if (sr.shadow) {
+                        R[4] = make_float4(sr.so.x, sr.so.y, sr.so.z, sr.stmax);
+                        R[5] = make_float4(sr.sd.x, sr.sd.y, sr.sd.z, __uint_as_float(pid | (sr.next ? 0x80000000u : 0u)));
+                        R[6] = make_float4(sr.contrib.x, sr.contrib.y, sr.contrib.z, 0.0f);
+                    }
+                }
+                sh += m;
+                // the path continues with its shadow ray, else its next ray; an ended path frees its record
+                const bool more = act && (sr.shadow || sr.next);
+                const unsigned long long mm = __ballot(more);
+                if (more) rtrace[(tt + mbcnt64(mm)) & kMask] = (uint16_t)(rid | (sr.shadow ? 0x100u : 0u));
+                tt += (uint32_t)__popcll(mm);
+                const bool ended = act && !more;
+                const unsigned long long me = __ballot(ended);
+                if (ended) rfree[(ft + mbcnt64(me)) & kMask] = (uint8_t)rid;
+                ft += (uint32_t)__popcll(me);
+                // the traversing lanes' ray setups, dead across the shading code, rebuilt from their
+                // records (a pure function of the ray: bit for bit the one trav_start made); idle lanes
+                // too (their r is a valid record, the setup unused), so no lane keeps the old one live
+                {
+                    const float4* R = rec + (size_t)r * kRecF4 + (mode == kShadow ? 4 : 0);
+                    const float4 ro = R[0], rd = R[1];
+                    T.R = ray_setup(ld3(ro), ld3(rd));
+                }
+                if (Q.diag) {
+                    ++n_pass;
+                    n_shaded += m;
+                    t_shade += __builtin_amdgcn_s_memrealtime() - ts0;
+                }
+            }
+        }
+
+        // ---- refill idle lanes: queued continuations first, then new paths (chunks of the XCD's counter)
+        unsigned long long idle = __ballot(mode == kIdle);
+        if (idle != 0ull && tt != th) {
+            const uint32_t j = mbcnt64(idle);
+            const uint32_t take = min((uint32_t)__popcll(idle), tt - th);
+            if (mode == kIdle && j < take) {
+                const uint32_t e = rtrace[(th + j) & kMask];
+                r = e & 0xffu;
+                const float4* R = rec + (size_t)r * kRecF4;
+                if (e & 0x100u) {
+                    const float4 so = R[4], sd = R[5];
+                    spid = __float_as_uint(sd.w);
+                    trav_start(T, ld3(so), ld3(sd), so.w);
+                    mode = kShadow;
+                    n_shadow++;
+                } else {
+                    const float4 ro = R[0], rd = R[1];
+                    trav_start(T, ld3(ro), ld3(rd), INFINITY);
+                    mode = kClosest;
+                    n_closest++;
+                }
+            }
+            th += take;
+            idle = __ballot(mode == kIdle);
+        }
+        const bool refill = __popcll(idle) >= Q.refill_min || idle == ~0ull;
+        if (wnext >= wend && !exhausted && refill && ft != fh) {
+            uint32_t base = 0;
+            if (lane == 0) base = atomicAdd(Q.W.counts + cslot(kCntChunkFinish + (int)(blockIdx.x & 7u)), 1u);
+            base = ((__builtin_amdgcn_readfirstlane(base) << 3) | (blockIdx.x & 7u)) * kChunk;
+            if (base >= n) {
+                exhausted = true;
+                if (Q.diag) {
+                    it_x = iters;
+                    t_x = (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_start);
+                }
+            } else {
+                wnext = base;
+                wend = min(base + kChunk, n);
+            }
+        }
+        if (idle != 0ull && wnext < wend && refill) {
+            const uint32_t j = mbcnt64(idle);
+            const uint32_t take = min(min((uint32_t)__popcll(idle), wend - wnext), ft - fh);
+            if (mode == kIdle && j < take) {
+                const uint32_t e = dense_entry(qs, wnext + j, Q.seg_cap);
+                const float4* src = qin + 2 * (size_t)e;
+                const float4 o = (RT_TRACE_NT & 2) ? ld_stream(&src[0]) : src[0];
+                const float4 d = (RT_TRACE_NT & 2) ? ld_stream(&src[1]) : src[1];
+                const uint32_t pid = __float_as_uint(o.w), state = __float_as_uint(d.w);
+                const float4 c = state == 0u ? make_float4(1.0f, 1.0f, 1.0f, 0.0f)
+                                 : (RT_TRACE_NT & 2) ? ld_stream(&Q.W.qc[cur][e]) : Q.W.qc[cur][e];
+                const uint3 pm = path_meta(P, Q, pid);
+                r = rfree[(fh + j) & kMask];
+                float4* R = rec + (size_t)r * kRecF4;
+                R[0] = o;
+                R[1] = d;
+                R[2] = c;
+                R[7] = make_float4(__uint_as_float(pm.x), __uint_as_float(pm.y), __uint_as_float(pm.z), 0.0f);
+                trav_start(T, ld3(o), ld3(d), INFINITY);
+                mode = kClosest;
+                n_closest++;
+            }
+            fh += take;
+            wnext += take;
+        }
+        if (__ballot(mode != kIdle) == 0ull) {
+            if (exhausted && tt == th && st == sh) break;   // every path of this wave has ended
+            continue;                                        // pending hits: the next pass shades them
+        }
+
+        if (Q.diag && exhausted) lanes_x += (uint32_t)__popcll(__ballot(mode != kIdle));
+        // ---- one traversal step (closest hit or shadow any-hit)
+        bool to_shade = false, to_free = false;
+        if (mode != kIdle) {
+            const bool any = mode == kShadow;
+            if (trav_step<COUNT>(S, T, any, stack, tc, overflow, T.best)) {
+                float4* R = rec + (size_t)r * kRecF4;
+                if (any) {
+                    if (!T.hit_any) {   // unoccluded: accum += contribution (:741-743)
+                        const float4 c = R[6];
+                        const uint32_t pid = spid & 0x7fffffffu;
+                        const float4 a = Q.W.p_accum[pid];
+                        Q.W.p_accum[pid] = make_float4(a.x + c.x, a.y + c.y, a.z + c.z, 0.0f);
+                    }
+                    if (spid >> 31) {   // the path's next ray, in this lane
+                        const float4 ro = R[0], rd = R[1];
+                        trav_start(T, ld3(ro), ld3(rd), INFINITY);
+                        mode = kClosest;
+                        n_closest++;
+                    } else {
+                        mode = kIdle;
+                        to_free = true;
+                    }
+                } else if (T.best_id == 0xffffffffu) {   // miss -> path ends (:321-322)
+                    mode = kIdle;
+                    to_free = true;
+                } else {
+                    R[3] = make_float4(T.best, __uint_as_float(T.best_id), T.bu / T.bdet, T.bv / T.bdet);
+                    mode = kIdle;
+                    to_shade = true;
+                }
+            }
+        }
+        const unsigned long long ms = __ballot(to_shade);
+        if (to_shade) rshade[(st + mbcnt64(ms)) & kMask] = (uint8_t)r;
+        st += (uint32_t)__popcll(ms);
+        const unsigned long long mf = __ballot(to_free);
+        if (to_free) rfree[(ft + mbcnt64(mf)) & kMask] = (uint8_t)r;
+        ft += (uint32_t)__popcll(mf);
+    }
+    if (Q.diag && lane == 0) {
+        const uint32_t dt = (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_start);
+        const bool x = it_x != 0xffffffffu;
+        const uint32_t ix = x ? it_x : iters, tx = x ? t_x : dt;
+        atomicAdd(&Q.W.counts[kWfStat + kStatDiagItPre], ix);
+        atomicAdd(&Q.W.counts[kWfStat + kStatDiagItPost], iters - ix);
+        atomicAdd(&Q.W.counts[kWfStat + kStatDiagTPre], tx);
+        atomicAdd(&Q.W.counts[kWfStat + kStatDiagTPost], dt - tx);
+        atomicAdd(&Q.W.counts[kWfStat + kStatDiagLanesPost], lanes_x);
+        atomicAdd(&Q.W.counts[kWfDiagExh + min(tx / 5000u, 63u)], 1u);
+        atomicAdd(&Q.W.counts[kWfStat + kStatDiagShadeT], (uint32_t)t_shade);
+        atomicAdd(&Q.W.counts[kWfStat + kStatDiagTotalT], dt);
+        atomicAdd(&Q.W.counts[kWfStat + kStatDiagPasses], n_pass);
+        atomicAdd(&Q.W.counts[kWfStat + kStatDiagShaded], n_shaded);
+        atomicMax(&Q.W.counts[cslot(kCntDiagIters)], iters);
+        atomicMax(&Q.W.counts[cslot(kCntDiagTime)], dt);
+        atomicAdd(&Q.W.counts[kWfDiagHist + min(dt / 5000u, 63u)], 1u);
+    }
     ts_end(Q, ts, &ts_done);
     flush_counters(P, n_closest, n_shadow, 0, tc, COUNT, overflow);
 }
@@ -1606,23 +1945,42 @@ static unsigned trace_grid_cap(const WfParams& Q) {
 
 // the finish launch: Q.finish_frac percent of the resident grid (frames in flight: the rest of the
 // machine stays free for the other frames' kernels)
-template <bool COUNT, bool FULL>
-static unsigned finish_full_cap() {   // resident blocks of the finish kernel, queried once
-    static const unsigned c = resident_grid(wf_finish_step<COUNT, FULL, false>, 2);
+template <bool COUNT, bool FULL, bool TEAM>
+static unsigned finish_full_cap() {   // resident blocks of the finish kernel instance, queried once
+    static const unsigned c = resident_grid(wf_finish_step<COUNT, FULL, TEAM>, 2);
     return c;
 }
 template <bool COUNT, bool FULL>
+static unsigned pool_full_cap() {   // resident blocks of the pooled finish kernel, queried once
+    static const unsigned c = resident_grid(wf_finish_pool<COUNT, FULL>, 2);
+    return c;
+}
+// the pooled finish kernel's records: kPoolRecs per wave of the largest resident grid of its instances
+size_t wavefront_pool_bytes() {
+    const unsigned g = std::max(std::max(pool_full_cap<false, false>(), pool_full_cap<false, true>()),
+                                std::max(pool_full_cap<true, false>(), pool_full_cap<true, true>()));
+    return (size_t)std::max(g, 8u) * (kBlock / 64) * kPoolRecs * kRecF4 * sizeof(float4);
+}
+template <bool COUNT, bool FULL>
 static void launch_finish(const DevScene& S, const WfParams& Q, int cur, uint32_t n, hipStream_t stream, int ts) {
-    // at least one block per XCD: each takes the chunks of its XCD's counter (wf_finish_step)
-    const unsigned cap = std::max(8u, finish_full_cap<COUNT, FULL>() * (unsigned)Q.finish_frac / 100u);
+    if (Q.pool) {   // grid <= pool_full_cap: the blocks' record pools fit fpool (wavefront_pool_bytes)
+        const unsigned pcap = std::max(8u, pool_full_cap<COUNT, FULL>() * (unsigned)Q.finish_frac / 100u / 8u * 8u);
+        hipLaunchKernelGGL((wf_finish_pool<COUNT, FULL>), dim3(std::max(8u, grid_for(n, pcap))), dim3(kBlock), 0, stream,
+                           S, Q.Pd, Q, cur, ts);
+        return;
+    }
+    // at least one block per XCD: each takes the chunks of its XCD's counter (wf_finish_step).
     // Q.team: the kernel with the team drain (a separate instance: its code would raise the plain
-    // kernel's register pressure)
-    if (Q.team)
+    // kernel's register pressure), sized by its own occupancy (its LDS and registers differ)
+    if (Q.team) {
+        const unsigned cap = std::max(8u, finish_full_cap<COUNT, FULL, true>() * (unsigned)Q.finish_frac / 100u);
         hipLaunchKernelGGL((wf_finish_step<COUNT, FULL, true>), dim3(std::max(8u, grid_for(n, cap))), dim3(kBlock), 0,
                            stream, S, Q.Pd, Q, cur, ts);
-    else
+    } else {
+        const unsigned cap = std::max(8u, finish_full_cap<COUNT, FULL, false>() * (unsigned)Q.finish_frac / 100u);
         hipLaunchKernelGGL((wf_finish_step<COUNT, FULL, false>), dim3(std::max(8u, grid_for(n, cap))), dim3(kBlock), 0,
                            stream, S, Q.Pd, Q, cur, ts);
+    }
 }
 
 static void launch_finish_any(const DevScene& S, const WfParams& Q, bool count, bool full, int cur, uint32_t n,
@@ -1782,8 +2140,10 @@ namespace {
 // argument), so after the first refusal frames are captured without them: the graphs then hold
 // the frame's launches, memsets and copies only, and the per-stage times of replayed frames are
 // not recorded (rt_stats kernel_ms; the frame's own time, taken outside the graphs, is).
-static bool g_graph_events = true;
-static bool g_ext_refused = false;   // set when a capture's external event record was refused
+// Process-wide and one-way (true -> false) for g_graph_events; g_ext_refused is the refusal flag of a
+// capture attempt.  Atomics: contexts on other threads may capture concurrently (ThreadLocal capture).
+static std::atomic<bool> g_graph_events{true};
+static thread_local bool g_ext_refused = false;   // set when this thread's capture had an external event record refused
 
 struct Enqueue {
     WfTimeline& T;
@@ -1807,12 +2167,13 @@ struct Enqueue {
         last = T.n_ev++;
         return true;
     }
-    // closes the span [previous mark, now) as `stage`
+    // closes the span [previous mark, now) as `stage`; without a previous mark (part 0 was captured
+    // untimed and this part is recorded eagerly) it only marks: there is no start event to time from
     bool span(int stage, const char** err) {
         if (capture && !g_graph_events) return true;
         const int a = last;
         if (!mark(err)) return false;
-        T.spans[T.n_spans++] = WfTimeline::Span{stage, a, last};
+        if (a >= 0) T.spans[T.n_spans++] = WfTimeline::Span{stage, a, last};
         return true;
     }
 };
@@ -2084,6 +2445,8 @@ bool run_wavefront(const DevScene& S, const FrameParams& P, WavefrontBuffers& W,
     // flight ±0), but not the smallest (C1 256x256x1: -7.5 %)
     Q.team = tu.team >= 0 ? tu.team : (Q.base_paths >= kTeamAutoMin && Q.base_paths <= kTeamAutoPaths ? 4 : 0);
     Q.fchunk = tu.fchunk;
+    Q.pool = tu.pool;
+    if (Q.pool) Q.team = 0;   // the pooled kernel has no team drain
     Q.spans = spans ? 1 : 0;
     Q.spp_div = make_fastdiv((uint32_t)Q.spp);
     Q.tile = P.tile_size;
@@ -2126,10 +2489,15 @@ bool run_wavefront(const DevScene& S, const FrameParams& P, WavefrontBuffers& W,
         // the device queries behind the grid sizes run before a stream is capturing (a capture
         // must hold stream work only)
         (void)trace_grid_cap(Q);
-        (void)finish_full_cap<false, false>();
-        (void)finish_full_cap<false, true>();
-        (void)finish_full_cap<true, false>();
-        (void)finish_full_cap<true, true>();
+        (void)finish_full_cap<false, false, false>();
+        (void)finish_full_cap<false, true, false>();
+        (void)finish_full_cap<true, false, false>();
+        (void)finish_full_cap<true, true, false>();
+        (void)finish_full_cap<false, false, true>();
+        (void)finish_full_cap<false, true, true>();
+        (void)finish_full_cap<true, false, true>();
+        (void)finish_full_cap<true, true, true>();
+        (void)wavefront_pool_bytes();
         return enqueue_wavefront(S, P, Q, count, full, maxExtra, extra_pass, stream, prev_done, *tl, err, graphs);
     }
     Q.dev_ctl = 0;

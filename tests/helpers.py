@@ -136,3 +136,59 @@ def write_triangle_soup(path, n=4000, seed=5):
         fh.writelines("f %d %d %d\n" % (3 * k + 1, 3 * k + 2, 3 * k + 3) for k in range(n))
     with open(os.path.join(os.path.dirname(path), "soup.mtl"), "w") as fh:
         fh.write("newmtl None\nKd 0.6 0.7 0.5\nd 1\n")
+
+
+def write_tie_scene(path, n=600, grid=24, seed=7):
+    """An OBJ whose closest hits tie exactly (equal t -> the smaller triangle id).
+    Part 1: n random triangles in a thin slab, written three times over the SAME vertex indices:
+    first under material Red, then Blue, then Green with the vertex order rotated (v1, v2, v0).
+    The Red and Blue copies are bit-identical world-space triangles (every ray hits both at the same
+    t, u, v), so only the id tie-break decides which material a hit shades -- the Red copy, whose
+    ids are smaller; a traversal (or a team member's merge) that lets the later copy win shows
+    blue.  The rotated Green copy ties up to the last bit of t.  Part 2: a grid x grid quad mesh
+    (two triangles per quad, shared edges and vertices) in front of the slab, for hits on shared
+    edges."""
+    import os
+    rng = np.random.default_rng(seed)
+    c = rng.uniform([-0.5, -0.5, -0.1], [0.5, 0.5, 0.1], size=(n, 3))
+    off = rng.normal(size=(n, 3, 3)) * np.array([0.07, 0.07, 0.02])
+    v = (c[:, None, :] + off).reshape(-1, 3)
+    lines = ["mtllib ties.mtl\n"]
+    lines += ["v %.6f %.6f %.6f\n" % tuple(p) for p in v]
+    for mat, rot in (("Red", False), ("Blue", False), ("Green", True)):
+        lines.append("usemtl %s\n" % mat)
+        for k in range(n):
+            a, b, cc = 3 * k + 1, 3 * k + 2, 3 * k + 3
+            lines.append("f %d %d %d\n" % ((b, cc, a) if rot else (a, b, cc)))
+    base = 3 * n
+    xs, ys = np.linspace(-0.6, 0.0, grid + 1), np.linspace(-0.6, 0.6, grid + 1)   # the left half
+    for y in ys:
+        for x in xs:
+            lines.append("v %.6f %.6f %.6f\n" % (x, y, 0.25 + 0.05 * x))
+    lines.append("usemtl Grid\n")
+    for j in range(grid):
+        for i in range(grid):
+            p00 = base + j * (grid + 1) + i + 1
+            p10, p01, p11 = p00 + 1, p00 + grid + 1, p00 + grid + 2
+            if (i + j) % 3 == 0:
+                continue   # holes: rays reach the slab behind
+            lines.append("f %d %d %d\n" % (p00, p10, p11))
+            lines.append("f %d %d %d\n" % (p00, p11, p01))
+    with open(path, "w") as fh:
+        fh.writelines(lines)
+    with open(os.path.join(os.path.dirname(path), "ties.mtl"), "w") as fh:
+        fh.write("newmtl Red\nKd 0.9 0.15 0.1\nd 1\nnewmtl Blue\nKd 0.1 0.2 0.9\nd 1\n"
+                 "newmtl Green\nKd 0.1 0.8 0.2\nd 1\nnewmtl Grid\nKd 0.7 0.7 0.7\nd 1\n")
+
+
+def traversal_scene(rt, assets, kind, tmpdir):
+    """The C1 room with the triangle soup ('soup') or the exact-tie scene ('ties') in front."""
+    import os
+    scene = rt.Scene.preset("c1", assets)
+    if kind == "soup":
+        write_triangle_soup(os.path.join(tmpdir, "soup.obj"))
+        scene.add_model(os.path.join(tmpdir, "soup.obj"), (0.0, 1.0, 0.0), scale=3.0)
+    else:
+        write_tie_scene(os.path.join(tmpdir, "ties.obj"))
+        scene.add_model(os.path.join(tmpdir, "ties.obj"), (0.0, 1.0, 0.5), rotation=(0.0, 0.3, 0.0), scale=3.0)
+    return scene

@@ -43,7 +43,7 @@ def test_ranks_share_one_gpu_gloo_gather_bitwise(tmp_path, n):
         tid = (np.arange(136)[:, None] // 64) * tiles_x + (np.arange(200)[None, :] // 64)
         owner = tid % n
         by_rank = {r: int(diff[owner == r].sum()) for r in range(n)}
-        np.save(os.path.join(ROOT, "gpurun_out", f"ranks{n}_one.npy"), a) if os.path.isdir(os.path.join(ROOT, "gpurun_out")) else None
-        np.save(os.path.join(ROOT, "gpurun_out", f"ranks{n}_many.npy"), b) if os.path.isdir(os.path.join(ROOT, "gpurun_out")) else None
+        ys, xs = np.nonzero(diff)
         pytest.fail(f"{int(diff.sum())} of {diff.size} pixels differ; by owning rank {by_rank}; "
-                    f"max |diff| {float(np.abs(a - b).max())}")
+                    f"max |diff| {float(np.abs(a - b).max())}; first differing pixels (y, x) "
+                    f"{list(zip(ys[:8].tolist(), xs[:8].tolist()))} (both frames kept in {tmp_path})")

@@ -256,6 +256,20 @@ def test_reference_fan_out_is_bounded_by_bytes(rt, d):
         _scene(rt, root)
 
 
+def test_internal_reference_fan_out_is_bounded_by_bytes(rt, d):
+    # many internal references next to one large array: each internal arc snapshots the layer it
+    # resolves against (those copies were charged one prim each, not their bytes); the
+    # byte budget now stops it with an error after a bounded amount of copying
+    n = 1 << 20
+    pts = ", ".join("(%d, 0, 0)" % (k % 7) for k in range(n))
+    # the arcs target a tiny prim: the merges copy nothing, only the snapshots copy the array
+    refs = "".join('    def "c%d" (\n        references = </Tiny>\n    )\n    {\n    }\n' % j for j in range(2048))
+    root = _write(d, "int_fan.usda", HEAD % "" + 'def Mesh "Src"\n{\n    point3f[] points = [%s]\n}\n' % pts +
+                  'def Xform "Tiny"\n{\n}\n' + 'def Xform "F"\n{\n' + refs + "}\n")
+    with pytest.raises(rt.RTError, match="larger than"):
+        _scene(rt, root)
+
+
 def _box_prims(path, counts=(4,), idx=(0, 1, 2, 3)):
     return [dict(path=path, type="Mesh", attrs=[
         dict(name="faceVertexCounts", type="int[]", value=list(counts)),

@@ -1,6 +1,7 @@
 import csv, collections, glob, sys
 agg=collections.defaultdict(lambda: collections.defaultdict(float))
-for f in sorted(glob.glob('gpurun_out/pmc/p*/run_counter_collection.csv')):
+d = sys.argv[2] if len(sys.argv) > 2 else 'gpurun_out/pmc'
+for f in sorted(glob.glob(d + '/p*/run_counter_collection.csv')):
     for r in csv.DictReader(open(f)):
         k=r['Kernel_Name'].split('(')[0].replace('void ','')
         if 'rocclr' in k: continue
@@ -16,3 +17,4 @@ for k,v in agg.items():
     if g('SQ_ACTIVE_INST_VALU') and g('SQ_THREAD_CYCLES_VALU'): print('   -> lane util %.3f'%(g('SQ_THREAD_CYCLES_VALU')/(64*g('SQ_ACTIVE_INST_VALU'))))
     if g('TCP_TCC_READ_REQ_sum'): print('   -> avg L2 read latency %.1f cyc'%(g('TCP_TCC_READ_REQ_LATENCY_sum')/g('TCP_TCC_READ_REQ_sum')))
     if g('SQ_CYCLES'): print('   -> avg waves resident %.1f (per SE?)'%(g('SQ_LEVEL_WAVES')/g('SQ_CYCLES')))
+    if g('SQ_INSTS_VMEM_RD') and g('SQ_INST_LEVEL_VMEM'): print('   -> avg VMEM instr latency %.0f cyc (level / instrs)'%(g('SQ_INST_LEVEL_VMEM')/(g('SQ_INSTS_VMEM_RD')+g('SQ_INSTS_VMEM_WR'))))
