@@ -74,6 +74,17 @@ __device__ __forceinline__ void block_flush_counters(unsigned long long* counter
     }
 }
 
+// The same flush per wave (no block barrier): for kernels whose waves leave at different times.
+__device__ __forceinline__ void wave_flush_counters(unsigned long long* counters, uint32_t closest, uint32_t shadow,
+                                                    uint32_t nodes, uint32_t tris, uint32_t paths, bool overflow) {
+    const unsigned long long v[6] = {wave_sum(closest), wave_sum(shadow), wave_sum(nodes), wave_sum(tris), wave_sum(paths),
+                                     __ballot(overflow) != 0ull ? 1ull : 0ull};
+    const uint32_t lane = threadIdx.x & 63u;
+    #pragma unroll
+    for (int k = 0; k < 6; ++k)
+        if (lane == (uint32_t)k && v[k]) atomicAdd(&counters[cnt_word(k, blockIdx.x & (kCntReplicas - 1))], v[k]);
+}
+
 void launch_megakernel(const DevScene& S, const FrameParams& P, int nblocks, bool count, hipStream_t stream);
 
 // Wavefront pipeline (rt_wavefront.hip): path state SoA indexed by path id

@@ -60,6 +60,8 @@ struct Tuning {
                        // (=2 also the finish paths' segment counts: one atomic per path, slows the launch)
     bool host_ctl;     // RT_WF_HOST=1: host-driven rounds (queue sizes read back every round)
     int pool;          // RT_FINISH_POOL: 1 = the pooled finish kernel (wf_finish_pool), 0 = wf_finish_step
+    int consol;        // RT_CONSOL: wf_finish_step consolidates its block's waves every this many iterations
+                       // once every wave's queue ran out (0 = off)
     unsigned shade_blocks;   // RT_SHADE_BLOCKS: wf_shade grid (grid-stride loop), a multiple of 8; 2048 (1.6 waves
                              // of the resident grid) leaves CUs to the other frames in flight: C3g four in
                              // flight +1.3-2.2 % against 8192, one frame alone the same
@@ -81,6 +83,7 @@ static const Tuning& tuning() {
         v.host_ctl = env_int("RT_WF_HOST", 0) != 0;
         v.shade_blocks = (unsigned)std::max(8, env_int("RT_SHADE_BLOCKS", 2048)) / 8u * 8u;
         v.pool = env_int("RT_FINISH_POOL", 0);
+        v.consol = std::max(0, env_int("RT_CONSOL", 0));
         return v;
     }();
     return t;
@@ -236,6 +239,7 @@ struct WfParams {
     int team;              // wf_finish_step: lanes per query in the drain (0: no team drain)
     int fchunk;            // wf_finish_step: paths per chunk grab
     int pool;              // the finish launch runs wf_finish_pool (paths in per-wave record pools)
+    int consol;            // wf_finish_step (no team): block consolidation period in iterations (0 = off)
     int finish_frac;       // percent of the resident grid the finish launch takes
     int trace_frac;        // percent of the resident grid the bulk wf_trace launches take
     int spans;             // record device-clock launch spans (rt_set_device_spans)
@@ -362,6 +366,25 @@ __device__ __forceinline__ uint32_t dense_entry(const QueueShards& qs, uint32_t 
     #pragma unroll
     for (int j = 0; j < kShards - 1; ++j) {
         acc += back ? qs.S[j] : qs.L[j];
+        const bool past = g >= acc;
+        k = past ? (uint32_t)(j + 1) : k;
+        start = past ? acc : start;
+    }
+    const uint32_t i = g - start;
+    return k * seg_cap + (back ? seg_cap - 1u - i : i);
+}
+// The same from the shard counts held in LDS (L[k] at [k], S[k] at [kShards + k]): the finish
+// kernel reads them only at refill, so they need not occupy registers across its shading code.
+__device__ __forceinline__ uint32_t dense_entry_lds(const uint32_t* qsl, uint32_t g, uint32_t seg_cap) {
+    uint32_t ltot = 0;
+    #pragma unroll
+    for (int k = 0; k < kShards; ++k) ltot += qsl[k];
+    const bool back = g >= ltot;
+    if (back) g -= ltot;
+    uint32_t k = 0, start = 0, acc = 0;
+    #pragma unroll
+    for (int j = 0; j < kShards - 1; ++j) {
+        acc += back ? qsl[kShards + j] : qsl[j];
         const bool past = g >= acc;
         k = past ? (uint32_t)(j + 1) : k;
         start = past ? acc : start;
@@ -555,6 +578,12 @@ __device__ __forceinline__ bool trav_step(const DevScene& S, Trav& T, bool any, 
             bool f;
             test_node8_words(c, T.R, 0.0f, fminf(cull, T.best), a, b, cc, d, e, f);
             T.xp ^= a ^ (b << 3) ^ cc ^ d ^ e ^ (f ? 7u : 0u);
+        }
+#endif
+#if defined(RT_XP_DUP) && (RT_XP_DUP & 4)
+        {   // one more node's words loaded (a neighbour of this one) and consumed: the cost of the load alone
+            const NodeWords w2 = load_node8(S.nodes8, ni ^ 1u);
+            asm volatile("" :: "v"(w2.h0.x), "v"(w2.h1.x), "v"(w2.qx.x), "v"(w2.qy.x), "v"(w2.qz.x));
         }
 #endif
         test_node8_words(w, T.R, 0.0f, fminf(cull, T.best), T.g_hits, T.t_mask, T.t_valid, T.g_base, T.t_base, T.g_flip);
@@ -1055,17 +1084,38 @@ wf_finish_step(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int c
     __shared__ float lds_sray[6][kBlock];   // each lane's shadow ray (origin, direction)
     int* stack = &lds_stack[threadIdx.x];
     __shared__ uint32_t ts_done;
-    if (threadIdx.x == 0) ts_done = 0u;
+    // block consolidation (Q.consol, !TEAM): waves whose queue ran out, the waves' busy lanes at a
+    // consolidation round (0xffffffff: the wave has left), and the 16-lane transfer buffer
+    __shared__ uint32_t lds_nexh;
+    __shared__ uint32_t lds_cnt[kBlock / 64];
+    __shared__ uint32_t lds_xbuf[32][16];
+    __shared__ uint32_t lds_qs[2 * kShards];   // the finish queue's shard parts (dense_entry_lds)
+    if (threadIdx.x == 0) {
+        ts_done = 0u;
+        lds_nexh = 0u;
+    }
     ts_start(Q, ts);
-    const ShadeTabs halton = load_tabs(S, lds_halton, lds_mat);   // ends with a block barrier
+    uint32_t n;
+    {
+        const QueueShards qs = load_queue(Q.W.counts, cur, Q.seg_cap);   // front parts first: the likely-long paths
+        n = queue_len(qs);
+        #pragma unroll
+        for (int k = 0; k < kShards; ++k)
+            if (threadIdx.x == (unsigned)k) {
+                lds_qs[k] = qs.L[k];
+                lds_qs[kShards + k] = qs.S[k];
+            }
+    }
+    const ShadeTabs halton = load_tabs(S, lds_halton, lds_mat);   // ends with a block barrier (lds_qs written)
     const Uniforms& U = P.U;
-    const QueueShards qs = load_queue(Q.W.counts, cur, Q.seg_cap);   // front parts first: the likely-long paths
-    const uint32_t n = queue_len(qs);
     if (Q.dev_ctl) stat_add(Q, kStatFinish, 1u);
     if (Q.dev_ctl && n > 0) stat_add(Q, kStatRounds, 1u);
     const float4* qin = Q.W.q[cur];
     const uint32_t kChunk = (uint32_t)Q.fchunk;   // paths per grab
     constexpr int kIdle = 0, kClosest = 1, kShadow = 2, kReady = 3;
+    const bool consol = !TEAM && Q.consol > 0;
+    bool all_exh = false;     // every wave of the block has exhausted its queue (consolidation rounds run)
+    int since = 0;            // iterations since the last round
     TraceCounters tc{0, 0, 0};
     bool overflow = false;
     uint32_t n_closest = 0, n_shadow = 0;
@@ -1132,6 +1182,7 @@ wf_finish_step(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int c
             base = ((__builtin_amdgcn_readfirstlane(base) << 3) | (blockIdx.x & 7u)) * kChunk;
             if (base >= n) {
                 exhausted = true;
+                if (consol && lane_id() == 0) atomicAdd(&lds_nexh, 1u);
                 if (Q.diag && lane_id() == 0) {
                     RT_DX[0] = iters;
                     RT_DX[1] = (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_start);
@@ -1146,7 +1197,7 @@ wf_finish_step(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int c
             if (mode == kIdle) {
                 const uint32_t g = wnext + mbcnt64(idle);
                 if (g < wend) {
-                    const uint32_t e = dense_entry(qs, g, Q.seg_cap);
+                    const uint32_t e = dense_entry_lds(lds_qs, g, Q.seg_cap);
                     const float4* src = qin + 2 * (size_t)e;
                     const float4 o = (RT_TRACE_NT & 2) ? ld_stream(&src[0]) : src[0];
                     const float4 d = (RT_TRACE_NT & 2) ? ld_stream(&src[1]) : src[1];
@@ -1244,7 +1295,144 @@ wf_finish_step(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int c
             }
             if (Q.diag) t_shade += __builtin_amdgcn_s_memrealtime() - ts0;
         }
+
+        // ---- block consolidation (round 5).  Once every wave of the block has run out of queue, the
+        // waves drain their paths with fewer and fewer busy lanes, and each wave-instruction serves
+        // those few.  Every Q.consol iterations the live waves of the block meet (block barriers: a
+        // wave that has left no longer counts in them) and the busiest one takes over the paths of
+        // the others while they fit its idle lanes, each path with its whole state (query included:
+        // traversal registers, LDS stack entries and shadow ray); a wave left without paths ends.
+        // Every wave computes the same plan from the same counts, so all run the same barriers.  A
+        // path's arithmetic does not depend on the lane it runs in: the same bits.
+        if (consol && exhausted) {
+            if (!all_exh) all_exh = __builtin_amdgcn_readfirstlane(lds_nexh) == kBlock / 64;
+            if (all_exh && ++since >= Q.consol) {
+                since = 0;
+                const unsigned long long busy0 = __ballot(mode != kIdle);
+                const uint32_t wv = threadIdx.x >> 6;
+                __syncthreads();
+                if (lane_id() == 0) lds_cnt[wv] = (uint32_t)__popcll(busy0);
+                __syncthreads();
+                // the plan, in wave-uniform scalars (every array index a compile-time constant: a
+                // run-time index would put the array in scratch)
+                constexpr uint32_t kGone = 0xffffffffu;
+                uint32_t c[kBlock / 64];
+                #pragma unroll
+                for (int w = 0; w < kBlock / 64; ++w) c[w] = __builtin_amdgcn_readfirstlane(lds_cnt[w]);
+                // receiver: the busiest live wave (lowest index on ties)
+                uint32_t recv = 0, cr = 0;
+                bool any = false;
+                #pragma unroll
+                for (int w = 0; w < kBlock / 64; ++w)
+                    if (c[w] != kGone && (!any || c[w] > cr)) {
+                        recv = (uint32_t)w;
+                        cr = c[w];
+                        any = true;
+                    }
+                // donors: the other waves with paths, fewest first, while they fit its idle lanes;
+                // don_off[w] = the first receiving idle-lane rank of donor w (kGone: not a donor)
+                uint32_t don_off[kBlock / 64];
+                #pragma unroll
+                for (int w = 0; w < kBlock / 64; ++w) don_off[w] = kGone;
+                uint32_t cap = 64u - cr, taken = 0, assigned = 0;
+                bool stop = false;
+                #pragma unroll
+                for (int it = 0; it < kBlock / 64 - 1; ++it) {
+                    uint32_t bw = kBlock / 64, bc = kGone;
+                    #pragma unroll
+                    for (int w = 0; w < kBlock / 64; ++w)
+                        if ((uint32_t)w != recv && c[w] != kGone && c[w] > 0u && !((assigned >> w) & 1u) && c[w] < bc) {
+                            bw = (uint32_t)w;
+                            bc = c[w];
+                        }
+                    if (stop || bw == kBlock / 64 || bc > cap) {
+                        stop = true;
+                    } else {
+                        assigned |= 1u << bw;
+                        #pragma unroll
+                        for (int w = 0; w < kBlock / 64; ++w)
+                            if ((uint32_t)w == bw) don_off[w] = taken;
+                        taken += bc;
+                        cap -= bc;
+                    }
+                }
+                const uint32_t my_rank = mbcnt64(busy0);       // donor lanes: rank among the busy lanes
+                const uint32_t idle_rank = mbcnt64(~busy0);    // receiver lanes: rank among the idle lanes
+                #pragma unroll
+                for (int w = 0; w < kBlock / 64; ++w) {
+                    if (don_off[w] == kGone) continue;
+                    for (uint32_t ch = 0; ch * 16u < c[w]; ++ch) {
+                        if ((int)wv == w && mode != kIdle && my_rank >= ch * 16u && my_rank < ch * 16u + 16u) {
+                            const uint32_t k = my_rank - ch * 16u;
+                            const uint32_t v[32] = {pid, meta.x, meta.y, meta.w,
+                                                    __float_as_uint(p.color.x), __float_as_uint(p.color.y), __float_as_uint(p.color.z),
+                                                    __float_as_uint(p.accum.x), __float_as_uint(p.accum.y), __float_as_uint(p.accum.z),
+                                                    pack_state(p.bounce, p.tpass, p.step),
+                                                    __float_as_uint(rayO.x), __float_as_uint(rayO.y), __float_as_uint(rayO.z),
+                                                    __float_as_uint(rayD.x), __float_as_uint(rayD.y), __float_as_uint(rayD.z),
+                                                    __float_as_uint(contrib.x), __float_as_uint(contrib.y), __float_as_uint(contrib.z),
+                                                    __float_as_uint(T.best), __float_as_uint(T.bu), __float_as_uint(T.bv),
+                                                    __float_as_uint(T.bdet), T.best_id, T.g_base, T.g_hits, T.t_base, T.t_mask,
+                                                    T.t_valid,
+                                                    (uint32_t)mode | (T.g_flip ? 4u : 0u) | (T.hit_any ? 8u : 0u) | (next ? 16u : 0u) |
+                                                        ((uint32_t)T.sp << 8) | (min(segs, 0xffffu) << 16),
+                                                    threadIdx.x};
+                            #pragma unroll
+                            for (int q = 0; q < 32; ++q) lds_xbuf[q][k] = v[q];
+                            mode = kIdle;
+                        }
+                        __syncthreads();
+                        const uint32_t first = don_off[w] + ch * 16u, cnt = min(16u, c[w] - ch * 16u);
+                        if (wv == recv && !((busy0 >> lane_id()) & 1ull) && idle_rank >= first && idle_rank < first + cnt) {
+                            const uint32_t k = idle_rank - first;
+                            uint32_t v[32];
+                            #pragma unroll
+                            for (int q = 0; q < 32; ++q) v[q] = lds_xbuf[q][k];
+                            pid = v[0];
+                            meta = make_uint4(v[1], v[2], 0u, v[3]);
+                            p.color = mk3(__uint_as_float(v[4]), __uint_as_float(v[5]), __uint_as_float(v[6]));
+                            p.accum = mk3(__uint_as_float(v[7]), __uint_as_float(v[8]), __uint_as_float(v[9]));
+                            p.bounce = (int)(v[10] & 0xffu);
+                            p.tpass = (int)((v[10] >> 8) & 0xffu);
+                            p.step = (int)(v[10] >> 16);
+                            rayO = mk3(__uint_as_float(v[11]), __uint_as_float(v[12]), __uint_as_float(v[13]));
+                            rayD = mk3(__uint_as_float(v[14]), __uint_as_float(v[15]), __uint_as_float(v[16]));
+                            contrib = mk3(__uint_as_float(v[17]), __uint_as_float(v[18]), __uint_as_float(v[19]));
+                            T.best = __uint_as_float(v[20]);
+                            T.bu = __uint_as_float(v[21]);
+                            T.bv = __uint_as_float(v[22]);
+                            T.bdet = __uint_as_float(v[23]);
+                            T.best_id = v[24];
+                            T.g_base = v[25];
+                            T.g_hits = v[26];
+                            T.t_base = v[27];
+                            T.t_mask = v[28];
+                            T.t_valid = v[29];
+                            const uint32_t fl = v[30], src = v[31];
+                            mode = (int)(fl & 3u);
+                            T.g_flip = (fl & 4u) != 0u;
+                            T.hit_any = (fl & 8u) != 0u;
+                            next = (fl & 16u) != 0u;
+                            T.sp = (int)((fl >> 8) & 0xffu);
+                            segs = fl >> 16;
+                            for (int q = 0; q < T.sp; ++q) stack[q * kBlock] = lds_stack[q * kBlock + src];
+                            #pragma unroll
+                            for (int q = 0; q < 6; ++q) lds_sray[q][threadIdx.x] = lds_sray[q][src];
+                            if (mode == kShadow)
+                                T.R = ray_setup(mk3(lds_sray[0][threadIdx.x], lds_sray[1][threadIdx.x], lds_sray[2][threadIdx.x]),
+                                                mk3(lds_sray[3][threadIdx.x], lds_sray[4][threadIdx.x], lds_sray[5][threadIdx.x]));
+                            else
+                                T.R = ray_setup(rayO, rayD);
+                        }
+                        __syncthreads();
+                    }
+                }
+                // a wave left without paths leaves the loop at its next refill (its queue has run out)
+            }
+        }
     }
+    if (consol && lane_id() == 0) lds_cnt[threadIdx.x >> 6] = 0xffffffffu;   // this wave has left: no party to later rounds
+
     // ---- team drain (Q.team lanes per query).  The queue has run out and this wave holds at most
     // 64 / team paths: each moves to a team leader (lane team * r) and the team's lanes traverse its
     // query together, splitting the node groups and stack entries among themselves (XOR-paired
@@ -1497,7 +1685,10 @@ wf_finish_step(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int c
 #undef RT_DX
     RT_XP_SINK(T, Q.W.counts[cslot(kCntDiagSegs)]);
     ts_end(Q, ts, &ts_done);
-    flush_counters(P, n_closest, n_shadow, 0, tc, COUNT, overflow);
+    if (consol)   // waves leave at different times: no block barrier in the flush
+        wave_flush_counters(P.counters, n_closest, n_shadow, COUNT ? tc.nodes : 0u, COUNT ? tc.tris : 0u, 0u, overflow);
+    else
+        flush_counters(P, n_closest, n_shadow, 0, tc, COUNT, overflow);
 }
 
 // ---- finish, pooled: paths decoupled from lanes (round 5) ------------------------------------------------
@@ -2447,6 +2638,7 @@ bool run_wavefront(const DevScene& S, const FrameParams& P, WavefrontBuffers& W,
     Q.fchunk = tu.fchunk;
     Q.pool = tu.pool;
     if (Q.pool) Q.team = 0;   // the pooled kernel has no team drain
+    Q.consol = tu.consol;
     Q.spans = spans ? 1 : 0;
     Q.spp_div = make_fastdiv((uint32_t)Q.spp);
     Q.tile = P.tile_size;
