@@ -176,13 +176,23 @@ def run_pmc(a):
     return read_pmc(list(csvs.values())), csvs, None
 
 
+def _env_tuning(rt):
+    """The sweep tools' RT_* variables (tools/sweep.sh case files) as explicit rt_tuning fields and
+    Renderer options: the library reads no environment (rt_set_tuning), the harness does."""
+    tu = rt.tuning_from_env()
+    tu.pop("frames_in_flight", None)   # --frames-in-flight sets that
+    return tu
+
+
 def pmc_child(a):
     """--pmc-child: the workload with one frame in flight (kernels alone), warm-up frame + 3 frames;
     prints nothing.  Runs under rocprofv3 --pmc (run_pmc)."""
     rt = importlib.import_module("metal4-raytracing_amd")
     scene = rt.Scene.preset(a.scene)
+    tu = _env_tuning(rt)
+    tu.pop("graphs", None)
     R = rt.Renderer(scene, a.width, a.height, device=0, pipeline=a.pipeline, seed=3, sort_bins=a.sort_bins, bvh=a.bvh,
-                    frames_in_flight=1)
+                    frames_in_flight=1, tail_paths=tu.pop("tail_paths", 0), tuning=tu)
     R.samplesPerPixel = a.spp
     R.maxBounces = a.bounces
     tiles = (a.tile, a.emulate_rank, a.emulate_ranks) if a.emulate_ranks > 1 else None
@@ -368,9 +378,13 @@ def main():
     rt = importlib.import_module("metal4-raytracing_amd")
     scene = rt.Scene.preset(a.scene)
     t0 = time.time()
+    tu = _env_tuning(rt)
+    graphs_env = tu.pop("graphs", None)
     R = rt.Renderer(scene, a.width, a.height, device=local, pipeline=a.pipeline, seed=3, sort_bins=a.sort_bins,
-                    bvh=a.bvh, frames_in_flight=a.frames_in_flight)
+                    bvh=a.bvh, frames_in_flight=a.frames_in_flight, tail_paths=tu.pop("tail_paths", 0), tuning=tu)
     setup_s = time.time() - t0
+    if graphs_env is not None:
+        R.set_graphs(bool(graphs_env))
     if a.frames_in_flight == 1:
         # one frame at a time is the kernel-alone measurement: enqueue launch by launch, so every
         # stage's HIP events are recorded (graph replays carry none under torch's HIP runtime)

@@ -301,13 +301,44 @@ rt_status rt_set_counting(rt_ctx* ctx, int32_t enabled);
  * while enabled.  Off by default: the stamps cost ~1 % of a C3g frame.  Measurement only (no
  * reference counterpart). */
 rt_status rt_set_device_spans(rt_ctx* ctx, int32_t enabled);
-/* Wavefront frames captured once per frame slot as HIP graphs and replayed (default: on; the
- * environment's RT_GRAPH=0 turns the default off), or enqueued launch by launch (off) — the
+/* Wavefront frames captured once per frame slot as HIP graphs and replayed (default: on), or
+ * enqueued launch by launch (off) — the
  * replacement of the reference's per-frame command buffers (Renderer.swift:1405-1490).  Under a
  * HIP runtime that takes no timing events inside a graph, replayed frames record no per-stage
  * times (rt_stats kernel_ms); frames submitted with graphs off always do. */
 rt_status rt_set_graphs(rt_ctx* ctx, int32_t enabled);
 rt_status rt_get_stats(rt_ctx* ctx, rt_stats* out);
+
+/* Scheduling parameters of the wavefront kernels (no reference counterpart: the
+ * Metal driver schedules the reference's one kernel).  0 in any field selects the measured default;
+ * images are identical for every value.  The library reads no environment variable
+ * for these: only this call changes them, per context.  rt_set_tuning(ctx, NULL) restores the
+ * defaults; rt_get_tuning returns the values in effect (defaults resolved). */
+typedef struct rt_tuning {
+    int32_t trace_chunk;        /* rays per chunk grab of the bulk traversal launches (default 64) */
+    int32_t finish_chunk;       /* paths per chunk grab of the finish launch (default 64) */
+    int32_t refill_min;         /* traversal / finish waves refill once this many lanes are idle (default 8) */
+    int32_t shade_min;          /* the finish kernel shades once this many lanes wait for it (default 24) */
+    int32_t shade_min_drained;  /* the same once its queue has run out: > 0 lanes, < 0 that percentage of
+                                   the wave's busy lanes (default -50) */
+    int32_t team;               /* finish drain, lanes per query once a wave holds <= 64 / team paths:
+                                   0 = default (4 for frames of 256K .. 2.5M base paths, else off),
+                                   1 = off, 2 / 4 / 8 */
+    int32_t finish_grid_pct;    /* percent of the resident grid the finish launch takes (default by
+                                   frames in flight: 100 / 40 / 33 / 20 for 1 / 2 / 3 / 4+) */
+    int32_t trace_grid_pct;     /* percent of the resident grid the bulk traversal launches take
+                                   (default 100, 60 with four or more frames in flight) */
+    int32_t shade_blocks;       /* wf_shade grid, a multiple of 8 (default 2048) */
+    int32_t host_rounds;        /* 1: host-driven rounds (each round's queue size read back); default 0:
+                                   device-side round control, whole frames as HIP graphs */
+    int32_t log;                /* 1: per-round queue sizes, stage times and finish diagnostics on stderr
+                                   (host-driven rounds); 2: + per-path segment counts (slower) */
+    int32_t device_bvh;         /* rt_bvh_build_device topology: 0 = PLOC clustering (default),
+                                   1 = LBVH radix tree */
+    int32_t reserved[4];
+} rt_tuning;
+rt_status rt_set_tuning(rt_ctx* ctx, const rt_tuning* tuning);
+rt_status rt_get_tuning(const rt_ctx* ctx, rt_tuning* out);
 
 /* Library build identification (kernel code object arch etc). */
 const char* rt_version(void);

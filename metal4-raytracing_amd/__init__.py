@@ -17,7 +17,7 @@ import os
 import numpy as np
 
 from . import _abi
-from ._abi import (TEXTURE_SLOTS, Camera, Float3, Light, MaterialOverride, PackedFloat4x3, SceneDesc, Stats, TextureDesc,
+from ._abi import (TEXTURE_SLOTS, Tuning, Camera, Float3, Light, MaterialOverride, PackedFloat4x3, SceneDesc, Stats, TextureDesc,
                    TileSet, Uniforms,
                    f3)
 
@@ -255,6 +255,47 @@ _KNOBS = {
 }
 
 
+# Legacy environment names of the rt_tuning fields (and of three rt_opts / rt_set_graphs settings),
+# read by tuning_from_env for the test and bench harnesses only: the library itself reads none.
+_TUNING_ENV = {"RT_CHUNK": "trace_chunk", "RT_FCHUNK": "finish_chunk", "RT_REFILL_MIN": "refill_min",
+               "RT_SHADE_MIN": "shade_min", "RT_SHADE_MIN_X": "shade_min_drained", "RT_TEAM": "team",
+               "RT_FINISH_FRAC": "finish_grid_pct", "RT_TRACE_FRAC": "trace_grid_pct", "RT_SHADE_BLOCKS": "shade_blocks",
+               "RT_WF_HOST": "host_rounds", "RT_WF_LOG": "log", "RT_DEVICE_BVH": "device_bvh"}
+
+
+def tuning_from_env(environ=None):
+    """Harness convenience (bench.py, the tests' child processes): the rt_tuning fields named by the
+    legacy RT_* environment variables (RT_TEAM: 0 = off, as before; RT_DEVICE_BVH=lbvh), plus
+    'tail_paths' (RT_TAIL_RAYS), 'frames_in_flight' (RT_FRAMES_IN_FLIGHT) and 'graphs' (RT_GRAPH).
+    The library reads no environment variable: a caller sets these with Renderer(tuning=...) /
+    rt_set_tuning, rt_opts and rt_set_graphs."""
+    env = os.environ if environ is None else environ
+    out = {}
+    for name, field in _TUNING_ENV.items():
+        v = env.get(name)
+        if v is None or v == "":
+            continue
+        if field == "team":
+            out[field] = 1 if int(v) in (0, 1) else int(v)
+        elif field == "device_bvh":
+            out[field] = 1 if v == "lbvh" else 0
+        else:
+            out[field] = int(v)
+    for name, key in (("RT_TAIL_RAYS", "tail_paths"), ("RT_FRAMES_IN_FLIGHT", "frames_in_flight"), ("RT_GRAPH", "graphs")):
+        if env.get(name):
+            out[key] = int(env[name])
+    return out
+
+
+def _tuning_struct(fields):
+    t = Tuning()
+    for k, v in fields.items():
+        if not hasattr(t, k) or k == "reserved":
+            raise KeyError(f"unknown rt_tuning field {k!r}")
+        setattr(t, k, int(v))
+    return t
+
+
 class Renderer:
     """Renderer.swift for the hot path: owns a device context, the uniforms and the frame index.
 
@@ -263,7 +304,7 @@ class Renderer:
     """
 
     def __init__(self, scene, width, height, device=0, pipeline="wavefront", seed=1, stream=None, tail_paths=0,
-                 sort_bins=0, bvh="sah", frames_in_flight=0):
+                 sort_bins=0, bvh="sah", frames_in_flight=0, tuning=None):
         object.__setattr__(self, "_ctx", None)
         self.scene = scene
         self.width, self.height = int(width), int(height)
@@ -278,6 +319,8 @@ class Renderer:
         object.__setattr__(self, "_ctx", ctx)
         if stream is not None:
             _check(lib().rt_set_stream(ctx, C.c_void_p(stream)), ctx)
+        if tuning:
+            self.set_tuning(**tuning)
         d = scene.desc()
         self.light_count = int(d.light_count)
         _check(lib().rt_scene_upload(ctx, C.byref(d)), ctx)
@@ -323,6 +366,16 @@ class Renderer:
         self.__dict__["frameIndex"] = self.frameIndex + 1
         self.previousCamera = self.camera
         return u
+
+    def set_tuning(self, **fields):
+        """rt_set_tuning: the wavefront kernels' scheduling parameters (rt_tuning fields; omitted = default)."""
+        _check(lib().rt_set_tuning(self._ctx, C.byref(_tuning_struct(fields))), self._ctx)
+
+    def tuning(self):
+        """rt_get_tuning: the parameters in effect, defaults resolved."""
+        t = Tuning()
+        _check(lib().rt_get_tuning(self._ctx, C.byref(t)), self._ctx)
+        return {n: getattr(t, n) for n, _ in Tuning._fields_ if n != "reserved"}
 
     def wait(self):
         _check(lib().rt_wait(self._ctx), self._ctx)

@@ -204,6 +204,13 @@ class MaterialOverride(C.Structure):  # Model.swift:11-27
     ]
 
 
+class Tuning(C.Structure):
+    """rt_tuning (include/rt_api.h): the wavefront kernels' scheduling parameters, 0 = default."""
+    _fields_ = [(n, C.c_int32) for n in ("trace_chunk", "finish_chunk", "refill_min", "shade_min", "shade_min_drained",
+                                         "team", "finish_grid_pct", "trace_grid_pct", "shade_blocks", "host_rounds",
+                                         "log", "device_bvh")] + [("reserved", C.c_int32 * 4)]
+
+
 # enums (ShaderTypes.h)
 LightTypeUnused, LightTypeSunlight, LightTypeSpotlight, LightTypePointlight, LightTypeAreaLight = range(5)
 ShadingModePBR, ShadingModeLegacy = 0, 1
@@ -229,7 +236,8 @@ EXPORTED_SYMBOLS = [
     "rt_read_radiance", "rt_read_aux", "rt_tile_count", "rt_pack_tiles", "rt_unpack_tiles",
     "rt_pack_tiles_on", "rt_unpack_tiles_on", "rt_present", "rt_write_png",
     "rt_pack_tiles_host", "rt_unpack_tiles_host",
-    "rt_set_counting", "rt_set_device_spans", "rt_set_graphs", "rt_get_stats", "rt_version", "rt_debug_trace_host",
+    "rt_set_counting", "rt_set_device_spans", "rt_set_graphs", "rt_get_stats", "rt_set_tuning", "rt_get_tuning",
+    "rt_version", "rt_debug_trace_host",
     # rt_scene.h
     "rt_material_override_glass", "rt_scene_new", "rt_scene_free", "rt_scene_last_error",
     "rt_scene_add_obj", "rt_scene_add_usd", "rt_scene_add_procedural", "rt_scene_set_lights", "rt_scene_set_light_intensity",
@@ -277,6 +285,8 @@ def declare(lib):
         "rt_set_device_spans": (st, [vp, C.c_int32]),
         "rt_set_graphs": (st, [vp, C.c_int32]),
         "rt_get_stats": (st, [vp, P(Stats)]),
+        "rt_set_tuning": (st, [vp, P(Tuning)]),
+        "rt_get_tuning": (st, [vp, P(Tuning)]),
         "rt_version": (C.c_char_p, []),
         "rt_debug_trace_host": (st, [P(SceneDesc), P(C.c_float), P(C.c_float), C.c_uint32, C.c_int32, P(C.c_float),
                                      P(C.c_uint32), P(C.c_float), P(C.c_float), P(C.c_uint32), P(C.c_uint32)]),

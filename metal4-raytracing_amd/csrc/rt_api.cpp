@@ -39,7 +39,6 @@ struct MeshInfo {
 struct FrameSlot {
     DevBuf qc, accum, meta, q0, q1, hits, sq, counts, extra, sorted, sort_table, sort_total, params;
     DevBuf depth, gbuffer, counters;
-    DevBuf fpool;      // the pooled finish kernel's path records (wavefront_pool_bytes)
     DevBuf prim_hit;   // wavefront: per pixel, sample 0's last bounce-0 hit (id, u, v) for wf_motion
     WavefrontBuffers wf;
     WfTimeline wft;
@@ -51,8 +50,8 @@ struct FrameSlot {
     bool gbuf_written = false;                  // the slot's last frame wrote the G-buffer (enableDenoiseGBuffer)
     uint64_t seq = 0;                           // frame number (harvest order)
     int gen = 0;                                // geometry generation the frame reads
-    DevBuf* bufs[18] = {&qc, &accum, &meta, &q0, &q1, &hits, &sq, &counts, &extra, &sorted,
-                        &sort_table, &sort_total, &params, &depth, &gbuffer, &counters, &prim_hit, &fpool};
+    DevBuf* bufs[17] = {&qc, &accum, &meta, &q0, &q1, &hits, &sq, &counts, &extra, &sorted,
+                        &sort_table, &sort_total, &params, &depth, &gbuffer, &counters, &prim_hit};
 };
 // Per-frame geometry (what skinning, instance transforms and refit rewrite between frames), in
 // generations used round robin: frames read generation `gcur`; the first update after a frame
@@ -107,7 +106,9 @@ struct rt_ctx {
     std::string err;
     bool counting = false;
     bool spans = false;              // rt_set_device_spans
-    bool graphs = true;              // rt_set_graphs (and RT_GRAPH, read once)
+    bool graphs = true;              // rt_set_graphs
+    rt_tuning tuning_req{};          // rt_set_tuning as given (0 = default)
+    WfTuning tuning;                 // ... resolved
 
     // host scene copies
     std::vector<float4> h_pos, h_nrm;
@@ -306,7 +307,6 @@ static rt_status ensure_wavefront(rt_ctx* c, FrameSlot& fs, size_t own_px, int s
         if ((st = dev_alloc(c, fs.extra, px * 8))) return st;
         W.cap_pixels = px;
     }
-    if (!fs.fpool.p && (st = dev_alloc(c, fs.fpool, wavefront_pool_bytes()))) return st;
     if (c->sort_bins && !fs.sort_table.p) {
         if ((st = dev_alloc(c, fs.sort_table, (size_t)kSortMaxBins * kSortBlocks * 4))) return st;
         if ((st = dev_alloc(c, fs.sort_total, (size_t)kSortMaxBins * 4))) return st;
@@ -336,7 +336,6 @@ static rt_status ensure_wavefront(rt_ctx* c, FrameSlot& fs, size_t own_px, int s
     W.sorted = (float4*)fs.sorted.p;
     W.sort_table = (uint32_t*)fs.sort_table.p;
     W.sort_total = (uint32_t*)fs.sort_total.p;
-    W.fpool = (float4*)fs.fpool.p;
     return RT_OK;
 }
 
@@ -406,7 +405,6 @@ rt_status rt_create(const rt_opts* opts, rt_ctx** out) {
         FAIL((rt_ctx*)nullptr, RT_ERR_INVALID_ARG, "sort_bins must be a power of two in [1024, 4096]");
     }
     if (opts && opts->frames_in_flight > 0) c->max_in_flight = std::min(opts->frames_in_flight, kMaxSlots);
-    if (const char* e = getenv("RT_FRAMES_IN_FLIGHT")) c->max_in_flight = std::max(1, std::min(atoi(e), kMaxSlots));
     hipError_t e = hipSetDevice(c->device);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking);
     for (FrameSlot& f : c->slot) {
@@ -769,8 +767,7 @@ rt_status rt_bvh_build_device(rt_ctx* c) {
     LbvhInput in{(const float4*)g.pos.p, (const uint4*)c->d_tri_info.p, (const float*)g.inst.p, n};
     // PLOC topology + SAH-DP collapse by default; RT_DEVICE_BVH=lbvh selects the radix tree, whose
     // faster build wins for a small scene rebuilt every frame
-    static const bool lbvh_tree = getenv("RT_DEVICE_BVH") && !std::strcmp(getenv("RT_DEVICE_BVH"), "lbvh");
-    in.ploc = lbvh_tree ? 0 : 1;
+    in.ploc = c->tuning_req.device_bvh == 1 ? 0 : 1;   // rt_tuning.device_bvh: 1 = the LBVH radix tree
     LbvhOutput out{(Bvh8Node*)g.nodes.p, (float*)g.node_box.p, (uint32_t*)c->d_slot_to_tri.p,
                    (uint16_t*)g.tri_bin.p, (uint32_t*)c->d_levels.p, c->h_lbvh};
     LbvhResult res;
@@ -1120,10 +1117,9 @@ rt_status rt_render_frame(rt_ctx* c, const Uniforms* U, const rt_tile_set* tiles
         // finish threshold: with frames in flight the next frames' bulk rounds overlap this
         // frame's tail, so more bulk rounds and a shorter tail pay (kTailInFlight: C3g, 2 in
         // flight 1.25M paths against the one-frame-at-a-time optimum of 4M; 3 in flight 1M)
-        static const bool tail_env = getenv("RT_TAIL_RAYS") != nullptr;
-        const int tail = c->tail_paths ? c->tail_paths : (nfl > 1 && !tail_env ? kTailInFlight[nfl] : 0);
-        if (own > 0 && !run_wavefront(S, P, F.wf, own, c->counting, c->spans, tail, c->sort_bins, extra_pass, nfl, stream,
-                                      cross ? prev.done : nullptr, &F.wft, &F.wfs, &err, c->graphs))
+        const int tail = c->tail_paths ? c->tail_paths : (nfl > 1 ? kTailInFlight[nfl] : 0);
+        if (own > 0 && !run_wavefront(S, P, F.wf, c->tuning, own, c->counting, c->spans, tail, c->sort_bins, extra_pass,
+                                      nfl, stream, cross ? prev.done : nullptr, &F.wft, &F.wfs, &err, c->graphs))
             FAIL(c, RT_ERR_HIP, std::string("wavefront: ") + (err ? err : "?"));
         if (own == 0 && cross) HIPC(c, hipStreamWaitEvent(stream, prev.done, 0));
     } else {
@@ -1360,6 +1356,59 @@ rt_status rt_set_counting(rt_ctx* c, int32_t enabled) {
 rt_status rt_set_device_spans(rt_ctx* c, int32_t enabled) {
     if (!c) FAIL(c, RT_ERR_INVALID_ARG, "null ctx");
     c->spans = enabled != 0;
+    return RT_OK;
+}
+
+// rt_tuning (0 = default) -> the kernels' resolved parameters
+static WfTuning resolve_tuning(const rt_tuning& t) {
+    WfTuning w;
+    if (t.trace_chunk > 0) w.chunk = t.trace_chunk;
+    if (t.finish_chunk > 0) w.fchunk = t.finish_chunk;
+    if (t.refill_min > 0) w.refill_min = t.refill_min;
+    if (t.shade_min > 0) w.shade_min = t.shade_min;
+    if (t.shade_min_drained != 0) w.shade_min_x = t.shade_min_drained;
+    w.team = t.team == 0 ? -1 : t.team == 1 ? 0 : t.team;
+    if (t.finish_grid_pct > 0) w.finish_frac = std::min(t.finish_grid_pct, 100);
+    if (t.trace_grid_pct > 0) w.trace_frac = std::min(t.trace_grid_pct, 100);
+    if (t.shade_blocks > 0) w.shade_blocks = (unsigned)std::max(8, t.shade_blocks) / 8u * 8u;
+    w.host_ctl = t.host_rounds != 0;
+    w.log = std::max(0, t.log);
+    return w;
+}
+
+rt_status rt_set_tuning(rt_ctx* c, const rt_tuning* t) {
+    if (!c) FAIL(c, RT_ERR_INVALID_ARG, "null context");
+    rt_tuning v{};
+    if (t) v = *t;
+    if (v.team != 0 && v.team != 1 && v.team != 2 && v.team != 4 && v.team != 8)
+        FAIL(c, RT_ERR_INVALID_ARG, "rt_tuning.team must be 0 (default), 1 (off), 2, 4 or 8");
+    if (v.trace_chunk < 0 || v.finish_chunk < 0 || v.refill_min < 0 || v.refill_min > 64 || v.shade_min < 0 ||
+        v.shade_min > 64 || v.shade_min_drained > 64 || v.shade_min_drained < -100 || v.finish_grid_pct < 0 ||
+        v.trace_grid_pct < 0 || v.shade_blocks < 0 || v.log < 0 || v.log > 2 || v.device_bvh < 0 || v.device_bvh > 1)
+        FAIL(c, RT_ERR_INVALID_ARG, "rt_tuning field out of range");
+    // frames already in flight keep the parameters they were enqueued with (their graphs' keys)
+    c->tuning_req = v;
+    c->tuning = resolve_tuning(v);
+    return RT_OK;
+}
+
+rt_status rt_get_tuning(const rt_ctx* c, rt_tuning* out) {
+    if (!c || !out) FAIL((rt_ctx*)nullptr, RT_ERR_INVALID_ARG, "null argument");
+    const WfTuning& w = c->tuning;
+    rt_tuning t{};
+    t.trace_chunk = w.chunk;
+    t.finish_chunk = w.fchunk;
+    t.refill_min = w.refill_min;
+    t.shade_min = w.shade_min;
+    t.shade_min_drained = w.shade_min_x;
+    t.team = c->tuning_req.team;
+    t.finish_grid_pct = w.finish_frac;
+    t.trace_grid_pct = w.trace_frac;
+    t.shade_blocks = (int32_t)w.shade_blocks;
+    t.host_rounds = w.host_ctl ? 1 : 0;
+    t.log = w.log;
+    t.device_bvh = c->tuning_req.device_bvh;
+    *out = t;
     return RT_OK;
 }
 

@@ -74,17 +74,6 @@ __device__ __forceinline__ void block_flush_counters(unsigned long long* counter
     }
 }
 
-// The same flush per wave (no block barrier): for kernels whose waves leave at different times.
-__device__ __forceinline__ void wave_flush_counters(unsigned long long* counters, uint32_t closest, uint32_t shadow,
-                                                    uint32_t nodes, uint32_t tris, uint32_t paths, bool overflow) {
-    const unsigned long long v[6] = {wave_sum(closest), wave_sum(shadow), wave_sum(nodes), wave_sum(tris), wave_sum(paths),
-                                     __ballot(overflow) != 0ull ? 1ull : 0ull};
-    const uint32_t lane = threadIdx.x & 63u;
-    #pragma unroll
-    for (int k = 0; k < 6; ++k)
-        if (lane == (uint32_t)k && v[k]) atomicAdd(&counters[cnt_word(k, blockIdx.x & (kCntReplicas - 1))], v[k]);
-}
-
 void launch_megakernel(const DevScene& S, const FrameParams& P, int nblocks, bool count, hipStream_t stream);
 
 // Wavefront pipeline (rt_wavefront.hip): path state SoA indexed by path id
@@ -136,9 +125,6 @@ struct WavefrontBuffers {
     float4* sorted = nullptr;
     uint32_t* sort_table = nullptr;
     uint32_t* sort_total = nullptr;
-    // pooled finish kernel (wf_finish_pool): kPoolRecs path records of 128 B per wave of its
-    // resident grid (wavefront_pool_bytes)
-    float4* fpool = nullptr;
     size_t cap_paths = 0;         // base + extra paths
     size_t cap_pixels = 0;
     hipEvent_t ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
@@ -180,6 +166,26 @@ struct WfFrameStats {
     int finish_launches;
     int graph_mode;                 // kGraph*: how the frame was submitted
 };
+// The wavefront kernels' scheduling parameters, resolved (rt_tuning in rt_api.h: 0 = default there;
+// rt_api.cpp fills these in).  Per context: the library reads no environment variable for them.
+struct WfTuning {
+    uint32_t tail = 4194304;      // finish threshold one frame at a time (frames in flight: rt_api.cpp kTailInFlight)
+    int refill_min = 8;           // a wave refills once this many of its lanes are idle
+    int chunk = 64;               // rays per chunk grab of the traversal kernel
+    int fchunk = 64;              // paths per chunk grab of the finish kernel
+    int shade_min = 24;           // the finish kernel shades once this many lanes wait
+    int shade_min_x = -50;        // the same once its queue ran out (< 0: that percentage of the wave's busy lanes)
+    int team = -1;                // finish drain lanes per query (-1: 4 for frames of kTeamAutoMin .. kTeamAutoPaths
+                                  // base paths, off otherwise; 0: off; 2 / 4 / 8)
+    int finish_frac = 0;          // percent of the resident grid the finish launch takes (0 = by frames in flight)
+    int trace_frac = 0;           // percent of the resident grid the bulk wf_trace launches take (0 = by frames in flight)
+    int log = 0;                  // 1: per-round queue sizes, stage times and finish diagnostics on stderr;
+                                  // 2: also the finish paths' segment counts (one atomic per path)
+    bool host_ctl = false;        // host-driven rounds (queue sizes read back every round)
+    unsigned shade_blocks = 2048; // wf_shade grid (grid-stride loop), a multiple of 8: 1.6 waves of the resident
+                                  // grid leaves CUs to the other frames in flight
+};
+
 // Runs one frame; returns false on a HIP error (message in *err).
 // tail_paths: finish-kernel threshold (0 = default / RT_TAIL_RAYS).
 // Host-side record of a frame enqueued with device-side control: events between the launches and
@@ -213,13 +219,12 @@ constexpr int kGraphEager = 0, kGraphReplay = 1, kGraphCapture = 2, kGraphFallba
 // kernel takes 1 / in_flight of the resident grid and leaves the rest to the other frames).  prev_done (may be null): the previous frame, in flight on another
 // stream; the extra-sample pass and the resolve (which read its accumulation and motion outputs)
 // are ordered after it, everything before them overlaps it.
-bool run_wavefront(const DevScene& S, const FrameParams& P, WavefrontBuffers& W, int own_tiles, bool count, bool spans,
-                   int tail_paths, int sort_bins, bool extra_pass, int in_flight, hipStream_t stream,
-                   hipEvent_t prev_done, WfTimeline* tl, WfFrameStats* fs, const char** err, bool graphs = true);
+bool run_wavefront(const DevScene& S, const FrameParams& P, WavefrontBuffers& W, const WfTuning& tu, int own_tiles,
+                   bool count, bool spans, int tail_paths, int sort_bins, bool extra_pass, int in_flight,
+                   hipStream_t stream, hipEvent_t prev_done, WfTimeline* tl, WfFrameStats* fs, const char** err,
+                   bool graphs = true);
 bool wavefront_collect(const WavefrontBuffers& W, WfTimeline& T, WfFrameStats* fs, const char** err);
 size_t wavefront_queue_entries(size_t paths, int max_extra);
-// bytes of WavefrontBuffers::fpool: the pooled finish kernel's path records for its resident grid
-size_t wavefront_pool_bytes();
 
 // Packed-tile layout of the multi-GPU gather: element i of a rank's packed buffer is pixel
 // (i % T, (i / T) % T) of its (i / T^2)-th own tile; own tile k is tile id rank + k * nranks.

@@ -34,60 +34,9 @@ namespace rt {
 namespace {
 
 // frames of kTeamAutoMin .. kTeamAutoPaths base paths use the finish kernel's team drain by default
-// (RT_TEAM): the C3g rank shares gain, the tiny C1 frame (65K paths) loses 7.5 %
+// (rt_tuning.team = 0): the C3g rank shares gain, the tiny C1 frame (65K paths) loses 7.5 %
 constexpr uint32_t kTeamAutoPaths = 2500000u;
 constexpr uint32_t kTeamAutoMin = 262144u;
-
-static int env_int(const char* name, int dflt) {
-    const char* e = getenv(name);
-    return e ? atoi(e) : dflt;
-}
-
-// The scheduling parameters of the wavefront kernels: defaults from the C3g sweeps of DESIGN.md §3,
-// each overridable by one environment variable for tuning runs (read once).
-struct Tuning {
-    uint32_t tail;     // RT_TAIL_RAYS: finish threshold, one frame at a time (frames in flight: rt_api.cpp)
-    int refill_min;    // RT_REFILL_MIN: a wave refills once this many of its lanes are idle
-    int chunk;         // RT_CHUNK: rays per chunk grab of the traversal kernel
-    int fchunk;        // RT_FCHUNK: paths per chunk grab of the finish kernel
-    int shade_min;     // RT_SHADE_MIN: the finish kernel shades once this many lanes wait
-    int shade_min_x;   // RT_SHADE_MIN_X: the same once the finish queue is exhausted (< 0: that percentage of the wave's busy lanes)
-    int team;          // RT_TEAM: finish drain, lanes per query once a wave holds <= 64 / team paths (0 / 1: off;
-                       // unset: 4 for frames of kTeamAutoMin .. kTeamAutoPaths paths, off otherwise)
-    int finish_frac;   // RT_FINISH_FRAC: percent of the resident grid the finish launch takes (0 = by frames in flight)
-    int trace_frac;    // RT_TRACE_FRAC: percent of the resident grid the persistent wf_trace launches take (0 = by frames in flight)
-    int log;           // RT_WF_LOG=1: per-round queue sizes, stage times and finish diagnostics on stderr
-                       // (=2 also the finish paths' segment counts: one atomic per path, slows the launch)
-    bool host_ctl;     // RT_WF_HOST=1: host-driven rounds (queue sizes read back every round)
-    int pool;          // RT_FINISH_POOL: 1 = the pooled finish kernel (wf_finish_pool), 0 = wf_finish_step
-    int consol;        // RT_CONSOL: wf_finish_step consolidates its block's waves every this many iterations
-                       // once every wave's queue ran out (0 = off)
-    unsigned shade_blocks;   // RT_SHADE_BLOCKS: wf_shade grid (grid-stride loop), a multiple of 8; 2048 (1.6 waves
-                             // of the resident grid) leaves CUs to the other frames in flight: C3g four in
-                             // flight +1.3-2.2 % against 8192, one frame alone the same
-};
-static const Tuning& tuning() {
-    static const Tuning t = [] {
-        Tuning v;
-        v.tail = (uint32_t)env_int("RT_TAIL_RAYS", 4194304);
-        v.refill_min = env_int("RT_REFILL_MIN", 8);
-        v.chunk = std::max(1, env_int("RT_CHUNK", 64));
-        v.fchunk = std::max(1, env_int("RT_FCHUNK", 64));
-        v.shade_min = env_int("RT_SHADE_MIN", 24);
-        v.shade_min_x = env_int("RT_SHADE_MIN_X", -50);
-        v.team = env_int("RT_TEAM", -1);
-        if (v.team != -1 && v.team != 2 && v.team != 4 && v.team != 8) v.team = 0;
-        v.finish_frac = std::min(env_int("RT_FINISH_FRAC", 0), 100);
-        v.trace_frac = std::min(env_int("RT_TRACE_FRAC", 0), 100);
-        v.log = env_int("RT_WF_LOG", 0);
-        v.host_ctl = env_int("RT_WF_HOST", 0) != 0;
-        v.shade_blocks = (unsigned)std::max(8, env_int("RT_SHADE_BLOCKS", 2048)) / 8u * 8u;
-        v.pool = env_int("RT_FINISH_POOL", 0);
-        v.consol = std::max(0, env_int("RT_CONSOL", 0));
-        return v;
-    }();
-    return t;
-}
 
 __device__ __forceinline__ uint32_t lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
 __device__ __forceinline__ uint32_t mbcnt64(unsigned long long m) {
@@ -238,10 +187,9 @@ struct WfParams {
     int shade_min_x;       // wf_finish_step: the same once the launch's queue is exhausted (< 0: percent of busy lanes)
     int team;              // wf_finish_step: lanes per query in the drain (0: no team drain)
     int fchunk;            // wf_finish_step: paths per chunk grab
-    int pool;              // the finish launch runs wf_finish_pool (paths in per-wave record pools)
-    int consol;            // wf_finish_step (no team): block consolidation period in iterations (0 = off)
     int finish_frac;       // percent of the resident grid the finish launch takes
     int trace_frac;        // percent of the resident grid the bulk wf_trace launches take
+    unsigned shade_blocks; // wf_shade grid
     int spans;             // record device-clock launch spans (rt_set_device_spans)
     int dev_ctl;           // device-side control (enqueue_wavefront): kernels read their queue sizes from
                            // the counters and skip once the live count fell below `tail`
@@ -373,25 +321,6 @@ __device__ __forceinline__ uint32_t dense_entry(const QueueShards& qs, uint32_t 
     const uint32_t i = g - start;
     return k * seg_cap + (back ? seg_cap - 1u - i : i);
 }
-// The same from the shard counts held in LDS (L[k] at [k], S[k] at [kShards + k]): the finish
-// kernel reads them only at refill, so they need not occupy registers across its shading code.
-__device__ __forceinline__ uint32_t dense_entry_lds(const uint32_t* qsl, uint32_t g, uint32_t seg_cap) {
-    uint32_t ltot = 0;
-    #pragma unroll
-    for (int k = 0; k < kShards; ++k) ltot += qsl[k];
-    const bool back = g >= ltot;
-    if (back) g -= ltot;
-    uint32_t k = 0, start = 0, acc = 0;
-    #pragma unroll
-    for (int j = 0; j < kShards - 1; ++j) {
-        acc += back ? qsl[kShards + j] : qsl[j];
-        const bool past = g >= acc;
-        k = past ? (uint32_t)(j + 1) : k;
-        start = past ? acc : start;
-    }
-    const uint32_t i = g - start;
-    return k * seg_cap + (back ? seg_cap - 1u - i : i);
-}
 #ifndef RT_LONG_FIRST
 #define RT_LONG_FIRST 1   // 0: every continuation ray to the front (one-sided queues; A/B builds)
 #endif
@@ -442,15 +371,7 @@ struct Trav {
     uint32_t best_id, g_base, g_hits, t_base, t_mask, t_valid;
     bool g_flip, hit_any;
     int sp;
-#ifdef RT_XP_DUP
-    uint32_t xp;   // cost-attribution experiment: sink of the duplicated tests
-#endif
 };
-#ifdef RT_XP_DUP
-#define RT_XP_SINK(T, dst) do { if ((T).xp == 0x9e3779b9u) (dst) = 1u; } while (0)
-#else
-#define RT_XP_SINK(T, dst) do { } while (0)
-#endif
 
 __device__ __forceinline__ void trav_start(Trav& T, f3 o, f3 d, float tmax) {
     T.R = ray_setup(o, d);
@@ -464,9 +385,6 @@ __device__ __forceinline__ void trav_start(Trav& T, f3 o, f3 d, float tmax) {
     T.t_mask = 0;
     T.sp = 0;
     T.hit_any = false;
-#ifdef RT_XP_DUP
-    T.xp = 0;
-#endif
 }
 
 // One iteration of a query: up to two triangles of the last node test (both fetched before either
@@ -528,15 +446,6 @@ __device__ __forceinline__ bool trav_step(const DevScene& S, Trav& T, bool any, 
         const float4 b0 = tp1[0], b1 = tp1[1], b2 = tp1[2];   // = a when the lane has one triangle
         if (COUNT) tc.tris += two ? 2u : 1u;
         float t, u, v, dt;
-#if defined(RT_XP_DUP) && (RT_XP_DUP & 2)
-        {   // the first triangle's test once more on an opaque copy (its cost, not its result)
-            float4 c0 = a0, c1 = a1, c2 = a2;
-            asm volatile("" : "+v"(c0.x), "+v"(c0.y), "+v"(c0.z), "+v"(c1.x), "+v"(c1.y), "+v"(c1.z), "+v"(c2.x), "+v"(c2.y), "+v"(c2.z));
-            float t2 = 0, u2 = 0, v2 = 0, d2 = 0;
-            const bool h2 = intersect_triangle_vw(T.R.pre, T.R.o, ld3(c0), ld3(c1), ld3(c2), 0.0f, fminf(cull, T.best), &t2, &u2, &v2, &d2);
-            T.xp ^= h2 ? __float_as_uint(t2) ^ __float_as_uint(u2) : 1u;
-        }
-#endif
         if (RT_ISECT(ld3(a0), ld3(a1), ld3(a2))) {
             const uint32_t id = __float_as_uint(a0.w);
             if (any) {
@@ -568,24 +477,6 @@ __device__ __forceinline__ bool trav_step(const DevScene& S, Trav& T, bool any, 
         const uint32_t ni = next_node(T, stack, overflow);
         if (COUNT) tc.nodes++;
         const NodeWords w = load_node8(S.nodes8, ni);
-#if defined(RT_XP_DUP) && (RT_XP_DUP & 1)
-        {   // the node test once more on an opaque copy of its words (its cost, not its result)
-            NodeWords c = w;
-            asm volatile("" : "+v"(c.h0.x), "+v"(c.h0.y), "+v"(c.h0.z), "+v"(c.h0.w), "+v"(c.h1.x), "+v"(c.h1.y), "+v"(c.h1.z),
-                         "+v"(c.qx.x), "+v"(c.qx.y), "+v"(c.qx.z), "+v"(c.qx.w), "+v"(c.qy.x), "+v"(c.qy.y), "+v"(c.qy.z),
-                         "+v"(c.qy.w), "+v"(c.qz.x), "+v"(c.qz.y), "+v"(c.qz.z), "+v"(c.qz.w));
-            uint32_t a, b, cc, d, e;
-            bool f;
-            test_node8_words(c, T.R, 0.0f, fminf(cull, T.best), a, b, cc, d, e, f);
-            T.xp ^= a ^ (b << 3) ^ cc ^ d ^ e ^ (f ? 7u : 0u);
-        }
-#endif
-#if defined(RT_XP_DUP) && (RT_XP_DUP & 4)
-        {   // one more node's words loaded (a neighbour of this one) and consumed: the cost of the load alone
-            const NodeWords w2 = load_node8(S.nodes8, ni ^ 1u);
-            asm volatile("" :: "v"(w2.h0.x), "v"(w2.h1.x), "v"(w2.qx.x), "v"(w2.qy.x), "v"(w2.qz.x));
-        }
-#endif
         test_node8_words(w, T.R, 0.0f, fminf(cull, T.best), T.g_hits, T.t_mask, T.t_valid, T.g_base, T.t_base, T.g_flip);
     }
     return tdone || (T.t_mask == 0u && T.g_hits == 0u && T.sp == 0);
@@ -1058,7 +949,6 @@ wf_trace(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int cur, in
             }
         }
     }
-    RT_XP_SINK(T, Q.W.counts[cslot(kCntDiagSegs)]);
     ts_end(Q, ts, &ts_done);
     flush_counters(P, ANY ? 0 : rays, ANY ? rays : 0, 0, tc, COUNT, overflow, true);
 }
@@ -1084,38 +974,17 @@ wf_finish_step(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int c
     __shared__ float lds_sray[6][kBlock];   // each lane's shadow ray (origin, direction)
     int* stack = &lds_stack[threadIdx.x];
     __shared__ uint32_t ts_done;
-    // block consolidation (Q.consol, !TEAM): waves whose queue ran out, the waves' busy lanes at a
-    // consolidation round (0xffffffff: the wave has left), and the 16-lane transfer buffer
-    __shared__ uint32_t lds_nexh;
-    __shared__ uint32_t lds_cnt[kBlock / 64];
-    __shared__ uint32_t lds_xbuf[32][16];
-    __shared__ uint32_t lds_qs[2 * kShards];   // the finish queue's shard parts (dense_entry_lds)
-    if (threadIdx.x == 0) {
-        ts_done = 0u;
-        lds_nexh = 0u;
-    }
+    if (threadIdx.x == 0) ts_done = 0u;
     ts_start(Q, ts);
-    uint32_t n;
-    {
-        const QueueShards qs = load_queue(Q.W.counts, cur, Q.seg_cap);   // front parts first: the likely-long paths
-        n = queue_len(qs);
-        #pragma unroll
-        for (int k = 0; k < kShards; ++k)
-            if (threadIdx.x == (unsigned)k) {
-                lds_qs[k] = qs.L[k];
-                lds_qs[kShards + k] = qs.S[k];
-            }
-    }
-    const ShadeTabs halton = load_tabs(S, lds_halton, lds_mat);   // ends with a block barrier (lds_qs written)
+    const ShadeTabs halton = load_tabs(S, lds_halton, lds_mat);   // ends with a block barrier
     const Uniforms& U = P.U;
+    const QueueShards qs = load_queue(Q.W.counts, cur, Q.seg_cap);   // front parts first: the likely-long paths
+    const uint32_t n = queue_len(qs);
     if (Q.dev_ctl) stat_add(Q, kStatFinish, 1u);
     if (Q.dev_ctl && n > 0) stat_add(Q, kStatRounds, 1u);
     const float4* qin = Q.W.q[cur];
     const uint32_t kChunk = (uint32_t)Q.fchunk;   // paths per grab
     constexpr int kIdle = 0, kClosest = 1, kShadow = 2, kReady = 3;
-    const bool consol = !TEAM && Q.consol > 0;
-    bool all_exh = false;     // every wave of the block has exhausted its queue (consolidation rounds run)
-    int since = 0;            // iterations since the last round
     TraceCounters tc{0, 0, 0};
     bool overflow = false;
     uint32_t n_closest = 0, n_shadow = 0;
@@ -1182,7 +1051,6 @@ wf_finish_step(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int c
             base = ((__builtin_amdgcn_readfirstlane(base) << 3) | (blockIdx.x & 7u)) * kChunk;
             if (base >= n) {
                 exhausted = true;
-                if (consol && lane_id() == 0) atomicAdd(&lds_nexh, 1u);
                 if (Q.diag && lane_id() == 0) {
                     RT_DX[0] = iters;
                     RT_DX[1] = (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_start);
@@ -1197,7 +1065,7 @@ wf_finish_step(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int c
             if (mode == kIdle) {
                 const uint32_t g = wnext + mbcnt64(idle);
                 if (g < wend) {
-                    const uint32_t e = dense_entry_lds(lds_qs, g, Q.seg_cap);
+                    const uint32_t e = dense_entry(qs, g, Q.seg_cap);
                     const float4* src = qin + 2 * (size_t)e;
                     const float4 o = (RT_TRACE_NT & 2) ? ld_stream(&src[0]) : src[0];
                     const float4 d = (RT_TRACE_NT & 2) ? ld_stream(&src[1]) : src[1];
@@ -1296,142 +1164,7 @@ wf_finish_step(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int c
             if (Q.diag) t_shade += __builtin_amdgcn_s_memrealtime() - ts0;
         }
 
-        // ---- block consolidation (round 5).  Once every wave of the block has run out of queue, the
-        // waves drain their paths with fewer and fewer busy lanes, and each wave-instruction serves
-        // those few.  Every Q.consol iterations the live waves of the block meet (block barriers: a
-        // wave that has left no longer counts in them) and the busiest one takes over the paths of
-        // the others while they fit its idle lanes, each path with its whole state (query included:
-        // traversal registers, LDS stack entries and shadow ray); a wave left without paths ends.
-        // Every wave computes the same plan from the same counts, so all run the same barriers.  A
-        // path's arithmetic does not depend on the lane it runs in: the same bits.
-        if (consol && exhausted) {
-            if (!all_exh) all_exh = __builtin_amdgcn_readfirstlane(lds_nexh) == kBlock / 64;
-            if (all_exh && ++since >= Q.consol) {
-                since = 0;
-                const unsigned long long busy0 = __ballot(mode != kIdle);
-                const uint32_t wv = threadIdx.x >> 6;
-                __syncthreads();
-                if (lane_id() == 0) lds_cnt[wv] = (uint32_t)__popcll(busy0);
-                __syncthreads();
-                // the plan, in wave-uniform scalars (every array index a compile-time constant: a
-                // run-time index would put the array in scratch)
-                constexpr uint32_t kGone = 0xffffffffu;
-                uint32_t c[kBlock / 64];
-                #pragma unroll
-                for (int w = 0; w < kBlock / 64; ++w) c[w] = __builtin_amdgcn_readfirstlane(lds_cnt[w]);
-                // receiver: the busiest live wave (lowest index on ties)
-                uint32_t recv = 0, cr = 0;
-                bool any = false;
-                #pragma unroll
-                for (int w = 0; w < kBlock / 64; ++w)
-                    if (c[w] != kGone && (!any || c[w] > cr)) {
-                        recv = (uint32_t)w;
-                        cr = c[w];
-                        any = true;
-                    }
-                // donors: the other waves with paths, fewest first, while they fit its idle lanes;
-                // don_off[w] = the first receiving idle-lane rank of donor w (kGone: not a donor)
-                uint32_t don_off[kBlock / 64];
-                #pragma unroll
-                for (int w = 0; w < kBlock / 64; ++w) don_off[w] = kGone;
-                uint32_t cap = 64u - cr, taken = 0, assigned = 0;
-                bool stop = false;
-                #pragma unroll
-                for (int it = 0; it < kBlock / 64 - 1; ++it) {
-                    uint32_t bw = kBlock / 64, bc = kGone;
-                    #pragma unroll
-                    for (int w = 0; w < kBlock / 64; ++w)
-                        if ((uint32_t)w != recv && c[w] != kGone && c[w] > 0u && !((assigned >> w) & 1u) && c[w] < bc) {
-                            bw = (uint32_t)w;
-                            bc = c[w];
-                        }
-                    if (stop || bw == kBlock / 64 || bc > cap) {
-                        stop = true;
-                    } else {
-                        assigned |= 1u << bw;
-                        #pragma unroll
-                        for (int w = 0; w < kBlock / 64; ++w)
-                            if ((uint32_t)w == bw) don_off[w] = taken;
-                        taken += bc;
-                        cap -= bc;
-                    }
-                }
-                const uint32_t my_rank = mbcnt64(busy0);       // donor lanes: rank among the busy lanes
-                const uint32_t idle_rank = mbcnt64(~busy0);    // receiver lanes: rank among the idle lanes
-                #pragma unroll
-                for (int w = 0; w < kBlock / 64; ++w) {
-                    if (don_off[w] == kGone) continue;
-                    for (uint32_t ch = 0; ch * 16u < c[w]; ++ch) {
-                        if ((int)wv == w && mode != kIdle && my_rank >= ch * 16u && my_rank < ch * 16u + 16u) {
-                            const uint32_t k = my_rank - ch * 16u;
-                            const uint32_t v[32] = {pid, meta.x, meta.y, meta.w,
-                                                    __float_as_uint(p.color.x), __float_as_uint(p.color.y), __float_as_uint(p.color.z),
-                                                    __float_as_uint(p.accum.x), __float_as_uint(p.accum.y), __float_as_uint(p.accum.z),
-                                                    pack_state(p.bounce, p.tpass, p.step),
-                                                    __float_as_uint(rayO.x), __float_as_uint(rayO.y), __float_as_uint(rayO.z),
-                                                    __float_as_uint(rayD.x), __float_as_uint(rayD.y), __float_as_uint(rayD.z),
-                                                    __float_as_uint(contrib.x), __float_as_uint(contrib.y), __float_as_uint(contrib.z),
-                                                    __float_as_uint(T.best), __float_as_uint(T.bu), __float_as_uint(T.bv),
-                                                    __float_as_uint(T.bdet), T.best_id, T.g_base, T.g_hits, T.t_base, T.t_mask,
-                                                    T.t_valid,
-                                                    (uint32_t)mode | (T.g_flip ? 4u : 0u) | (T.hit_any ? 8u : 0u) | (next ? 16u : 0u) |
-                                                        ((uint32_t)T.sp << 8) | (min(segs, 0xffffu) << 16),
-                                                    threadIdx.x};
-                            #pragma unroll
-                            for (int q = 0; q < 32; ++q) lds_xbuf[q][k] = v[q];
-                            mode = kIdle;
-                        }
-                        __syncthreads();
-                        const uint32_t first = don_off[w] + ch * 16u, cnt = min(16u, c[w] - ch * 16u);
-                        if (wv == recv && !((busy0 >> lane_id()) & 1ull) && idle_rank >= first && idle_rank < first + cnt) {
-                            const uint32_t k = idle_rank - first;
-                            uint32_t v[32];
-                            #pragma unroll
-                            for (int q = 0; q < 32; ++q) v[q] = lds_xbuf[q][k];
-                            pid = v[0];
-                            meta = make_uint4(v[1], v[2], 0u, v[3]);
-                            p.color = mk3(__uint_as_float(v[4]), __uint_as_float(v[5]), __uint_as_float(v[6]));
-                            p.accum = mk3(__uint_as_float(v[7]), __uint_as_float(v[8]), __uint_as_float(v[9]));
-                            p.bounce = (int)(v[10] & 0xffu);
-                            p.tpass = (int)((v[10] >> 8) & 0xffu);
-                            p.step = (int)(v[10] >> 16);
-                            rayO = mk3(__uint_as_float(v[11]), __uint_as_float(v[12]), __uint_as_float(v[13]));
-                            rayD = mk3(__uint_as_float(v[14]), __uint_as_float(v[15]), __uint_as_float(v[16]));
-                            contrib = mk3(__uint_as_float(v[17]), __uint_as_float(v[18]), __uint_as_float(v[19]));
-                            T.best = __uint_as_float(v[20]);
-                            T.bu = __uint_as_float(v[21]);
-                            T.bv = __uint_as_float(v[22]);
-                            T.bdet = __uint_as_float(v[23]);
-                            T.best_id = v[24];
-                            T.g_base = v[25];
-                            T.g_hits = v[26];
-                            T.t_base = v[27];
-                            T.t_mask = v[28];
-                            T.t_valid = v[29];
-                            const uint32_t fl = v[30], src = v[31];
-                            mode = (int)(fl & 3u);
-                            T.g_flip = (fl & 4u) != 0u;
-                            T.hit_any = (fl & 8u) != 0u;
-                            next = (fl & 16u) != 0u;
-                            T.sp = (int)((fl >> 8) & 0xffu);
-                            segs = fl >> 16;
-                            for (int q = 0; q < T.sp; ++q) stack[q * kBlock] = lds_stack[q * kBlock + src];
-                            #pragma unroll
-                            for (int q = 0; q < 6; ++q) lds_sray[q][threadIdx.x] = lds_sray[q][src];
-                            if (mode == kShadow)
-                                T.R = ray_setup(mk3(lds_sray[0][threadIdx.x], lds_sray[1][threadIdx.x], lds_sray[2][threadIdx.x]),
-                                                mk3(lds_sray[3][threadIdx.x], lds_sray[4][threadIdx.x], lds_sray[5][threadIdx.x]));
-                            else
-                                T.R = ray_setup(rayO, rayD);
-                        }
-                        __syncthreads();
-                    }
-                }
-                // a wave left without paths leaves the loop at its next refill (its queue has run out)
-            }
-        }
     }
-    if (consol && lane_id() == 0) lds_cnt[threadIdx.x >> 6] = 0xffffffffu;   // this wave has left: no party to later rounds
 
     // ---- team drain (Q.team lanes per query).  The queue has run out and this wave holds at most
     // 64 / team paths: each moves to a team leader (lane team * r) and the team's lanes traverse its
@@ -1683,304 +1416,6 @@ wf_finish_step(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int c
         }
     }
 #undef RT_DX
-    RT_XP_SINK(T, Q.W.counts[cslot(kCntDiagSegs)]);
-    ts_end(Q, ts, &ts_done);
-    if (consol)   // waves leave at different times: no block barrier in the flush
-        wave_flush_counters(P.counters, n_closest, n_shadow, COUNT ? tc.nodes : 0u, COUNT ? tc.tris : 0u, 0u, overflow);
-    else
-        flush_counters(P, n_closest, n_shadow, 0, tc, COUNT, overflow);
-}
-
-// ---- finish, pooled: paths decoupled from lanes (round 5) ------------------------------------------------
-// wf_finish_step binds a path to a lane until the path ends: a lane whose closest hit is found
-// waits (kReady) until its wave shades, and a shading pass runs with the ~22 waiting lanes of 64
-// (profiles/r04_finish_experiments.txt; 28 % VALU lane utilisation over the launch).  Here a wave
-// owns kPoolRecs path records in global memory (128 B each, one cache line) and three rings of
-// record ids in LDS: free records, queries to trace (closest or shadow), and hits to shade.  A lane
-// whose query ends writes the hit into the path's record, pushes the record to the shade ring and
-// takes the next query at once; the wave shades once 64 hits are pending (or, after its queue ran
-// out, a share of what is left), all 64 lanes shading one record each while the traversing lanes
-// keep their queries.  Per path the operations run in the reference's order (shade, shadow ray,
-// next segment), so every path's result is bit for bit wf_finish_step's.  Records are only ever
-// touched by their own wave, in program order: no cross-wave synchronisation.
-//   record: [0] ray origin, w = path id   [1] ray direction, w = bounce | tpass << 8 | step << 16
-//           [2] throughput colour         [3] closest hit (t, id, u, v)
-//           [4] shadow origin, w = tmax   [5] shadow direction, w = path id | next ray << 31
-//           [6] shadow contribution       [7] (pixel, sample, Halton index)
-constexpr int kPoolRecs = 256;   // path records per wave (ring indices are one byte)
-constexpr int kRecF4 = 8;        // float4 words per record
-
-template <bool COUNT, bool FULL>
-__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 4)))
-wf_finish_pool(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int cur, int ts) {
-    const FrameParams& P = *Pp;   // per-frame parameters in device memory
-    if (cur < 0) cur = (int)__builtin_amdgcn_readfirstlane(Q.W.counts[cslot(kCntFinishQ)]);   // dev_ctl
-    __shared__ int lds_stack[kStackSize * kBlock];
-    __shared__ HaltonDim lds_halton[kHaltonLds];
-    __shared__ MatRec lds_mat[kMatLds];
-    __shared__ uint8_t lds_free[kBlock / 64][kPoolRecs];
-    __shared__ uint8_t lds_shade[kBlock / 64][kPoolRecs];
-    __shared__ uint16_t lds_trace[kBlock / 64][kPoolRecs];   // record id | 0x100 for a shadow query
-    int* stack = &lds_stack[threadIdx.x];
-    __shared__ uint32_t ts_done;
-    if (threadIdx.x == 0) ts_done = 0u;
-    ts_start(Q, ts);
-    const uint32_t wv = threadIdx.x >> 6, lane = lane_id();
-    uint8_t* const rfree = lds_free[wv];
-    uint8_t* const rshade = lds_shade[wv];
-    uint16_t* const rtrace = lds_trace[wv];
-    for (uint32_t i = lane; i < (uint32_t)kPoolRecs; i += 64u) rfree[i] = (uint8_t)i;
-    const ShadeTabs halton = load_tabs(S, lds_halton, lds_mat);   // ends with a block barrier
-    const Uniforms& U = P.U;
-    const QueueShards qs = load_queue(Q.W.counts, cur, Q.seg_cap);   // front parts first: the likely-long paths
-    const uint32_t n = queue_len(qs);
-    if (Q.dev_ctl) stat_add(Q, kStatFinish, 1u);
-    if (Q.dev_ctl && n > 0) stat_add(Q, kStatRounds, 1u);
-    const float4* qin = Q.W.q[cur];
-    const uint32_t kChunk = (uint32_t)Q.fchunk;   // paths per grab
-    float4* const rec = Q.W.fpool + ((size_t)blockIdx.x * (kBlock / 64) + wv) * (size_t)(kPoolRecs * kRecF4);
-    constexpr uint32_t kMask = kPoolRecs - 1;
-    constexpr int kIdle = 0, kClosest = 1, kShadow = 2;
-    // ring positions (wave-uniform): free [fh, ft), queries [th, tt), hits [sh, st)
-    uint32_t fh = 0, ft = kPoolRecs, th = 0, tt = 0, sh = 0, st = 0;
-    TraceCounters tc{0, 0, 0};
-    bool overflow = false;
-    uint32_t n_closest = 0, n_shadow = 0;
-    f2 zero2;
-    zero2.x = 0.0f;
-    zero2.y = 0.0f;
-    uint32_t wnext = 0, wend = 0;
-    bool exhausted = false;
-    int mode = kIdle;
-    uint32_t r = 0;      // the lane's record while it traverses
-    uint32_t spid = 0;   // shadow query: path id | next ray << 31
-    Trav T;
-    trav_start(T, mk3(0, 0, 0), mk3(1, 0, 0), 0.0f);
-    // diagnostics (Q.diag, RT_WF_LOG), as wf_finish_step's: iterations, ticks and busy lanes before /
-    // after the wave's queue ran out, time and lanes in shading passes (wave-uniform registers)
-    uint32_t iters = 0, it_x = 0xffffffffu, t_x = 0, lanes_x = 0, n_pass = 0, n_shaded = 0;
-    uint64_t t_shade = 0;
-    const uint64_t t_start = Q.diag ? __builtin_amdgcn_s_memrealtime() : 0;
-
-    while (true) {
-        ++iters;
-        // ---- shading pass: every lane shades one pending hit (:324-774); traversing lanes keep their query
-        {
-            const uint32_t npend = st - sh;
-            bool pass = npend >= 64u;
-            if (!pass && npend > 0u && exhausted) {
-                const unsigned long long busy = __ballot(mode != kIdle);
-                const int thr = Q.shade_min_x < 0 ? max(1, -Q.shade_min_x * (__popcll(busy) + (int)npend) / 100)
-                                                  : max(1, Q.shade_min_x);
-                pass = (int)npend >= thr || (busy == 0ull && tt == th);
-            }
-            if (pass) {
-                const uint64_t ts0 = Q.diag ? __builtin_amdgcn_s_memrealtime() : 0;
-                const uint32_t m = min(npend, 64u);
-                const bool act = lane < m;
-                uint32_t rid = 0;
-                StepResult sr;
-                sr.next = false;
-                sr.shadow = false;
-                if (act) {
-                    rid = rshade[(sh + lane) & kMask];
-                    float4* R = rec + (size_t)rid * kRecF4;
-                    const float4 o = R[0], d = R[1], c = R[2], hv = R[3], mt = R[7];
-                    const uint32_t pid = __float_as_uint(o.w), state = __float_as_uint(d.w);
-                    Hit h;
-                    h.t = hv.x;
-                    h.id = __float_as_uint(hv.y);
-                    h.u = hv.z;
-                    h.v = hv.w;
-                    const uint32_t pix = __float_as_uint(mt.x);
-                    const int sample = (int)__float_as_uint(mt.y), hidx = (int)__float_as_uint(mt.z);
-                    // FULL=false: shade_step runs on a zero accumulator and the stored one is updated only
-                    // when the emission term is non-zero (as wf_shade: a + (0 + x) == a + x bit for bit)
-                    const float4 a = FULL ? Q.W.p_accum[pid] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-                    PathRegs p;
-                    p.color = ld3(c);
-                    p.accum = ld3(a);
-                    p.bounce = (int)(state & 0xffu);
-                    p.tpass = (int)((state >> 8) & 0xffu);
-                    p.step = (int)(state >> 16);
-                    f3 rayO = ld3(o), rayD = ld3(d);
-                    shade_step<FULL, false>(S, U, halton, hidx, sample, rayO, rayD, h, p, sample == 0 && p.step == 0, zero2,
-                                            false, zero2, sr);
-                    write_pixel_outputs(P, pix, sr, h, FULL);
-                    if (__float_as_uint(p.accum.x) != __float_as_uint(a.x) || __float_as_uint(p.accum.y) != __float_as_uint(a.y) ||
-                        __float_as_uint(p.accum.z) != __float_as_uint(a.z)) {
-                        if (!FULL) {
-                            const float4 s = Q.W.p_accum[pid];
-                            p.accum = mk3(s.x + p.accum.x, s.y + p.accum.y, s.z + p.accum.z);
-                        }
-                        Q.W.p_accum[pid] = make_float4(p.accum.x, p.accum.y, p.accum.z, 0.0f);
-                    }
-                    if (sr.next) {
-                        R[0] = make_float4(rayO.x, rayO.y, rayO.z, o.w);
-                        R[1] = make_float4(rayD.x, rayD.y, rayD.z, __uint_as_float(pack_state(p.bounce, p.tpass, p.step)));
-                        R[2] = make_float4(p.color.x, p.color.y, p.color.z, 0.0f);
-                    }
-                    if (sr.shadow) {
-                        R[4] = make_float4(sr.so.x, sr.so.y, sr.so.z, sr.stmax);
-                        R[5] = make_float4(sr.sd.x, sr.sd.y, sr.sd.z, __uint_as_float(pid | (sr.next ? 0x80000000u : 0u)));
-                        R[6] = make_float4(sr.contrib.x, sr.contrib.y, sr.contrib.z, 0.0f);
-                    }
-                }
-                sh += m;
-                // the path continues with its shadow ray, else its next ray; an ended path frees its record
-                const bool more = act && (sr.shadow || sr.next);
-                const unsigned long long mm = __ballot(more);
-                if (more) rtrace[(tt + mbcnt64(mm)) & kMask] = (uint16_t)(rid | (sr.shadow ? 0x100u : 0u));
-                tt += (uint32_t)__popcll(mm);
-                const bool ended = act && !more;
-                const unsigned long long me = __ballot(ended);
-                if (ended) rfree[(ft + mbcnt64(me)) & kMask] = (uint8_t)rid;
-                ft += (uint32_t)__popcll(me);
-                // the traversing lanes' ray setups, dead across the shading code, rebuilt from their
-                // records (a pure function of the ray: bit for bit the one trav_start made); idle lanes
-                // too (their r is a valid record, the setup unused), so no lane keeps the old one live
-                {
-                    const float4* R = rec + (size_t)r * kRecF4 + (mode == kShadow ? 4 : 0);
-                    const float4 ro = R[0], rd = R[1];
-                    T.R = ray_setup(ld3(ro), ld3(rd));
-                }
-                if (Q.diag) {
-                    ++n_pass;
-                    n_shaded += m;
-                    t_shade += __builtin_amdgcn_s_memrealtime() - ts0;
-                }
-            }
-        }
-
-        // ---- refill idle lanes: queued continuations first, then new paths (chunks of the XCD's counter)
-        unsigned long long idle = __ballot(mode == kIdle);
-        if (idle != 0ull && tt != th) {
-            const uint32_t j = mbcnt64(idle);
-            const uint32_t take = min((uint32_t)__popcll(idle), tt - th);
-            if (mode == kIdle && j < take) {
-                const uint32_t e = rtrace[(th + j) & kMask];
-                r = e & 0xffu;
-                const float4* R = rec + (size_t)r * kRecF4;
-                if (e & 0x100u) {
-                    const float4 so = R[4], sd = R[5];
-                    spid = __float_as_uint(sd.w);
-                    trav_start(T, ld3(so), ld3(sd), so.w);
-                    mode = kShadow;
-                    n_shadow++;
-                } else {
-                    const float4 ro = R[0], rd = R[1];
-                    trav_start(T, ld3(ro), ld3(rd), INFINITY);
-                    mode = kClosest;
-                    n_closest++;
-                }
-            }
-            th += take;
-            idle = __ballot(mode == kIdle);
-        }
-        const bool refill = __popcll(idle) >= Q.refill_min || idle == ~0ull;
-        if (wnext >= wend && !exhausted && refill && ft != fh) {
-            uint32_t base = 0;
-            if (lane == 0) base = atomicAdd(Q.W.counts + cslot(kCntChunkFinish + (int)(blockIdx.x & 7u)), 1u);
-            base = ((__builtin_amdgcn_readfirstlane(base) << 3) | (blockIdx.x & 7u)) * kChunk;
-            if (base >= n) {
-                exhausted = true;
-                if (Q.diag) {
-                    it_x = iters;
-                    t_x = (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_start);
-                }
-            } else {
-                wnext = base;
-                wend = min(base + kChunk, n);
-            }
-        }
-        if (idle != 0ull && wnext < wend && refill) {
-            const uint32_t j = mbcnt64(idle);
-            const uint32_t take = min(min((uint32_t)__popcll(idle), wend - wnext), ft - fh);
-            if (mode == kIdle && j < take) {
-                const uint32_t e = dense_entry(qs, wnext + j, Q.seg_cap);
-                const float4* src = qin + 2 * (size_t)e;
-                const float4 o = (RT_TRACE_NT & 2) ? ld_stream(&src[0]) : src[0];
-                const float4 d = (RT_TRACE_NT & 2) ? ld_stream(&src[1]) : src[1];
-                const uint32_t pid = __float_as_uint(o.w), state = __float_as_uint(d.w);
-                const float4 c = state == 0u ? make_float4(1.0f, 1.0f, 1.0f, 0.0f)
-                                 : (RT_TRACE_NT & 2) ? ld_stream(&Q.W.qc[cur][e]) : Q.W.qc[cur][e];
-                const uint3 pm = path_meta(P, Q, pid);
-                r = rfree[(fh + j) & kMask];
-                float4* R = rec + (size_t)r * kRecF4;
-                R[0] = o;
-                R[1] = d;
-                R[2] = c;
-                R[7] = make_float4(__uint_as_float(pm.x), __uint_as_float(pm.y), __uint_as_float(pm.z), 0.0f);
-                trav_start(T, ld3(o), ld3(d), INFINITY);
-                mode = kClosest;
-                n_closest++;
-            }
-            fh += take;
-            wnext += take;
-        }
-        if (__ballot(mode != kIdle) == 0ull) {
-            if (exhausted && tt == th && st == sh) break;   // every path of this wave has ended
-            continue;                                        // pending hits: the next pass shades them
-        }
-
-        if (Q.diag && exhausted) lanes_x += (uint32_t)__popcll(__ballot(mode != kIdle));
-        // ---- one traversal step (closest hit or shadow any-hit)
-        bool to_shade = false, to_free = false;
-        if (mode != kIdle) {
-            const bool any = mode == kShadow;
-            if (trav_step<COUNT>(S, T, any, stack, tc, overflow, T.best)) {
-                float4* R = rec + (size_t)r * kRecF4;
-                if (any) {
-                    if (!T.hit_any) {   // unoccluded: accum += contribution (:741-743)
-                        const float4 c = R[6];
-                        const uint32_t pid = spid & 0x7fffffffu;
-                        const float4 a = Q.W.p_accum[pid];
-                        Q.W.p_accum[pid] = make_float4(a.x + c.x, a.y + c.y, a.z + c.z, 0.0f);
-                    }
-                    if (spid >> 31) {   // the path's next ray, in this lane
-                        const float4 ro = R[0], rd = R[1];
-                        trav_start(T, ld3(ro), ld3(rd), INFINITY);
-                        mode = kClosest;
-                        n_closest++;
-                    } else {
-                        mode = kIdle;
-                        to_free = true;
-                    }
-                } else if (T.best_id == 0xffffffffu) {   // miss -> path ends (:321-322)
-                    mode = kIdle;
-                    to_free = true;
-                } else {
-                    R[3] = make_float4(T.best, __uint_as_float(T.best_id), T.bu / T.bdet, T.bv / T.bdet);
-                    mode = kIdle;
-                    to_shade = true;
-                }
-            }
-        }
-        const unsigned long long ms = __ballot(to_shade);
-        if (to_shade) rshade[(st + mbcnt64(ms)) & kMask] = (uint8_t)r;
-        st += (uint32_t)__popcll(ms);
-        const unsigned long long mf = __ballot(to_free);
-        if (to_free) rfree[(ft + mbcnt64(mf)) & kMask] = (uint8_t)r;
-        ft += (uint32_t)__popcll(mf);
-    }
-    if (Q.diag && lane == 0) {
-        const uint32_t dt = (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_start);
-        const bool x = it_x != 0xffffffffu;
-        const uint32_t ix = x ? it_x : iters, tx = x ? t_x : dt;
-        atomicAdd(&Q.W.counts[kWfStat + kStatDiagItPre], ix);
-        atomicAdd(&Q.W.counts[kWfStat + kStatDiagItPost], iters - ix);
-        atomicAdd(&Q.W.counts[kWfStat + kStatDiagTPre], tx);
-        atomicAdd(&Q.W.counts[kWfStat + kStatDiagTPost], dt - tx);
-        atomicAdd(&Q.W.counts[kWfStat + kStatDiagLanesPost], lanes_x);
-        atomicAdd(&Q.W.counts[kWfDiagExh + min(tx / 5000u, 63u)], 1u);
-        atomicAdd(&Q.W.counts[kWfStat + kStatDiagShadeT], (uint32_t)t_shade);
-        atomicAdd(&Q.W.counts[kWfStat + kStatDiagTotalT], dt);
-        atomicAdd(&Q.W.counts[kWfStat + kStatDiagPasses], n_pass);
-        atomicAdd(&Q.W.counts[kWfStat + kStatDiagShaded], n_shaded);
-        atomicMax(&Q.W.counts[cslot(kCntDiagIters)], iters);
-        atomicMax(&Q.W.counts[cslot(kCntDiagTime)], dt);
-        atomicAdd(&Q.W.counts[kWfDiagHist + min(dt / 5000u, 63u)], 1u);
-    }
     ts_end(Q, ts, &ts_done);
     flush_counters(P, n_closest, n_shadow, 0, tc, COUNT, overflow);
 }
@@ -2142,24 +1577,7 @@ static unsigned finish_full_cap() {   // resident blocks of the finish kernel in
     return c;
 }
 template <bool COUNT, bool FULL>
-static unsigned pool_full_cap() {   // resident blocks of the pooled finish kernel, queried once
-    static const unsigned c = resident_grid(wf_finish_pool<COUNT, FULL>, 2);
-    return c;
-}
-// the pooled finish kernel's records: kPoolRecs per wave of the largest resident grid of its instances
-size_t wavefront_pool_bytes() {
-    const unsigned g = std::max(std::max(pool_full_cap<false, false>(), pool_full_cap<false, true>()),
-                                std::max(pool_full_cap<true, false>(), pool_full_cap<true, true>()));
-    return (size_t)std::max(g, 8u) * (kBlock / 64) * kPoolRecs * kRecF4 * sizeof(float4);
-}
-template <bool COUNT, bool FULL>
 static void launch_finish(const DevScene& S, const WfParams& Q, int cur, uint32_t n, hipStream_t stream, int ts) {
-    if (Q.pool) {   // grid <= pool_full_cap: the blocks' record pools fit fpool (wavefront_pool_bytes)
-        const unsigned pcap = std::max(8u, pool_full_cap<COUNT, FULL>() * (unsigned)Q.finish_frac / 100u / 8u * 8u);
-        hipLaunchKernelGGL((wf_finish_pool<COUNT, FULL>), dim3(std::max(8u, grid_for(n, pcap))), dim3(kBlock), 0, stream,
-                           S, Q.Pd, Q, cur, ts);
-        return;
-    }
     // at least one block per XCD: each takes the chunks of its XCD's counter (wf_finish_step).
     // Q.team: the kernel with the team drain (a separate instance: its code would raise the plain
     // kernel's register pressure), sized by its own occupancy (its LDS and registers differ)
@@ -2256,7 +1674,7 @@ static bool iterate(const DevScene& S, const FrameParams& P, WfParams& Q, int& c
         }
         int next = 1 - cur;
         WF_CHECK(hipEventRecord(W.ev[0], stream));
-        unsigned g = grid_for(n, tuning().shade_blocks);
+        unsigned g = grid_for(n, Q.shade_blocks);
         unsigned gt = grid_for(n, trace_grid_cap(Q));
         if (count) hipLaunchKernelGGL((wf_trace<false, true>), dim3(gt), dim3(kBlock), 0, stream, S, Q.Pd, Q, cur, -1);
         else hipLaunchKernelGGL((wf_trace<false, false>), dim3(gt), dim3(kBlock), 0, stream, S, Q.Pd, Q, cur, -1);
@@ -2381,7 +1799,7 @@ static bool enqueue_pass(const DevScene& S, const FrameParams& P, const WfParams
                          int ts, Enqueue& E, const char** err) {
     hipStream_t stream = E.stream;
     if (!Q.spans) ts = -1;   // no device-clock spans: the kernels skip the stamps
-    const unsigned gt = trace_grid_cap(Q), g = tuning().shade_blocks;
+    const unsigned gt = trace_grid_cap(Q), g = Q.shade_blocks;
     for (int k = 0; k < rounds; ++k) {
         const int cur = k & 1;
         const bool kHitSort = Q.sort_bins != 0;
@@ -2471,10 +1889,6 @@ static bool record_part(const DevScene& S, const FrameParams& P, WfParams& Q, bo
                      : record_rest(S, P, Q, count, full, maxExtra, with_extra, stream, T, capture, err);
 }
 
-static bool graphs_on() {   // frames are captured into HIP graphs and replayed (RT_GRAPH=0: eager enqueue)
-    static const bool v = env_int("RT_GRAPH", 1) != 0;
-    return v;
-}
 
 // part `part` of the frame (record_part), eagerly or captured into T.exec[part] and launched
 static bool capture_part(const DevScene& S, const FrameParams& P, WfParams& Q, bool count, bool full, int maxExtra,
@@ -2532,7 +1946,6 @@ static bool enqueue_wavefront(const DevScene& S, const FrameParams& P, WfParams&
     Q.dev_ctl = 1;
     Q.finish_q = 0;   // set by record_base from the round count
     const bool with_extra = maxExtra > 0 && extra_pass;
-    graphs = graphs && graphs_on();
     if (!graphs || T.graph_failed) {
         T.graph_mode = graphs ? kGraphFallback : kGraphEager;
         if (!record_base(S, P, Q, count, full, stream, T, false, err)) return false;
@@ -2613,10 +2026,10 @@ bool wavefront_collect(const WavefrontBuffers& W, WfTimeline& T, WfFrameStats* f
     return true;
 }
 
-bool run_wavefront(const DevScene& S, const FrameParams& P, WavefrontBuffers& W, int own_tiles, bool count, bool spans,
-                   int tail_paths, int sort_bins, bool extra_pass, int in_flight, hipStream_t stream,
-                   hipEvent_t prev_done, WfTimeline* tl, WfFrameStats* fs, const char** err, bool graphs) {
-    const Tuning& tu = tuning();
+bool run_wavefront(const DevScene& S, const FrameParams& P, WavefrontBuffers& W, const WfTuning& tu, int own_tiles,
+                   bool count, bool spans, int tail_paths, int sort_bins, bool extra_pass, int in_flight,
+                   hipStream_t stream, hipEvent_t prev_done, WfTimeline* tl, WfFrameStats* fs, const char** err,
+                   bool graphs) {
     WfParams Q;
     std::memset(&Q, 0, sizeof Q);   // no stray padding bytes (frame-graph key)
     Q.W = W;
@@ -2636,9 +2049,7 @@ bool run_wavefront(const DevScene& S, const FrameParams& P, WavefrontBuffers& W,
     // flight ±0), but not the smallest (C1 256x256x1: -7.5 %)
     Q.team = tu.team >= 0 ? tu.team : (Q.base_paths >= kTeamAutoMin && Q.base_paths <= kTeamAutoPaths ? 4 : 0);
     Q.fchunk = tu.fchunk;
-    Q.pool = tu.pool;
-    if (Q.pool) Q.team = 0;   // the pooled kernel has no team drain
-    Q.consol = tu.consol;
+    Q.shade_blocks = tu.shade_blocks;
     Q.spans = spans ? 1 : 0;
     Q.spp_div = make_fastdiv((uint32_t)Q.spp);
     Q.tile = P.tile_size;
@@ -2689,7 +2100,6 @@ bool run_wavefront(const DevScene& S, const FrameParams& P, WavefrontBuffers& W,
         (void)finish_full_cap<false, true, true>();
         (void)finish_full_cap<true, false, true>();
         (void)finish_full_cap<true, true, true>();
-        (void)wavefront_pool_bytes();
         return enqueue_wavefront(S, P, Q, count, full, maxExtra, extra_pass, stream, prev_done, *tl, err, graphs);
     }
     Q.dev_ctl = 0;

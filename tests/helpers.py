@@ -33,8 +33,20 @@ _VARIANTS = {"megakernel": ("megakernel", 0, 0), "wavefront": ("wavefront", 0, 0
 
 
 def make_renderer(rt, scene, W, H, pipeline="wavefront", **kw):
+    """A Renderer of the given test pipeline variant.  The legacy RT_* variables of the test's own
+    environment (the env-variant tests' child processes set them) are applied through rt_set_tuning /
+    rt_set_graphs: the library reads no environment."""
     pl, tail, sort_bins = _VARIANTS[pipeline]
-    return rt.Renderer(scene, W, H, pipeline=pl, tail_paths=tail, sort_bins=sort_bins, **kw)
+    env = rt.tuning_from_env()
+    graphs = env.pop("graphs", None)
+    env_tail = env.pop("tail_paths", None)
+    fif = env.pop("frames_in_flight", None)
+    if fif is not None:
+        kw.setdefault("frames_in_flight", fif)
+    R = rt.Renderer(scene, W, H, pipeline=pl, tail_paths=tail or env_tail or 0, sort_bins=sort_bins, tuning=env, **kw)
+    if graphs is not None:
+        R.set_graphs(bool(graphs))
+    return R
 
 
 # ---- the textured test scene (tests/test_gpu_textures.py, tests/golden tex case) -------------------

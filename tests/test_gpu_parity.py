@@ -327,3 +327,29 @@ def test_light_types_parity(rt, orc, assets, kinds, mode, pipeline):
         assert np.array_equal(gd, o["depth"]) and np.array_equal(gm, o["motion"])
         assert st.closest_rays == o["closest_rays"] and st.shadow_rays == o["shadow_rays"]
     assert float(np.max(g[..., :3])) > 0.0
+
+
+def test_tuning_api_roundtrip_and_validation(rt, assets):
+    """rt_set_tuning / rt_get_tuning (the library reads no environment for its scheduling): defaults
+    resolved, a set value read back, out-of-range values refused, the frame unchanged by them."""
+    scene = rt.Scene.preset("c1", assets)
+    R = rt.Renderer(scene, 64, 48, seed=2)
+    d = R.tuning()
+    assert d["trace_chunk"] == 64 and d["finish_chunk"] == 64 and d["shade_blocks"] == 2048 and d["team"] == 0
+    R.samplesPerPixel, R.maxBounces = 1, 3
+    R.draw()
+    R.wait()
+    a = R.radiance()
+    R.set_tuning(finish_chunk=5, team=4, shade_min_drained=-100, refill_min=3)
+    t = R.tuning()
+    assert t["finish_chunk"] == 5 and t["team"] == 4 and t["shade_min_drained"] == -100 and t["refill_min"] == 3
+    R.frameIndex = 0
+    R.draw()
+    R.wait()
+    assert np.array_equal(R.radiance(), a)
+    for bad in ({"team": 3}, {"refill_min": 65}, {"log": 3}, {"shade_min_drained": -101}):
+        with pytest.raises(rt.RTError):
+            R.set_tuning(**bad)
+    R.set_tuning()
+    assert R.tuning() == d
+    R.close()

@@ -8,7 +8,7 @@ min-id tie-break of DESIGN.md §4 picks the material), against the CPU oracle (R
 Instances: wf_trace (the bulk pipeline: every bounce through extend / connect launches), the plain
 finish kernel (wf_finish_step: the whole small frame goes to the finish), its team drain at 2, 4
 and 8 lanes per query (RT_TEAM; RT_FCHUNK=1 makes every wave's paths few, so the drain engages at
-once), and the pooled finish kernel (RT_FINISH_POOL).  The 512x512 frames (262,144 base paths) sit
+once).  The 512x512 frames (262,144 base paths) sit
 inside the team drain's default range (kTeamAutoMin .. kTeamAutoPaths), so its default instance
 runs there without any switch."""
 import os
@@ -36,17 +36,14 @@ def _run(env, specs, pipes):
 
 @pytest.mark.parametrize("env", [{}, {"RT_TEAM": "0"}, {"RT_TEAM": "2", "RT_FCHUNK": "1"}, {"RT_TEAM": "4", "RT_FCHUNK": "1"},
                                  {"RT_TEAM": "8", "RT_FCHUNK": "1"}, {"RT_TEAM": "4", "RT_FCHUNK": "5", "RT_SHADE_MIN_X": "1"},
-                                 {"RT_FINISH_POOL": "1"}, {"RT_FINISH_POOL": "1", "RT_FCHUNK": "1", "RT_SHADE_MIN_X": "1"},
-                                 {"RT_CONSOL": "1", "RT_TEAM": "0"}, {"RT_CONSOL": "2", "RT_TEAM": "0", "RT_FCHUNK": "1"}],
-                         ids=["default", "noteam", "team2", "team4", "team8", "team4_chunk5", "pool", "pool_chunk1", "consol1",
-                              "consol2_chunk1"])
+                                 ],
+                         ids=["default", "noteam", "team2", "team4", "team8", "team4_chunk5"])
 def test_traversal_instances_small(env):
     _run(env, SMALL, PIPES)
 
 
-@pytest.mark.parametrize("env", [{}, {"RT_TEAM": "2"}, {"RT_TEAM": "8"}, {"RT_FINISH_POOL": "1"},
-                                 {"RT_CONSOL": "4", "RT_TEAM": "0"}],
-                         ids=["default_team4", "team2", "team8", "pool", "consol4"])
+@pytest.mark.parametrize("env", [{}, {"RT_TEAM": "2"}, {"RT_TEAM": "8"}, {"RT_TEAM": "0"}],
+                         ids=["default_team4", "team2", "team8", "noteam"])
 def test_traversal_instances_team_range(env):
     """512 x 512 x 1 spp, 3 bounces: 262,144 base paths, the default team drain's range."""
     _run(env, "soup:512:512:1:3,ties:512:512:1:3", "wavefront")
