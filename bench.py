@@ -358,7 +358,12 @@ def main():
         barrier()
         dt = time.perf_counter() - t0
         tot = torch.tensor([dt, float(a.steps * (StubFrames.RAYS + StubFrames.RAYS // 2))], dtype=torch.float64)
+        per_rank = None
         if n > 1:
+            allt = [torch.zeros_like(tot) for _ in range(n)]
+            dist.all_gather(allt, tot)
+            per_rank = [{"rank": r, "ms_per_step": round(float(x[0]) / max(a.steps, 1) * 1e3, 3),
+                         "rays_per_frame": int(float(x[1]) / max(a.steps, 1))} for r, x in enumerate(allt)]
             mx, sm = tot.clone(), tot.clone()
             dist.all_reduce(mx, op=dist.ReduceOp.MAX)
             dist.all_reduce(sm, op=dist.ReduceOp.SUM)
@@ -369,7 +374,8 @@ def main():
             print(json.dumps({"metric": "dry-run (stub frames, gloo)", "value": rays / dt / 1e9, "unit": "Grays/s",
                               "n_gpus": n, "world_size": n, "steps": a.steps, "warmup": a.warmup,
                               "ms_per_step": dt / a.steps * 1e3, "higher_is_better": True, "scaling": "strong",
-                              "vs_baseline": None, "dtype": "f32", "data": "stub", "config": {"workload": "dry-run"}}),
+                              "vs_baseline": None, "dtype": "f32", "data": "stub",
+                              "config": {"workload": "dry-run", "per_rank": per_rank}}),
                   flush=True)
         if n > 1:
             dist.destroy_process_group()
@@ -469,7 +475,14 @@ def main():
 
     tot = torch.tensor([dt, float(rays), float(closest), kms_local, gather_ms], dtype=torch.float64,
                        device="cpu" if gloo else dev)
+    per_rank = None
     if n > 1:
+        # every rank's own figures (load balance of the tile split)
+        allt = [torch.zeros_like(tot) for _ in range(n)]
+        dist.all_gather(allt, tot)
+        per_rank = [{"rank": r, "ms_per_step": round(float(x[0]) / a.steps * 1e3, 3),
+                     "rays_per_frame": int(float(x[1]) / a.steps), "kernel_ms_per_frame": round(float(x[3]), 3),
+                     "gather_ms_per_step": round(float(x[4]), 4)} for r, x in enumerate(t.cpu() for t in allt)]
         mx = tot.clone()
         dist.all_reduce(mx, op=dist.ReduceOp.MAX)
         sm = tot.clone()
@@ -554,6 +567,9 @@ def main():
             # side of the RCCL gather (max over ranks), and its share of the step
             "gather_ms_per_step": round(gather_ms, 4) if n > 1 else None,
             "gather_share": round(gather_ms / ms_per_step, 4) if n > 1 else None,
+            # multi-rank: each rank's wall ms per step (to its own end of the timed region), rays
+            # and summed kernel ms per frame (ranks sharing one GPU share its CUs)
+            "per_rank": per_rank,
         },
         "roofline": roof,
         "cpu_baseline": cpu,
@@ -656,10 +672,13 @@ def roofline(alone, shared, pmc, pmc_err, ms_frame_alone, ms_per_step, pmc_csvs)
     d = next(k for k in kernels if k["kernel"] == dom["kernel"])
     r = {
         "bound": "hbm", "peak": HBM_PEAK_GBS, "unit": "GB/s", "kernel": dom["kernel"],
-        "achieved": d["hbm_GBs"] if d["hbm_GBs"] else d["achieved_algorithmic_GBs"],
-        "frac": d["frac"] if d["frac"] is not None else d["frac_algorithmic"],
+        # HBM bytes from the PMC pass only: without one, achieved / frac stay null and the
+        # algorithmic-byte figures below are the only rate (they count L2 / MALL hits as well, so
+        # they are not an HBM fraction and can exceed 1)
+        "achieved": d["hbm_GBs"],
+        "frac": d["frac"],
         "frac_source": "pmc: rocprofv3 FETCH_SIZE x 2 + WRITE_SIZE per launch, kernels alone, over the launch time alone"
-        if d["frac"] is not None else "algorithmic bytes (no PMC pass: " + (pmc_err or "--no-pmc") + ")",
+        if d["frac"] is not None else "none: no PMC pass (" + (pmc_err or "--no-pmc") + "); see frac_algorithmic",
         "traffic": d["traffic"], "launch_ms": d["launch_ms"], "ms_per_frame_alone": d["ms_per_frame"],
         "frame_ms_alone": round(ms_frame_alone, 4) if ms_frame_alone else None,
         "algorithmic_bytes_per_launch": d["algorithmic_bytes_per_launch"],

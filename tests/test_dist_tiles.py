@@ -123,6 +123,9 @@ def test_bench_launcher_starts_ranks(n):
     assert len(lines) == 1, r.stdout
     d = json.loads(lines[0])
     assert d["n_gpus"] == n and d["world_size"] == n and d["steps"] == 3 and d["value"] > 0
+    pr = d["config"]["per_rank"]   # every rank's own figures, gathered to rank 0
+    assert [x["rank"] for x in pr] == list(range(n)) and all(x["ms_per_step"] > 0 for x in pr)
+    assert sum(x["rays_per_frame"] for x in pr) * 3 / (d["ms_per_step"] * 3e-3) / 1e9 == pytest.approx(d["value"], rel=1e-6)
 
 
 @pytest.mark.timeout(120)

@@ -68,3 +68,7 @@ def test_bench_emulated_rank_and_animation():
     d = _run("--scene", "c5", "--width", "128", "--height", "96", "--spp", "1", "--bounces", "2", "--steps", "3",
              "--warmup", "1", "--no-cpu", "--no-pmc", "--animate", "--emulate-ranks", "2")
     assert d["value"] > 0 and d["config"]["animate"] is True and d["cpu_baseline"] is None
+    # --no-pmc: no HBM byte count, so no HBM fraction; the algorithmic rate is reported beside it
+    r = d["roofline"]
+    assert r["frac"] is None and r["achieved"] is None and r["traffic"] is None
+    assert r["frac_source"].startswith("none") and r["frac_algorithmic"] > 0
