@@ -517,6 +517,10 @@ def main():
     else:   # --no-isolated: the shared-GPU launches, flagged
         alone, shared, ms_frame, stage_alone = table, None, None, None
     roof = roofline(alone, shared, pmc, pmc_err, ms_frame, ms_per_step, pmc_csvs)
+    if roof.get("shade_l2_hit") is not None:
+        roof["shade_l2_hit_kernel"] = ("wf_shade on hit-sorted input (--sort-bins)" if a.sort_bins > 0 else
+                                       "wf_shade of the default pipeline: hits shaded in queue order, no ray or hit sort "
+                                       "(the sorts measured slower, DESIGN.md §3.5)")
     if alone is table and s1.frames_in_flight > 1:
         roof["not_a_kernel_measurement"] = True
     stage_ms = (np.array(list(s1.total_kernel_ms)) - np.array(list(s0.total_kernel_ms))) / a.steps
@@ -689,6 +693,9 @@ def roofline(alone, shared, pmc, pmc_err, ms_frame_alone, ms_per_step, pmc_csvs)
         # north star: the L2 hit rate of the shade kernel (it shades the hits of the rays as the
         # extend launch traced them), measured in this run
         "shade_l2_hit": next((k["l2_hit"] for k in kernels if k["kernel"].startswith("rt::wf_shade")), None),
+        # which shade kernel that is: the default pipeline shades hits in queue order (no ray or hit
+        # sort; the sorts were measured slower)
+        "shade_l2_hit_kernel": None,   # set by main(): which shade kernel that is
         "pmc_files": {c: os.path.relpath(p, ROOT) if p.startswith(ROOT) else p for c, p in pmc_csvs.items()} or None,
         "kernels": kernels,
     }
