@@ -14,3 +14,6 @@ for m in usda usdc usdz png obj; do
   ASAN_OPTIONS=detect_leaks=1:abort_on_error=1 UBSAN_OPTIONS=print_stacktrace=1 \
     $B/fuzz_host $m $B/seeds/seed.$m ${ITERS:-3000} ${SEED:-1}
 done
+# internal-reference fan-out over a large array (fewer iterations: each input is ~100 KB)
+ASAN_OPTIONS=detect_leaks=1:abort_on_error=1 UBSAN_OPTIONS=print_stacktrace=1 \
+  $B/fuzz_host usda $B/seeds/seed_fanout.usda $(( ${ITERS:-3000} / 10 + 1 )) ${SEED:-1}

@@ -43,6 +43,13 @@ def Xform "World" (
     }
 }
 """,
+    # internal-reference fan-out over a layer holding one large array (ADVICE r04: every internal
+    # arc's layer snapshot is charged against the composed-bytes budget)
+    "seed_fanout.usda": b"#usda 1.0\n"
+    + b'def Mesh "Src"\n{\n    int[] faceVertexCounts = [3]\n    int[] faceVertexIndices = [0, 1, 2]\n'
+    + b"    point3f[] points = [" + b", ".join(b"(%d, %d, 1)" % (i, i % 7) for i in range(4096)) + b"]\n}\n"
+    + b'def Xform "Tiny"\n{\n}\n'
+    + b"".join(b'def Xform "R%d" (\n    references = </Tiny>\n)\n{\n}\n' % i for i in range(256)),
     "seed.usdc": crate,
     "seed.usdz": W.write_usdz("robot.usdc", crate, [("textures/tex.png", TEX)]),
     "seed.png": TEX,
