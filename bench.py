@@ -519,8 +519,8 @@ def main():
     roof = roofline(alone, shared, pmc, pmc_err, ms_frame, ms_per_step, pmc_csvs)
     if roof.get("shade_l2_hit") is not None:
         roof["shade_l2_hit_kernel"] = ("wf_shade on hit-sorted input (--sort-bins)" if a.sort_bins > 0 else
-                                       "wf_shade of the default pipeline: hits shaded in queue order, no ray or hit sort "
-                                       "(the sorts measured slower, DESIGN.md §3.5)")
+                                       "wf_shade of the default pipeline: hits shaded in queue order (rays grouped by "
+                                       "octant inside each block's appends only; no queue-wide ray or hit sort, DESIGN.md §3.5)")
     if alone is table and s1.frames_in_flight > 1:
         roof["not_a_kernel_measurement"] = True
     stage_ms = (np.array(list(s1.total_kernel_ms)) - np.array(list(s0.total_kernel_ms))) / a.steps

@@ -100,6 +100,37 @@ __device__ __forceinline__ void block_alloc3(const bool (&pr)[3], uint32_t* cons
     __syncthreads();
 }
 
+// block_alloc3 with the continuation rays (pr[1] front, pr[2] back) of the block grouped by the
+// direction octant `oct` (3 bits) inside each part's range: a per-block counting sort of the
+// appends through LDS atomics (the rank inside an octant is arbitrary), no separate sort pass.
+struct BlockAllocOct {
+    uint32_t cnt[3][8];    // shadow uses [0][0]
+    uint32_t base[3][8];
+};
+__device__ __forceinline__ void block_alloc3_oct(const bool (&pr)[3], uint32_t oct, uint32_t* const (&ctr)[3],
+                                                 BlockAllocOct& sh, uint32_t (&out)[3]) {
+    if (threadIdx.x < 24) (&sh.cnt[0][0])[threadIdx.x] = 0u;
+    __syncthreads();
+    uint32_t rank[3] = {0u, 0u, 0u};
+    #pragma unroll
+    for (int i = 0; i < 3; ++i)
+        if (pr[i]) rank[i] = atomicAdd(&sh.cnt[i][i ? oct : 0u], 1u);
+    __syncthreads();
+    if (threadIdx.x < 3) {
+        const int i = threadIdx.x;
+        uint32_t tot = 0, pre[8];
+        #pragma unroll
+        for (int o = 0; o < 8; ++o) { pre[o] = tot; tot += sh.cnt[i][o]; }
+        const uint32_t b = tot ? atomicAdd(ctr[i], tot) : 0u;
+        #pragma unroll
+        for (int o = 0; o < 8; ++o) sh.base[i][o] = b + pre[o];
+    }
+    __syncthreads();
+    #pragma unroll
+    for (int i = 0; i < 3; ++i) out[i] = sh.base[i][i ? oct : 0u] + rank[i];
+    __syncthreads();
+}
+
 // Block-aggregated allocation of v slots per thread (wave scan + LDS prefix, one atomic per block).
 __device__ __forceinline__ uint32_t block_alloc_n(uint32_t v, uint32_t* counter, BlockAlloc& sh) {
     const int wave = threadIdx.x >> 6;
@@ -590,12 +621,18 @@ __device__ __forceinline__ float4 ld_stream(const float4* p) {
     return make_float4(v.x, v.y, v.z, v.w);
 }
 __device__ __forceinline__ float4 ld_shade(const float4* p) { return RT_SHADE_NT ? ld_stream(p) : *p; }
+#ifndef RT_SHADE_OCT
+#define RT_SHADE_OCT 1   // continuation rays grouped by direction octant inside each block's appends (0: A/B builds)
+#endif
 template <bool FULL, bool SORTED>
 __global__ void __launch_bounds__(kBlock) wf_shade(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int cur) {
     const FrameParams& P = *Pp;   // per-frame parameters in device memory
     __shared__ HaltonDim lds_halton[kHaltonLds];
     __shared__ MatRec lds_mat[kMatLds];
     __shared__ BlockAlloc3 ba3;
+#if RT_SHADE_OCT
+    __shared__ BlockAllocOct bao;
+#endif
     if (tail_mode(Q)) return;
     const ShadeTabs halton = load_tabs(S, lds_halton, lds_mat);
     const Uniforms& U = P.U;
@@ -697,7 +734,12 @@ __global__ void __launch_bounds__(kBlock) wf_shade(DevScene S, const FrameParams
         uint32_t* const ctr[3] = {&Q.W.counts[cslot(kCntShadowQ + shard)], &Q.W.counts[cslot(next * kShards + shard)],
                                   &Q.W.counts[cslot(kCntBack + next * kShards + shard)]};
         uint32_t slots[3];
+#if RT_SHADE_OCT
+        const uint32_t oct = (rayD.x < 0.0f ? 1u : 0u) | (rayD.y < 0.0f ? 2u : 0u) | (rayD.z < 0.0f ? 4u : 0u);
+        block_alloc3_oct(pr, oct, ctr, bao, slots);
+#else
         block_alloc3(pr, ctr, ba3, slots);
+#endif
         const uint32_t ns = slots[0], nr = front ? slots[1] : Q.seg_cap - 1u - slots[2];
         if (r.shadow) {
             sqout[3 * (size_t)ns] = make_float4(r.so.x, r.so.y, r.so.z, __uint_as_float(pid));
