@@ -697,6 +697,8 @@ rt_status rt_bvh_build(rt_ctx* c) {
         }
         c->world_dirty = false;
     }
+    // wf_trace's cooperative triangle phase packs a triangle slot / id with a lane into 32 bits
+    if (c->num_tris >= (1u << 26)) FAIL(c, RT_ERR_UNSUPPORTED, "more than 2^26 triangles");
     if (!build_bvh8_fit(c->h_world.data(), c->num_tris, c->bvh, c->bvh8))
         FAIL(c, RT_ERR_UNSUPPORTED, "BVH deeper than the traversal stack at every depth limit");
     if (c->bvh8.nodes.size() >= (1u << 23)) FAIL(c, RT_ERR_UNSUPPORTED, "BVH too large (2^23 nodes)");
@@ -748,6 +750,7 @@ rt_status rt_bvh_build_device(rt_ctx* c) {
     if (!c) FAIL(c, RT_ERR_INVALID_ARG, "null ctx");
     if (!c->scene_ready) FAIL(c, RT_ERR_STATE, "rt_bvh_build_device before rt_scene_upload");
     if (c->num_tris < 2) return rt_bvh_build(c);   // nothing to sort: the host path is exact and instant
+    if (c->num_tris >= (1u << 26)) FAIL(c, RT_ERR_UNSUPPORTED, "more than 2^26 triangles");
     HIPC(c, hipSetDevice(c->device));
     // into the update generation on the update stream: frames in flight keep their tree
     rt_status st = begin_update(c);

@@ -448,6 +448,17 @@ __device__ __forceinline__ uint32_t next_node(Trav& T, int* stack, bool& overflo
     return T.g_base + (uint32_t)r;
 }
 
+// The node half of a traversal step: the next node of the current group (or the stack), its five
+// 16-B words from global memory, the 8-wide test.
+template <bool COUNT>
+__device__ __forceinline__ void node_step(const DevScene& S, Trav& T, int* stack, TraceCounters& tc, bool& overflow,
+                                          float cull) {
+    const uint32_t ni = next_node(T, stack, overflow);
+    if (COUNT) tc.nodes++;
+    const NodeWords w = load_node8(S.nodes8, ni);
+    test_node8_words(w, T.R, 0.0f, fminf(cull, T.best), T.g_hits, T.t_mask, T.t_valid, T.g_base, T.t_base, T.g_flip);
+}
+
 // `cull`: the distance bound of the box and triangle tests together with T.best (the lower of the
 // two); lower than T.best in the finish kernel's team drain (the closest hit any member of the team
 // has found), where T.best stays this lane's own hit.
@@ -504,12 +515,7 @@ __device__ __forceinline__ bool trav_step(const DevScene& S, Trav& T, bool any, 
             }
         }
     }
-    if (!tdone && T.t_mask == 0u && (T.g_hits != 0u || T.sp > 0)) {
-        const uint32_t ni = next_node(T, stack, overflow);
-        if (COUNT) tc.nodes++;
-        const NodeWords w = load_node8(S.nodes8, ni);
-        test_node8_words(w, T.R, 0.0f, fminf(cull, T.best), T.g_hits, T.t_mask, T.t_valid, T.g_base, T.t_base, T.g_flip);
-    }
+    if (!tdone && T.t_mask == 0u && (T.g_hits != 0u || T.sp > 0)) node_step<COUNT>(S, T, stack, tc, overflow, cull);
     return tdone || (T.t_mask == 0u && T.g_hits == 0u && T.sp == 0);
 #undef RT_ISECT
 }
@@ -856,8 +862,110 @@ __global__ void __launch_bounds__(kSortThreads) wf_sort_scatter(DevScene S, WfPa
 // wave by one traversal step (trav_step); a lane whose query ended takes the next ray of the
 // wave's chunk once at least Q.refill_min lanes are idle.  A wave therefore runs ~(steps of its
 // rays) / 64 iterations instead of (slowest ray) x (rays per lane).
+// ---- cooperative triangle phase (wf_trace) -----------------------------------------------------------
+// Instead of every lane testing up to two of its own pending triangles per iteration (the triangle
+// blocks then run with ~a third of the lanes busy), the wave lays the pending triangles of all its
+// lanes (up to kCoopTake per lane, 64 in all) out as jobs, one per lane: the job lane fetches its
+// owner's ray with ds_bpermute, tests the triangle against the owner's bound from the start of the
+// phase, and writes a hit as a 64-bit key (t's magnitude bits, triangle id, job lane) to its LDS
+// slot; the owner takes the minimum key over its jobs' slots -- ordered by (t, id), the
+// lexicographic minimum the serial loop keeps -- fetches that job's (t, V, W, det) and updates its
+// closest hit if (t, id) is below its own; any-hit owners end at any hit.  Every triangle of the
+// owner's list is tested against a bound at least its serial bound, and the minimum is exact, so
+// the result is the serial traversal's, bit for bit.  Triangle slot and id must stay below 2^26
+// (the host checks).
+#ifndef RT_TRACE_COOP
+#define RT_TRACE_COOP 0   // 1: the cooperative triangle phase in wf_trace (A/B builds; measured slower)
+#endif
+// Orders one wave's LDS accesses across its lanes (the stores of some lanes before the loads of
+// others): a compiler barrier plus wavefront-scope fences; the hardware keeps a wave's LDS
+// operations in order.
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    // an LDS atomic without return is not ordered before the wave's next LDS load: wait for the
+    // wave's LDS operations to complete (lgkmcnt(0); vmcnt / expcnt untouched)
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+constexpr uint32_t kCoopTake = 4;   // triangles per lane and iteration
+constexpr uint32_t kCoopIdBits = 26;
+template <bool ANY, bool COUNT>
+__device__ __forceinline__ void coop_tri_phase(const DevScene& S, Trav& T, bool owner, uint32_t* job,
+                                               unsigned long long* key, TraceCounters& tc, bool& tdone) {
+    const uint32_t lane = lane_id();
+    const uint32_t c = owner ? min((uint32_t)__builtin_popcount(T.t_mask), kCoopTake) : 0u;
+    // exclusive prefix of the counts over the wave (c < 8: three ballots)
+    const unsigned long long b0 = __ballot(c & 1u), b1 = __ballot(c & 2u), b2 = __ballot(c & 4u);
+    const uint32_t pre = mbcnt64(b0) + 2u * mbcnt64(b1) + 4u * mbcnt64(b2);
+    const uint32_t total = (uint32_t)__popcll(b0) + 2u * (uint32_t)__popcll(b1) + 4u * (uint32_t)__popcll(b2);
+    const uint32_t take = pre >= 64u ? 0u : min(c, 64u - pre);
+    key[lane] = ~0ull;
+    uint32_t m = T.t_mask;
+    for (uint32_t k = 0; k < take; ++k) {
+        const int b = lowest_bit(m);
+        m &= m - 1u;
+        job[pre + k] = tri_slot(T.t_base, T.t_valid, b) | (lane << kCoopIdBits);
+    }
+    wave_lds_sync();   // job table and cleared keys before the jobs read / post to them
+    const uint32_t njobs = min(total, 64u);
+    const bool has_job = lane < njobs;
+    const uint32_t e = has_job ? job[lane] : (lane << kCoopIdBits);
+    const uint32_t own = e >> kCoopIdBits;
+    // the owner's ray and bound, with every lane active (a bpermute from an inactive lane reads 0)
+    const int src = (int)own;
+    RayPre pre_o;
+    pre_o.kx = __shfl(T.R.pre.kx, src);
+    pre_o.ky = __shfl(T.R.pre.ky, src);
+    pre_o.kz = __shfl(T.R.pre.kz, src);
+    pre_o.Sx = __shfl(T.R.pre.Sx, src);
+    pre_o.Sy = __shfl(T.R.pre.Sy, src);
+    pre_o.Sz = __shfl(T.R.pre.Sz, src);
+    const f3 o_o = mk3(__shfl(T.R.o.x, src), __shfl(T.R.o.y, src), __shfl(T.R.o.z, src));
+    const float bound = __shfl(T.best, src);
+    float t = 0.0f, V = 0.0f, W = 0.0f, dt = 1.0f;
+    if (has_job) {
+        const float4* tp = S.tris + 3 * (size_t)(e & ((1u << kCoopIdBits) - 1u));
+        const float4 a0 = tp[0], a1 = tp[1], a2 = tp[2];
+        if (COUNT) tc.tris++;
+        if (intersect_triangle_vw(pre_o, o_o, ld3(a0), ld3(a1), ld3(a2), 0.0f, bound, &t, &V, &W, &dt)) {
+            const uint32_t id = __float_as_uint(a0.w);
+            const unsigned long long kv = ((unsigned long long)(__float_as_uint(t) & 0x7fffffffu) << 32) |
+                                          ((unsigned long long)id << 6) | lane;
+            key[lane] = kv;   // this job's result
+        }
+    }
+    wave_lds_sync();   // every job's result before the owners read them
+    // the owner's minimum over its own jobs' slots (a ds_min_u64 into one slot per owner measured
+    // wrong results under load: garbage frames in bulk mode; the owner's own loop over <= 4 slots is exact)
+    unsigned long long kmin = ~0ull;
+    for (uint32_t k = 0; k < take; ++k) kmin = min(kmin, key[pre + k]);
+    const int wl = (int)(kmin & 63u);
+    const float wt = __shfl(t, wl), wV = __shfl(V, wl), wW = __shfl(W, wl), wdt = __shfl(dt, wl);
+    if (owner) {
+        T.t_mask = m;
+        if (kmin != ~0ull) {
+            const uint32_t wid = (uint32_t)(kmin >> 6) & ((1u << kCoopIdBits) - 1u);
+            if (ANY) {
+                T.hit_any = true;
+                tdone = true;
+            } else if (wt < T.best || (wt == T.best && wid < T.best_id)) {
+                T.best = wt;
+                T.best_id = wid;
+                T.bu = wV;
+                T.bv = wW;
+                T.bdet = wdt;
+            }
+        }
+    }
+}
+
 #ifndef RT_EXTEND_WAVES
+#if RT_TRACE_COOP
+#define RT_EXTEND_WAVES 7   // the cooperative phase needs 70 VGPRs (20 B of scratch at 64)
+#else
 #define RT_EXTEND_WAVES 8   // 64 VGPRs, no scratch (final round-2 node test; at 70 VGPRs it took 7 waves)
+#endif
 #endif
 template <bool ANY, bool COUNT>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ANY ? 8 : RT_EXTEND_WAVES, ANY ? 8 : RT_EXTEND_WAVES)))
@@ -865,6 +973,10 @@ wf_trace(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int cur, in
     const FrameParams& P = *Pp;   // per-frame parameters in device memory
     __shared__ int lds_stack[kStackSize * kBlock];
     int* stack = &lds_stack[threadIdx.x];
+#if RT_TRACE_COOP
+    __shared__ uint32_t lds_job[kBlock];              // per wave: 64 jobs (triangle slot | owner lane << 26)
+    __shared__ unsigned long long lds_key[kBlock];    // per lane: the best (t, id, job lane) posted to it
+#endif
     if (Q.dev_ctl) {
         // device-side round control: extend decides (uniformly, from the counters) whether this
         // round runs in bulk or the rest of the pass goes to the finish launch
@@ -970,9 +1082,20 @@ wf_trace(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int cur, in
             wnext += (uint32_t)__popcll(idle);
         }
         if (__ballot(active) == 0ull) break;
+#if RT_TRACE_COOP
+        if (COUNT && active) ++steps;
+        bool done = false;
+        if (__ballot(active && T.t_mask != 0u) != 0ull)   // wave-uniform: every lane serves as a job lane
+            coop_tri_phase<ANY, COUNT>(S, T, active && T.t_mask != 0u, &lds_job[threadIdx.x & ~63u],
+                                       &lds_key[threadIdx.x & ~63u], tc, done);
+        if (!active) continue;
+        if (!done && T.t_mask == 0u && (T.g_hits != 0u || T.sp > 0)) node_step<COUNT>(S, T, stack, tc, overflow, T.best);
+        if (done || (T.t_mask == 0u && T.g_hits == 0u && T.sp == 0)) {
+#else
         if (!active) continue;
         if (COUNT) ++steps;
         if (trav_step<COUNT>(S, T, ANY, stack, tc, overflow, T.best)) {
+#endif
             active = false;
             if (COUNT && Q.diag) {   // steps-per-ray histogram (log2 bins) of the counting frame
                 atomicAdd(&Q.W.counts[kWfDiagSteps + (ANY ? 32 : 0) + (31 - __builtin_clz(steps))], 1u);
