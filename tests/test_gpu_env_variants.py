@@ -1,5 +1,6 @@
-"""Runtime variants selected by environment switches (read once per process, so each runs in a
-child process): host-driven rounds (RT_WF_HOST=1: queue sizes read back every round instead of
+"""Runtime scheduling variants, each in a child process whose legacy RT_* environment switches
+tests/helpers.make_renderer maps onto the library's rt_set_tuning / rt_set_graphs (the library
+itself reads no environment): host-driven rounds (RT_WF_HOST=1: queue sizes read back every round instead of
 the device-side round control), eager enqueue without frame graphs (RT_GRAPH=0), and the finish
 kernel's scheduling knobs at other values (odd chunk sizes, an absolute shading threshold after the
 queue runs out, the long-first order's chunks split over few blocks, the finish drain's team

@@ -1,8 +1,8 @@
 """Child process of test_gpu_traversal_variants.py: the adversarial closest-hit scenes (the
 triangle soup and the exact-tie scene, tests/helpers.py) through the given pipelines, against the
 CPU oracle, in a process whose environment selects a traversal instance (RT_TEAM lanes per query
-in the finish kernel's drain, RT_FINISH_POOL, RT_FCHUNK ...: the library reads RT_* once per
-process).  Prints one line per case; exits non-zero on the first mismatch."""
+in the finish kernel's drain, RT_FCHUNK ...: tests/helpers.make_renderer maps these onto the
+library's rt_set_tuning).  Prints one line per case; exits non-zero on the first mismatch."""
 import importlib
 import os
 import sys
