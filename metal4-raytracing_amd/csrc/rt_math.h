@@ -111,6 +111,38 @@ RT_HD float halton_fast(int i, const HaltonDim& h) {
     return r;
 }
 
+// halton_fast for base 2 (dimension 0) in closed form: the loop adds the bits of i, lowest first,
+// at weights 2^-1, 2^-2, ...; each sum is exact until 24 significant bits are held, the next bit is
+// a tie (exactly half an ulp: round to even) and every later bit is below half an ulp.  So the
+// result is the bit-reversed fraction cut to 24 significant bits plus that one tie.  Bit-identical
+// to the loop for every int (checked exhaustively over all 2^31 positive i: tools/halton2_check.c).
+RT_HD uint32_t bitrev32(uint32_t x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_bitreverse32(x);
+#else
+    x = ((x >> 1) & 0x55555555u) | ((x & 0x55555555u) << 1);
+    x = ((x >> 2) & 0x33333333u) | ((x & 0x33333333u) << 2);
+    x = ((x >> 4) & 0x0f0f0f0fu) | ((x & 0x0f0f0f0fu) << 4);
+    x = ((x >> 8) & 0x00ff00ffu) | ((x & 0x00ff00ffu) << 8);
+    return (x >> 16) | (x << 16);
+#endif
+}
+RT_HD float halton_base2(int i) {
+    if (i <= 0) return 0.0f;
+    const uint32_t b = bitrev32((uint32_t)i);   // i's bits as a 32-bit fraction (bit 31 = weight 1/2)
+    uint32_t r = b;
+    const int drop = 8 - __builtin_clz(b);      // bits below the 24 kept from the leading one
+    if (drop > 0) {
+        const uint32_t half = (b >> (drop - 1)) & 1u, last = (b >> drop) & 1u;
+        r = b & ~((1u << drop) - 1u);
+        if (half & last) {
+            r += 1u << drop;
+            if (r == 0u) return 1.0f;           // carried out of the fraction
+        }
+    }
+    return (float)r * 2.3283064365386963e-10f;  // exact: <= 24 significant bits, times 2^-32
+}
+
 // ---- sampling helpers ------------------------------------------------------------------------
 // Raytracing.metal:79-89
 RT_HD f3 sampleCosineWeightedHemisphere(float ux, float uy) {

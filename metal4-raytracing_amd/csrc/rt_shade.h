@@ -28,6 +28,7 @@ struct ShadeTabs {
     const Material* mat_glob;
     int n_mat_lds;             // = number of materials when they fit in LDS, else 0
     __device__ __forceinline__ float operator()(int i, int d) const {
+        if (d == 0) return halton_base2(i);   // base 2: closed form (bit-identical, rt_math.h)
         return halton_fast(i, d < kHaltonLds ? lds[d] : glob[d]);
     }
     __device__ __forceinline__ MatRec material(int slot) const {
