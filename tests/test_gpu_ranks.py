@@ -37,7 +37,7 @@ def test_ranks_share_one_gpu_gloo_gather_bitwise(tmp_path, n):
     assert many["config"]["rays_per_frame"] == one["config"]["rays_per_frame"]
     pr = many["config"]["per_rank"]   # each rank's own figures (load balance of the split)
     assert [x["rank"] for x in pr] == list(range(n)) and all(x["ms_per_step"] > 0 for x in pr)
-    assert sum(x["rays_per_frame"] for x in pr) == many["config"]["rays_per_frame"]
+    assert abs(sum(x["rays_per_frame"] for x in pr) - many["config"]["rays_per_frame"]) <= n   # per-rank truncation
     a, b = np.load(tmp_path / "one.npy"), np.load(tmp_path / "many.npy")
     assert a.shape == b.shape == (136, 200, 4)
     diff = np.any(a != b, axis=-1)
