@@ -44,6 +44,13 @@ RT_HD f3 cross(f3 a, f3 b) {
     return mk3(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
 }
 RT_HD float length(f3 a) { return sqrtf(dot(a, a)); }
+// length(a) < c / length(a) > c for the constants the shading code compares against, without the
+// square root: sqrtf and round-to-nearest are monotonic, so each comparison is one on dot(a, a)
+// against the first / last float on the other side -- the same result for every input (found and
+// checked over every non-negative float: tools/sqrt_thresholds.c, tests/test_sqrt_thresholds.py).
+RT_HD bool length_lt_1e10(f3 a) { return dot(a, a) < 0x1.79ca1p-67f; }    // length(a) < 1e-10f
+RT_HD bool length_lt_1e3(f3 a) { return dot(a, a) < 0x1.0c6f7ap-20f; }    // length(a) < 0.001f
+RT_HD bool length_gt_1e4(f3 a) { return dot(a, a) > 0x1.5798eep-27f; }    // length(a) > 0.0001f
 // normalize(v) = v * (1/sqrt(dot(v,v)))  (Metal: v * rsqrt(dot(v,v)))
 RT_HD f3 normalize(f3 a) { float inv = 1.0f / sqrtf(dot(a, a)); return a * inv; }
 RT_HD float clampf(float x, float lo, float hi) { return fminf(fmaxf(x, lo), hi); }

@@ -195,7 +195,7 @@ __device__ __forceinline__ void shade_step(const DevScene& S, const Uniforms& U,
 
     f3 objN = (bu * ld3(rn1) + bv * ld3(rn2)) + bw * ld3(rn0);                     // :391
     f3 Ng = normalize(xform(M, objN, 0.0f));                                          // :392-393
-    if (length(objN) < 1e-10f) Ng = -rayD;                                            // :395-397
+    if (length_lt_1e10(objN)) Ng = -rayD;                                             // :395-397
 
     f3 albedo = ld3(mat.base);                                                        // :399
     float roughness = 1.0f, metallic = 0.0f;                                          // :431-441
@@ -390,8 +390,8 @@ __device__ __forceinline__ void shade_step(const DevScene& S, const Uniforms& U,
         f3 L = normalize(Ldir);
         float NdotL = saturate(dot(shadingNormal, L));
         f3 legacyColor = p.color * albedo;
-        if (length(legacyColor) < 0.001f) return;
-        if (length(lightColor) > 0.0001f && NdotL > 0.0f) {
+        if (length_lt_1e3(legacyColor)) return;
+        if (length_gt_1e4(lightColor) && NdotL > 0.0f) {
             r.shadow = true;
             r.so = origin;
             r.sd = Ldir;
@@ -399,7 +399,7 @@ __device__ __forceinline__ void shade_step(const DevScene& S, const Uniforms& U,
             r.contrib = (legacyColor * lightColor) * NdotL;
         }
         p.color = legacyColor * ao;
-        if (length(p.color) < 0.001f) return;
+        if (length_lt_1e3(p.color)) return;
         float r0 = halton(hidx, 2 + p.step * 5 + 3), r1 = halton(hidx, 2 + p.step * 5 + 4);
         rayD = alignHemisphereWithNormal(sampleCosineWeightedHemisphere(r0, r1), shadingNormal);
         rayO = origin;
@@ -410,7 +410,7 @@ __device__ __forceinline__ void shade_step(const DevScene& S, const Uniforms& U,
         return;
     }
 
-    if (length(lightColor) > 0.0001f) {                                               // :692-744
+    if (length_gt_1e4(lightColor)) {                                                  // :692-744
         f3 L = normalize(Ldir);
         f3 H = normalize(V + L);
         float NdotL = saturate(dot(shadingNormal, L));
@@ -434,7 +434,7 @@ __device__ __forceinline__ void shade_step(const DevScene& S, const Uniforms& U,
     }
 
     p.color = p.color * ((diffuseColor * (1.0f - metallic)) * ao);                    // :748
-    if (length(p.color) < 0.001f) return;                                             // :751-753
+    if (length_lt_1e3(p.color)) return;                                               // :751-753
     float r0 = halton(hidx, 2 + p.step * 5 + 3), r1 = halton(hidx, 2 + p.step * 5 + 4);  // :763-764
     rayD = alignHemisphereWithNormal(sampleCosineWeightedHemisphere(r0, r1), shadingNormal);
     rayO = origin;                                                                    // :769-770
