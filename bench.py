@@ -31,12 +31,14 @@ import time
 import numpy as np
 
 # Hardware queues per process, fixed before anything initialises HIP so every run sees the same
-# count: RT_HW_QUEUES if set, else the caller's GPU_MAX_HW_QUEUES, else four (HIP's default, also
-# what the GPU boxes export).  Small frames (a multi-GPU rank's share) keep as many frames in
-# flight as there are queues, up to eight (rt_api.cpp small_frame_slots); with the final round-2
-# kernels four queues / four slots measured 4.21 / 4.24 Grays/s per rank against eight / eight
-# 4.11 / 4.10.
-os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("RT_HW_QUEUES") or os.environ.get("GPU_MAX_HW_QUEUES") or "4"
+# count: RT_HW_QUEUES if set, else eight (the library keeps one frame in flight per queue, up to
+# eight: rt_api.cpp small_frame_slots).  Since the slot streams stopped waiting on the context
+# stream (round 5), eight queues / eight frames in flight measured, against HIP's default four
+# (which the GPU boxes export): C3g 9.47-9.51 vs 9.26-9.31 Grays/s at 20 steps, 9.55-9.56 vs
+# 9.35-9.38 at 32; configs[1] 10.03 vs 9.78; the 8-way rank share 6.76 vs 6.18; configs[3] +-0;
+# but the animated configs[4] (skin + refit every frame) 10.21-10.33 vs 10.77-10.86, so --animate
+# keeps four (profiles/r05_finish_experiments.txt).
+os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("RT_HW_QUEUES") or ("4" if "--animate" in sys.argv else "8")
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
@@ -217,7 +219,7 @@ def parse(argv=None):
     p.add_argument("--sort-bins", type=int, default=0, help="hit-sort bins (0 = library default, -1 = no sort)")
     p.add_argument("--bvh", default="sah", choices=["sah", "lbvh"], help="host binned-SAH or on-device LBVH build")
     p.add_argument("--frames-in-flight", type=int, default=0,
-                   help="frames the renderer overlaps (0 = library default: one per hardware queue, 4 with the queues set here, 8 with RT_HW_QUEUES=8, within a 96 GB budget; 1 = one at a time)")
+                   help="frames the renderer overlaps (0 = library default: one per hardware queue: 8 with the queues set here (4 with --animate or RT_HW_QUEUES=4), within a 96 GB budget; 1 = one at a time)")
     p.add_argument("--animate", action="store_true",
                    help="configs[4] shape: skin every skinned mesh at t = frame/60 s and refit the BVH before each frame")
     p.add_argument("--rebuild", action="store_true", help="with --animate: rebuild the BVH on the device instead of refitting")

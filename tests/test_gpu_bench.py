@@ -21,26 +21,26 @@ def _run(*args):
 
 
 def test_bench_line_contract():
-    # 8 steps over four frame slots: each slot's first timed frame may capture, the later ones replay
-    d = _run("--scene", "c1", "--width", "128", "--height", "96", "--spp", "2", "--bounces", "3", "--steps", "8",
-             "--warmup", "1", "--cpu-seconds", "0.5")
+    # 12 steps over eight frame slots: each slot's first frame may capture, the later ones replay
+    d = _run("--scene", "c1", "--width", "128", "--height", "96", "--spp", "2", "--bounces", "3", "--steps", "12",
+             "--warmup", "4", "--cpu-seconds", "0.5")
     for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
               "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"):
         assert k in d, k
-    assert d["n_gpus"] == 1 and d["steps"] == 8 and d["value"] > 0 and d["unit"] == "Grays/s"
+    assert d["n_gpus"] == 1 and d["steps"] == 12 and d["value"] > 0 and d["unit"] == "Grays/s"
     r = d["roofline"]
     for k in ("bound", "achieved", "peak", "unit", "frac", "traffic"):
         assert k in r, k
     assert r["bound"] == "hbm" and r["peak"] == 8000.0 and r["frac"] > 0
     cb = d["cpu_baseline"]
     assert cb["value"] > 0 and cb["kind"] == "port" and cb["cores"] >= 1
-    # a small frame (< 8M allocated paths) keeps four frames in flight: bench.py fixes HIP's
-    # hardware queues at four (rt_api.cpp small_frame_slots)
-    assert d["config"]["frames_in_flight"] == 4
+    # one frame in flight per hardware queue: bench.py fixes HIP's hardware queues at eight
+    # (rt_api.cpp small_frame_slots)
+    assert d["config"]["frames_in_flight"] == 8
     _roofline_consistent(d)
     # the timed frames replay captured HIP graphs
     g = d["config"]["graphs"]
-    assert g["fallbacks"] == 0 and g["eager"] == 0 and g["replays"] >= 4 and g["replays"] + g["captures"] == 8
+    assert g["fallbacks"] == 0 and g["eager"] == 0 and g["replays"] >= 4 and g["replays"] + g["captures"] == 12
 
 
 def _roofline_consistent(d):
