@@ -96,6 +96,11 @@ static int small_frame_slots() {
     }();
     return n;
 }
+// Frames below this many allocated paths keep at most four slots: a configs[0]-sized frame (65K
+// paths, ~0.05 ms) on eight slots / eight queues ran bimodally, 2.04-2.10 or 0.55-0.62 Grays/s
+// (3 of 6 runs slow), against 2.10-2.54 on four (round 5); the 8-way C3g share (1M paths) gains
+// 9 % from eight slots and was steady.
+constexpr uint64_t kSmallFramePaths = 1ull << 19;
 }  // namespace
 
 struct rt_ctx {
@@ -1019,8 +1024,9 @@ rt_status rt_render_frame(rt_ctx* c, const Uniforms* U, const rt_tile_set* tiles
     int nfl = 1;
     if (wavefront && c->stream == c->own_stream) {
         const uint64_t frame_paths = (uint64_t)own * ts * ts * (uint64_t)(spp + max_extra);
+        const uint64_t slots = frame_paths < kSmallFramePaths ? std::min(4, small_frame_slots()) : small_frame_slots();
         nfl = c->max_in_flight > 0 ? c->max_in_flight
-                                   : (int)std::max<uint64_t>(2, std::min<uint64_t>(small_frame_slots(),
+                                   : (int)std::max<uint64_t>(2, std::min<uint64_t>(slots,
                                                                               kSlotBudget / (frame_paths * kSlotBytesPerPath + 1)));
     }
     const int k = c->frame_no > 0 ? (c->last_slot + 1) % nfl : 0;
