@@ -38,7 +38,9 @@ import numpy as np
 # 9.35-9.38 at 32; configs[1] 10.03 vs 9.78; the 8-way rank share 6.76 vs 6.18; configs[3] +-0;
 # but the animated configs[4] (skin + refit every frame) 10.21-10.33 vs 10.77-10.86, so --animate
 # keeps four (profiles/r05_finish_experiments.txt).
-os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("RT_HW_QUEUES") or ("4" if "--animate" in sys.argv else "8")
+# (Only when run as a program: tests import this module for its helpers.)
+if __name__ == "__main__":
+    os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("RT_HW_QUEUES") or ("4" if "--animate" in sys.argv else "8")
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)

@@ -96,8 +96,9 @@ def test_in_flight_then_megakernel_frame(rt, assets):
         assert np.array_equal(out[0][1], mot)
 
 
-# 0: the library default for a rank's small frame (eight slots with eight hardware queues)
-@pytest.mark.parametrize("fif,expect", [(2, 2), (0, 8 if int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) >= 8 else 4)])
+# 0: the library default for a rank's small frame: at most four slots below 512K paths
+# (rt_api.cpp kSmallFramePaths), whatever the hardware queue count
+@pytest.mark.parametrize("fif,expect", [(2, 2), (0, 4)])
 def test_in_flight_tile_gather(rt, assets, fif, expect):
     """Two ranks' renderers (tile split, frames in flight) with the per-frame gather enqueued on
     a separate stream without host waits (rank 1 packs, rank 0 unpacks, the pattern of
