@@ -101,6 +101,8 @@ static int small_frame_slots() {
 // (3 of 6 runs slow), against 2.10-2.54 on four (round 5); the 8-way C3g share (1M paths) gains
 // 9 % from eight slots and was steady.
 constexpr uint64_t kSmallFramePaths = 1ull << 19;
+constexpr uint64_t kSmallShareBasePaths = 2500000;   // see rt_render_frame's tail
+constexpr int kTailShare = 786432;
 }  // namespace
 
 struct rt_ctx {
@@ -1136,7 +1138,11 @@ rt_status rt_render_frame(rt_ctx* c, const Uniforms* U, const rt_tile_set* tiles
         // finish threshold: with frames in flight the next frames' bulk rounds overlap this
         // frame's tail, so more bulk rounds and a shorter tail pay (kTailInFlight: C3g, 2 in
         // flight 1.25M paths against the one-frame-at-a-time optimum of 4M; 3 in flight 1M)
-        const int tail = c->tail_paths ? c->tail_paths : (nfl > 1 ? kTailInFlight[nfl] : 0);
+        int tail = c->tail_paths ? c->tail_paths : (nfl > 1 ? kTailInFlight[nfl] : 0);
+        // eight frames in flight and a frame of at most 2.5M base paths (a multi-GPU rank's share):
+        // 768K (round 5, finish on 12 % of the grid: 8-way share 7.02 -> 7.20, 4-way 8.44 -> 8.54
+        // Grays/s; 1M hands the 8-way share's whole frame to the finish: 6.08)
+        if (!c->tail_paths && nfl >= 8 && (uint64_t)own * ts * ts * (uint64_t)spp <= kSmallShareBasePaths) tail = kTailShare;
         if (own > 0 && !run_wavefront(S, P, F.wf, c->tuning, own, c->counting, c->spans, tail, c->sort_bins, extra_pass,
                                       nfl, stream, cross ? prev.done : nullptr, &F.wft, &F.wfs, &err, c->graphs))
             FAIL(c, RT_ERR_HIP, std::string("wavefront: ") + (err ? err : "?"));
