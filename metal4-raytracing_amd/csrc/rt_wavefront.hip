@@ -2230,12 +2230,12 @@ bool run_wavefront(const DevScene& S, const FrameParams& P, WavefrontBuffers& W,
     // leaving CUs to the other frames' kernels (C3g 8.51-8.64 -> 8.61-8.72 Grays/s over five
     // alternating pairs, 75 % +0.5 %; the 8-way rank share at 75 % +0.9 %); fewer frames: all of it
     Q.trace_frac = tu.trace_frac > 0 ? tu.trace_frac : (in_flight >= 4 ? 60 : 100);
-    // eight frames in flight of at most kTeamAutoPaths base paths (a multi-GPU rank's share): 12 %
-    // (round 5, after the slots stopped serialising: 8-way rank share 6.76 -> 7.02, 4-way 8.14 ->
-    // 8.44, 2-way 9.12 -> 9.35 Grays/s; 8 % +-0, 33 % -10 %; the whole C3g frame +-0 and configs[3]'s
-    // 16.6M-path rank share -2 %, so larger frames keep 20 %)
+    // eight frames in flight of at most 6M base paths (a multi-GPU rank's share): 12 % (round 5,
+    // after the slots stopped serialising: 8-way rank share 6.76 -> 7.02, 4-way 8.14 -> 8.44, 2-way
+    // (4.1M paths) 9.12 -> 9.35 Grays/s; 8 % +-0, 33 % -10 %; the whole C3g frame (8.3M) +-0 and
+    // configs[3]'s 16.6M-path rank share -2 %, so larger frames keep 20 %)
     Q.finish_frac = tu.finish_frac > 0 ? tu.finish_frac
-                  : (in_flight >= 8 && Q.base_paths <= kTeamAutoPaths) ? 12
+                  : (in_flight >= 8 && Q.base_paths <= 6000000u) ? 12
                   : in_flight >= 4 ? 20 : in_flight == 2 ? 40 : (in_flight > 1 ? 100 / in_flight : 100);
     if (sort_bins && (sort_bins < kSortMinBins || sort_bins > kSortMaxBins || (sort_bins & (sort_bins - 1)) ||
                       !S.tri_bin || !W.sorted)) {
