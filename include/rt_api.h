@@ -313,10 +313,13 @@ rt_status rt_get_stats(rt_ctx* ctx, rt_stats* out);
  * Metal driver schedules the reference's one kernel).  0 in any field selects the measured default;
  * images are identical for every value.  The library reads no environment variable
  * for these: only this call changes them, per context.  rt_set_tuning(ctx, NULL) restores the
- * defaults; rt_get_tuning returns the values in effect (defaults resolved). */
+ * defaults; a field outside its stated range is RT_ERR_INVALID_ARG.  rt_get_tuning returns the
+ * values in effect for the fields with a fixed default; team, finish_grid_pct and trace_grid_pct
+ * read back 0 when left at their default, which is chosen per frame from the frame size and the
+ * frames in flight (rt_stats reports the frame's rounds and launches, not these choices). */
 typedef struct rt_tuning {
-    int32_t trace_chunk;        /* rays per chunk grab of the bulk traversal launches (default 64) */
-    int32_t finish_chunk;       /* paths per chunk grab of the finish launch (default 64) */
+    int32_t trace_chunk;        /* rays per chunk grab of the bulk traversal launches (default 64; <= 4096) */
+    int32_t finish_chunk;       /* paths per chunk grab of the finish launch (default 64; <= 4096) */
     int32_t refill_min;         /* traversal / finish waves refill once this many lanes are idle (default 8) */
     int32_t shade_min;          /* the finish kernel shades once this many lanes wait for it (default 24) */
     int32_t shade_min_drained;  /* the same once its queue has run out: > 0 lanes, < 0 that percentage of
@@ -328,7 +331,7 @@ typedef struct rt_tuning {
                                    frames in flight: 100 / 40 / 33 / 20 for 1 / 2 / 3 / 4+) */
     int32_t trace_grid_pct;     /* percent of the resident grid the bulk traversal launches take
                                    (default 100, 60 with four or more frames in flight) */
-    int32_t shade_blocks;       /* wf_shade grid, a multiple of 8 (default 2048) */
+    int32_t shade_blocks;       /* wf_shade grid, a multiple of 8 (default 2048; <= 65536) */
     int32_t host_rounds;        /* 1: host-driven rounds (each round's queue size read back); default 0:
                                    device-side round control, whole frames as HIP graphs */
     int32_t log;                /* 1: per-round queue sizes, stage times and finish diagnostics on stderr

@@ -103,6 +103,12 @@ static int small_frame_slots() {
 constexpr uint64_t kSmallFramePaths = 1ull << 19;
 constexpr uint64_t kSmallShareBasePaths = 2500000;   // see rt_render_frame's tail
 constexpr int kTailShare = 786432;
+// rt_set_tuning bounds: a chunk grab past the end of a queue still adds the chunk size to its
+// 32-bit counter, once per wave (at most ~16K waves resident); 4096 x 16K stays far below 2^32
+// minus any queue the library allocates.  The shade grid is grid-stride, so more blocks than
+// 64K buy nothing.
+constexpr int kMaxTuneChunk = 4096;
+constexpr int kMaxTuneShadeBlocks = 65536;
 }  // namespace
 
 struct rt_ctx {
@@ -708,7 +714,8 @@ rt_status rt_bvh_build(rt_ctx* c) {
         }
         c->world_dirty = false;
     }
-    // wf_trace's cooperative triangle phase packs a triangle slot / id with a lane into 32 bits
+    // the size the host and device builders are tested to (the device build's 64-bit Morton keys
+    // carry the triangle id beside the Morton bits)
     if (c->num_tris >= (1u << 26)) FAIL(c, RT_ERR_UNSUPPORTED, "more than 2^26 triangles");
     if (!build_bvh8_fit(c->h_world.data(), c->num_tris, c->bvh, c->bvh8))
         FAIL(c, RT_ERR_UNSUPPORTED, "BVH deeper than the traversal stack at every depth limit");
@@ -1410,9 +1417,13 @@ rt_status rt_set_tuning(rt_ctx* c, const rt_tuning* t) {
     if (t) v = *t;
     if (v.team != 0 && v.team != 1 && v.team != 2 && v.team != 4 && v.team != 8)
         FAIL(c, RT_ERR_INVALID_ARG, "rt_tuning.team must be 0 (default), 1 (off), 2, 4 or 8");
-    if (v.trace_chunk < 0 || v.finish_chunk < 0 || v.refill_min < 0 || v.refill_min > 64 || v.shade_min < 0 ||
-        v.shade_min > 64 || v.shade_min_drained > 64 || v.shade_min_drained < -100 || v.finish_grid_pct < 0 ||
-        v.trace_grid_pct < 0 || v.shade_blocks < 0 || v.log < 0 || v.log > 2 || v.device_bvh < 0 || v.device_bvh > 1)
+    // chunk grabs are 32-bit atomicAdds of the chunk size by every wave of the grid (and base + chunk
+    // is formed in 32 bits): bounded so that neither can wrap for any queue the library allocates
+    if (v.trace_chunk < 0 || v.trace_chunk > kMaxTuneChunk || v.finish_chunk < 0 || v.finish_chunk > kMaxTuneChunk ||
+        v.refill_min < 0 || v.refill_min > 64 || v.shade_min < 0 || v.shade_min > 64 || v.shade_min_drained > 64 ||
+        v.shade_min_drained < -100 || v.finish_grid_pct < 0 || v.finish_grid_pct > 100 || v.trace_grid_pct < 0 ||
+        v.trace_grid_pct > 100 || v.shade_blocks < 0 || v.shade_blocks > kMaxTuneShadeBlocks || v.log < 0 || v.log > 2 ||
+        v.device_bvh < 0 || v.device_bvh > 1)
         FAIL(c, RT_ERR_INVALID_ARG, "rt_tuning field out of range");
     // frames already in flight keep the parameters they were enqueued with (their graphs' keys)
     c->tuning_req = v;

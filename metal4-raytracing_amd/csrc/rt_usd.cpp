@@ -1705,16 +1705,23 @@ private:
             }
             for (int b : bodies)
                 if (!merge(L, p, L, b, L.prims[b].path, L.prims[p].path)) return false;
+            // the internal arcs of one round all read this layer's namespace as it stood before the
+            // round's merges (as in USD, where the arcs of one list target the authored namespace,
+            // not each other's results): one snapshot per round, taken before the round's arcs merge
+            // and charged once against the byte budget (thousands of rounds next to one large array
+            // still fail fast instead of copying the layer thousands of times)
+            auto is_internal = [&](const Arc& a) { return a.asset.empty() || (a.resolved && a.asset == id); };
+            std::shared_ptr<const Stage> snapshot;
+            if (std::any_of(arcs.begin(), arcs.end(), is_internal)) {
+                if (!spend(L.prims.size()) || !spend_bytes(stage_bytes(L))) return false;
+                snapshot = std::make_shared<const Stage>(L);
+            }
             for (const Arc& a : arcs) {
-                if (!spend(1 + (a.asset.empty() ? L.prims.size() : 0))) return false;
+                if (!spend(1)) return false;
                 std::shared_ptr<const Stage> S;
-                const bool internal = a.asset.empty() || (a.resolved && a.asset == id);
-                // an internal arc reads this layer's namespace as it stands: a snapshot, whose copy
-                // is charged against the byte budget like a merge (thousands of internal arcs next to
-                // one large array must fail fast, not copy the layer thousands of times)
+                const bool internal = is_internal(a);
                 if (internal) {
-                    if (!spend_bytes(stage_bytes(L))) return false;
-                    S = std::make_shared<const Stage>(L);
+                    S = snapshot;
                 } else if (!(S = load(a.resolved ? a.asset : resolve(id, a.asset), depth + 1))) return false;
                 const int t = target(*S, a);
                 if (t <= 0) return fail("reference target " + (a.path.empty() ? "(default prim)" : a.path) + " not found in " +

@@ -69,40 +69,11 @@ __device__ __forceinline__ uint32_t block_alloc(bool pred, uint32_t* counter, Bl
     return r;
 }
 
-// Three block-aggregated allocations at once (wf_shade: shadow ray, front / back continuation ray).
-struct BlockAlloc3 {
-    uint32_t w[3][kBlock / 64];
-};
-__device__ __forceinline__ void block_alloc3(const bool (&pr)[3], uint32_t* const (&ctr)[3], BlockAlloc3& sh,
-                                             uint32_t (&out)[3]) {
-    const int wave = threadIdx.x >> 6;
-    unsigned long long m[3];
-    #pragma unroll
-    for (int i = 0; i < 3; ++i) m[i] = __ballot(pr[i]);
-    if (lane_id() == 0) {
-        #pragma unroll
-        for (int i = 0; i < 3; ++i) sh.w[i][wave] = (uint32_t)__popcll(m[i]);
-    }
-    __syncthreads();
-    if (threadIdx.x < 3) {
-        uint32_t* w = sh.w[threadIdx.x];
-        const uint32_t c0 = w[0], c1 = w[1], c2 = w[2], c3 = w[3];
-        const uint32_t tot = c0 + c1 + c2 + c3;
-        const uint32_t b = tot ? atomicAdd(ctr[threadIdx.x], tot) : 0u;
-        w[0] = b;
-        w[1] = b + c0;
-        w[2] = b + c0 + c1;
-        w[3] = b + c0 + c1 + c2;
-    }
-    __syncthreads();
-    #pragma unroll
-    for (int i = 0; i < 3; ++i) out[i] = sh.w[i][wave] + mbcnt64(m[i]);
-    __syncthreads();
-}
-
-// block_alloc3 with the continuation rays (pr[1] front, pr[2] back) of the block grouped by the
-// direction octant `oct` (3 bits) inside each part's range: a per-block counting sort of the
-// appends through LDS atomics (the rank inside an octant is arbitrary), no separate sort pass.
+// Three block-aggregated allocations at once (wf_shade: pr[0] shadow ray, pr[1] front / pr[2] back
+// continuation ray), one returning global atomic per part and block, with the continuation rays
+// grouped by the direction octant `oct` (3 bits) inside each part's range: a per-block counting
+// sort of the appends through LDS atomics (the rank inside an octant is arbitrary), no separate
+// sort pass.
 struct BlockAllocOct {
     uint32_t cnt[3][8];    // shadow uses [0][0]
     uint32_t base[3][8];
@@ -352,11 +323,8 @@ __device__ __forceinline__ uint32_t dense_entry(const QueueShards& qs, uint32_t 
     const uint32_t i = g - start;
     return k * seg_cap + (back ? seg_cap - 1u - i : i);
 }
-#ifndef RT_LONG_FIRST
-#define RT_LONG_FIRST 1   // 0: every continuation ray to the front (one-sided queues; A/B builds)
-#endif
 __device__ __forceinline__ bool likely_long(const PathRegs& p) {
-    return !RT_LONG_FIRST || p.tpass > 0 || p.bounce < p.step;
+    return p.tpass > 0 || p.bounce < p.step;
 }
 
 // A path's state between launches: its accumulator here (indexed by path id), its throughput
@@ -613,32 +581,21 @@ __global__ void __launch_bounds__(kBlock) wf_generate(DevScene S, const FramePar
 // blocks of XCD k (blockIdx % 8) shade the k-th eighth of it, so one XCD's L2 serves one scene
 // region and the rays / shadow rays it appends to its queue shard stay grouped by region for
 // the next extend / connect launches (which hand shard k's range to XCD k).
-#ifndef RT_SHADE_NT
-#define RT_SHADE_NT 1   // wf_shade streams its queue entries with nontemporal loads (0: plain loads; A/B builds)
-#endif
-#ifndef RT_TRACE_NT
-#define RT_TRACE_NT 2   // bit 0: wf_trace (extend), bit 1: the finish refill read their queue entries nontemporally
-                        // (the extend entries are read again by wf_shade: bit 0 slows it)
-#endif
-// a 16-B load of data read once (nontemporal: it does not displace the lines gathered beside it)
+// a 16-B load of data read once (nontemporal: it does not displace the lines gathered beside it).
+// wf_shade and the finish refill read their queue entries this way; wf_trace (extend) does not
+// (wf_shade reads the same entries again: nontemporal extend loads slowed it, round 4)
 __device__ __forceinline__ float4 ld_stream(const float4* p) {
     typedef float v4f __attribute__((ext_vector_type(4)));
     const v4f v = __builtin_nontemporal_load(reinterpret_cast<const v4f*>(p));
     return make_float4(v.x, v.y, v.z, v.w);
 }
-__device__ __forceinline__ float4 ld_shade(const float4* p) { return RT_SHADE_NT ? ld_stream(p) : *p; }
-#ifndef RT_SHADE_OCT
-#define RT_SHADE_OCT 1   // continuation rays grouped by direction octant inside each block's appends (0: A/B builds)
-#endif
+__device__ __forceinline__ float4 ld_shade(const float4* p) { return ld_stream(p); }
 template <bool FULL, bool SORTED>
 __global__ void __launch_bounds__(kBlock) wf_shade(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int cur) {
     const FrameParams& P = *Pp;   // per-frame parameters in device memory
     __shared__ HaltonDim lds_halton[kHaltonLds];
     __shared__ MatRec lds_mat[kMatLds];
-    __shared__ BlockAlloc3 ba3;
-#if RT_SHADE_OCT
     __shared__ BlockAllocOct bao;
-#endif
     if (tail_mode(Q)) return;
     const ShadeTabs halton = load_tabs(S, lds_halton, lds_mat);
     const Uniforms& U = P.U;
@@ -740,12 +697,9 @@ __global__ void __launch_bounds__(kBlock) wf_shade(DevScene S, const FrameParams
         uint32_t* const ctr[3] = {&Q.W.counts[cslot(kCntShadowQ + shard)], &Q.W.counts[cslot(next * kShards + shard)],
                                   &Q.W.counts[cslot(kCntBack + next * kShards + shard)]};
         uint32_t slots[3];
-#if RT_SHADE_OCT
+        // continuation rays grouped by direction octant inside the block's range (round 5: +-0, kept)
         const uint32_t oct = (rayD.x < 0.0f ? 1u : 0u) | (rayD.y < 0.0f ? 2u : 0u) | (rayD.z < 0.0f ? 4u : 0u);
         block_alloc3_oct(pr, oct, ctr, bao, slots);
-#else
-        block_alloc3(pr, ctr, ba3, slots);
-#endif
         const uint32_t ns = slots[0], nr = front ? slots[1] : Q.seg_cap - 1u - slots[2];
         if (r.shadow) {
             sqout[3 * (size_t)ns] = make_float4(r.so.x, r.so.y, r.so.z, __uint_as_float(pid));
@@ -862,121 +816,12 @@ __global__ void __launch_bounds__(kSortThreads) wf_sort_scatter(DevScene S, WfPa
 // wave by one traversal step (trav_step); a lane whose query ended takes the next ray of the
 // wave's chunk once at least Q.refill_min lanes are idle.  A wave therefore runs ~(steps of its
 // rays) / 64 iterations instead of (slowest ray) x (rays per lane).
-// ---- cooperative triangle phase (wf_trace) -----------------------------------------------------------
-// Instead of every lane testing up to two of its own pending triangles per iteration (the triangle
-// blocks then run with ~a third of the lanes busy), the wave lays the pending triangles of all its
-// lanes (up to kCoopTake per lane, 64 in all) out as jobs, one per lane: the job lane fetches its
-// owner's ray with ds_bpermute, tests the triangle against the owner's bound from the start of the
-// phase, and writes a hit as a 64-bit key (t's magnitude bits, triangle id, job lane) to its LDS
-// slot; the owner takes the minimum key over its jobs' slots -- ordered by (t, id), the
-// lexicographic minimum the serial loop keeps -- fetches that job's (t, V, W, det) and updates its
-// closest hit if (t, id) is below its own; any-hit owners end at any hit.  Every triangle of the
-// owner's list is tested against a bound at least its serial bound, and the minimum is exact, so
-// the result is the serial traversal's, bit for bit.  Triangle slot and id must stay below 2^26
-// (the host checks).
-#ifndef RT_TRACE_COOP
-#define RT_TRACE_COOP 0   // 1: the cooperative triangle phase in wf_trace (A/B builds; measured slower)
-#endif
-// Orders one wave's LDS accesses across its lanes (the stores of some lanes before the loads of
-// others): a compiler barrier plus wavefront-scope fences; the hardware keeps a wave's LDS
-// operations in order.
-__device__ __forceinline__ void wave_lds_sync() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    // an LDS atomic without return is not ordered before the wave's next LDS load: wait for the
-    // wave's LDS operations to complete (lgkmcnt(0); vmcnt / expcnt untouched)
-    __builtin_amdgcn_s_waitcnt(0xC07F);
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-constexpr uint32_t kCoopTake = 4;   // triangles per lane and iteration
-constexpr uint32_t kCoopIdBits = 26;
 template <bool ANY, bool COUNT>
-__device__ __forceinline__ void coop_tri_phase(const DevScene& S, Trav& T, bool owner, uint32_t* job,
-                                               unsigned long long* key, TraceCounters& tc, bool& tdone) {
-    const uint32_t lane = lane_id();
-    const uint32_t c = owner ? min((uint32_t)__builtin_popcount(T.t_mask), kCoopTake) : 0u;
-    // exclusive prefix of the counts over the wave (c < 8: three ballots)
-    const unsigned long long b0 = __ballot(c & 1u), b1 = __ballot(c & 2u), b2 = __ballot(c & 4u);
-    const uint32_t pre = mbcnt64(b0) + 2u * mbcnt64(b1) + 4u * mbcnt64(b2);
-    const uint32_t total = (uint32_t)__popcll(b0) + 2u * (uint32_t)__popcll(b1) + 4u * (uint32_t)__popcll(b2);
-    const uint32_t take = pre >= 64u ? 0u : min(c, 64u - pre);
-    key[lane] = ~0ull;
-    uint32_t m = T.t_mask;
-    for (uint32_t k = 0; k < take; ++k) {
-        const int b = lowest_bit(m);
-        m &= m - 1u;
-        job[pre + k] = tri_slot(T.t_base, T.t_valid, b) | (lane << kCoopIdBits);
-    }
-    wave_lds_sync();   // job table and cleared keys before the jobs read / post to them
-    const uint32_t njobs = min(total, 64u);
-    const bool has_job = lane < njobs;
-    const uint32_t e = has_job ? job[lane] : (lane << kCoopIdBits);
-    const uint32_t own = e >> kCoopIdBits;
-    // the owner's ray and bound, with every lane active (a bpermute from an inactive lane reads 0)
-    const int src = (int)own;
-    RayPre pre_o;
-    pre_o.kx = __shfl(T.R.pre.kx, src);
-    pre_o.ky = __shfl(T.R.pre.ky, src);
-    pre_o.kz = __shfl(T.R.pre.kz, src);
-    pre_o.Sx = __shfl(T.R.pre.Sx, src);
-    pre_o.Sy = __shfl(T.R.pre.Sy, src);
-    pre_o.Sz = __shfl(T.R.pre.Sz, src);
-    const f3 o_o = mk3(__shfl(T.R.o.x, src), __shfl(T.R.o.y, src), __shfl(T.R.o.z, src));
-    const float bound = __shfl(T.best, src);
-    float t = 0.0f, V = 0.0f, W = 0.0f, dt = 1.0f;
-    if (has_job) {
-        const float4* tp = S.tris + 3 * (size_t)(e & ((1u << kCoopIdBits) - 1u));
-        const float4 a0 = tp[0], a1 = tp[1], a2 = tp[2];
-        if (COUNT) tc.tris++;
-        if (intersect_triangle_vw(pre_o, o_o, ld3(a0), ld3(a1), ld3(a2), 0.0f, bound, &t, &V, &W, &dt)) {
-            const uint32_t id = __float_as_uint(a0.w);
-            const unsigned long long kv = ((unsigned long long)(__float_as_uint(t) & 0x7fffffffu) << 32) |
-                                          ((unsigned long long)id << 6) | lane;
-            key[lane] = kv;   // this job's result
-        }
-    }
-    wave_lds_sync();   // every job's result before the owners read them
-    // the owner's minimum over its own jobs' slots (a ds_min_u64 into one slot per owner measured
-    // wrong results under load: garbage frames in bulk mode; the owner's own loop over <= 4 slots is exact)
-    unsigned long long kmin = ~0ull;
-    for (uint32_t k = 0; k < take; ++k) kmin = min(kmin, key[pre + k]);
-    const int wl = (int)(kmin & 63u);
-    const float wt = __shfl(t, wl), wV = __shfl(V, wl), wW = __shfl(W, wl), wdt = __shfl(dt, wl);
-    if (owner) {
-        T.t_mask = m;
-        if (kmin != ~0ull) {
-            const uint32_t wid = (uint32_t)(kmin >> 6) & ((1u << kCoopIdBits) - 1u);
-            if (ANY) {
-                T.hit_any = true;
-                tdone = true;
-            } else if (wt < T.best || (wt == T.best && wid < T.best_id)) {
-                T.best = wt;
-                T.best_id = wid;
-                T.bu = wV;
-                T.bv = wW;
-                T.bdet = wdt;
-            }
-        }
-    }
-}
-
-#ifndef RT_EXTEND_WAVES
-#if RT_TRACE_COOP
-#define RT_EXTEND_WAVES 7   // the cooperative phase needs 70 VGPRs (20 B of scratch at 64)
-#else
-#define RT_EXTEND_WAVES 8   // 64 VGPRs, no scratch (final round-2 node test; at 70 VGPRs it took 7 waves)
-#endif
-#endif
-template <bool ANY, bool COUNT>
-__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ANY ? 8 : RT_EXTEND_WAVES, ANY ? 8 : RT_EXTEND_WAVES)))
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8)))
 wf_trace(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int cur, int ts) {
     const FrameParams& P = *Pp;   // per-frame parameters in device memory
     __shared__ int lds_stack[kStackSize * kBlock];
     int* stack = &lds_stack[threadIdx.x];
-#if RT_TRACE_COOP
-    __shared__ uint32_t lds_job[kBlock];              // per wave: 64 jobs (triangle slot | owner lane << 26)
-    __shared__ unsigned long long lds_key[kBlock];    // per lane: the best (t, id, job lane) posted to it
-#endif
     if (Q.dev_ctl) {
         // device-side round control: extend decides (uniformly, from the counters) whether this
         // round runs in bulk or the rest of the pass goes to the finish launch
@@ -1068,11 +913,8 @@ wf_trace(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int cur, in
                 uint32_t g = wnext + mbcnt64(idle);
                 if (g < wend) {
                     e = ebase + (ANY ? g : seg_pos(g, xl, Q.seg_cap));
-                    // an extend entry is read once here (nontemporal: RT_TRACE_NT); a shadow entry
-                    // again when its ray is unoccluded
-                    const bool nt = !ANY && (RT_TRACE_NT & 1);
-                    float4 o4 = nt ? ld_stream(&qin[(size_t)qstride * e]) : qin[(size_t)qstride * e];
-                    float4 d4 = nt ? ld_stream(&qin[(size_t)qstride * e + 1]) : qin[(size_t)qstride * e + 1];
+                    float4 o4 = qin[(size_t)qstride * e];
+                    float4 d4 = qin[(size_t)qstride * e + 1];
                     trav_start(T, ld3(o4), ld3(d4), ANY ? d4.w : INFINITY);
                     active = true;
                     rays++;
@@ -1082,20 +924,9 @@ wf_trace(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int cur, in
             wnext += (uint32_t)__popcll(idle);
         }
         if (__ballot(active) == 0ull) break;
-#if RT_TRACE_COOP
-        if (COUNT && active) ++steps;
-        bool done = false;
-        if (__ballot(active && T.t_mask != 0u) != 0ull)   // wave-uniform: every lane serves as a job lane
-            coop_tri_phase<ANY, COUNT>(S, T, active && T.t_mask != 0u, &lds_job[threadIdx.x & ~63u],
-                                       &lds_key[threadIdx.x & ~63u], tc, done);
-        if (!active) continue;
-        if (!done && T.t_mask == 0u && (T.g_hits != 0u || T.sp > 0)) node_step<COUNT>(S, T, stack, tc, overflow, T.best);
-        if (done || (T.t_mask == 0u && T.g_hits == 0u && T.sp == 0)) {
-#else
         if (!active) continue;
         if (COUNT) ++steps;
         if (trav_step<COUNT>(S, T, ANY, stack, tc, overflow, T.best)) {
-#endif
             active = false;
             if (COUNT && Q.diag) {   // steps-per-ray histogram (log2 bins) of the counting frame
                 atomicAdd(&Q.W.counts[kWfDiagSteps + (ANY ? 32 : 0) + (31 - __builtin_clz(steps))], 1u);
@@ -1232,14 +1063,14 @@ wf_finish_step(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int c
                 if (g < wend) {
                     const uint32_t e = dense_entry(qs, g, Q.seg_cap);
                     const float4* src = qin + 2 * (size_t)e;
-                    const float4 o = (RT_TRACE_NT & 2) ? ld_stream(&src[0]) : src[0];
-                    const float4 d = (RT_TRACE_NT & 2) ? ld_stream(&src[1]) : src[1];
+                    const float4 o = ld_stream(&src[0]);
+                    const float4 d = ld_stream(&src[1]);
                     pid = __float_as_uint(o.w);
                     const uint32_t state = __float_as_uint(d.w);
                     const uint3 pm = path_meta(P, Q, pid);
                     meta = make_uint4(pm.x, pm.y, state, pm.z);
                     const float4 c = state == 0u ? make_float4(1.0f, 1.0f, 1.0f, 0.0f)
-                                     : (RT_TRACE_NT & 2) ? ld_stream(&Q.W.qc[cur][e]) : Q.W.qc[cur][e];
+                                     : ld_stream(&Q.W.qc[cur][e]);
                     const float4 a = Q.W.p_accum[pid];
                     p.color = mk3(c.x, c.y, c.z);
                     p.accum = mk3(a.x, a.y, a.z);

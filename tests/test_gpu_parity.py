@@ -347,7 +347,9 @@ def test_tuning_api_roundtrip_and_validation(rt, assets):
     R.draw()
     R.wait()
     assert np.array_equal(R.radiance(), a)
-    for bad in ({"team": 3}, {"refill_min": 65}, {"log": 3}, {"shade_min_drained": -101}):
+    assert d["finish_grid_pct"] == 0 and d["trace_grid_pct"] == 0   # chosen per frame (rt_api.h)
+    for bad in ({"team": 3}, {"refill_min": 65}, {"log": 3}, {"shade_min_drained": -101}, {"trace_chunk": 4097},
+                {"finish_chunk": 1 << 30}, {"shade_blocks": 65537}, {"finish_grid_pct": 101}):
         with pytest.raises(rt.RTError):
             R.set_tuning(**bad)
     R.set_tuning()

@@ -270,6 +270,21 @@ def test_internal_reference_fan_out_is_bounded_by_bytes(rt, d):
         _scene(rt, root)
 
 
+def test_many_internal_references_of_one_prim_share_a_snapshot(rt, d):
+    # one prim with 300 internal references next to a 2M-point array (24 MB of attribute data):
+    # the arcs of one list read one snapshot of the layer, charged once (charged per
+    # arc, 300 x 24 MB went past the 4 GiB budget and a legitimate layer failed to compose)
+    n = 1 << 21
+    pts = ", ".join("(%d, 0, 0)" % (k % 7) for k in range(n))
+    tiny = "".join('def Xform "T%d"\n{\n%s}\n' % (j, BOX.replace('"Box"', '"K%d"' % j)) for j in range(300))
+    refs = ", ".join("</T%d>" % j for j in range(300))
+    src = ('def Mesh "Src"\n{\n    int[] faceVertexCounts = [3]\n    int[] faceVertexIndices = [0, 1, 2]\n'
+           '    point3f[] points = [%s]\n}\n' % pts)
+    root = _write(d, "int_many.usda", HEAD % "" + src + tiny + 'def Xform "F" (\n    references = [%s]\n)\n{\n}\n' % refs)
+    sc = _scene(rt, root)   # composes (no "larger than" error)
+    assert sc.desc().mesh_count == 1 + 300 + 300   # Src, the T boxes, and their copies under F
+
+
 def _box_prims(path, counts=(4,), idx=(0, 1, 2, 3)):
     return [dict(path=path, type="Mesh", attrs=[
         dict(name="faceVertexCounts", type="int[]", value=list(counts)),
