@@ -539,7 +539,9 @@ def main():
         "value": round(value, 4),
         "unit": "Grays/s",
         "n_gpus": n,
-        "world_size": n,
+        # the communicator's own count (a multi-rank line proves the collective saw every rank)
+        "world_size": dist.get_world_size() if n > 1 else 1,
+        "dist_backend": dist.get_backend() if n > 1 else None,
         "steps": a.steps,
         "warmup": a.warmup,
         "ms_per_step": round(ms_per_step, 3),

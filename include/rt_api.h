@@ -245,6 +245,11 @@ rt_status rt_wait(rt_ctx* ctx);
  * motion W*H*2 (pixels, +Y down), G-buffer 4 planes of W*H*4 (diffuse, specular, normal,
  * roughness) or NULL. Rows are in the kernel's tid.y order (row 0 = bottom of the view). */
 rt_status rt_read_radiance(rt_ctx* ctx, float* rgba);
+/* The same radiance as RGBA16F (uint16_t bit patterns, W*H*4), the format the reference's
+ * accumulation texture holds (Renderer.swift:685, Raytracing.metal:819): the fp32 target rounded
+ * to nearest even on the device (overflow to infinity, fp16 denormals kept); 8 B per pixel read
+ * back instead of 16. */
+rt_status rt_read_radiance_half(rt_ctx* ctx, uint16_t* rgba);
 rt_status rt_read_aux(rt_ctx* ctx, float* depth, float* motion, float* gbuffer);
 
 /* Display output (FramePresenter.swift:103-238, Shaders.metal:39-52): the newest radiance,

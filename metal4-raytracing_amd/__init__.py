@@ -402,6 +402,13 @@ class Renderer:
         _check(lib().rt_read_radiance(self._ctx, out.ctypes.data_as(C.POINTER(C.c_float))), self._ctx)
         return out
 
+    def radiance_half(self):
+        """rt_read_radiance_half: the radiance as RGBA16F (the reference's accumulation format,
+        Renderer.swift:685), rounded to nearest even on the device; (H, W, 4) float16."""
+        out = np.empty((self.height, self.width, 4), dtype=np.float16)
+        _check(lib().rt_read_radiance_half(self._ctx, out.ctypes.data_as(C.POINTER(C.c_uint16))), self._ctx)
+        return out
+
     def aux(self, gbuffer=False):
         depth = np.empty((self.height, self.width), dtype=np.float32)
         motion = np.empty((self.height, self.width, 2), dtype=np.float32)

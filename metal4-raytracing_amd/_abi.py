@@ -233,7 +233,7 @@ EXPORTED_SYMBOLS = [
     # rt_api.h
     "rt_create", "rt_destroy", "rt_last_error", "rt_set_stream", "rt_scene_upload", "rt_bvh_build",
     "rt_bvh_build_device", "rt_bvh_refit", "rt_set_instance_transforms", "rt_skin", "rt_resize", "rt_render_frame", "rt_wait",
-    "rt_read_radiance", "rt_read_aux", "rt_tile_count", "rt_pack_tiles", "rt_unpack_tiles",
+    "rt_read_radiance", "rt_read_radiance_half", "rt_read_aux", "rt_tile_count", "rt_pack_tiles", "rt_unpack_tiles",
     "rt_pack_tiles_on", "rt_unpack_tiles_on", "rt_present", "rt_write_png",
     "rt_pack_tiles_host", "rt_unpack_tiles_host",
     "rt_set_counting", "rt_set_device_spans", "rt_set_graphs", "rt_get_stats", "rt_set_tuning", "rt_get_tuning",
@@ -271,6 +271,7 @@ def declare(lib):
         "rt_render_frame": (st, [vp, P(Uniforms), P(TileSet)]),
         "rt_wait": (st, [vp]),
         "rt_read_radiance": (st, [vp, P(C.c_float)]),
+        "rt_read_radiance_half": (st, [vp, P(C.c_uint16)]),
         "rt_read_aux": (st, [vp, P(C.c_float), P(C.c_float), P(C.c_float)]),
         "rt_tile_count": (C.c_int32, [C.c_int32, C.c_int32, P(TileSet)]),
         "rt_pack_tiles": (st, [vp, P(TileSet), vp]),

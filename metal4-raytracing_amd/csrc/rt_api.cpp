@@ -172,6 +172,7 @@ struct rt_ctx {
     uint32_t last_frame_index = 0;   // Uniforms.frameIndex of the newest frame
     // display output (rt_present): temporal-scaler history at the output size, sRGB thresholds
     DevBuf d_hist[2], d_hdepth[2], d_present_out, d_present_thr;
+    DevBuf d_half;   // rt_read_radiance_half staging (RGBA16F)
     int hist_w = 0, hist_h = 0, hist_idx = 0;
     bool hist_valid = false;
     DevBuf d_den[4];   // RT_SCALER_DENOISED scratch at render size: ping, pong, guide, albedo
@@ -287,7 +288,7 @@ static size_t ctx_bytes(const rt_ctx* c) {
                            &c->d_accum[0], &c->d_accum[1], &c->d_lbvh_scratch,
                            &c->d_tex_texels, &c->d_tex_info, &c->d_mat_tex, &c->d_uv, &c->d_tex_lut,
                            &c->d_hist[0], &c->d_hist[1], &c->d_hdepth[0], &c->d_hdepth[1], &c->d_present_out,
-                           &c->d_present_thr, &c->d_den[0], &c->d_den[1], &c->d_den[2], &c->d_den[3]};
+                           &c->d_present_thr, &c->d_den[0], &c->d_den[1], &c->d_den[2], &c->d_den[3], &c->d_half};
     size_t s = 0;
     for (auto* b : all) s += b->bytes;
     for (const DevBuf& b : c->d_motion) s += b.bytes;
@@ -468,7 +469,7 @@ rt_status rt_destroy(rt_ctx* c) {
                      &c->d_accum[1], &c->d_lbvh_scratch, &c->d_tex_texels, &c->d_tex_info,
                      &c->d_mat_tex, &c->d_uv, &c->d_tex_lut, &c->d_hist[0], &c->d_hist[1], &c->d_hdepth[0],
                      &c->d_hdepth[1], &c->d_present_out, &c->d_present_thr, &c->d_den[0], &c->d_den[1],
-                     &c->d_den[2], &c->d_den[3]};
+                     &c->d_den[2], &c->d_den[3], &c->d_half};
     for (auto* b : all) dev_free(*b);
     for (DevBuf& b : c->d_motion) dev_free(b);
     for (Geo& g : c->geo)
@@ -1203,6 +1204,20 @@ rt_status rt_read_radiance(rt_ctx* c, float* rgba) {
     rt_status st = rt_wait(c);
     if (st) return st;
     HIPC(c, hipMemcpy(rgba, c->d_accum[c->read_idx].p, (size_t)c->width * c->height * 16, hipMemcpyDeviceToHost));
+    return RT_OK;
+}
+
+rt_status rt_read_radiance_half(rt_ctx* c, uint16_t* rgba) {
+    if (!c || !rgba) FAIL(c, RT_ERR_INVALID_ARG, "null argument");
+    if (!c->width) FAIL(c, RT_ERR_STATE, "no targets");
+    rt_status st = rt_wait(c);
+    if (st) return st;
+    const size_t n = (size_t)c->width * c->height;
+    if ((st = dev_alloc(c, c->d_half, n * 8))) return st;
+    launch_to_half((const float4*)c->d_accum[c->read_idx].p, (ushort4*)c->d_half.p, n, c->stream);
+    HIPC(c, hipGetLastError());
+    HIPC(c, hipMemcpyAsync(rgba, c->d_half.p, n * 8, hipMemcpyDeviceToHost, c->stream));
+    HIPC(c, hipStreamSynchronize(c->stream));
     return RT_OK;
 }
 

@@ -279,6 +279,7 @@ void launch_pack_tiles(const float4* src, float4* dst, int width, int height, in
                        int tiles_x, int own, hipStream_t s);
 void launch_unpack_tiles(const float4* src, float4* dst, int width, int height, int tile, int rank, int nranks,
                          int tiles_x, int own, hipStream_t s);
+void launch_to_half(const float4* src, ushort4* dst, size_t n, hipStream_t s);
 void launch_skin(const float4* rest_pos, const float4* rest_nrm, const ushort4* jidx, const float4* jw,
                  const float* joints, float4* out_pos, float4* out_nrm, uint32_t n, hipStream_t s);
 // flatten also reduces max |world coordinate| into *maxabs_bits (float bits; zero it first)

@@ -39,6 +39,22 @@ void launch_unpack_tiles(const float4* src, float4* dst, int width, int height, 
                        tile, rank, nranks, tiles_x, own);
 }
 
+// ---- RGBA16F readback (the reference's accumulation format, Renderer.swift:685) ----------------
+// fp32 -> fp16 round to nearest even (v_cvt_f16_f32 in the default rounding mode; fp16 denormals
+// kept, overflow to infinity), 8 B per pixel out
+__global__ void to_half_k(const float4* __restrict__ src, ushort4* __restrict__ dst, size_t n) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const float4 v = src[i];
+    const _Float16 h[4] = {(_Float16)v.x, (_Float16)v.y, (_Float16)v.z, (_Float16)v.w};
+    dst[i] = make_ushort4(__builtin_bit_cast(uint16_t, h[0]), __builtin_bit_cast(uint16_t, h[1]),
+                          __builtin_bit_cast(uint16_t, h[2]), __builtin_bit_cast(uint16_t, h[3]));
+}
+void launch_to_half(const float4* src, ushort4* dst, size_t n, hipStream_t s) {
+    if (!n) return;
+    hipLaunchKernelGGL(to_half_k, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, src, dst, n);
+}
+
 // ---- skinning (Skinning.metal:7-49) ---------------------------------------------------------
 __device__ __forceinline__ float4 m4v(const float* m, float x, float y, float z, float w) {
     // float4x4 * float4, column-major: ((c0*x + c1*y) + c2*z) + c3*w

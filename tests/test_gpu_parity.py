@@ -355,3 +355,21 @@ def test_tuning_api_roundtrip_and_validation(rt, assets):
     R.set_tuning()
     assert R.tuning() == d
     R.close()
+
+
+def test_radiance_half_is_fp32_rounded_to_nearest(rt, assets):
+    """rt_read_radiance_half (RGBA16F, Renderer.swift:685): the fp32 target rounded to nearest even,
+    bit for bit what numpy's float32 -> float16 conversion gives; on a PBR frame and an EMA frame."""
+    scene = rt.Scene.preset("c1", assets)
+    R = rt.Renderer(scene, 96, 64, seed=4)
+    R.samplesPerPixel, R.maxBounces = 2, 3
+    for _ in range(2):
+        R.draw()
+        R.wait()
+        a = R.radiance()
+        h = R.radiance_half()
+        assert h.dtype == np.float16 and h.shape == a.shape
+        want = a.astype(np.float16)
+        assert np.array_equal(h.view(np.uint16), want.view(np.uint16))
+        assert float(np.max(a[..., :3])) > 0.0
+    R.close()
