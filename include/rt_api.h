@@ -211,6 +211,13 @@ typedef struct rt_stats {
     uint64_t total_graph_captures;
     uint64_t total_graph_fallbacks;
     uint64_t total_graph_eager;
+    /* tree quality (rt_tuning.refit_rebuild_pct): device rebuilds a degraded refit triggered, and the
+       node-area sum (the sum of the 8-wide node boxes' areas: the SAH node term, proportional to the
+       node visits of the scene's rays) of the last build and of the last refit read back (0 before
+       the first refit; a rebuild leaves the refit figure that triggered it) */
+    uint64_t total_auto_rebuilds;
+    float bvh_cost_built;
+    float bvh_cost_refit;
 } rt_stats;
 
 rt_status rt_create(const rt_opts* opts, rt_ctx** out);
@@ -343,7 +350,13 @@ typedef struct rt_tuning {
                                    (host-driven rounds); 2: + per-path segment counts (slower) */
     int32_t device_bvh;         /* rt_bvh_build_device topology: 0 = PLOC clustering (default),
                                    1 = LBVH radix tree */
-    int32_t reserved[4];
+    int32_t refit_rebuild_pct;  /* rt_bvh_refit keeps the topology and grows the boxes of moved
+                                   geometry; once a refit's node-area sum (rt_stats.bvh_cost_refit)
+                                   exceeds this percentage of the last build's, the next
+                                   rt_bvh_refit or rt_render_frame rebuilds the tree on the device
+                                   (rt_bvh_build_device) instead.  0 = default (150), < 0 = never.
+                                   Images are the same either way. */
+    int32_t reserved[3];
 } rt_tuning;
 rt_status rt_set_tuning(rt_ctx* ctx, const rt_tuning* tuning);
 rt_status rt_get_tuning(const rt_ctx* ctx, rt_tuning* out);

@@ -190,6 +190,9 @@ class Stats(C.Structure):
         ("total_graph_captures", C.c_uint64),
         ("total_graph_fallbacks", C.c_uint64),
         ("total_graph_eager", C.c_uint64),
+        ("total_auto_rebuilds", C.c_uint64),
+        ("bvh_cost_built", C.c_float),
+        ("bvh_cost_refit", C.c_float),
     ]
 
 
@@ -208,7 +211,7 @@ class Tuning(C.Structure):
     """rt_tuning (include/rt_api.h): the wavefront kernels' scheduling parameters, 0 = default."""
     _fields_ = [(n, C.c_int32) for n in ("trace_chunk", "finish_chunk", "refill_min", "shade_min", "shade_min_drained",
                                          "team", "finish_grid_pct", "trace_grid_pct", "shade_blocks", "host_rounds",
-                                         "log", "device_bvh")] + [("reserved", C.c_int32 * 4)]
+                                         "log", "device_bvh", "refit_rebuild_pct")] + [("reserved", C.c_int32 * 3)]
 
 
 # enums (ShaderTypes.h)

@@ -161,6 +161,14 @@ struct rt_ctx {
     DevBuf d_slot_to_tri, d_levels, d_maxabs, d_lbvh_scratch;
     uint32_t num_nodes8 = 0;
     uint32_t* h_lbvh = nullptr;   // pinned word for the device builder's level counts
+    // tree quality under refit (rt_tuning.refit_rebuild_pct): the node-area sum (launch_bvh_cost)
+    // of the last build and of the last refit, the latter read back asynchronously
+    DevBuf d_cost;
+    float* h_cost = nullptr;
+    hipEvent_t cost_ev = nullptr;
+    bool cost_pending = false;
+    float cost_built = 0.0f, cost_refit = 0.0f;
+    uint64_t auto_rebuilds = 0;
     DevBuf d_random, d_accum[2];
     // Motion vectors rotate over kMaxSlots + 1 targets: a wavefront frame writes d_motion[m + 1]
     // and reads the previous frame's d_motion[m], so it never overwrites a target an older frame
@@ -288,7 +296,7 @@ static size_t ctx_bytes(const rt_ctx* c) {
                            &c->d_accum[0], &c->d_accum[1], &c->d_lbvh_scratch,
                            &c->d_tex_texels, &c->d_tex_info, &c->d_mat_tex, &c->d_uv, &c->d_tex_lut,
                            &c->d_hist[0], &c->d_hist[1], &c->d_hdepth[0], &c->d_hdepth[1], &c->d_present_out,
-                           &c->d_present_thr, &c->d_den[0], &c->d_den[1], &c->d_den[2], &c->d_den[3], &c->d_half};
+                           &c->d_present_thr, &c->d_den[0], &c->d_den[1], &c->d_den[2], &c->d_den[3], &c->d_half, &c->d_cost};
     size_t s = 0;
     for (auto* b : all) s += b->bytes;
     for (const DevBuf& b : c->d_motion) s += b.bytes;
@@ -469,7 +477,7 @@ rt_status rt_destroy(rt_ctx* c) {
                      &c->d_accum[1], &c->d_lbvh_scratch, &c->d_tex_texels, &c->d_tex_info,
                      &c->d_mat_tex, &c->d_uv, &c->d_tex_lut, &c->d_hist[0], &c->d_hist[1], &c->d_hdepth[0],
                      &c->d_hdepth[1], &c->d_present_out, &c->d_present_thr, &c->d_den[0], &c->d_den[1],
-                     &c->d_den[2], &c->d_den[3], &c->d_half};
+                     &c->d_den[2], &c->d_den[3], &c->d_half, &c->d_cost};
     for (auto* b : all) dev_free(*b);
     for (DevBuf& b : c->d_motion) dev_free(b);
     for (Geo& g : c->geo)
@@ -477,6 +485,8 @@ rt_status rt_destroy(rt_ctx* c) {
     if (c->uev) (void)hipEventDestroy(c->uev);
     if (c->ustream) (void)hipStreamDestroy(c->ustream);
     if (c->h_lbvh) (void)hipHostFree(c->h_lbvh);
+    if (c->h_cost) (void)hipHostFree(c->h_cost);
+    if (c->cost_ev) (void)hipEventDestroy(c->cost_ev);
     if (c->scene_ev) (void)hipEventDestroy(c->scene_ev);
     for (FrameSlot& f : c->slot) {
         for (DevBuf* b : f.bufs) dev_free(*b);
@@ -696,6 +706,50 @@ rt_status rt_scene_upload(rt_ctx* c, const rt_scene_desc* sd) {
     return RT_OK;
 }
 
+// The node-area sum of the current generation's tree (launch_bvh_cost) on the update stream: read
+// back at once (sync = true, after a build) or into the pinned word with an event (after a refit).
+static rt_status bvh_cost(rt_ctx* c, bool sync) {
+    if (rt_status st = dev_alloc(c, c->d_cost, 4)) return st;
+    if (!c->h_cost) HIPC(c, hipHostMalloc((void**)&c->h_cost, 16, 0));
+    if (!c->cost_ev) HIPC(c, hipEventCreateWithFlags(&c->cost_ev, hipEventDisableTiming));
+    launch_bvh_cost((const float*)c->G().node_box.p, c->num_nodes8, (float*)c->d_cost.p, c->ustream);
+    HIPC(c, hipGetLastError());
+    HIPC(c, hipMemcpyAsync(c->h_cost, c->d_cost.p, 4, hipMemcpyDeviceToHost, c->ustream));
+    if (sync) {
+        HIPC(c, hipStreamSynchronize(c->ustream));
+        c->cost_built = *c->h_cost;   // cost_refit keeps the last refit's figure (rt_stats)
+        c->cost_pending = false;
+    } else {
+        HIPC(c, hipEventRecord(c->cost_ev, c->ustream));
+        c->cost_pending = true;
+    }
+    return RT_OK;
+}
+
+// rt_tuning.refit_rebuild_pct: 0 = the default, < 0 = never
+constexpr int kRefitRebuildPctDefault = 150;
+static int refit_rebuild_pct(const rt_ctx* c) {
+    const int p = c->tuning_req.refit_rebuild_pct;
+    return p == 0 ? kRefitRebuildPctDefault : p;
+}
+
+// Once the last refit's node-area sum has arrived: if it grew past refit_rebuild_pct percent of
+// the last build's, rebuild on the device from the current geometry (the reference rebuilds its
+// acceleration structures where a refit is not enough, Renderer.swift:1252-1277).  Images do not
+// depend on the tree (conservative boxes): this only restores traversal speed.
+static rt_status check_refit_quality(rt_ctx* c, bool* rebuilt) {
+    *rebuilt = false;
+    if (!c->cost_pending || hipEventQuery(c->cost_ev) != hipSuccess) return RT_OK;
+    c->cost_pending = false;
+    c->cost_refit = *c->h_cost;
+    const int pct = refit_rebuild_pct(c);
+    if (pct <= 0 || !(c->cost_built > 0.0f) || !(c->cost_refit * 100.0f > c->cost_built * (float)pct)) return RT_OK;
+    if (rt_status st = rt_bvh_build_device(c)) return st;
+    c->auto_rebuilds++;
+    *rebuilt = true;
+    return RT_OK;
+}
+
 rt_status rt_bvh_build(rt_ctx* c) {
     if (!c) FAIL(c, RT_ERR_INVALID_ARG, "null ctx");
     if (!c->scene_ready) FAIL(c, RT_ERR_STATE, "rt_bvh_build before rt_scene_upload");
@@ -722,15 +776,10 @@ rt_status rt_bvh_build(rt_ctx* c) {
         FAIL(c, RT_ERR_UNSUPPORTED, "BVH deeper than the traversal stack at every depth limit");
     if (c->bvh8.nodes.size() >= (1u << 23)) FAIL(c, RT_ERR_UNSUPPORTED, "BVH too large (2^23 nodes)");
     const uint32_t n = c->num_tris;
-    std::vector<float4> tris(3 * (size_t)n);
+    std::vector<float> tris((size_t)kTriFloats * n);   // 64-B records (rt_device.h)
     for (uint32_t k = 0; k < n; ++k) {
-        uint32_t id = c->bvh8.tri_order[k];
-        const float* w = &c->h_world[9 * (size_t)id];
-        float idf;
-        std::memcpy(&idf, &id, 4);
-        tris[3 * k + 0] = make_float4(w[0], w[1], w[2], idf);
-        tris[3 * k + 1] = make_float4(w[3], w[4], w[5], 0.0f);
-        tris[3 * k + 2] = make_float4(w[6], w[7], w[8], 0.0f);
+        const uint32_t id = c->bvh8.tri_order[k];
+        tri_store(&tris[(size_t)kTriFloats * k], &c->h_world[9 * (size_t)id], id);
     }
     // nodes grouped by depth for the level-synchronous refit (BFS order: parent < child)
     const size_t nn = c->bvh8.nodes.size();
@@ -749,7 +798,7 @@ rt_status rt_bvh_build(rt_ctx* c) {
     rt_status st;
     Geo& g = c->G();
     hipStream_t us = c->ustream;
-    if ((st = dev_upload(c, g.tris, tris.data(), tris.size() * 16, us))) return st;
+    if ((st = dev_upload(c, g.tris, tris.data(), tris.size() * 4, us))) return st;
     if ((st = dev_upload(c, g.nodes, c->bvh8.nodes.data(), nn * sizeof(Bvh8Node), us))) return st;
     if ((st = dev_upload(c, g.node_box, c->bvh8.node_box.data(), c->bvh8.node_box.size() * 4, us))) return st;
     if ((st = dev_upload(c, c->d_slot_to_tri, c->bvh8.tri_order.data(), (size_t)n * 4, us))) return st;
@@ -758,6 +807,8 @@ rt_status rt_bvh_build(rt_ctx* c) {
     std::vector<uint16_t> tri_bin(n);
     for (uint32_t k = 0; k < n; ++k) tri_bin[c->bvh8.tri_order[k]] = (uint16_t)(((uint64_t)k * kSortMaxBins) / n);
     if ((st = dev_upload(c, g.tri_bin, tri_bin.data(), (size_t)n * 2, us))) return st;
+    c->num_nodes8 = (uint32_t)nn;
+    if ((st = bvh_cost(c, true))) return st;
     HIPC(c, hipStreamSynchronize(us));   // the host arrays are the copies' sources
     g.num_nodes8 = (uint32_t)nn;
     c->num_nodes8 = (uint32_t)nn;
@@ -783,7 +834,7 @@ rt_status rt_bvh_build_device(rt_ctx* c) {
     if ((st = dev_alloc(c, c->d_slot_to_tri, (size_t)n * 4))) return st;
     if ((st = dev_alloc(c, g.tri_bin, (size_t)n * 2))) return st;
     if ((st = dev_alloc(c, c->d_levels, (size_t)n * 4))) return st;
-    if ((st = dev_alloc(c, g.tris, (size_t)n * 48))) return st;
+    if ((st = dev_alloc(c, g.tris, (size_t)n * kTriFloats * 4))) return st;
     if ((st = dev_alloc(c, c->d_maxabs, 4))) return st;
     if (!c->h_lbvh) HIPC(c, hipHostMalloc((void**)&c->h_lbvh, 16, 0));
     LbvhInput in{(const float4*)g.pos.p, (const uint4*)c->d_tri_info.p, (const float*)g.inst.p, n};
@@ -801,7 +852,7 @@ rt_status rt_bvh_build_device(rt_ctx* c) {
     // world-space triangles in the new slot order
     HIPC(c, hipMemsetAsync(c->d_maxabs.p, 0, 4, us));
     launch_flatten((const uint4*)c->d_tri_info.p, (const uint32_t*)c->d_slot_to_tri.p, (const float4*)g.pos.p,
-                   (const float*)g.inst.p, (float4*)g.tris.p, n, (unsigned*)c->d_maxabs.p, us);
+                   (const float*)g.inst.p, (float*)g.tris.p, n, (unsigned*)c->d_maxabs.p, us);
     HIPC(c, hipGetLastError());
     HIPC(c, hipStreamSynchronize(us));
     if (res.num_nodes >= (1u << 23)) FAIL(c, RT_ERR_UNSUPPORTED, "BVH too large (2^23 nodes)");
@@ -812,27 +863,32 @@ rt_status rt_bvh_build_device(rt_ctx* c) {
     c->num_nodes8 = res.num_nodes;
     g.num_nodes8 = res.num_nodes;
     c->bvh_ready = true;
-    return RT_OK;
+    return bvh_cost(c, true);
 }
 
 rt_status rt_bvh_refit(rt_ctx* c) {
     if (!c) FAIL(c, RT_ERR_INVALID_ARG, "null ctx");
     if (!c->bvh_ready) FAIL(c, RT_ERR_STATE, "rt_bvh_refit before rt_bvh_build");
     HIPC(c, hipSetDevice(c->device));
+    bool rebuilt = false;
+    if (rt_status qst = check_refit_quality(c, &rebuilt)) return qst;
+    if (rebuilt) return RT_OK;         // the new tree is built from the current geometry
     rt_status st = begin_update(c);   // frames in flight keep their generation
     if (!st) st = dev_alloc(c, c->d_maxabs, 4);
     if (st) return st;
     Geo& g = c->G();
     HIPC(c, hipMemsetAsync(c->d_maxabs.p, 0, 4, c->ustream));
     launch_flatten((const uint4*)c->d_tri_info.p, (const uint32_t*)c->d_slot_to_tri.p, (const float4*)g.pos.p,
-                   (const float*)g.inst.p, (float4*)g.tris.p, c->num_tris, (unsigned*)c->d_maxabs.p, c->ustream);
+                   (const float*)g.inst.p, (float*)g.tris.p, c->num_tris, (unsigned*)c->d_maxabs.p, c->ustream);
     for (int d = (int)c->level_off.size() - 2; d >= 0; --d) {
         uint32_t off = c->level_off[d], cnt = c->level_off[d + 1] - off;
-        launch_refit8_level((Bvh8Node*)g.nodes.p, (float*)g.node_box.p, (const float4*)g.tris.p,
+        launch_refit8_level((Bvh8Node*)g.nodes.p, (float*)g.node_box.p, (const float*)g.tris.p,
                             (const uint32_t*)c->d_levels.p + off, cnt, c->bvh8.pad, (const unsigned*)c->d_maxabs.p,
                             c->ustream);
     }
     HIPC(c, hipGetLastError());
+    // the refitted tree's node-area sum, read back without a host wait (check_refit_quality)
+    if (refit_rebuild_pct(c) > 0) return bvh_cost(c, false);
     return RT_OK;
 }
 
@@ -1014,6 +1070,10 @@ rt_status rt_render_frame(rt_ctx* c, const Uniforms* U, const rt_tile_set* tiles
     if (U->maxBounces > RT_MAX_BOUNCES) FAIL(c, RT_ERR_UNSUPPORTED, "maxBounces > 12 exceeds the Halton table");
     if (U->samplesPerPixel > 4096 || U->motionSamplingMaxExtraSamples > 4096) FAIL(c, RT_ERR_INVALID_ARG, "bad spp");
     HIPC(c, hipSetDevice(c->device));
+    {   // a refit that degraded the tree past rt_tuning.refit_rebuild_pct: rebuild before this frame
+        bool rebuilt = false;
+        if (rt_status qst = check_refit_quality(c, &rebuilt)) return qst;
+    }
     int ts, rank, nranks, tiles_x, own;
     rt_status st = resolve_tiles(c, tiles, ts, rank, nranks, tiles_x, own);
     if (st) return st;
@@ -1083,7 +1143,7 @@ rt_status rt_render_frame(rt_ctx* c, const Uniforms* U, const rt_tile_set* tiles
     }
     DevScene S;
     std::memset(&S, 0, sizeof S);   // no stray padding bytes: the frame-graph key compares S byte for byte
-    S.tris = (const float4*)geo.tris.p;
+    S.tris = (const float*)geo.tris.p;
     S.nodes8 = (const Bvh8Node*)geo.nodes.p;
     S.tri_info = (const uint4*)c->d_tri_info.p;
     S.pos = (const float4*)geo.pos.p;
@@ -1438,7 +1498,7 @@ rt_status rt_set_tuning(rt_ctx* c, const rt_tuning* t) {
         v.refill_min < 0 || v.refill_min > 64 || v.shade_min < 0 || v.shade_min > 64 || v.shade_min_drained > 64 ||
         v.shade_min_drained < -100 || v.finish_grid_pct < 0 || v.finish_grid_pct > 100 || v.trace_grid_pct < 0 ||
         v.trace_grid_pct > 100 || v.shade_blocks < 0 || v.shade_blocks > kMaxTuneShadeBlocks || v.log < 0 || v.log > 2 ||
-        v.device_bvh < 0 || v.device_bvh > 1)
+        v.device_bvh < 0 || v.device_bvh > 1 || (v.refit_rebuild_pct > 0 && v.refit_rebuild_pct < 100))
         FAIL(c, RT_ERR_INVALID_ARG, "rt_tuning field out of range");
     // frames already in flight keep the parameters they were enqueued with (their graphs' keys)
     c->tuning_req = v;
@@ -1462,6 +1522,7 @@ rt_status rt_get_tuning(const rt_ctx* c, rt_tuning* out) {
     t.host_rounds = w.host_ctl ? 1 : 0;
     t.log = w.log;
     t.device_bvh = c->tuning_req.device_bvh;
+    t.refit_rebuild_pct = refit_rebuild_pct(c);
     *out = t;
     return RT_OK;
 }
@@ -1500,6 +1561,9 @@ rt_status rt_get_stats(rt_ctx* c, rt_stats* out) {
     out->total_graph_captures = T.total_graph_captures;
     out->total_graph_fallbacks = T.total_graph_fallbacks;
     out->total_graph_eager = T.total_graph_eager;
+    out->total_auto_rebuilds = c->auto_rebuilds;
+    out->bvh_cost_built = c->cost_built;
+    out->bvh_cost_refit = c->cost_refit;
     return RT_OK;
 }
 
@@ -1527,15 +1591,10 @@ rt_status rt_debug_trace_host(const rt_scene_desc* sd, const float* rays, const 
     BvhResult bvh2;
     Bvh8Result bvh;
     if (!build_bvh8_fit(world.data(), nt, bvh2, bvh)) FAIL((rt_ctx*)nullptr, RT_ERR_UNSUPPORTED, "BVH too deep");
-    std::vector<float4> tris(3 * (size_t)nt);
+    std::vector<float> tris((size_t)kTriFloats * nt);
     for (uint32_t k = 0; k < nt; ++k) {
-        uint32_t id = bvh.tri_order[k];
-        const float* w = &world[9 * (size_t)id];
-        float idf;
-        std::memcpy(&idf, &id, 4);
-        tris[3 * k] = make_float4(w[0], w[1], w[2], idf);
-        tris[3 * k + 1] = make_float4(w[3], w[4], w[5], 0.0f);
-        tris[3 * k + 2] = make_float4(w[6], w[7], w[8], 0.0f);
+        const uint32_t id = bvh.tri_order[k];
+        tri_store(&tris[(size_t)kTriFloats * k], &world[9 * (size_t)id], id);
     }
     DevScene S;
     std::memset(&S, 0, sizeof S);

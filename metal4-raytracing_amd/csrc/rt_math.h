@@ -188,64 +188,43 @@ RT_HD f3 fresnelSchlick(float cosTheta, f3 F0) {
 // Watertight ray/triangle (Woop, Benthin, Wald, JCGT 2013), no culling, t in [tmin, tmax].
 // Barycentrics follow Metal's triangle_barycentric_coord (Raytracing.metal:63-73):
 // u weights vertex 1, v weights vertex 2, 1-u-v weights vertex 0.
+// The axes are cycled, never swapped: kz = the largest |d| component, kx = kz + 1, ky = kz + 2
+// (mod 3).  (Woop et al. swap kx / ky when d[kz] < 0 to keep the winding for back-face culling;
+// with no culling the swap negates U, V, W, det and T together, which leaves t, u, v and every
+// accept / reject decision unchanged up to the sign of exact zeros -- DESIGN.md §4; the oracle
+// states the same.)  Without the swap, a vertex's (kz, kx, ky) components are three consecutive
+// floats of (x, y, z, x, y) starting at kz: the triangle record stores each vertex that way and a
+// lane loads its ray's window directly (rt_device.h tri_window), no per-component selects.
 struct RayPre {
-    int kx, ky, kz;
+    int kz;
     float Sx, Sy, Sz;
 };
 RT_HD float comp(f3 v, int k) { return k == 0 ? v.x : (k == 1 ? v.y : v.z); }
+// (v[kz], v[kx], v[ky]) as (x, y, z)
+RT_HD f3 rot3(f3 v, int kz) { return kz == 0 ? mk3(v.x, v.y, v.z) : (kz == 1 ? mk3(v.y, v.z, v.x) : mk3(v.z, v.x, v.y)); }
 RT_HD RayPre ray_precompute(f3 d) {
     RayPre p;
     float ax = fabsf(d.x), ay = fabsf(d.y), az = fabsf(d.z);
     int kz = (ax > ay) ? ((ax > az) ? 0 : 2) : ((ay > az) ? 1 : 2);
-    int kx = kz + 1; if (kx == 3) kx = 0;
-    int ky = kx + 1; if (ky == 3) ky = 0;
-    float dz = comp(d, kz);
-    if (dz < 0.0f) { int t = kx; kx = ky; ky = t; }
-    p.kx = kx; p.ky = ky; p.kz = kz;
-    p.Sx = comp(d, kx) / dz;
-    p.Sy = comp(d, ky) / dz;
-    p.Sz = 1.0f / dz;
+    const f3 r = rot3(d, kz);   // (d[kz], d[kx], d[ky])
+    p.kz = kz;
+    p.Sx = r.y / r.x;
+    p.Sy = r.z / r.x;
+    p.Sz = 1.0f / r.x;
     return p;
 }
-// Returns true on hit and writes t, u, v.
-RT_HD bool intersect_triangle(const RayPre& p, f3 o, f3 v0, f3 v1, f3 v2, float tmin, float tmax,
-                              float* t_out, float* u_out, float* v_out) {
-    f3 A = v0 - o, B = v1 - o, C = v2 - o;
-    float Akz = comp(A, p.kz), Bkz = comp(B, p.kz), Ckz = comp(C, p.kz);
-    float Ax = comp(A, p.kx) - p.Sx * Akz;
-    float Ay = comp(A, p.ky) - p.Sy * Akz;
-    float Bx = comp(B, p.kx) - p.Sx * Bkz;
-    float By = comp(B, p.ky) - p.Sy * Bkz;
-    float Cx = comp(C, p.kx) - p.Sx * Ckz;
-    float Cy = comp(C, p.ky) - p.Sy * Ckz;
-    float U = Cx * By - Cy * Bx;
-    float V = Ax * Cy - Ay * Cx;
-    float W = Bx * Ay - By * Ax;
-    if ((U < 0.0f || V < 0.0f || W < 0.0f) && (U > 0.0f || V > 0.0f || W > 0.0f)) return false;
-    float det = (U + V) + W;
-    if (det == 0.0f) return false;
-    float Az = p.Sz * Akz, Bz = p.Sz * Bkz, Cz = p.Sz * Ckz;
-    float T = (U * Az + V * Bz) + W * Cz;
-    float t = T / det;
-    if (!(t >= tmin && t <= tmax)) return false;
-    *t_out = t;
-    *u_out = V / det;
-    *v_out = W / det;
-    return true;
-}
-// The same test, leaving the barycentric divisions to the caller: writes t and the unnormalised
-// (V, W, det), so u = V / det and v = W / det (bit for bit the values above) are formed once for
-// the closest hit instead of for every candidate.
-RT_HD bool intersect_triangle_vw(const RayPre& p, f3 o, f3 v0, f3 v1, f3 v2, float tmin, float tmax,
-                                 float* t_out, float* V_out, float* W_out, float* det_out) {
-    f3 A = v0 - o, B = v1 - o, C = v2 - o;
-    float Akz = comp(A, p.kz), Bkz = comp(B, p.kz), Ckz = comp(C, p.kz);
-    float Ax = comp(A, p.kx) - p.Sx * Akz;
-    float Ay = comp(A, p.ky) - p.Sy * Akz;
-    float Bx = comp(B, p.kx) - p.Sx * Bkz;
-    float By = comp(B, p.ky) - p.Sy * Bkz;
-    float Cx = comp(C, p.kx) - p.Sx * Ckz;
-    float Cy = comp(C, p.ky) - p.Sy * Ckz;
+// Vertices a, b, c and the origin o already in (kz, kx, ky) order (rot3 / tri_window).
+// Returns true on hit and writes t and the unnormalised (V, W, det): u = V / det, v = W / det
+// (the divisions happen once, for the closest hit, not for every candidate).
+RT_HD bool intersect_rot(const RayPre& p, f3 o, f3 a, f3 b, f3 c, float tmin, float tmax,
+                         float* t_out, float* V_out, float* W_out, float* det_out) {
+    const float Akz = a.x - o.x, Bkz = b.x - o.x, Ckz = c.x - o.x;
+    const float Ax = (a.y - o.y) - p.Sx * Akz;
+    const float Ay = (a.z - o.z) - p.Sy * Akz;
+    const float Bx = (b.y - o.y) - p.Sx * Bkz;
+    const float By = (b.z - o.z) - p.Sy * Bkz;
+    const float Cx = (c.y - o.y) - p.Sx * Ckz;
+    const float Cy = (c.z - o.z) - p.Sy * Ckz;
     float U = Cx * By - Cy * Bx;
     float V = Ax * Cy - Ay * Cx;
     float W = Bx * Ay - By * Ax;
@@ -261,6 +240,12 @@ RT_HD bool intersect_triangle_vw(const RayPre& p, f3 o, f3 v0, f3 v1, f3 v2, flo
     *W_out = W;
     *det_out = det;
     return true;
+}
+// The same test on world-space vertices (host tools).
+RT_HD bool intersect_triangle_vw(const RayPre& p, f3 o, f3 v0, f3 v1, f3 v2, float tmin, float tmax,
+                                 float* t_out, float* V_out, float* W_out, float* det_out) {
+    return intersect_rot(p, rot3(o, p.kz), rot3(v0, p.kz), rot3(v1, p.kz), rot3(v2, p.kz), tmin, tmax, t_out, V_out,
+                         W_out, det_out);
 }
 
 }  // namespace rt

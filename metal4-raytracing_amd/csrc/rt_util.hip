@@ -120,7 +120,7 @@ void launch_tri_nrm(const uint4* tri_info, const float4* nrm, float4* tri_nrm, u
 
 // ---- flatten world-space triangles into BVH slot order ----------------------------------------
 __global__ void flatten_k(const uint4* __restrict__ tri_info, const uint32_t* __restrict__ slot_to_tri,
-                          const float4* __restrict__ pos, const float* __restrict__ inst, float4* __restrict__ tris,
+                          const float4* __restrict__ pos, const float* __restrict__ inst, float* __restrict__ tris,
                           uint32_t n, unsigned* __restrict__ maxabs_bits) {
     __shared__ float red[4];
     uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
@@ -130,12 +130,21 @@ __global__ void flatten_k(const uint4* __restrict__ tri_info, const uint32_t* __
         uint4 ti = tri_info[id];
         const float* M = inst + 12 * (ti.w >> 8);
         uint32_t vi[3] = {ti.x, ti.y, ti.z};
+        float w9[9];
         #pragma unroll
         for (int q = 0; q < 3; ++q) {
             f3 w = xform(M, ld3(pos[vi[q]]), 1.0f);
-            tris[3 * k + q] = make_float4(w.x, w.y, w.z, q == 0 ? __uint_as_float(id) : 0.0f);
+            w9[3 * q] = w.x;
+            w9[3 * q + 1] = w.y;
+            w9[3 * q + 2] = w.z;
             m = fmaxf(m, fmaxf(fabsf(w.x), fmaxf(fabsf(w.y), fabsf(w.z))));
         }
+        // the 64-B record (rt_device.h tri_store), written as four 16-B stores
+        float r[kTriFloats];
+        tri_store(r, w9, id);
+        float4* dst = reinterpret_cast<float4*>(tris + (size_t)kTriFloats * k);
+        #pragma unroll
+        for (int q = 0; q < 4; ++q) dst[q] = make_float4(r[4 * q], r[4 * q + 1], r[4 * q + 2], r[4 * q + 3]);
     }
     // block max of |coordinate| -> one atomic per block (non-negative floats order as their bits)
     #pragma unroll
@@ -146,10 +155,37 @@ __global__ void flatten_k(const uint4* __restrict__ tri_info, const uint32_t* __
         atomicMax(maxabs_bits, __float_as_uint(fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]))));
 }
 void launch_flatten(const uint4* tri_info, const uint32_t* slot_to_tri, const float4* pos, const float* inst,
-                    float4* tris, uint32_t n, unsigned* maxabs_bits, hipStream_t s) {
+                    float* tris, uint32_t n, unsigned* maxabs_bits, hipStream_t s) {
     if (!n) return;
     hipLaunchKernelGGL(flatten_k, dim3((n + 255) / 256), dim3(256), 0, s, tri_info, slot_to_tri, pos, inst, tris, n,
                        maxabs_bits);
+}
+
+// ---- tree quality after a refit: the node-area sum ------------------------------------------------
+// sum over the 8-wide nodes of area(node box): proportional to the expected node visits of the rays
+// crossing the scene (the node term of the SAH cost, not normalised by the root box, which a moved
+// instance also grows).  One block, a fixed reduction order (deterministic); ~10 us for the
+// dragon's 71K nodes.  A refit keeps the topology and grows the boxes of moved geometry; rt_api.cpp
+// compares this against the value at the last build and rebuilds on the device when it has grown
+// past rt_tuning.refit_rebuild_pct.
+__device__ __forceinline__ float box_area(const float* b) {
+    const float dx = b[3] - b[0], dy = b[4] - b[1], dz = b[5] - b[2];
+    return (dx >= 0.0f && dy >= 0.0f && dz >= 0.0f) ? 2.0f * ((dx * dy + dy * dz) + dz * dx) : 0.0f;
+}
+__global__ void __launch_bounds__(1024) bvh_cost_k(const float* __restrict__ node_box, uint32_t nn, float* __restrict__ out) {
+    __shared__ double red[1024];
+    double s = 0.0;
+    for (uint32_t n = threadIdx.x; n < nn; n += 1024) s += (double)box_area(node_box + 6 * (size_t)n);
+    red[threadIdx.x] = s;
+    __syncthreads();
+    for (int w = 512; w > 0; w >>= 1) {
+        if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) *out = (float)red[0];
+}
+void launch_bvh_cost(const float* node_box, uint32_t nn, float* out, hipStream_t s) {
+    hipLaunchKernelGGL(bvh_cost_k, dim3(1), dim3(1024), 0, s, node_box, nn, out);
 }
 
 // ---- level-synchronous refit of the 8-wide BVH: one launch per level, deepest first -------------
@@ -157,7 +193,7 @@ void launch_flatten(const uint4* tri_info, const uint32_t* slot_to_tri, const fl
 // triangles + pad), re-quantizes them exactly as quantize_bvh8_node does on the host (double
 // precision, outward rounding), and stores its own box for its parent.
 __global__ void refit8_level_k(Bvh8Node* __restrict__ nodes, float* __restrict__ node_box,
-                               const float4* __restrict__ tris, const uint32_t* __restrict__ level_nodes,
+                               const float* __restrict__ tris, const uint32_t* __restrict__ level_nodes,
                                uint32_t count, float pad_min, const unsigned* __restrict__ maxabs_bits) {
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= count) return;
@@ -170,7 +206,7 @@ __global__ void refit8_level_k(Bvh8Node* __restrict__ nodes, float* __restrict__
     double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
     for (int c = 0; c < 8; ++c) {
         // unused slots carry an empty quantized box (qlo = 255 > qhi = 0 on x)
-        used[c] = !(nd.q[c] == 255 && nd.q[8 + c] == 0);
+        used[c] = !(nd.get_q(c) == 255 && nd.get_q(8 + c) == 0);
         if (!used[c]) continue;
         const uint32_t k_int = (uint32_t)nd.axis_k >> 4;
         float l[3] = {INFINITY, INFINITY, INFINITY}, h[3] = {-INFINITY, -INFINITY, -INFINITY};
@@ -182,7 +218,7 @@ __global__ void refit8_level_k(Bvh8Node* __restrict__ nodes, float* __restrict__
             const uint32_t first = nd.tri_base + bvh8_leaf_first(nd.tri_valid, j), n = bvh8_leaf_count(nd.tri_valid, j);
             for (uint32_t t = 0; t < n; ++t)
                 for (int q = 0; q < 3; ++q) {
-                    float4 v = tris[3 * (size_t)(first + t) + q];
+                    const f3 v = tri_vertex(tri_rec(tris, first + t), q);
                     l[0] = fminf(l[0], v.x); h[0] = fmaxf(h[0], v.x);
                     l[1] = fminf(l[1], v.y); h[1] = fmaxf(h[1], v.y);
                     l[2] = fminf(l[2], v.z); h[2] = fmaxf(h[2], v.z);
@@ -218,15 +254,15 @@ __global__ void refit8_level_k(Bvh8Node* __restrict__ nodes, float* __restrict__
                 ql = (uint8_t)fmax(0.0, fmin(255.0, fl));
                 qh = (uint8_t)fmax(0.0, fmin(255.0, fh));
             }
-            nd.q[16 * a + c] = ql;
-            nd.q[16 * a + 8 + c] = qh;
+            nd.set_q(16 * a + c, ql);
+            nd.set_q(16 * a + 8 + c, qh);
         }
         node_box[6 * (size_t)ni + a] = (float)lo[a];
         node_box[6 * (size_t)ni + 3 + a] = (float)hi[a];
     }
     nodes[ni] = nd;
 }
-void launch_refit8_level(Bvh8Node* nodes, float* node_box, const float4* tris, const uint32_t* level_nodes,
+void launch_refit8_level(Bvh8Node* nodes, float* node_box, const float* tris, const uint32_t* level_nodes,
                          uint32_t count, float pad_min, const unsigned* maxabs_bits, hipStream_t s) {
     if (!count) return;
     hipLaunchKernelGGL(refit8_level_k, dim3((count + 127) / 128), dim3(128), 0, s, nodes, node_box, tris, level_nodes,

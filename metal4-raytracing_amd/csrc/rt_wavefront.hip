@@ -423,7 +423,7 @@ __device__ __forceinline__ void node_step(const DevScene& S, Trav& T, int* stack
                                           float cull) {
     const uint32_t ni = next_node(T, stack, overflow);
     if (COUNT) tc.nodes++;
-    const NodeWords w = load_node8(S.nodes8, ni);
+    const NodeWords w = load_node8(S.nodes8, ni, T.R.dneg);
     test_node8_words(w, T.R, 0.0f, fminf(cull, T.best), T.g_hits, T.t_mask, T.t_valid, T.g_base, T.t_base, T.g_flip);
 }
 
@@ -446,18 +446,23 @@ __device__ __forceinline__ bool trav_step(const DevScene& S, Trav& T, bool any, 
         // round 3's bug, kept as a build-time switch to show the parity tests catch it
         // (tests/test_gpu_traversal_variants.py): both triangles against the bound from before the step
         const float stale_bound = fminf(cull, T.best);
-#define RT_ISECT(v0, v1, v2) intersect_triangle_vw(T.R.pre, T.R.o, v0, v1, v2, 0.0f, stale_bound, &t, &u, &v, &dt)
+#define RT_ISECT(a, b, c) intersect_rot(T.R.pre, T.R.o, a, b, c, 0.0f, stale_bound, &t, &u, &v, &dt)
 #else
-#define RT_ISECT(v0, v1, v2) intersect_triangle_vw(T.R.pre, T.R.o, v0, v1, v2, 0.0f, fminf(cull, T.best), &t, &u, &v, &dt)
+#define RT_ISECT(a, b, c) intersect_rot(T.R.pre, T.R.o, a, b, c, 0.0f, fminf(cull, T.best), &t, &u, &v, &dt)
 #endif
-        const float4* tp0 = S.tris + 3 * (size_t)tri_slot(T.t_base, T.t_valid, k0);
-        const float4* tp1 = S.tris + 3 * (size_t)tri_slot(T.t_base, T.t_valid, k1);
-        const float4 a0 = tp0[0], a1 = tp0[1], a2 = tp0[2];
-        const float4 b0 = tp1[0], b1 = tp1[1], b2 = tp1[2];   // = a when the lane has one triangle
+        // each vertex as the ray's (kz, kx, ky) window of its record: three 12-B loads and the id
+        // per triangle, all in the slot's 64-B line (rt_device.h); both triangles' loads issue
+        // before either test
+        const uint32_t kz = (uint32_t)T.R.pre.kz;
+        const uint32_t f0 = tri_slot(T.t_base, T.t_valid, k0) * (uint32_t)kTriFloats + kz;
+        const uint32_t f1 = tri_slot(T.t_base, T.t_valid, k1) * (uint32_t)kTriFloats + kz;
+        const f3 a0 = tri_window_at(S.tris, f0), a1 = tri_window_at(S.tris, f0 + 5u), a2 = tri_window_at(S.tris, f0 + 10u);
+        const f3 b0 = tri_window_at(S.tris, f1), b1 = tri_window_at(S.tris, f1 + 5u), b2 = tri_window_at(S.tris, f1 + 10u);   // = a for one triangle
+        const uint32_t ida = tri_id_at(S.tris, f0 - kz), idb = tri_id_at(S.tris, f1 - kz);
         if (COUNT) tc.tris += two ? 2u : 1u;
         float t, u, v, dt;
-        if (RT_ISECT(ld3(a0), ld3(a1), ld3(a2))) {
-            const uint32_t id = __float_as_uint(a0.w);
+        if (RT_ISECT(a0, a1, a2)) {
+            const uint32_t id = ida;
             if (any) {
                 T.hit_any = true;
                 tdone = true;
@@ -469,8 +474,8 @@ __device__ __forceinline__ bool trav_step(const DevScene& S, Trav& T, bool any, 
                 T.bv = v;
             }
         }
-        if (two && !tdone && RT_ISECT(ld3(b0), ld3(b1), ld3(b2))) {
-            const uint32_t id = __float_as_uint(b0.w);
+        if (two && !tdone && RT_ISECT(b0, b1, b2)) {
+            const uint32_t id = idb;
             if (any) {
                 T.hit_any = true;
                 tdone = true;
@@ -817,7 +822,10 @@ __global__ void __launch_bounds__(kSortThreads) wf_sort_scatter(DevScene S, WfPa
 // wave's chunk once at least Q.refill_min lanes are idle.  A wave therefore runs ~(steps of its
 // rays) / 64 iterations instead of (slowest ray) x (rays per lane).
 template <bool ANY, bool COUNT>
-__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8)))
+#ifndef RT_EXTEND_WAVES
+#define RT_EXTEND_WAVES 8
+#endif
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ANY ? 8 : RT_EXTEND_WAVES, ANY ? 8 : RT_EXTEND_WAVES)))
 wf_trace(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int cur, int ts) {
     const FrameParams& P = *Pp;   // per-frame parameters in device memory
     __shared__ int lds_stack[kStackSize * kBlock];

@@ -353,7 +353,11 @@ uint32_t rt_oracle_scene_triangles(const rt_oracle_scene* s) { return s ? s->ntr
 /* ---------------------------------------------------------------- intersection */
 /* Watertight ray/triangle test (Woop, Benthin, Wald 2013) standing in for the Metal
  * intersector<triangle_data, instancing> (Raytracing.metal:301-318): opaque, no culling,
- * t in [tmin, tmax]; u weights vertex 1, v weights vertex 2 (:63-73). */
+ * t in [tmin, tmax]; u weights vertex 1, v weights vertex 2 (:63-73).  The axes are cycled
+ * (kx = kz + 1, ky = kz + 2 mod 3) and never swapped: Woop et al. swap kx / ky when d[kz] < 0 to
+ * keep the winding for back-face culling; without culling the swap negates U, V, W, det and T
+ * together, which leaves t, u, v and every accept / reject decision unchanged up to the sign of
+ * exact zeros. */
 typedef struct { int kx, ky, kz; float Sx, Sy, Sz; } OPre;
 
 static OPre opre(V3 d) {
@@ -363,7 +367,6 @@ static OPre opre(V3 d) {
     int kx = kz + 1; if (kx == 3) kx = 0;
     int ky = kx + 1; if (ky == 3) ky = 0;
     float dz = vcomp(d, kz);
-    if (dz < 0.0f) { int tt = kx; kx = ky; ky = tt; }
     p.kx = kx; p.ky = ky; p.kz = kz;
     p.Sx = vcomp(d, kx) / dz;
     p.Sy = vcomp(d, ky) / dz;

@@ -25,12 +25,17 @@ static f3 ldf3(const rt_float3& v) { return mk3(v.x, v.y, v.z); }
 
 // VALU issues per block (ISA of wf_trace<false,false>, round 3)
 static double C_HEAD = 20, C_TRI1 = 95, C_TRI2 = 92, C_NODE = 194, C_STACK = 25, C_REFILL = 110;
+// edge-sharing pair (pair_bvh8_leaves): the second triangle of a flagged pair reuses two sheared
+// vertices and the diagonal's products of the first (C_TRI2 less two vertex setups of ~13 issues
+// and two load address computations); C_PSEL: the pair-first selection per triangle step
+static double C_PAIR2 = 60, C_PSEL = 4;
 
 struct Lane {
     bool active = false;
     RaySetup R;
+    f3 o;   // world-space origin (R.o is in the triangle test's rotated frame)
     float best;
-    uint32_t best_id, g_base, g_hits, t_base, t_mask, t_valid;
+    uint32_t best_id, g_base, g_hits, t_base, t_mask, t_valid, t_pair = 0;
     bool g_flip;
     int sp;
     uint32_t stack[64];
@@ -52,6 +57,7 @@ struct Policy {
     int defer_root = 0;     // root-node triangles tested after the rest of the tree, if their leaf box is still in reach
     int coop = 0;           // > 0: the wave tests every pending triangle of the tri-phase lanes in batches of 64
                             // (one per lane, owner's ray via LDS / bpermute); coop = per-batch overhead issues
+    int pairs = 0;          // 1: edge-sharing pairs of a leaf (Bvh8Node::reserved) tested as one pair step
 };
 
 struct Scene8 {
@@ -61,6 +67,7 @@ struct Scene8 {
 
 static void start(Lane& L, const Ray& r) {
     L.R = ray_setup(r.o, r.d);
+    L.o = r.o;
     L.best = INFINITY;
     L.best_id = 0xffffffffu;
     L.g_base = 0;
@@ -81,7 +88,8 @@ static bool tri_test(const Scene8& S, Lane& L, uint32_t slot) {
     if (!g_tri_tests.empty()) g_tri_tests[slot]++;
     g_tris += 1;
     float t, u, v, dt;
-    if (intersect_triangle_vw(L.R.pre, L.R.o, ld3(tp[0]), ld3(tp[1]), ld3(tp[2]), 0.0f, L.best, &t, &u, &v, &dt)) {
+    const int kz = L.R.pre.kz;
+    if (intersect_rot(L.R.pre, L.R.o, rot3(ld3(tp[0]), kz), rot3(ld3(tp[1]), kz), rot3(ld3(tp[2]), kz), 0.0f, L.best, &t, &u, &v, &dt)) {
         const uint32_t id = __builtin_bit_cast(uint32_t, tp[0].w);
         if (t < L.best || id < L.best_id) {
             L.best = t;
@@ -94,16 +102,16 @@ static bool tri_test(const Scene8& S, Lane& L, uint32_t slot) {
 static bool node_work(const Lane& L) { return L.g_hits != 0u || L.sp > 0; }
 
 // min entry distance of the hit leaf children of node ni (the slab math of test_node8_words)
-static float leaf_tn(const Scene8& S, uint32_t ni, const RaySetup& R, float tmax) {
+static float leaf_tn(const Scene8& S, uint32_t ni, const RaySetup& R, f3 org, float tmax) {
     const Bvh8Node& n = S.nodes[ni];
     const int k = n.axis_k >> 4;
     float best = INFINITY;
     for (int c = k; c < 8; ++c) {
         float tn = 0.0f, tf = tmax * 1.0000004f;
-        const float inv[3] = {R.ix, R.iy, R.iz}, o[3] = {R.o.x, R.o.y, R.o.z};
+        const float inv[3] = {R.ix, R.iy, R.iz}, o[3] = {org.x, org.y, org.z};
         for (int a = 0; a < 3; ++a) {
             const float sc = ldexpf(1.0f, (int)n.e[a] - 127);
-            const float lo = n.p[a] + n.q[16 * a + c] * sc, hi = n.p[a] + n.q[16 * a + 8 + c] * sc;
+            const float lo = n.p[a] + n.get_q(16 * a + c) * sc, hi = n.p[a] + n.get_q(16 * a + 8 + c) * sc;
             float t0 = (lo - o[a]) * inv[a], t1 = (hi - o[a]) * inv[a];
             if (t0 > t1) std::swap(t0, t1);
             tn = std::max(tn, t0);
@@ -129,9 +137,10 @@ static void node_step(const Scene8& S, Lane& L) {
     const uint32_t ni = L.g_base + (uint32_t)r;
     g_nodes += 1;
     test_node8(S.nodes.data(), ni, L.R, 0.0f, L.best, L.g_hits, L.t_mask, L.t_valid, L.g_base, L.t_base, L.g_flip);
+    L.t_pair = S.nodes[ni].reserved;
     if (g_defer_root && ni == 0 && L.t_mask) {
         L.r_mask = L.t_mask;
-        L.r_tn = leaf_tn(S, 0, L.R, L.best);
+        L.r_tn = leaf_tn(S, 0, L.R, L.o, L.best);
         L.t_mask = 0;
     }
 }
@@ -193,8 +202,8 @@ static Result simulate(const Scene8& S, const std::vector<Ray>& rays, const Poli
                     if (!node_work(L) || (L.t_mask && L.p_mask) || P.postpone_thr == 0) ++blocked;
                 }
             const bool tri_phase = want_tri > 0 && (P.postpone_thr == 0 || want_tri >= P.postpone_thr || blocked > 0);
-            bool any_t[8] = {}, any_node = false, any_stack = false;
-            int n_t[8] = {}, n_node = 0;
+            bool any_t[8] = {}, any_node = false, any_stack = false, any_pair = false;
+            int n_t[8] = {}, n_node = 0, n_pair = 0;
             for (auto& L : lanes) {
                 if (!L.active) continue;
                 bool did_tri = false;
@@ -203,7 +212,18 @@ static Result simulate(const Scene8& S, const std::vector<Ray>& rays, const Poli
                         L.t_mask = L.p_mask; L.t_base = L.p_base; L.t_valid = L.p_valid; L.p_mask = 0;
                     }
                     const int lim = P.coop ? 64 : P.tris_per_step;
-                    for (int k = 0; k < lim && L.t_mask; ++k) {
+                    const uint32_t pm = P.pairs ? (L.t_mask & L.t_pair) : 0u;
+                    if (pm) {   // the pair first: the first triangle's block, then the pair block
+                        const int b = lowest_bit(pm);
+                        L.t_mask &= ~(3u << b);
+                        tri_test(S, L, tri_slot(L.t_base, L.t_valid, b));
+                        tri_test(S, L, tri_slot(L.t_base, L.t_valid, b + 1));
+                        any_t[0] = true;
+                        ++n_t[0];
+                        any_pair = true;
+                        ++n_pair;
+                    }
+                    for (int k = 0; !pm && k < lim && L.t_mask; ++k) {
                         const int b = lowest_bit(L.t_mask);
                         L.t_mask &= L.t_mask - 1u;
                         tri_test(S, L, tri_slot(L.t_base, L.t_valid, b));
@@ -251,6 +271,8 @@ static Result simulate(const Scene8& S, const std::vector<Ray>& rays, const Poli
                 res.blk_lanes[2] += n_t[0] * C_TRI1;
                 n_t[0] = 0;
             }
+            if (any_pair) { cost += C_PAIR2; res.blk_iss[2] += C_PAIR2; res.blk_lanes[2] += n_pair * C_PAIR2; res.lane_valu += n_pair * C_PAIR2; }
+            if (P.pairs && any_t[0]) { cost += C_PSEL; res.blk_iss[2] += C_PSEL; res.blk_lanes[2] += n_t[0] * C_PSEL; res.lane_valu += n_t[0] * C_PSEL; }
             for (int k = 0; k < 8; ++k) if (any_t[k] && n_t[k]) { cost += k ? C_TRI2 : C_TRI1; res.blk_iss[2] += k ? C_TRI2 : C_TRI1; res.blk_lanes[2] += n_t[k] * (k ? C_TRI2 : C_TRI1); }
             res.blk_iss[0] += C_HEAD; res.blk_lanes[0] += nact * C_HEAD;
             if (any_node) { res.blk_iss[3] += C_NODE; res.blk_lanes[3] += n_node * C_NODE; }
@@ -274,17 +296,22 @@ int main(int argc, char** argv) {
     rt_scene_desc D;
     rt_scene_get_desc(sc, &D);
     std::vector<float> world;
+    std::vector<uint32_t> tinfo;   // per triangle (i0, i1, i2, inst << 8): global vertex indices, as tri_info
+    uint32_t vbase = 0;
     for (uint32_t m = 0; m < D.mesh_count; ++m) {
         const rt_mesh_desc& M = D.meshes[m];
         const float* T = &M.transform.columns[0][0];
         for (uint32_t s = 0; s < M.submesh_count; ++s) {
             const rt_submesh_desc& SM = M.submeshes[s];
             for (uint32_t i = 0; i < SM.index_count; ++i) {
+                tinfo.push_back(vbase + SM.indices[i]);
+                if (i % 3 == 2) tinfo.push_back(m << 8);
                 const rt_float3& p = M.positions[SM.indices[i]];
                 for (int r = 0; r < 3; ++r)
                     world.push_back(((T[0 + r] * p.x + T[3 + r] * p.y) + T[6 + r] * p.z) + T[9 + r] * 1.0f);
             }
         }
+        vbase += M.vertex_count;
     }
     const uint32_t n = (uint32_t)(world.size() / 9);
     fprintf(stderr, "%u triangles; building\n", n);
@@ -294,6 +321,11 @@ int main(int argc, char** argv) {
         b2 = build_bvh2(world.data(), n, 1, limit);
         b8 = collapse_bvh8_dp(b2, 1.0f, getenv("SIM_CPRIM") ? (float)atof(getenv("SIM_CPRIM")) : 0.5f);
         if (b8.max_depth <= 16) break;
+    }
+    uint32_t npairs = 0;
+    if (getenv("SIM_PAIRS")) {
+        npairs = pair_bvh8_leaves(b8, tinfo.data(), world.data());
+        fprintf(stderr, "%u edge-sharing pairs flagged in leaves (%u triangles)\n", npairs, n);
     }
     Scene8 S;
     S.nodes = b8.nodes;
@@ -328,7 +360,10 @@ int main(int argc, char** argv) {
     TraceCounters tc{0, 0, 0};
     std::vector<int> stackbuf(16 * kBlock);
     DevScene DS{};
-    DS.tris = S.tris.data();
+    std::vector<float> recs((size_t)kTriFloats * b8.tri_order.size());   // the product's 64-B records for trace8
+    for (size_t k = 0; k < b8.tri_order.size(); ++k)
+        tri_store(&recs[(size_t)kTriFloats * k], &world[9 * (size_t)b8.tri_order[k]], b8.tri_order[k]);
+    DS.tris = recs.data();
     DS.nodes8 = S.nodes.data();
     for (const Ray& r : prim) {
         Hit h;
@@ -349,6 +384,7 @@ int main(int argc, char** argv) {
     fprintf(stderr, "%zu primary, %zu secondary rays\n", prim.size(), sec.size());
     std::vector<Policy> pols;
     pols.push_back(Policy{"current (refill 8, 2 tris)", 8, 2, 0});
+    if (getenv("SIM_PAIRS")) pols.push_back(Policy{"edge-sharing pairs", 8, 2, 0, 0, 0, 1});
     pols.push_back(Policy{"refill 16", 16, 2, 0});
     pols.push_back(Policy{"1 tri per step", 8, 1, 0});
     pols.push_back(Policy{"4 tris per step", 8, 4, 0});
