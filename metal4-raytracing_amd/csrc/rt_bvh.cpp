@@ -365,8 +365,8 @@ void quantize_bvh8_node(Bvh8Node& nd, const float clo[8][3], const float chi[8][
                 ql = (uint8_t)std::max(0.0, std::min(255.0, fl));
                 qh = (uint8_t)std::max(0.0, std::min(255.0, fh));
             }
-            nd.set_q(16 * a + c, ql);
-            nd.set_q(16 * a + 8 + c, qh);
+            nd.q[16 * a + c] = ql;
+            nd.q[16 * a + 8 + c] = qh;
         }
     }
 }

@@ -34,13 +34,10 @@ struct BvhResult {
     float pad = 0.0f;                  // absolute box padding used
 };
 
-// Compressed 8-wide node (128 B, one cache line; after Ylitie, Karras, Laine, HPG 2017).
-// Child boxes are quantized to 8-bit integers q in [0, 255] per plane against the node's origin p
-// and per-axis power-of-two scale 2^e, rounded outward, so the dequantized box p + q * 2^e always
-// encloses the (padded) BVH2 box it came from: traversal stays conservative and exact.  Each q is
-// stored as the fp16 number q (exact: integers up to 2048 are), so the node test converts and
-// scales a plane in one v_fma_mix_f32 (fp16 source) instead of v_cvt_f32_ubyte + v_fma_f32: the
-// same float value, so the same test (round 6; the 80-B node held the bytes).
+// Compressed 8-wide node (80 B = five 16-byte loads; after Ylitie, Karras, Laine, HPG 2017).
+// Child boxes are quantized to 8 bits per plane against the node's origin p and per-axis
+// power-of-two scale 2^e, rounded outward, so the dequantized box p + q * 2^e always encloses
+// the (padded) BVH2 box it came from: traversal stays conservative and exact.
 //   slots: the k internal children first (slot r = rank r, node index child_base + r), then the
 //            leaves (leaf j in slot k + j), then unused slots with an empty box (qlo = 255 > qhi = 0)
 //   k:       bits 4..7 of axis_k (bits 0..1: the sort axis)
@@ -51,24 +48,7 @@ struct BvhResult {
 //            (the leaf bits spread to nibbles, & tri_valid) without per-child branches.
 //   axis: children of each kind are sorted by centroid along `axis`; rays with d[axis] < 0 visit
 //   them in reverse slot order (approximate front-to-back order for closest-hit culling).
-// Plane order of q (16 B per group of 8 children): [qlo.x 0..7][qhi.x 0..7][qlo.y ..][qhi.y ..][qlo.z ..][qhi.z ..];
-// a ray loads its near and far group of each axis directly (lo or hi by the sign of its direction).
-#if defined(__HIPCC__)
-#define RT_BVH_HD __host__ __device__
-#else
-#define RT_BVH_HD
-#endif
-// fp16 bit pattern of the integer q in [0, 255] (exact) and back
-RT_BVH_HD inline uint16_t q_f16bits(uint32_t q) {
-    if (q == 0u) return 0u;
-    const int e = 31 - __builtin_clz(q);   // 2^e <= q < 2^(e + 1), e <= 7
-    return (uint16_t)(((uint32_t)(e + 15) << 10) | ((q << (10 - e)) & 0x3ffu));
-}
-RT_BVH_HD inline uint32_t f16bits_q(uint16_t b) {
-    if (b == 0u) return 0u;
-    const int e = (int)(b >> 10) - 15;
-    return (0x400u | (b & 0x3ffu)) >> (10 - e);
-}
+// Byte order of q: [qlo.x 0..7][qhi.x 0..7][qlo.y ..][qhi.y ..][qlo.z ..][qhi.z ..].
 struct alignas(16) Bvh8Node {
     float p[3];
     uint8_t e[3];     // biased exponents (e + 127): scale = 2^(e - 127)
@@ -76,12 +56,10 @@ struct alignas(16) Bvh8Node {
     uint32_t child_base;
     uint32_t tri_base;
     uint32_t tri_valid;
-    uint32_t reserved;
-    uint16_t q[48];   // fp16 bits of the quantized planes (q_f16bits)
-    RT_BVH_HD void set_q(int i, uint32_t v) { q[i] = q_f16bits(v); }
-    RT_BVH_HD uint32_t get_q(int i) const { return f16bits_q(q[i]); }
+    uint32_t reserved;   // pair_bvh8_leaves: bit 4j + i = leaf j's triangles i, i + 1 form an edge-sharing pair
+    uint8_t q[48];
 };
-static_assert(sizeof(Bvh8Node) == 128, "wide node is 128 B");
+static_assert(sizeof(Bvh8Node) == 80, "wide node is 80 B");
 
 struct Bvh8Result {
     std::vector<Bvh8Node> nodes;
@@ -97,6 +75,11 @@ struct Bvh8Result {
 // sum(A(node) * c_node) + sum(A(leaf) * c_prim * triangles).  Best on a BVH2 with 1-triangle leaves.
 Bvh8Result collapse_bvh8_dp(const BvhResult& b2, float c_node, float c_prim);
 
+#if defined(__HIPCC__)
+#define RT_BVH_HD __host__ __device__
+#else
+#define RT_BVH_HD
+#endif
 // Leaf j of a node: its first triangle slot (relative to tri_base) and its triangle count.
 RT_BVH_HD inline uint32_t bvh8_leaf_first(uint32_t tri_valid, int j) {
     return (uint32_t)__builtin_popcount(j ? tri_valid & ((1u << (4 * j)) - 1u) : 0u);

@@ -114,7 +114,7 @@ struct RaySetup {
     RayPre pre;
     float ix, iy, iz;   // 1 / d (safe)
     float ox, oy, oz;   // o * (1 / d)
-    uint32_t dneg;      // bit a = (1 / d[a] < 0)
+    uint32_t dneg;      // bit a = (d[a] < 0)
 };
 
 __host__ __device__ __forceinline__ RaySetup ray_setup(f3 o, f3 d) {
@@ -137,36 +137,33 @@ __host__ __device__ __forceinline__ RaySetup ray_setup(f3 o, f3 d) {
     R.ox = o.x * R.ix;
     R.oy = o.y * R.iy;
     R.oz = o.z * R.iz;
-    // bit a: the hi plane is the near one on axis a (ix < 0; for d = -0 too, whose reciprocal is
-    // -1e30): the node test's load selection (load_node8) and the slot-order flip
-    R.dneg = (R.ix < 0.0f ? 1u : 0u) | (R.iy < 0.0f ? 2u : 0u) | (R.iz < 0.0f ? 4u : 0u);
+    R.dneg = (d.x < 0.0f ? 1u : 0u) | (d.y < 0.0f ? 2u : 0u) | (d.z < 0.0f ? 4u : 0u);
     return R;
 }
 
 __host__ __device__ __forceinline__ float byte_f(uint32_t w, int b) { return (float)((w >> (8 * b)) & 0xffu); }
 
-// The node words one ray reads (eight 16-byte loads, one 128-B line): the header, and per axis the
-// near and the far group of the eight children's planes -- lo or hi by the sign of the ray's
-// direction on that axis (R.dneg), chosen by the load address instead of per-component selects.
+// Slab-test the 8 children of node `ni` (five 16-byte loads).  Returns the internal children hit
+// (bit r = internal rank r), the triangles to test (bit k = triangle tri_base + k), and the
+// traversal direction of the node's slot order.
+// The five 16-byte words of a node (from global memory or an LDS copy).
+struct NodeU3 { uint32_t x, y, z; };   // child_base, tri_base, tri_valid (the reserved word is not read)
 struct NodeWords {
     float4 h0;
-    uint4 h1, nx, fx, ny, fy, nz, fz;
+    NodeU3 h1;
+    uint4 qx, qy, qz;
 };
 // (32-bit byte offsets from the array base: the loads take the uniform base in SGPRs and one
 // 32-bit offset per lane, no 64-bit address arithmetic; node arrays stay below 2^23 nodes)
-__host__ __device__ __forceinline__ NodeWords load_node8(const Bvh8Node* nodes, uint32_t ni, uint32_t dneg) {
+__host__ __device__ __forceinline__ NodeWords load_node8(const Bvh8Node* nodes, uint32_t ni) {
     const char* base = reinterpret_cast<const char*>(nodes);
     const uint32_t o = ni * (uint32_t)sizeof(Bvh8Node);
-    const uint32_t sx = (dneg & 1u) << 4, sy = (dneg & 2u) << 3, sz = (dneg & 4u) << 2;   // 16 B: hi first
     NodeWords w;
     w.h0 = *reinterpret_cast<const float4*>(base + o);
-    w.h1 = *reinterpret_cast<const uint4*>(base + (o + 16u));
-    w.nx = *reinterpret_cast<const uint4*>(base + (o + 32u + sx));
-    w.fx = *reinterpret_cast<const uint4*>(base + (o + 48u - sx));
-    w.ny = *reinterpret_cast<const uint4*>(base + (o + 64u + sy));
-    w.fy = *reinterpret_cast<const uint4*>(base + (o + 80u - sy));
-    w.nz = *reinterpret_cast<const uint4*>(base + (o + 96u + sz));
-    w.fz = *reinterpret_cast<const uint4*>(base + (o + 112u - sz));
+    w.h1 = *reinterpret_cast<const NodeU3*>(base + (o + 16u));   // 12 B: 76 of the node's 80 B are read
+    w.qx = *reinterpret_cast<const uint4*>(base + (o + 32u));
+    w.qy = *reinterpret_cast<const uint4*>(base + (o + 48u));
+    w.qz = *reinterpret_cast<const uint4*>(base + (o + 64u));
     return w;
 }
 
@@ -182,20 +179,6 @@ __host__ __device__ __forceinline__ uint32_t tri_slot(uint32_t tri_base, uint32_
     return tri_base + (uint32_t)__builtin_popcount(tri_valid & ((1u << k) - 1u));
 }
 
-// q * a + b for the fp16 plane of child c in a group of eight (two per dword): on the device one
-// v_fma_mix_f32 reading the fp16 half directly; the same single-rounding fma of the same exact
-// value as fmaf((float)q, a, b)
-__host__ __device__ __forceinline__ float plane_fma(const uint4& g, int c, float a, float b) {
-    const uint32_t w = c < 2 ? g.x : c < 4 ? g.y : c < 6 ? g.z : g.w;
-#if defined(__HIP_DEVICE_COMPILE__)
-    typedef _Float16 h2 __attribute__((ext_vector_type(2)));
-    const h2 h = __builtin_bit_cast(h2, w);
-    return __builtin_fmaf((float)((c & 1) ? h.y : h.x), a, b);
-#else
-    return __builtin_fmaf((float)f16bits_q((uint16_t)((c & 1) ? (w >> 16) : (w & 0xffffu))), a, b);
-#endif
-}
-
 // Slab-test the 8 children of a node.  Outputs: the internal children hit (bit r = internal rank r
 // = slot r), the triangles to test (nibble space: bit 4j + i = triangle i of leaf j, see
 // tri_slot), the node's tri_valid word, and the traversal direction of the slot order.
@@ -205,7 +188,8 @@ __host__ __device__ __forceinline__ void test_node8_words(const NodeWords& W, co
                                                           uint32_t& ihits, uint32_t& tmask, uint32_t& tvalid,
                                                           uint32_t& child_base, uint32_t& tri_base, bool& flip) {
     const float4 h0 = W.h0;
-    const uint4 h1 = W.h1;
+    const NodeU3 h1 = W.h1;
+    const uint4 qx = W.qx, qy = W.qy, qz = W.qz;
     const uint32_t ew = __builtin_bit_cast(uint32_t, h0.w);
     const float sx = __builtin_bit_cast(float, (ew & 0xffu) << 23);
     const float sy = __builtin_bit_cast(float, ((ew >> 8) & 0xffu) << 23);
@@ -216,13 +200,24 @@ __host__ __device__ __forceinline__ void test_node8_words(const NodeWords& W, co
     const float bx = __builtin_fmaf(h0.x, R.ix, -R.ox);
     const float by = __builtin_fmaf(h0.y, R.iy, -R.oy);
     const float bz = __builtin_fmaf(h0.z, R.iz, -R.oz);
+    // near / far planes by direction sign
+    const uint32_t nx0 = R.ix >= 0.0f ? qx.x : qx.z, nx1 = R.ix >= 0.0f ? qx.y : qx.w;
+    const uint32_t fx0 = R.ix >= 0.0f ? qx.z : qx.x, fx1 = R.ix >= 0.0f ? qx.w : qx.y;
+    const uint32_t ny0 = R.iy >= 0.0f ? qy.x : qy.z, ny1 = R.iy >= 0.0f ? qy.y : qy.w;
+    const uint32_t fy0 = R.iy >= 0.0f ? qy.z : qy.x, fy1 = R.iy >= 0.0f ? qy.w : qy.y;
+    const uint32_t nz0 = R.iz >= 0.0f ? qz.x : qz.z, nz1 = R.iz >= 0.0f ? qz.y : qz.w;
+    const uint32_t fz0 = R.iz >= 0.0f ? qz.z : qz.x, fz1 = R.iz >= 0.0f ? qz.w : qz.y;
     const float tf_max = tmax * 1.0000004f;
     uint32_t hm = 0;
     #pragma unroll
     for (int c = 0; c < 8; ++c) {
-        const float tnx = plane_fma(W.nx, c, ax, bx), tfx = plane_fma(W.fx, c, ax, bx);
-        const float tny = plane_fma(W.ny, c, ay, by), tfy = plane_fma(W.fy, c, ay, by);
-        const float tnz = plane_fma(W.nz, c, az, bz), tfz = plane_fma(W.fz, c, az, bz);
+        const int b = c & 3;
+        const uint32_t wnx = c < 4 ? nx0 : nx1, wfx = c < 4 ? fx0 : fx1;
+        const uint32_t wny = c < 4 ? ny0 : ny1, wfy = c < 4 ? fy0 : fy1;
+        const uint32_t wnz = c < 4 ? nz0 : nz1, wfz = c < 4 ? fz0 : fz1;
+        const float tnx = __builtin_fmaf(byte_f(wnx, b), ax, bx), tfx = __builtin_fmaf(byte_f(wfx, b), ax, bx);
+        const float tny = __builtin_fmaf(byte_f(wny, b), ay, by), tfy = __builtin_fmaf(byte_f(wfy, b), ay, by);
+        const float tnz = __builtin_fmaf(byte_f(wnz, b), az, bz), tfz = __builtin_fmaf(byte_f(wfz, b), az, bz);
         const float tn = fmaxf(fmaxf(tnx, tny), fmaxf(tnz, tmin));
         const float tf = fminf(fminf(tfx, tfy), fminf(tfz, tf_max));
         const bool hit = tn <= tf;
@@ -239,7 +234,7 @@ __host__ __device__ __forceinline__ void test_node8_words(const NodeWords& W, co
 __host__ __device__ __forceinline__ void test_node8(const Bvh8Node* nodes, uint32_t ni, const RaySetup& R, float tmin,
                                                     float tmax, uint32_t& ihits, uint32_t& tmask, uint32_t& tvalid,
                                                     uint32_t& child_base, uint32_t& tri_base, bool& flip) {
-    test_node8_words(load_node8(nodes, ni, R.dneg), R, tmin, tmax, ihits, tmask, tvalid, child_base, tri_base, flip);
+    test_node8_words(load_node8(nodes, ni), R, tmin, tmax, ihits, tmask, tvalid, child_base, tri_base, flip);
 }
 
 __host__ __device__ __forceinline__ int lowest_bit(uint32_t m) { return __builtin_ctz(m); }

@@ -638,8 +638,8 @@ __device__ void quantize_node(Bvh8Node& nd, const Item* items, int n_items) {
                 ql = (uint8_t)fmax(0.0, fmin(255.0, fl));
                 qh = (uint8_t)fmax(0.0, fmin(255.0, fh));
             }
-            nd.set_q(16 * a + c, ql);
-            nd.set_q(16 * a + 8 + c, qh);
+            nd.q[16 * a + c] = ql;
+            nd.q[16 * a + 8 + c] = qh;
         }
     }
 }

@@ -206,7 +206,7 @@ __global__ void refit8_level_k(Bvh8Node* __restrict__ nodes, float* __restrict__
     double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
     for (int c = 0; c < 8; ++c) {
         // unused slots carry an empty quantized box (qlo = 255 > qhi = 0 on x)
-        used[c] = !(nd.get_q(c) == 255 && nd.get_q(8 + c) == 0);
+        used[c] = !(nd.q[c] == 255 && nd.q[8 + c] == 0);
         if (!used[c]) continue;
         const uint32_t k_int = (uint32_t)nd.axis_k >> 4;
         float l[3] = {INFINITY, INFINITY, INFINITY}, h[3] = {-INFINITY, -INFINITY, -INFINITY};
@@ -254,8 +254,8 @@ __global__ void refit8_level_k(Bvh8Node* __restrict__ nodes, float* __restrict__
                 ql = (uint8_t)fmax(0.0, fmin(255.0, fl));
                 qh = (uint8_t)fmax(0.0, fmin(255.0, fh));
             }
-            nd.set_q(16 * a + c, ql);
-            nd.set_q(16 * a + 8 + c, qh);
+            nd.q[16 * a + c] = ql;
+            nd.q[16 * a + 8 + c] = qh;
         }
         node_box[6 * (size_t)ni + a] = (float)lo[a];
         node_box[6 * (size_t)ni + 3 + a] = (float)hi[a];

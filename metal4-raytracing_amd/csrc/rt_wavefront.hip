@@ -423,7 +423,7 @@ __device__ __forceinline__ void node_step(const DevScene& S, Trav& T, int* stack
                                           float cull) {
     const uint32_t ni = next_node(T, stack, overflow);
     if (COUNT) tc.nodes++;
-    const NodeWords w = load_node8(S.nodes8, ni, T.R.dneg);
+    const NodeWords w = load_node8(S.nodes8, ni);
     test_node8_words(w, T.R, 0.0f, fminf(cull, T.best), T.g_hits, T.t_mask, T.t_valid, T.g_base, T.t_base, T.g_flip);
 }
 
@@ -457,8 +457,9 @@ __device__ __forceinline__ bool trav_step(const DevScene& S, Trav& T, bool any, 
         const uint32_t f0 = tri_slot(T.t_base, T.t_valid, k0) * (uint32_t)kTriFloats + kz;
         const uint32_t f1 = tri_slot(T.t_base, T.t_valid, k1) * (uint32_t)kTriFloats + kz;
         const f3 a0 = tri_window_at(S.tris, f0), a1 = tri_window_at(S.tris, f0 + 5u), a2 = tri_window_at(S.tris, f0 + 10u);
+        const uint32_t ida = tri_id_at(S.tris, f0 - kz);
         const f3 b0 = tri_window_at(S.tris, f1), b1 = tri_window_at(S.tris, f1 + 5u), b2 = tri_window_at(S.tris, f1 + 10u);   // = a for one triangle
-        const uint32_t ida = tri_id_at(S.tris, f0 - kz), idb = tri_id_at(S.tris, f1 - kz);
+        const uint32_t idb = tri_id_at(S.tris, f1 - kz);
         if (COUNT) tc.tris += two ? 2u : 1u;
         float t, u, v, dt;
         if (RT_ISECT(a0, a1, a2)) {

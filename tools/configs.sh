@@ -16,9 +16,11 @@ import json, sys
 d = json.loads([x for x in open(sys.argv[1]) if x.startswith("{")][-1])
 r, c = d["roofline"], d["cpu_baseline"]
 assert r["frac"] is not None and r["frac"] < 1, r.get("frac_source")
+v = (r.get("valu_issue") or {}).get(r["kernel"]) or {}
 print(sys.argv[2], d["value"], "ms/step", d["ms_per_step"], "ms/frame", d.get("ms_per_frame"), "fif", d["config"]["frames_in_flight"],
       r["kernel"][:24], "frac(pmc)", r["frac"], "l2_hit", r["l2_hit"] and r["l2_hit"].get(r["kernel"]),
-      "alg_GBs", r.get("achieved_algorithmic"), "cpu", c and c["value"], flush=True)
+      "alg_GBs", r.get("achieved_algorithmic"), "valu_issue", v.get("frac_valu_issue"), "lane_util", v.get("lane_util"),
+      "visits", d["config"].get("visits_per_ray"), "cpu", c and c["value"], flush=True)
 PY
 }
 run c1 --scene c1 --width 256 --height 256 --spp 1 --bounces 1 --steps 400 --warmup 20 --cpu-seconds 6

@@ -111,7 +111,7 @@ static float leaf_tn(const Scene8& S, uint32_t ni, const RaySetup& R, f3 org, fl
         const float inv[3] = {R.ix, R.iy, R.iz}, o[3] = {org.x, org.y, org.z};
         for (int a = 0; a < 3; ++a) {
             const float sc = ldexpf(1.0f, (int)n.e[a] - 127);
-            const float lo = n.p[a] + n.get_q(16 * a + c) * sc, hi = n.p[a] + n.get_q(16 * a + 8 + c) * sc;
+            const float lo = n.p[a] + n.q[16 * a + c] * sc, hi = n.p[a] + n.q[16 * a + 8 + c] * sc;
             float t0 = (lo - o[a]) * inv[a], t1 = (hi - o[a]) * inv[a];
             if (t0 > t1) std::swap(t0, t1);
             tn = std::max(tn, t0);
