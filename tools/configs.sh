@@ -26,6 +26,10 @@ PY
 run c1 --scene c1 --width 256 --height 256 --spp 1 --bounces 1 --steps 400 --warmup 20 --cpu-seconds 6
 run c2 --scene c2 --width 1280 --height 720 --spp 4 --bounces 4 --steps 128 --warmup 8 --cpu-seconds 6
 run c3g --steps 64 --warmup 6 --cpu-seconds 6
+# the frames in flight a reference user would see: three (Renderer.swift:207) and the library's default
+# without GPU_MAX_HW_QUEUES (four hardware queues -> four slots)
+run c3g_fif3 --steps 64 --warmup 6 --frames-in-flight 3 --no-cpu
+(export RT_HW_QUEUES=4; run c3g_q4 --steps 64 --warmup 6 --no-cpu) || exit 1
 run c3d --scene c3d --steps 32 --warmup 4 --cpu-seconds 6
 run c3r --scene c3r --steps 32 --warmup 4 --cpu-seconds 6
 run c5 --scene c5 --bounces 2 --animate --steps 64 --warmup 4 --cpu-seconds 6
