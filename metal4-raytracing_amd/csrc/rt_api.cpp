@@ -99,7 +99,10 @@ static int small_frame_slots() {
 // Frames below this many allocated paths keep at most four slots: a configs[0]-sized frame (65K
 // paths, ~0.05 ms) on eight slots / eight queues ran bimodally, 2.04-2.10 or 0.55-0.62 Grays/s
 // (3 of 6 runs slow), against 2.10-2.54 on four (round 5); the 8-way C3g share (1M paths) gains
-// 9 % from eight slots and was steady.
+// 9 % from eight slots and was steady.  Round 6 traced six such runs (profiles/r06_c1_bimodal.txt):
+// the kernels take the same time in slow and fast runs, the slow ones overlap their frames less
+// (0.94-1.10 kernels at once against 1.38) -- slot streams sharing hardware queues serialise a
+// frame whose GPU work is ~0.12 ms; at four slots there is queue room to spare.
 constexpr uint64_t kSmallFramePaths = 1ull << 19;
 constexpr uint64_t kSmallShareBasePaths = 2500000;   // see rt_render_frame's tail
 constexpr int kTailShare = 786432;
