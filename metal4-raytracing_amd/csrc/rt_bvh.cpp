@@ -597,40 +597,4 @@ void emit_bvh8_node(const BvhResult& b2, const Job& job, std::vector<WItem>& ite
 }
 }  // namespace
 
-uint32_t pair_bvh8_leaves(Bvh8Result& b8, const uint32_t* ti, const float* world) {
-    // B = (A.v0, A.v2, D): same vertex, same instance, bitwise-equal world coordinates
-    auto same_vertex = [&](uint32_t a, int va, uint32_t b, int vb) {
-        return ti[4 * (size_t)a + va] == ti[4 * (size_t)b + vb] && (ti[4 * (size_t)a + 3] >> 8) == (ti[4 * (size_t)b + 3] >> 8) &&
-               std::memcmp(&world[9 * (size_t)a + 3 * va], &world[9 * (size_t)b + 3 * vb], 12) == 0;
-    };
-    auto fan = [&](uint32_t a, uint32_t b) { return same_vertex(a, 0, b, 0) && same_vertex(a, 2, b, 1); };
-    uint32_t pairs = 0;
-    for (Bvh8Node& nd : b8.nodes) {
-        nd.reserved = 0u;
-        for (int j = 0; j < 8; ++j) {
-            const uint32_t cnt = bvh8_leaf_count(nd.tri_valid, j);
-            if (cnt < 2) continue;
-            uint32_t* t = &b8.tri_order[nd.tri_base + bvh8_leaf_first(nd.tri_valid, j)];
-            uint32_t order[4], n = 0;
-            bool used[4] = {false, false, false, false};
-            for (uint32_t a = 0; a < cnt && n + 1 < cnt; ++a) {   // greedy: pairs first, A before B
-                if (used[a]) continue;
-                for (uint32_t b = 0; b < cnt; ++b) {
-                    if (b == a || used[b] || !fan(t[a], t[b])) continue;
-                    nd.reserved |= 1u << (4 * j + n);
-                    order[n++] = t[a];
-                    order[n++] = t[b];
-                    used[a] = used[b] = true;
-                    ++pairs;
-                    break;
-                }
-            }
-            for (uint32_t a = 0; a < cnt; ++a)
-                if (!used[a]) order[n++] = t[a];
-            std::memcpy(t, order, 4 * cnt);
-        }
-    }
-    return pairs;
-}
-
 }  // namespace rt

@@ -56,7 +56,7 @@ struct alignas(16) Bvh8Node {
     uint32_t child_base;
     uint32_t tri_base;
     uint32_t tri_valid;
-    uint32_t reserved;   // pair_bvh8_leaves: bit 4j + i = leaf j's triangles i, i + 1 form an edge-sharing pair
+    uint32_t reserved;
     uint8_t q[48];
 };
 static_assert(sizeof(Bvh8Node) == 80, "wide node is 80 B");
@@ -85,17 +85,6 @@ RT_BVH_HD inline uint32_t bvh8_leaf_first(uint32_t tri_valid, int j) {
     return (uint32_t)__builtin_popcount(j ? tri_valid & ((1u << (4 * j)) - 1u) : 0u);
 }
 RT_BVH_HD inline uint32_t bvh8_leaf_count(uint32_t tri_valid, int j) { return (uint32_t)__builtin_popcount((tri_valid >> (4 * j)) & 15u); }
-
-// Edge-sharing triangle pairs inside the leaves (DESIGN.md §3.1 "Triangle pairs").  Two triangles
-// of one leaf with vertices A = (a, b, c) and B = (a, c, d) -- the halves of a quad split along its
-// a-c diagonal, the fan split the OBJ loader and the procedural meshes emit -- move to leaf
-// positions (0, 1) or (2, 3), A first, and bit 4j + i (i = 0 or 2) of Bvh8Node::reserved is set.
-// The traversal tests such a pair with four sheared vertices instead of six and forms the
-// diagonal's two edge products once; the order of triangles inside a leaf never changes a
-// closest-hit or any-hit result.  tri_info4: per original triangle (i0, i1, i2, inst << 8 | submesh);
-// world: 9 floats per original triangle (the shared vertices must be bitwise equal there).
-// Returns the number of pairs flagged.
-uint32_t pair_bvh8_leaves(Bvh8Result& b8, const uint32_t* tri_info4, const float* world);
 
 // Re-quantize node n from its children's boxes (children: node_box of internal children, leaf
 // triangle bounds from tri_verts in BVH8 triangle order, padded).  Host mirror of the refit kernel.

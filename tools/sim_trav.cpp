@@ -81,6 +81,52 @@ static void start(Lane& L, const Ray& r) {
     L.steps = 0;
 }
 
+// Edge-sharing triangle pairs inside the leaves (DESIGN.md §3.1 "Triangle pairs").  Two triangles
+// of one leaf with vertices A = (a, b, c) and B = (a, c, d) -- the halves of a quad split along its
+// a-c diagonal, the fan split the OBJ loader and the procedural meshes emit -- move to leaf
+// positions (0, 1) or (2, 3), A first, and bit 4j + i (i = 0 or 2) of Bvh8Node::reserved (this model only: the product does not pair) is set.
+// The traversal tests such a pair with four sheared vertices instead of six and forms the
+// diagonal's two edge products once; the order of triangles inside a leaf never changes a
+// closest-hit or any-hit result.  tri_info4: per original triangle (i0, i1, i2, inst << 8 | submesh);
+// world: 9 floats per original triangle (the shared vertices must be bitwise equal there).
+// Returns the number of pairs flagged.
+static uint32_t pair_bvh8_leaves(Bvh8Result& b8, const uint32_t* ti, const float* world) {
+    // B = (A.v0, A.v2, D): same vertex, same instance, bitwise-equal world coordinates
+    auto same_vertex = [&](uint32_t a, int va, uint32_t b, int vb) {
+        return ti[4 * (size_t)a + va] == ti[4 * (size_t)b + vb] && (ti[4 * (size_t)a + 3] >> 8) == (ti[4 * (size_t)b + 3] >> 8) &&
+               std::memcmp(&world[9 * (size_t)a + 3 * va], &world[9 * (size_t)b + 3 * vb], 12) == 0;
+    };
+    auto fan = [&](uint32_t a, uint32_t b) { return same_vertex(a, 0, b, 0) && same_vertex(a, 2, b, 1); };
+    uint32_t pairs = 0;
+    for (Bvh8Node& nd : b8.nodes) {
+        nd.reserved = 0u;
+        for (int j = 0; j < 8; ++j) {
+            const uint32_t cnt = bvh8_leaf_count(nd.tri_valid, j);
+            if (cnt < 2) continue;
+            uint32_t* t = &b8.tri_order[nd.tri_base + bvh8_leaf_first(nd.tri_valid, j)];
+            uint32_t order[4], n = 0;
+            bool used[4] = {false, false, false, false};
+            for (uint32_t a = 0; a < cnt && n + 1 < cnt; ++a) {   // greedy: pairs first, A before B
+                if (used[a]) continue;
+                for (uint32_t b = 0; b < cnt; ++b) {
+                    if (b == a || used[b] || !fan(t[a], t[b])) continue;
+                    nd.reserved |= 1u << (4 * j + n);
+                    order[n++] = t[a];
+                    order[n++] = t[b];
+                    used[a] = used[b] = true;
+                    ++pairs;
+                    break;
+                }
+            }
+            for (uint32_t a = 0; a < cnt; ++a)
+                if (!used[a]) order[n++] = t[a];
+            std::memcpy(t, order, 4 * cnt);
+        }
+    }
+    return pairs;
+}
+
+
 static std::vector<uint32_t> g_tri_tests;
 static double g_nodes = 0, g_tris = 0;
 static bool tri_test(const Scene8& S, Lane& L, uint32_t slot) {
