@@ -427,42 +427,12 @@ __device__ __forceinline__ void node_step(const DevScene& S, Trav& T, int* stack
     test_node8_words(w, T.R, 0.0f, fminf(cull, T.best), T.g_hits, T.t_mask, T.t_valid, T.g_base, T.t_base, T.g_flip);
 }
 
-// ---- the root node's leaf triangles in LDS (RT_ROOT_TRIS) ------------------------------------------------
-// The root's leaves hold the scene's largest triangles (C3g: the floor and back-wall quads, 64 % of
-// the secondary rays' triangle tests, profiles/r05_finish_experiments.txt), and they occupy the first
-// slots.  Each block stages up to kRootTris of them in LDS, every (triangle, kz) window pre-rotated and
-// padded to 16 B with the id in w: a lane testing one of them reads three aligned ds_read_b128 instead
-// of four global loads (the vector-memory path paces the traversal).
-#ifndef RT_ROOT_TRIS
-#define RT_ROOT_TRIS 0
-#endif
-constexpr uint32_t kRootTris = 8;
-struct RootTris {
-    const float4* w;   // [slot][kz][vertex]: (v[kz], v[kx], v[ky], id)
-    uint32_t n;        // staged slots: 0 .. n - 1
-};
-// every thread of the block calls it (one __syncthreads)
-__device__ __forceinline__ RootTris stage_root_tris(const DevScene& S, float4* lds) {
-    uint32_t n = 0;
-#if RT_ROOT_TRIS
-    const uint4 h1 = *reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(S.nodes8) + 16);
-    n = h1.y == 0u ? min((uint32_t)__builtin_popcount(h1.z), kRootTris) : 0u;   // the root's triangles are slots 0..
-    for (uint32_t i = threadIdx.x; i < n * 9u; i += blockDim.x) {
-        const uint32_t slot = i / 9u, kz = (i / 3u) % 3u, v = i % 3u;
-        const f3 w = tri_window_at(S.tris, slot * (uint32_t)kTriFloats + 5u * v + kz);
-        lds[i] = make_float4(w.x, w.y, w.z, __uint_as_float(tri_id_at(S.tris, slot * (uint32_t)kTriFloats)));
-    }
-    __syncthreads();
-#endif
-    return RootTris{lds, n};
-}
-
 // `cull`: the distance bound of the box and triangle tests together with T.best (the lower of the
 // two); lower than T.best in the finish kernel's team drain (the closest hit any member of the team
 // has found), where T.best stays this lane's own hit.
 template <bool COUNT>
 __device__ __forceinline__ bool trav_step(const DevScene& S, Trav& T, bool any, int* stack, TraceCounters& tc,
-                                          bool& overflow, float cull, const RootTris& RT) {
+                                          bool& overflow, float cull) {
     bool tdone = false;
     if (T.t_mask != 0u) {
         const int k0 = lowest_bit(T.t_mask);
@@ -484,35 +454,12 @@ __device__ __forceinline__ bool trav_step(const DevScene& S, Trav& T, bool any, 
         // per triangle, all in the slot's 64-B line (rt_device.h); both triangles' loads issue
         // before either test
         const uint32_t kz = (uint32_t)T.R.pre.kz;
-        const uint32_t s0 = tri_slot(T.t_base, T.t_valid, k0), s1 = tri_slot(T.t_base, T.t_valid, k1);
-        f3 a0, a1, a2, b0, b1, b2;   // b = a for one triangle
-        uint32_t ida, idb;
-#if RT_ROOT_TRIS
-        if (s0 < RT.n) {
-            const float4* w = RT.w + (s0 * 3u + kz) * 3u;
-            const float4 x0 = w[0], x1 = w[1], x2 = w[2];
-            a0 = ld3(x0), a1 = ld3(x1), a2 = ld3(x2);
-            ida = __float_as_uint(x0.w);
-        } else
-#endif
-        {
-            const uint32_t f0 = s0 * (uint32_t)kTriFloats + kz;
-            a0 = tri_window_at(S.tris, f0), a1 = tri_window_at(S.tris, f0 + 5u), a2 = tri_window_at(S.tris, f0 + 10u);
-            ida = tri_id_at(S.tris, f0 - kz);
-        }
-#if RT_ROOT_TRIS
-        if (s1 < RT.n) {
-            const float4* w = RT.w + (s1 * 3u + kz) * 3u;
-            const float4 x0 = w[0], x1 = w[1], x2 = w[2];
-            b0 = ld3(x0), b1 = ld3(x1), b2 = ld3(x2);
-            idb = __float_as_uint(x0.w);
-        } else
-#endif
-        {
-            const uint32_t f1 = s1 * (uint32_t)kTriFloats + kz;
-            b0 = tri_window_at(S.tris, f1), b1 = tri_window_at(S.tris, f1 + 5u), b2 = tri_window_at(S.tris, f1 + 10u);
-            idb = tri_id_at(S.tris, f1 - kz);
-        }
+        const uint32_t f0 = tri_slot(T.t_base, T.t_valid, k0) * (uint32_t)kTriFloats + kz;
+        const uint32_t f1 = tri_slot(T.t_base, T.t_valid, k1) * (uint32_t)kTriFloats + kz;
+        const f3 a0 = tri_window_at(S.tris, f0), a1 = tri_window_at(S.tris, f0 + 5u), a2 = tri_window_at(S.tris, f0 + 10u);
+        const uint32_t ida = tri_id_at(S.tris, f0 - kz);
+        const f3 b0 = tri_window_at(S.tris, f1), b1 = tri_window_at(S.tris, f1 + 5u), b2 = tri_window_at(S.tris, f1 + 10u);   // = a for one triangle
+        const uint32_t idb = tri_id_at(S.tris, f1 - kz);
         if (COUNT) tc.tris += two ? 2u : 1u;
         float t, u, v, dt;
         if (RT_ISECT(a0, a1, a2)) {
@@ -901,11 +848,9 @@ wf_trace(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int cur, in
         }
     }
     __shared__ uint32_t ts_done;
-    __shared__ float4 lds_root[RT_ROOT_TRIS ? kRootTris * 9 : 1];
     if (threadIdx.x == 0) ts_done = 0u;
     ts_start(Q, ts);
     __syncthreads();
-    const RootTris RT = stage_root_tris(S, lds_root);
     // the shadow queue is one-sided, a ray queue two-sided (front / back parts)
     const uint32_t n = ANY ? load_prefix(Q.W.counts + cslot(kCntShadowQ)).end[kShards - 1]
                            : queue_len(load_queue(Q.W.counts, cur, Q.seg_cap));
@@ -990,7 +935,7 @@ wf_trace(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int cur, in
         if (__ballot(active) == 0ull) break;
         if (!active) continue;
         if (COUNT) ++steps;
-        if (trav_step<COUNT>(S, T, ANY, stack, tc, overflow, T.best, RT)) {
+        if (trav_step<COUNT>(S, T, ANY, stack, tc, overflow, T.best)) {
             active = false;
             if (COUNT && Q.diag) {   // steps-per-ray histogram (log2 bins) of the counting frame
                 atomicAdd(&Q.W.counts[kWfDiagSteps + (ANY ? 32 : 0) + (31 - __builtin_clz(steps))], 1u);
@@ -1037,8 +982,6 @@ wf_finish_step(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int c
     if (threadIdx.x == 0) ts_done = 0u;
     ts_start(Q, ts);
     const ShadeTabs halton = load_tabs(S, lds_halton, lds_mat);   // ends with a block barrier
-    __shared__ float4 lds_root[RT_ROOT_TRIS ? kRootTris * 9 : 1];
-    const RootTris RT = stage_root_tris(S, lds_root);
     const Uniforms& U = P.U;
     const QueueShards qs = load_queue(Q.W.counts, cur, Q.seg_cap);   // front parts first: the likely-long paths
     const uint32_t n = queue_len(qs);
@@ -1162,7 +1105,7 @@ wf_finish_step(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int c
         // ---- one traversal step (closest hit or shadow any-hit)
         if (mode == kClosest || mode == kShadow) {
             const bool any = mode == kShadow;
-            if (trav_step<COUNT>(S, T, any, stack, tc, overflow, T.best, RT)) {
+            if (trav_step<COUNT>(S, T, any, stack, tc, overflow, T.best)) {
                 if (any) {   // shadow ray done: unoccluded -> add its contribution (:741-743)
                     if (!T.hit_any) p.accum = p.accum + contrib;
                     if (next) {
@@ -1336,7 +1279,7 @@ wf_finish_step(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int c
             fresh = false;
             // one traversal step of every member with work
             if (team_on && !(T.t_mask == 0u && T.g_hits == 0u && T.sp == 0))
-                (void)trav_step<COUNT>(S, T, any, stack, tc, overflow, cull, RT);
+                (void)trav_step<COUNT>(S, T, any, stack, tc, overflow, cull);
             // occluder anywhere in the team; the team's closest hit so far (the cull bound)
             int hit = (any && T.hit_any) ? 1 : 0;
             float bt = T.best;
