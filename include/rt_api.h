@@ -342,7 +342,8 @@ typedef struct rt_tuning {
     int32_t finish_grid_pct;    /* percent of the resident grid the finish launch takes (default by
                                    frames in flight: 100 / 40 / 33 / 20 for 1 / 2 / 3 / 4+) */
     int32_t trace_grid_pct;     /* percent of the resident grid the bulk traversal launches take
-                                   (default 100, 60 with four or more frames in flight) */
+                                   (default 100; 60 with four to seven frames in flight; with eight,
+                                   20 / 30 / 40 for frames of up to 2.5M / 6M / more base paths) */
     int32_t shade_blocks;       /* wf_shade grid, a multiple of 8 (default 2048; <= 65536) */
     int32_t host_rounds;        /* 1: host-driven rounds (each round's queue size read back); default 0:
                                    device-side round control, whole frames as HIP graphs */

@@ -2069,7 +2069,14 @@ bool run_wavefront(const DevScene& S, const FrameParams& P, WavefrontBuffers& W,
     // four or more frames in flight: the bulk traversal launches take 60 % of the resident grid,
     // leaving CUs to the other frames' kernels (C3g 8.51-8.64 -> 8.61-8.72 Grays/s over five
     // alternating pairs, 75 % +0.5 %; the 8-way rank share at 75 % +0.9 %); fewer frames: all of it
-    Q.trace_frac = tu.trace_frac > 0 ? tu.trace_frac : (in_flight >= 4 ? 60 : 100);
+    // eight frames in flight (round 6): the smaller the frame, the smaller the share, so that more
+    // frames' bulk rounds run side by side -- 20 % up to 2.5M base paths (8-way C3g rank share 7.26 ->
+    // 7.51-7.54 Grays/s, 4-way 8.59 -> 8.87-8.88; 15 % 7.46-7.49), 30 % up to 6M (2-way 9.29 ->
+    // 9.47-9.55), 40 % above (the whole C3g frame 9.74-9.83 -> 9.82-9.91; 50 % 9.80-9.81)
+    // (profiles/r06_experiments.txt)
+    Q.trace_frac = tu.trace_frac > 0 ? tu.trace_frac
+                 : in_flight >= 8 ? (Q.base_paths <= 2500000u ? 20 : Q.base_paths <= 6000000u ? 30 : 40)
+                 : in_flight >= 4 ? 60 : 100;
     // eight frames in flight of at most 6M base paths (a multi-GPU rank's share): 12 % (round 5,
     // after the slots stopped serialising: 8-way rank share 6.76 -> 7.02, 4-way 8.14 -> 8.44, 2-way
     // (4.1M paths) 9.12 -> 9.35 Grays/s; 8 % +-0, 33 % -10 %; the whole C3g frame (8.3M) +-0 and
