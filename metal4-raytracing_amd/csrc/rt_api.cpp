@@ -67,7 +67,10 @@ struct Geo {
     DevBuf* all[10] = {&pos, &prev_pos, &nrm, &inst, &prev_inst, &tris, &nodes, &node_box, &tri_bin, &tri_nrm};
     uint32_t num_nodes8 = 0;
 };
-constexpr int kMaxSlots = 8;
+#ifndef RT_MAX_SLOTS
+#define RT_MAX_SLOTS 8
+#endif
+constexpr int kMaxSlots = RT_MAX_SLOTS;
 constexpr int kGens = kMaxSlots;   // generations allocated at most (ngens of them in use)
 // default finish threshold with 2 / 3 / 4 frames in flight (C3g sweeps: 1.25M, 1M and 512K paths;
 // round 2, with the DP-collapsed tree and the lighter shading kernels, two slots: 2M 5.88 / 5.89,
@@ -77,7 +80,8 @@ constexpr int kGens = kMaxSlots;   // generations allocated at most (ngens of th
 // in round 2, with the finish kernel on 20 % of the grid)
 // Final round-2 kernels, 8-way share with four slots: 256K 4.14 / 4.13, 512K 4.25 / 4.26, 768K
 // 4.32 / 4.30 Grays/s per rank -> 768K for four slots.
-constexpr int kTailInFlight[kMaxSlots + 1] = {0, 0, 1310720, 1048576, 786432, 524288, 524288, 524288, 524288};
+constexpr int kTailInFlightTab[9] = {0, 0, 1310720, 1048576, 786432, 524288, 524288, 524288, 524288};
+constexpr int kTailInFlight(int nfl) { return kTailInFlightTab[nfl < 8 ? nfl : 8]; }
 // Default frames in flight (render_frame): their buffers, ~300 B per allocated path (pixels x (spp +
 // motion-adaptive extra samples)) and slot (128 B path state and ray slots + 176 B of queues), stay
 // within kSlotBudget of the 288 GB (1080p x 4 + 2 extra: 3.7 GB a slot; configs[3]'s 3840x2160x16
@@ -1209,7 +1213,7 @@ rt_status rt_render_frame(rt_ctx* c, const Uniforms* U, const rt_tile_set* tiles
         // finish threshold: with frames in flight the next frames' bulk rounds overlap this
         // frame's tail, so more bulk rounds and a shorter tail pay (kTailInFlight: C3g, 2 in
         // flight 1.25M paths against the one-frame-at-a-time optimum of 4M; 3 in flight 1M)
-        int tail = c->tail_paths ? c->tail_paths : (nfl > 1 ? kTailInFlight[nfl] : 0);
+        int tail = c->tail_paths ? c->tail_paths : (nfl > 1 ? kTailInFlight(nfl) : 0);
         // eight frames in flight and a frame of at most 2.5M base paths (a multi-GPU rank's share):
         // 768K (round 5, finish on 12 % of the grid: 8-way share 7.02 -> 7.20, 4-way 8.44 -> 8.54
         // Grays/s; 1M hands the 8-way share's whole frame to the finish: 6.08)
