@@ -19,14 +19,26 @@ struct MatRec {
 };
 constexpr int kMatLds = 128;   // material records staged in LDS per block (4 KB)
 
-// Per-block lookup tables of the shading code: the first Halton dimensions and the scene's
-// material records in LDS (global memory beyond what was staged).
+constexpr int kInstLds = 32;   // instance matrices staged in LDS per block (48 B each, 1.5 KB)
+constexpr int kLightLds = 8;   // lights staged in LDS per block (128 B each, 1 KB)
+
+// Per-block lookup tables of the shading code: the first Halton dimensions, the scene's
+// material records, instance matrices and lights in LDS (global memory beyond what was staged).
+// A hit's instance matrix is the third load of a dependent chain (queue entry -> tri_nrm ->
+// matrix) and its light record waits on the Halton light choice; from LDS each costs an LDS round
+// trip instead of an L2 one (wf_shade 0.336 -> 0.310 ms per launch).
 struct ShadeTabs {
     const HaltonDim* lds;
     const HaltonDim* glob;
     const MatRec* mat_lds;
     const Material* mat_glob;
     int n_mat_lds;             // = number of materials when they fit in LDS, else 0
+    const float4* inst_lds;    // 3 float4 per instance: the 12 floats of its packed 4x3
+    const float* inst_glob;
+    int n_inst_lds;            // = number of instances when they fit in LDS, else 0
+    const Light* light_lds;
+    const Light* light_glob;
+    int n_light_lds;           // = lightCount when the lights fit in LDS, else 0
     __device__ __forceinline__ float operator()(int i, int d) const {
         if (d == 0) return halton_base2(i);   // base 2: closed form (bit-identical, rt_math.h)
         return halton_fast(i, d < kHaltonLds ? lds[d] : glob[d]);
@@ -39,11 +51,21 @@ struct ShadeTabs {
         r.emis = make_float4(m.emission.x, m.emission.y, m.emission.z, m.refractionIndex);
         return r;
     }
+    // The instance's 12 floats and the light record, from LDS when staged: one pointer that may
+    // point to either (flat loads), which measured faster than a branch between an LDS and a
+    // global load of the same record (wf_shade 0.310 vs 0.313 ms; both branches' registers)
+    __device__ __forceinline__ const float* instance(int k) const {
+        return k < n_inst_lds ? reinterpret_cast<const float*>(inst_lds + 3 * k) : inst_glob + 12 * (size_t)k;
+    }
+    __device__ __forceinline__ const Light& light(int k) const { return k < n_light_lds ? light_lds[k] : light_glob[k]; }
 };
 
-// Stages the Halton dimensions and the material records of the scene in LDS; every thread of
-// the block calls it (ends with a barrier).
-__device__ __forceinline__ ShadeTabs load_tabs(const DevScene& S, HaltonDim* lds_halton, MatRec* lds_mat) {
+// Stages the Halton dimensions and the material records, instance matrices and lights of the
+// scene in LDS (each table only when its LDS array is given and the scene's table fits); every
+// thread of the block calls it (ends with a barrier).
+__device__ __forceinline__ ShadeTabs load_tabs(const DevScene& S, HaltonDim* lds_halton, MatRec* lds_mat,
+                                               float4* lds_inst = nullptr, Light* lds_light = nullptr,
+                                               int light_count = 0) {
     for (int i = threadIdx.x; i < kHaltonLds; i += blockDim.x) lds_halton[i] = S.halton[i];
     const int n_mat = (lds_mat && S.num_materials <= kMatLds) ? S.num_materials : 0;
     for (int i = threadIdx.x; i < n_mat; i += blockDim.x) {
@@ -51,8 +73,15 @@ __device__ __forceinline__ ShadeTabs load_tabs(const DevScene& S, HaltonDim* lds
         lds_mat[i].base = make_float4(m.baseColor.x, m.baseColor.y, m.baseColor.z, m.opacity);
         lds_mat[i].emis = make_float4(m.emission.x, m.emission.y, m.emission.z, m.refractionIndex);
     }
+    const int n_inst_all = S.max_submeshes > 0 ? S.num_materials / S.max_submeshes : 0;
+    const int n_inst = (lds_inst && n_inst_all <= kInstLds) ? n_inst_all : 0;
+    const float4* ig = reinterpret_cast<const float4*>(S.inst);
+    for (int i = threadIdx.x; i < 3 * n_inst; i += blockDim.x) lds_inst[i] = ig[i];
+    const int n_light = (lds_light && light_count <= kLightLds) ? light_count : 0;
+    for (int i = threadIdx.x; i < n_light; i += blockDim.x) lds_light[i] = S.lights[i];
     __syncthreads();
-    return ShadeTabs{lds_halton, S.halton, lds_mat, S.materials, n_mat};
+    return ShadeTabs{lds_halton, S.halton, lds_mat, S.materials, n_mat, lds_inst, S.inst, n_inst,
+                     lds_light, S.lights, n_light};
 }
 
 struct PathRegs {
@@ -181,7 +210,7 @@ __device__ __forceinline__ void shade_step(const DevScene& S, const Uniforms& U,
     const uint32_t tw = __float_as_uint(rn1.w);
     int instanceIndex = (int)(tw >> 8);
     int geometryIndex = (int)(tw & 0xffu);
-    const float* M = S.inst + 12 * instanceIndex;                                       // :329-333
+    const float* M = halton.instance(instanceIndex);                                    // :329-333 (LDS)
     f3 P_ = rayO + rayD * h.t;                                                          // :336
     const MatRec mat = halton.material(instanceIndex * S.max_submeshes + geometryIndex); // :337-339 (LDS)
     float bu = h.u, bv = h.v, bw = (1.0f - bu) - bv;                                    // :63-65
@@ -348,7 +377,7 @@ __device__ __forceinline__ void shade_step(const DevScene& S, const Uniforms& U,
 
     float lightSample = halton(hidx, 2 + p.step * 6 + 0);                             // :588-591
     int lightIndex = min((int)(lightSample * (float)U.lightCount), U.lightCount - 1);
-    const Light& light = S.lights[lightIndex];
+    const Light& light = halton.light(lightIndex);                                      // (LDS)
     f3 Ldir, lightColor;
     float lightDistance;
     f3 lpos = ldf3(light.position), lcol = ldf3(light.color);

@@ -601,9 +601,11 @@ __global__ void __launch_bounds__(kBlock) wf_shade(DevScene S, const FrameParams
     const FrameParams& P = *Pp;   // per-frame parameters in device memory
     __shared__ HaltonDim lds_halton[kHaltonLds];
     __shared__ MatRec lds_mat[kMatLds];
+    __shared__ float4 lds_inst[3 * kInstLds];
+    __shared__ Light lds_light[kLightLds];
     __shared__ BlockAllocOct bao;
     if (tail_mode(Q)) return;
-    const ShadeTabs halton = load_tabs(S, lds_halton, lds_mat);
+    const ShadeTabs halton = load_tabs(S, lds_halton, lds_mat, lds_inst, lds_light, P.U.lightCount);
     const Uniforms& U = P.U;
     const int next = 1 - cur;
     const int shard = blockIdx.x & (kShards - 1);
@@ -632,8 +634,16 @@ __global__ void __launch_bounds__(kBlock) wf_shade(DevScene S, const FrameParams
             }
         ebase = (uint32_t)shard * Q.seg_cap;
     }
+#if RT_XP_SHADE_PF
+    float4 hv_next = make_float4(0.0f, 0.0f, 0.0f, 0.0f);   // the next entry's hit, loaded one iteration ahead
+    if (!SORTED && beg + threadIdx.x < end) hv_next = ld_shade(&Q.W.hits[ebase + seg_pos(beg + threadIdx.x, lk, Q.seg_cap)]);
+#endif
     for (uint32_t base = beg; base < end; base += stride) {
         uint32_t g = base + threadIdx.x;
+#if RT_XP_SHADE_PF
+        const float4 hv_cur = hv_next;
+        if (!SORTED && g + stride < end) hv_next = ld_shade(&Q.W.hits[ebase + seg_pos(g + stride, lk, Q.seg_cap)]);
+#endif
         StepResult r;
         r.next = false;
         r.shadow = false;
@@ -653,7 +663,11 @@ __global__ void __launch_bounds__(kBlock) wf_shade(DevScene S, const FrameParams
                 const uint32_t e = ebase + seg_pos(g, lk, Q.seg_cap);
                 o = ld_shade(&qin[2 * (size_t)e]);
                 d = ld_shade(&qin[2 * (size_t)e + 1]);
+#if RT_XP_SHADE_PF
+                hv = hv_cur;
+#else
                 hv = ld_shade(&Q.W.hits[e]);
+#endif
                 ce = e;
             }
             pid = __float_as_uint(o.w);
@@ -976,12 +990,14 @@ wf_finish_step(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int c
     __shared__ int lds_stack[kStackSize * kBlock];
     __shared__ HaltonDim lds_halton[kHaltonLds];
     __shared__ MatRec lds_mat[kMatLds];
+    __shared__ float4 lds_inst[3 * kInstLds];
+    __shared__ Light lds_light[kLightLds];
     __shared__ float lds_sray[6][kBlock];   // each lane's shadow ray (origin, direction)
     int* stack = &lds_stack[threadIdx.x];
     __shared__ uint32_t ts_done;
     if (threadIdx.x == 0) ts_done = 0u;
     ts_start(Q, ts);
-    const ShadeTabs halton = load_tabs(S, lds_halton, lds_mat);   // ends with a block barrier
+    const ShadeTabs halton = load_tabs(S, lds_halton, lds_mat, lds_inst, lds_light, P.U.lightCount);   // ends with a block barrier
     const Uniforms& U = P.U;
     const QueueShards qs = load_queue(Q.W.counts, cur, Q.seg_cap);   // front parts first: the likely-long paths
     const uint32_t n = queue_len(qs);
