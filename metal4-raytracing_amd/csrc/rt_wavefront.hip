@@ -634,16 +634,8 @@ __global__ void __launch_bounds__(kBlock) wf_shade(DevScene S, const FrameParams
             }
         ebase = (uint32_t)shard * Q.seg_cap;
     }
-#if RT_XP_SHADE_PF
-    float4 hv_next = make_float4(0.0f, 0.0f, 0.0f, 0.0f);   // the next entry's hit, loaded one iteration ahead
-    if (!SORTED && beg + threadIdx.x < end) hv_next = ld_shade(&Q.W.hits[ebase + seg_pos(beg + threadIdx.x, lk, Q.seg_cap)]);
-#endif
     for (uint32_t base = beg; base < end; base += stride) {
         uint32_t g = base + threadIdx.x;
-#if RT_XP_SHADE_PF
-        const float4 hv_cur = hv_next;
-        if (!SORTED && g + stride < end) hv_next = ld_shade(&Q.W.hits[ebase + seg_pos(g + stride, lk, Q.seg_cap)]);
-#endif
         StepResult r;
         r.next = false;
         r.shadow = false;
@@ -663,11 +655,7 @@ __global__ void __launch_bounds__(kBlock) wf_shade(DevScene S, const FrameParams
                 const uint32_t e = ebase + seg_pos(g, lk, Q.seg_cap);
                 o = ld_shade(&qin[2 * (size_t)e]);
                 d = ld_shade(&qin[2 * (size_t)e + 1]);
-#if RT_XP_SHADE_PF
-                hv = hv_cur;
-#else
                 hv = ld_shade(&Q.W.hits[e]);
-#endif
                 ce = e;
             }
             pid = __float_as_uint(o.w);
@@ -678,10 +666,17 @@ __global__ void __launch_bounds__(kBlock) wf_shade(DevScene S, const FrameParams
             h.v = hv.w;
             if (h.id != 0xffffffffu) {                                           // miss -> path ends (:321-322)
                 const uint32_t state = __float_as_uint(d.w);
-                const uint3 pm = path_meta(P, Q, pid);
-                const uint4 meta = make_uint4(pm.x, pm.y, state, pm.z);
                 const float4 c = state == 0u ? make_float4(1.0f, 1.0f, 1.0f, 0.0f)
                                              : (SORTED ? Q.W.sorted[ce] : ld_shade(&Q.W.qc[cur][ce]));
+                // a continuation ray past bounce 0 carries its Halton index in qc.w: the pixel and sample
+                // (and the per-pixel random offset behind them) are read only at bounce 0 (:342-389)
+                uint4 meta;
+                if ((state & 0xffu) != 0u) {
+                    meta = make_uint4(0u, 1u, state, __float_as_uint(c.w));
+                } else {
+                    const uint3 pm = path_meta(P, Q, pid);
+                    meta = make_uint4(pm.x, pm.y, state, pm.z);
+                }
                 // FULL=false: shade_step only adds color * emission to accum (:585), so it runs on a
                 // zero accumulator and the stored one is read and updated only when that term is
                 // non-zero (accum is never -0, so a + (0 + x) == a + x bit for bit); FULL (debug
@@ -701,7 +696,7 @@ __global__ void __launch_bounds__(kBlock) wf_shade(DevScene S, const FrameParams
                 write_pixel_outputs(P, meta.x, r, h, FULL);
                 nstate = pack_state(p.bounce, p.tpass, p.step);
                 front = likely_long(p);
-                ncol = make_float4(p.color.x, p.color.y, p.color.z, 0.0f);
+                ncol = make_float4(p.color.x, p.color.y, p.color.z, __uint_as_float(meta.w));   // w: Halton index
                 // radiance only changes on emissive hits (:585-586): skip the store otherwise
                 if (__float_as_uint(p.accum.x) != __float_as_uint(a.x) || __float_as_uint(p.accum.y) != __float_as_uint(a.y) ||
                     __float_as_uint(p.accum.z) != __float_as_uint(a.z)) {
@@ -1092,10 +1087,14 @@ wf_finish_step(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int c
                     const float4 d = ld_stream(&src[1]);
                     pid = __float_as_uint(o.w);
                     const uint32_t state = __float_as_uint(d.w);
-                    const uint3 pm = path_meta(P, Q, pid);
-                    meta = make_uint4(pm.x, pm.y, state, pm.z);
                     const float4 c = state == 0u ? make_float4(1.0f, 1.0f, 1.0f, 0.0f)
                                      : ld_stream(&Q.W.qc[cur][e]);
+                    if ((state & 0xffu) != 0u) {   // past bounce 0: the Halton index from qc.w (wf_shade)
+                        meta = make_uint4(0u, 1u, state, __float_as_uint(c.w));
+                    } else {
+                        const uint3 pm = path_meta(P, Q, pid);
+                        meta = make_uint4(pm.x, pm.y, state, pm.z);
+                    }
                     const float4 a = Q.W.p_accum[pid];
                     p.color = mk3(c.x, c.y, c.z);
                     p.accum = mk3(a.x, a.y, a.z);
