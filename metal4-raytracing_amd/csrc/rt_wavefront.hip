@@ -825,7 +825,6 @@ __global__ void __launch_bounds__(kSortThreads) wf_sort_scatter(DevScene S, WfPa
     }
 }
 
-#if RT_XP_CONNECT_BATCH
 // connect: the accumulation of the unoccluded shadow rays of a wave, batched (one lane per pending
 // entry: its path id and contribution from the shadow queue, then accum += contribution, :741-743)
 // so the wave waits for these dependent loads once per up to 64 rays, not once per finishing step.
@@ -846,7 +845,6 @@ __device__ __forceinline__ void connect_flush(const WfParams& Q, const float4* q
     __builtin_amdgcn_wave_barrier();
     npend = 0;
 }
-#endif
 
 // ---- persistent traversal with per-lane refill (extend: ANY = false, connect: ANY = true) -----------
 // The grid is the resident capacity.  Each XCD (blockIdx % 8) owns queue shard k (what its own shade blocks appended) and hands
@@ -933,11 +931,9 @@ wf_trace(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int cur, in
     Trav T;
     trav_start(T, mk3(0, 0, 0), mk3(1, 0, 0), 0.0f);
     uint32_t steps = 0;   // COUNT: iterations the current ray has taken
-#if RT_XP_CONNECT_BATCH
     __shared__ uint32_t lds_pend_all[ANY ? kBlock : 1];
     uint32_t* const lds_pend = &lds_pend_all[ANY ? (threadIdx.x & ~63u) : 0u];   // the wave's 64 slots
     uint32_t npend = 0;   // wave-uniform
-#endif
 
     while (true) {
         // refill idle lanes from the wave's chunk
@@ -969,7 +965,6 @@ wf_trace(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int cur, in
             }
             wnext += (uint32_t)__popcll(idle);
         }
-#if RT_XP_CONNECT_BATCH
         if (__ballot(active) == 0ull) {
             if (ANY) connect_flush(Q, qin, lds_pend, npend);
             break;
@@ -997,30 +992,6 @@ wf_trace(DevScene S, const FrameParams* __restrict__ Pp, WfParams Q, int cur, in
             }
         }
     }
-#else
-        if (__ballot(active) == 0ull) break;
-        if (!active) continue;
-        if (COUNT) ++steps;
-        if (trav_step<COUNT>(S, T, ANY, stack, tc, overflow, T.best)) {
-            active = false;
-            if (COUNT && Q.diag) {   // steps-per-ray histogram (log2 bins) of the counting frame
-                atomicAdd(&Q.W.counts[kWfDiagSteps + (ANY ? 32 : 0) + (31 - __builtin_clz(steps))], 1u);
-                atomicMax(&Q.W.counts[kWfDiagSteps + 64 + (ANY ? 1 : 0)], steps);
-            }
-            if (ANY) {
-                if (!T.hit_any) {   // unoccluded: accum += contribution (:741-743)
-                    float4 o4 = qin[(size_t)qstride * e];
-                    uint32_t pid = __float_as_uint(o4.w);
-                    float4 c = qin[(size_t)qstride * e + 2];
-                    float4 a = Q.W.p_accum[pid];
-                    Q.W.p_accum[pid] = make_float4(a.x + c.x, a.y + c.y, a.z + c.z, 0.0f);
-                }
-            } else {
-                Q.W.hits[e] = make_float4(T.best, __uint_as_float(T.best_id), T.bu / T.bdet, T.bv / T.bdet);
-            }
-        }
-    }
-#endif
     ts_end(Q, ts, &ts_done);
     flush_counters(P, ANY ? 0 : rays, ANY ? rays : 0, 0, tc, COUNT, overflow, true);
 }
